@@ -1,0 +1,50 @@
+# Builds the product library turboinfer_amd/lib/libturboinfer_amd.so for gfx950 (MI355X):
+#   HIP kernels (turboinfer_amd/csrc/kernels/*.hip) + the C-ABI shim and the C++20 host
+#   library (turboinfer_amd/csrc/host/*.cpp, public headers under include/).
+# `make test-bins` builds the C++ API tests under tests/cpp/.
+# The test oracle is built separately by oracle/Makefile (never linked in here).
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+JOBS    ?= 8
+BUILD   := build
+LIBDIR  := turboinfer_amd/lib
+LIB     := $(LIBDIR)/libturboinfer_amd.so
+
+COMMON  := -std=c++20 -O3 -fPIC -Iinclude -Iturboinfer_amd/csrc/kernels -Wall -Wno-unused-result -Wno-unused-value
+DEVFLAGS:= $(COMMON) --offload-arch=$(ARCH) -fno-gpu-rdc
+
+KERN    := $(wildcard turboinfer_amd/csrc/kernels/*.hip)
+HOST    := $(wildcard turboinfer_amd/csrc/host/*.cpp)
+KOBJ    := $(patsubst turboinfer_amd/csrc/kernels/%.hip,$(BUILD)/k_%.o,$(KERN))
+HOBJ    := $(patsubst turboinfer_amd/csrc/host/%.cpp,$(BUILD)/h_%.o,$(HOST))
+HDRS    := $(wildcard include/*.h) $(wildcard include/turboinfer/*/*.hpp) $(wildcard include/turboinfer/*.hpp) \
+           $(wildcard turboinfer_amd/csrc/kernels/*.hpp) $(wildcard turboinfer_amd/csrc/host/*.hpp)
+
+all: $(LIB)
+
+$(BUILD)/k_ops_exact.o: turboinfer_amd/csrc/kernels/ops_exact.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(DEVFLAGS) -ffp-contract=off -c $< -o $@
+
+$(BUILD)/k_%.o: turboinfer_amd/csrc/kernels/%.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(DEVFLAGS) -c $< -o $@
+
+$(BUILD)/h_%.o: turboinfer_amd/csrc/host/%.cpp $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(COMMON) -ffp-contract=off -x hip --offload-arch=$(ARCH) -c $< -o $@
+
+$(LIB): $(KOBJ) $(HOBJ)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(KOBJ) $(HOBJ) -Wl,-soname,libturboinfer_amd.so
+
+CPPTESTS := $(patsubst tests/cpp/%.cpp,$(BUILD)/tests/%,$(wildcard tests/cpp/*.cpp))
+test-bins: $(CPPTESTS)
+$(BUILD)/tests/%: tests/cpp/%.cpp $(LIB)
+	@mkdir -p $(BUILD)/tests
+	$(HIPCC) -std=c++20 -O2 -Iinclude $< -o $@ -L$(LIBDIR) -lturboinfer_amd -Wl,-rpath,$(abspath $(LIBDIR))
+
+clean:
+	rm -rf $(BUILD) $(LIBDIR)
+
+.PHONY: all clean test-bins

@@ -1,0 +1,106 @@
+/*
+ * ti_engine.h -- extern "C" decode engine: the device-resident state behind
+ * turboinfer::model::InferenceEngine (its pimpl InferenceEngineImpl,
+ * include/turboinfer/model/inference_engine.hpp:214 in the reference) exported as a flat
+ * C-ABI so the benchmark, the tests and other-language hosts can drive it.
+ *
+ * Replaces, per decode step, InferenceEngine::forward_pass_incremental
+ * (src/model/inference_engine.cpp:1493-1552) -> TransformerLayer::forward_incremental
+ * (:244-279) -> KVCache::update_incremental (:78-160), plus greedy sample_next_token
+ * (:1554-1673, top_k = 1) and the generate() loop (:734-802).
+ *
+ * One engine = one device + one HIP stream + B decode streams (requests) whose fp16 KV
+ * caches live in that device's HBM.  Independent engines on different devices are
+ * independent replicas (no collectives).
+ */
+#ifndef TI_ENGINE_H
+#define TI_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ti_engine ti_engine;
+
+typedef struct ti_engine_config {
+  int32_t vocab, hidden, layers, heads, kv_heads, head_dim, inter;
+  float rope_theta;        /* ModelMetadata::rope_theta (reference default 10000) */
+  float eps;               /* rms_norm eps, reference default 1e-5 (tensor_engine.hpp:185) */
+  int32_t bits;            /* weight format: 4 (INT4 g128), 8 (INT8 g128), 16 (fp16) */
+  int32_t max_seq;         /* KV slots per stream */
+  int32_t max_batch;       /* decode streams held by the engine */
+  int32_t compat;          /* 1 = reference_compat: placeholder embeddings, attention
+                              bypass, ReLU FFN, fp32 weights (benchmark plumbing model) */
+  int32_t device;
+  int32_t attn_splits;     /* 0 = auto */
+} ti_engine_config;
+
+enum ti_slot {
+  TI_W_Q = 0, TI_W_K, TI_W_V, TI_W_O, TI_W_GATE, TI_W_UP, TI_W_DOWN, /* per layer, [K][N] */
+  TI_W_LM_HEAD,                                                    /* [hidden][vocab]   */
+  TI_V_ATTN_NORM, TI_V_FFN_NORM,                                   /* per layer, [hidden] */
+  TI_V_OUT_NORM,                                                   /* [hidden] */
+  TI_E_EMBED                                                       /* [vocab][hidden]   */
+};
+
+int ti_engine_create(const ti_engine_config* cfg, ti_engine** out);
+int ti_engine_destroy(ti_engine* e);
+int ti_engine_get_stream(ti_engine* e, void** stream);
+int ti_engine_memory(ti_engine* e, size_t* weight_bytes, size_t* kv_bytes);
+
+/* Upload one tensor given in the reference layout (fp32 host memory); linear weights are
+ * quantized + packed per the engine's bits (scale_mode: ti_hip.h TI_SCALE_*). */
+int ti_engine_set_tensor(ti_engine* e, int slot, int layer, const float* data, int scale_mode);
+/* Synthetic model of SURVEY 8(d) generated on the device (bit-identical to the oracle's
+ * or_model_synth for the same seed / jitter). */
+int ti_engine_synth(ti_engine* e, uint64_t seed, float norm_jitter);
+/* Fill KV slots [0, n) of `stream` (all layers) with seeded fp16 U(-1,1) (or_model_fill_kv). */
+int ti_engine_fill_kv(ti_engine* e, int stream, int n, uint64_t seed);
+
+/* Greedy generation for n_streams independent requests, entirely on the device: every
+ * stream starts at position start_pos[s] (NULL = 0), consumes its prompt one token per
+ * step, then feeds back its argmax.  out_tokens [n_streams][max_new] receives the first
+ * max_new generated tokens; last_logits (nullable) [n_streams][vocab] the logits of the
+ * final step. */
+int ti_engine_generate(ti_engine* e, int n_streams, const int32_t* prompts, const int32_t* prompt_lens,
+                       int prompt_stride, const int32_t* start_pos, int max_new, int32_t* out_tokens,
+                       float* last_logits);
+
+/* One decode step: token[s] at position pos[s] for each stream; logits [n][vocab] to host
+ * (used for non-greedy sampling and per-step parity). */
+int ti_engine_step(ti_engine* e, int n_streams, const int32_t* tokens, const int32_t* pos, float* logits);
+
+/* reference_compat step (compat engines): placeholder row offset, logits [vocab] to host. */
+int ti_engine_compat_step(ti_engine* e, int placeholder_offset, float* logits);
+
+/* Benchmark replay: every stream decodes at fixed position kv_len - 1 (reads
+ * exactly kv_len cache slots), greedy feedback from start_token.  prepare captures the
+ * step graph; run enqueues `steps` replays without synchronising. */
+int ti_engine_replay_prepare(ti_engine* e, int n_streams, int kv_len, int start_token);
+int ti_engine_replay_run(ti_engine* e, int steps);
+int ti_engine_sync(ti_engine* e);
+/* tokens decided by the last replay step, [n_streams] */
+int ti_engine_last_tokens(ti_engine* e, int n_streams, int32_t* tokens);
+
+/* Live per-kernel timing: launch the step's linears of class `which` (0 qkv, 1 o, 2 gate/up,
+ * 3 down, 4 lm_head, 5 attention) `reps` times back to back between two HIP events on the
+ * engine stream.  avg_us = average per launch; bytes = algorithmic HBM bytes per launch. */
+int ti_engine_time_kernel(ti_engine* e, int which, int n_streams, int kv_len, int reps, double* avg_us,
+                          double* bytes);
+
+/* ------------------------------------------------------------- host helpers */
+/* RoPE (cos, sin) pairs for each of npos positions: out [npos][head_dim/2][2], computed on the
+ * host with the reference formula (tensor_engine.cpp:1561-1566, 1595-1597) in fp32 libm. */
+int ti_rope_table(const float* pos, int npos, int head_dim, float theta, float* out);
+/* InferenceEngine::sample_next_token (inference_engine.cpp:1554-1673) with the uniform draw u
+ * supplied: temperature, top-k (std::sort ranking, reference tie order), softmax, top-p. */
+int ti_sample_token(const float* logits, int vocab, float temperature, int top_k, float top_p, float u,
+                    int* token, float* logprob);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TI_ENGINE_H */

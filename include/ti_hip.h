@@ -1,0 +1,211 @@
+/*
+ * ti_hip.h -- the flat extern "C" boundary between the turboinfer C++20 host library
+ * and the hand-written gfx950 (MI355X / CDNA4) HIP kernels of the decode hot path.
+ *
+ * Plain pointers and sizes only (no C++ or torch types).  Every function returns
+ * TI_OK (0) or a TI_ERR_* code; ti_last_error() returns the thread's last message.
+ * Pointers documented "device" must be device memory (ti_malloc or hipMalloc).
+ * Streams are hipStream_t values passed as void* (NULL = default stream).
+ *
+ * Which reference interface each entry replaces (paths relative to the reference
+ * repository, juliuspleunes4/TurboInfer @ 2025-09-05):
+ *   ti_gemm_wq_a16        TensorEngine::matmul -> matmul_3d_2d      src/core/tensor_engine.cpp:490-528, 594-640
+ *                         (+ the convert_dtype "dequant" of int weights :2218-2284, scale restored)
+ *                         + fused rms_norm :1452-1508 prologue, add :1626-1678 / silu :900-923 /
+ *                         multiply :1680-1743 / apply_rope :1510-1624 epilogues, KV append
+ *                         (KVCache::update_incremental, src/model/inference_engine.cpp:78-160)
+ *   ti_attn_decode        TensorEngine::multi_head_attention :1149-1252 -> attention_fast_incremental :1254-1388
+ *   ti_wpack_host         Quantizer::quantize_tensor / quantize_to_int{4,8}
+ *                         src/optimize/quantization.cpp:36-64, 662-693 (per group of 128, packed)
+ *   ti_matmul_f32         TensorEngine::matmul (fp32, bit-exact k-ascending fma chain)
+ *   ti_rms_norm_f32       TensorEngine::rms_norm  :1452-1508 (bit-exact reduction order)
+ *   ti_rope_f32           TensorEngine::apply_rope :1510-1624 (host cos/sin table, same fma pattern)
+ *   ti_silu_f32 / ti_add_f32 / ti_mul_f32 / ti_relu_f32   :900-923, :1626-1743, :828-869
+ *   ti_softmax_f32        TensorEngine::softmax :925-1043 (same fast_exp_avx2 polynomial :262-302)
+ *   ti_argmax_f32         greedy InferenceEngine::sample_next_token (top_k = 1) :1554-1673
+ */
+#ifndef TI_HIP_H
+#define TI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* ti_stream_t;
+
+enum ti_status {
+  TI_OK = 0,
+  TI_ERR_ARG = 1,          /* bad shape / argument (host-side check, nothing launched) */
+  TI_ERR_HIP = 2,          /* HIP runtime error */
+  TI_ERR_UNSUPPORTED = 3,  /* configuration not supported by the kernels */
+  TI_ERR_NOMEM = 4,
+  TI_ERR_NODEV = 5         /* no gfx950 device visible */
+};
+
+const char* ti_last_error(void);
+
+/* ------------------------------------------------------------ device plumbing */
+int ti_device_count(int* count);
+int ti_init(int device);                          /* select device, check it is gfx950 */
+int ti_device_name(int device, char* buf, int len);
+int ti_malloc(void** ptr, size_t bytes);
+int ti_free(void* ptr);
+int ti_memcpy_h2d(void* dst, const void* src, size_t bytes, ti_stream_t s);
+int ti_memcpy_d2h(void* dst, const void* src, size_t bytes, ti_stream_t s);
+int ti_memcpy_d2d(void* dst, const void* src, size_t bytes, ti_stream_t s);
+int ti_memset(void* ptr, int value, size_t bytes, ti_stream_t s);
+int ti_stream_create(ti_stream_t* s);
+int ti_stream_destroy(ti_stream_t s);
+int ti_stream_sync(ti_stream_t s);
+int ti_device_sync(void);
+int ti_event_create(void** ev);
+int ti_event_destroy(void* ev);
+int ti_event_record(void* ev, ti_stream_t s);
+int ti_event_elapsed_ms(void* start, void* stop, float* ms); /* synchronises on stop */
+
+/* -------------------------------------------- packed quantized linear weights
+ * A linear layer y = x @ W with the reference's W[K][N] row-major layout
+ * (inference_engine.cpp:299-301) is stored as tiles of 16 output rows x 128 k:
+ *   bits 4 : 1 KiB per tile,  nibble q+8 (q in [-7,7], reference symmetric int4 range)
+ *   bits 8 : 2 KiB per tile,  int8 q in [-128,127]
+ *   bits 16: 4 KiB per tile,  fp16 weights (no scale)
+ * tiles ordered [N/16][K/128]; inside a tile, 1 KiB chunk c holds for lane l (0..63)
+ * at byte 1024*c + 16*l the k-run of output row (l & 15) starting at
+ * k = 32*(l >> 4) + c*(32/chunks) -- one coalesced dwordx4 per lane per chunk.
+ * Group scales (bits 4/8): fp16, [N/16][K/128][16].
+ * K must be a multiple of 128 and N a multiple of 16. */
+enum ti_scale_mode { TI_SCALE_GROUP = 0, TI_SCALE_TENSOR = 1, TI_SCALE_UNIT = 2 };
+enum ti_row_map { TI_ROWS_CONCAT = 0, TI_ROWS_INTERLEAVE8 = 1 };
+
+size_t ti_wpack_tile_bytes(int bits, int K, int N);
+size_t ti_wpack_scale_bytes(int bits, int K, int N);
+
+/* Quantize + pack the fp32 [K][N_src] matrix w (host memory) into the host buffers of
+ * a fused weight with N_total output rows.  Source column c lands on output row
+ *   TI_ROWS_CONCAT      : row_offset + c
+ *   TI_ROWS_INTERLEAVE8 : 16*(c/8) + (c%8) + row_offset   (row_offset 0 = gate, 8 = up)
+ * scale_mode: per group of 128 (absmax/7 or /127, reference quantize_to_int* formula per
+ * group), one per-tensor scale (reference Quantizer), or unit (reference raw cast). */
+int ti_wpack_host(const float* w, int K, int N_src, int N_total, int bits, int scale_mode,
+                  int row_map, int row_offset, void* tiles, uint16_t* scales);
+
+/* The synthetic model of SURVEY 8(d) generated straight into device tiles:
+ * element (k, c) of tensor `tensor_id` = u(seed, tensor_id, k*N_src + c) * amp,
+ * amp = sqrtf(3)/sqrtf(K) (u: or_synth_unit), quantized per group like ti_wpack_host. */
+int ti_wsynth_device(uint64_t seed, uint32_t tensor_id, int K, int N_src, int N_total, int bits,
+                     int row_map, int row_offset, void* tiles, uint16_t* scales, ti_stream_t s);
+/* dst[i] = fp16(u(seed, tensor_id, i) * mul) (+ add, fp32 variant) for i < n. */
+int ti_fill_uniform_f16(uint64_t seed, uint32_t tensor_id, uint64_t n, float mul, uint16_t* dst,
+                        ti_stream_t s);
+int ti_fill_uniform_f32(uint64_t seed, uint32_t tensor_id, uint64_t n, float mul, float add,
+                        float* dst, ti_stream_t s);
+/* Synthetic KV for one stream of one layer: slots [0, n) of dst ([kv_heads][max_seq][head_dim]
+ * fp16) from the oracle's [pos][kv_heads*head_dim] uniform stream (or_model_fill_kv). */
+int ti_fill_kv_uniform(uint64_t seed, uint32_t tensor_id, int n, int kv_heads, int head_dim, int max_seq,
+                       uint16_t* dst, ti_stream_t s);
+
+/* ---------------------------------------------------- fused decode GEMM/GEMV
+ * y[m][n] = sum_k xa[m][k] * W[k][n], m < M <= 16, with
+ *   xa = fp16(x)                               (x_kind TI_X_F16 / TI_X_F32), or
+ *   xa = fp16((x / sqrt(mean(x^2)+eps)) * nw)  (x_kind TI_X_F32_RMSNORM; fused rms_norm)
+ * fp16 x fp16 products on MFMA v_mfma_f32_16x16x32_f16, fp32 accumulation, group scale
+ * applied in fp32 per 128-k group.  Epilogue (all outputs of one call): */
+enum ti_x_kind { TI_X_F16 = 0, TI_X_F32 = 1, TI_X_F32_RMSNORM = 2 };
+enum ti_epilogue_kind {
+  TI_EPI_STORE_F32 = 0,      /* out_f32[m*ldo + n] = y                                  */
+  TI_EPI_STORE_F16 = 1,      /* out_f16[m*ldo + n] = fp16(y)                             */
+  TI_EPI_RESID_F32 = 2,      /* out_f32[m*ldo + n] += y          (residual add, in place) */
+  TI_EPI_SILU_MUL_F16 = 3,   /* rows interleaved by 8 (gate,up): out_f16[m*ldo + j] =
+                                fp16(up_j * silu(gate_j)), N/2 outputs                   */
+  TI_EPI_QKV_ROPE_KV = 4,    /* rows [q | k | v]: RoPE(pos[m]) on q and k, q -> out_f32,
+                                k, v -> fp16 KV cache slot pos[m]                        */
+  TI_EPI_LOGITS_ARGMAX = 5   /* out_f32 logits + atomicMax of (value, -index) into argmax[m] */
+};
+
+typedef struct ti_epilogue {
+  int32_t kind;
+  int32_t ldo;                       /* output leading dimension (elements) */
+  void* out;                         /* device output base */
+  /* TI_EPI_QKV_ROPE_KV */
+  int32_t q_dim, kv_dim, head_dim, max_seq;
+  const int32_t* pos;                /* device [M] token positions */
+  const float* rope_cs;              /* device [max_seq][head_dim/2] (cos, sin) pairs */
+  uint16_t* k_cache;                 /* device fp16, this layer: [stream][kv_head][max_seq][head_dim] */
+  uint16_t* v_cache;
+  int64_t kv_stream_stride;          /* elements between streams */
+  /* TI_EPI_LOGITS_ARGMAX */
+  unsigned long long* argmax;        /* device [M] keys, zeroed before the call */
+  int32_t* step_ctr;                 /* device counter += advance by one thread (nullable) */
+  int32_t advance;
+  int32_t _pad;
+} ti_epilogue;
+
+int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind,
+                   int ldx, const float* norm_w, float eps, int M, int N, int K,
+                   const ti_epilogue* epi, ti_stream_t s);
+/* LDS bytes one workgroup of ti_gemm_wq_a16 needs for M rows of K (<= 160 KiB). */
+int ti_gemm_lds_bytes(int M, int K);
+/* One-time kernel attribute setup; call before capturing ti_gemm_wq_a16 into a graph. */
+int ti_gemm_prepare(void);
+
+/* ------------------------------------------------------------- decode attention
+ * Single-query attention of M streams against their fp16 KV caches, GQA aware:
+ * q fp32 [M][heads*head_dim]; stream m attends to cache slots [0, pos[m]] of layer cache
+ * k_cache/v_cache ([stream][kv_head][max_seq][head_dim], stream stride kv_stream_stride).
+ * Split-K over the sequence (flash-decoding): `splits` partial (max, sum, o) per
+ * (stream, head) in workspace, then a combine pass writes fp16 out [M][heads*head_dim].
+ * head_dim 64 or 128; heads/kv_heads in {1, 2, 4, 8}. */
+size_t ti_attn_workspace_bytes(int M, int heads, int head_dim, int splits);
+int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                   int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
+                   int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
+                   ti_stream_t s);
+
+/* ------------------------------------------------------- step begin (device loop)
+ * One block per stream: picks the token of this step (prompt token while step < n_in[m],
+ * else the previous step's argmax), records fed-back tokens, gathers the fp16 embedding row
+ * into h (fp32), sets pos[m] = base_pos[m] + *step_ctr, clears argmax[m].
+ * placeholder_first >= 0 selects the reference_compat placeholder embedding
+ * 0.1f*((offset + i) % 100) (inference_engine.cpp:1444-1448, 1509-1512) with offset
+ * placeholder_first on step 0 and 0 afterwards. */
+typedef struct ti_step_args {
+  const uint16_t* emb;               /* [vocab][hidden] fp16 */
+  float* h;                          /* [M][hidden] */
+  int32_t hidden, M, vocab, in_stride, out_stride, placeholder_first;
+  const int32_t* in_tokens;          /* [M][in_stride] */
+  const int32_t* n_in;               /* [M] */
+  unsigned long long* argmax;        /* [M] */
+  int32_t* out_tokens;               /* [M][out_stride] generated tokens */
+  int32_t* pos;                      /* [M] */
+  const int32_t* base_pos;           /* [M] */
+  const int32_t* step_ctr;
+} ti_step_args;
+int ti_step_begin(const ti_step_args* a, ti_stream_t s);
+
+/* -------------------------------------------------------------- fp32 op level */
+/* y[r][n] (+)= sum_k a[r][k]*b[k][n], b the reference [K][N] fp32 layout, one fmaf per k
+ * in ascending order (bit-identical to matmul_3d_2d).  mode: 0 store, 1 relu(store),
+ * 2 y = resid + sum (resid may alias y). */
+int ti_matmul_f32(const float* a, const float* b, float* y, const float* resid, int rows, int K,
+                  int N, int mode, ti_stream_t s);
+int ti_rms_norm_f32(const float* x, const float* w, float* y, int rows, int n, float eps,
+                    ti_stream_t s);
+/* x [B][heads][S][D] fp32; cs [S*B or S][D/2][2] (cos, sin) computed by the caller with the
+ * reference formula; pos_2d selects per-(b,s) rows of cs. */
+int ti_rope_f32(const float* x, float* y, const float* cs, int B, int heads, int S, int D, int pos_2d,
+                ti_stream_t s);
+int ti_silu_f32(const float* x, float* y, int64_t n, ti_stream_t s);
+int ti_relu_f32(const float* x, float* y, int64_t n, ti_stream_t s);
+int ti_add_f32(const float* a, const float* b, float* y, int64_t n, ti_stream_t s);
+int ti_mul_f32(const float* a, const float* b, float* y, int64_t n, ti_stream_t s);
+int ti_softmax_f32(const float* x, float* y, int rows, int n, float temperature, ti_stream_t s);
+/* out[r] = argmax_n x[r][n], lowest index on ties. */
+int ti_argmax_f32(const float* x, int32_t* out, int rows, int n, ti_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TI_HIP_H */

@@ -1,0 +1,110 @@
+"""CPU-side checks of the product library: it loads, exports every symbol the C headers
+declare, host-side argument checks fail with TI_ERR_ARG without touching a GPU, and the
+host weight packer is bit-identical to the oracle's group quantizer."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import turboinfer_amd as T
+from conftest import ROOT
+from packing import unpack_tiles
+
+
+def header_functions(path):
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\**\s+\**(ti_[a-z0-9_]+)\s*\(", src, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not os.path.exists(T.LIB_PATH):
+        T.build()
+    return T.lib()
+
+
+def test_exports_every_declared_symbol(L):
+    declared = header_functions(os.path.join(ROOT, "include", "ti_hip.h")) + \
+        header_functions(os.path.join(ROOT, "include", "ti_engine.h"))
+    assert len(declared) >= 50
+    missing = [f for f in declared if not hasattr(L, f)]
+    assert not missing, missing
+    assert sorted(declared) == sorted(T.EXPORTED)
+
+
+def test_argument_errors_are_reported_without_launch(L):
+    ep = T.Epilogue()
+    ep.kind = T.EPI_STORE_F32
+    ep.ldo = 16
+    ep.out = 1234
+    # M out of range
+    rc = L.ti_gemm_wq_a16(1, 1, 4, 1, T.X_F16, 128, None, 1e-5, 0, 16, 128, C.byref(ep), None)
+    assert rc == 1 and b"M must be" in L.ti_last_error()
+    # K not a multiple of 128
+    rc = L.ti_gemm_wq_a16(1, 1, 4, 1, T.X_F16, 129, None, 1e-5, 1, 16, 129, C.byref(ep), None)
+    assert rc == 1 and b"K %" in L.ti_last_error()
+    # bad bits
+    rc = L.ti_gemm_wq_a16(1, 1, 3, 1, T.X_F16, 128, None, 1e-5, 1, 16, 128, C.byref(ep), None)
+    assert rc == 1
+    # attention head_dim unsupported
+    rc = L.ti_attn_decode(1, 1, 1, 1 << 20, 16, 1, 1, 4, 4, 96, 1, 1, 1, None)
+    assert rc == 3
+    # GQA group not supported
+    rc = L.ti_attn_decode(1, 1, 1, 1 << 20, 16, 1, 1, 12, 4, 128, 1, 1, 1, None)
+    assert rc in (1, 3)
+
+
+def test_engine_config_validation(L):
+    cfg = T.EngineConfig(1000, 256, 2, 4, 4, 64, 512, 1e4, 1e-5, 4, 64, 1, 0, 0, 0)
+    h = C.c_void_p()
+    rc = L.ti_engine_create(C.byref(cfg), C.byref(h))
+    assert rc != 0   # vocab 1000 not a multiple of 16 (or no device here)
+    cfg = T.EngineConfig(1024, 256, 2, 6, 4, 64, 512, 1e4, 1e-5, 4, 64, 1, 0, 0, 0)
+    assert L.ti_engine_create(C.byref(cfg), C.byref(h)) != 0  # heads % kv_heads
+
+
+@pytest.mark.parametrize("bits", [4, 8, 16])
+@pytest.mark.parametrize("scale_mode", [0, 1])
+def test_host_packer_matches_oracle_quantizer(oracle, bits, scale_mode):
+    if bits == 16 and scale_mode:
+        pytest.skip("fp16 weights carry no scale")
+    K, N = 256, 48
+    w = (np.random.RandomState(7).standard_normal((K, N)) * 0.03).astype(np.float32)
+    tiles, scales = T.wpack_host(w, bits, scale_mode=scale_mode)
+    q, s = unpack_tiles(tiles, scales, bits, K, N)
+    if bits == 16:
+        np.testing.assert_array_equal(q.view(np.uint16), w.T.astype(np.float16).view(np.uint16))
+        return
+    qo, so = oracle.quantize_groups(w, bits, 128, scale_mode)
+    np.testing.assert_array_equal(q, qo)
+    np.testing.assert_array_equal(s, so)
+
+
+def test_host_packer_fused_rows(oracle):
+    """QKV concatenation and gate/up interleave-by-8 land each source column on its row."""
+    K, I = 128, 32
+    g = (np.random.RandomState(1).standard_normal((K, I)) * 0.05).astype(np.float32)
+    u = (np.random.RandomState(2).standard_normal((K, I)) * 0.05).astype(np.float32)
+    tiles, scales = T.wpack_host(g, 4, n_total=2 * I, row_map=T.ROWS_INTERLEAVE8, row_offset=0)
+    T.wpack_host(u, 4, n_total=2 * I, row_map=T.ROWS_INTERLEAVE8, row_offset=8, tiles=tiles, scales=scales)
+    q, s = unpack_tiles(tiles, scales, 4, K, 2 * I)
+    qg, sg = oracle.quantize_groups(g, 4)
+    qu, su = oracle.quantize_groups(u, 4)
+    for c in range(I):
+        rg = 16 * (c // 8) + c % 8
+        np.testing.assert_array_equal(q[rg], qg[c])
+        np.testing.assert_array_equal(q[rg + 8], qu[c])
+        assert s[rg, 0] == sg[c, 0] and s[rg + 8, 0] == su[c, 0]
+
+
+def test_int4_range_is_reference_symmetric(oracle):
+    """INT4 values stay in [-7, 7] like quantize_to_int4's symmetric clamp (quantization.cpp:684-686)."""
+    w = (np.random.RandomState(5).standard_normal((128, 16)) * 10).astype(np.float32)
+    tiles, scales = T.wpack_host(w, 4)
+    q, _ = unpack_tiles(tiles, scales, 4, 128, 16)
+    assert q.min() >= -7 and q.max() <= 7 and q.min() == -7 or q.max() == 7

@@ -1,0 +1,363 @@
+"""Kernel-level parity of the HIP path (through the ti_hip.h C-ABI) against the oracle.
+
+Tolerances: the decode GEMM computes with fp16 activations (the A operand of
+v_mfma_f32_16x16x32_f16) and exact int4/int8 x fp16-scale weights, fp32 accumulation.  The
+expected values below are computed in float64 from the SAME fp16-rounded activations and the
+oracle's dequantized weights, so the only difference left is fp32 summation order:
+|err| <= 2e-5 * sum_k |x_k w_k| (+1e-6).  Attention reads an fp16 KV cache and writes fp16:
+rtol 4e-3 against the oracle's fp32 attention on the same (fp16-rounded) cache.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import inp
+from packing import unpack_tiles
+
+pytestmark = pytest.mark.gpu
+
+f16 = np.float16
+f32 = np.float32
+
+
+def dev(ti, a):
+    return ti.DeviceBuffer.from_array(np.ascontiguousarray(a))
+
+
+def packed_weight(ti, oracle, w, bits, n_total=None, row_map=0, row_offset=0, tiles=None, scales=None):
+    """pack on the host, return (tiles, scales, dequantized W [K][N] as the GPU sees it)."""
+    tiles, scales = ti.wpack_host(w, bits, n_total=n_total, row_map=row_map, row_offset=row_offset,
+                                  tiles=tiles, scales=scales)
+    return tiles, scales
+
+
+def deq(oracle, w, bits):
+    if bits == 16:
+        return w.astype(f16).astype(f32)
+    q, s = oracle.quantize_groups(w, bits)
+    return oracle.dequantize_groups(q, s)
+
+
+def gemm(ti, tiles_d, scales_d, bits, x_d, x_kind, ldx, M, N, K, ep, norm_d=None, eps=1e-5):
+    L = ti.lib()
+    import ctypes as C
+    ti.check(L.ti_gemm_wq_a16(tiles_d.ptr, scales_d.ptr if scales_d is not None else None, bits, x_d.ptr, x_kind,
+                              ldx, norm_d.ptr if norm_d is not None else None, eps, M, N, K, C.byref(ep), None))
+    ti.sync()
+
+
+def assert_close_dot(y, ref, xa, wf, rel=2e-5):
+    bound = rel * (np.abs(xa).astype(np.float64) @ np.abs(wf).astype(np.float64)) + 1e-6
+    err = np.abs(y.astype(np.float64) - ref)
+    assert np.all(err <= bound), f"max err {err.max()} vs bound {bound[err > bound][:4]}"
+
+
+@pytest.mark.parametrize("bits", [4, 8, 16])
+@pytest.mark.parametrize("M,K,N", [(1, 128, 16), (1, 4096, 256), (3, 384, 80), (16, 1024, 64), (2, 11008, 32)])
+def test_gemm_store(ti, oracle, bits, M, K, N):
+    rng = np.random.RandomState(M * 1000 + K + N + bits)
+    w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
+    x = rng.standard_normal((M, K)).astype(f32)
+    tiles, scales = ti.wpack_host(w, bits)
+    td, sd = dev(ti, tiles), (dev(ti, scales) if bits != 16 else None)
+    xd = dev(ti, x)
+    yd = ti.DeviceBuffer(M * N * 4)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F32, N, yd.ptr
+    gemm(ti, td, sd, bits, xd, ti.X_F32, K, M, N, K, ep)
+    y = yd.download(f32, (M, N))
+    xa = x.astype(f16).astype(f32)
+    wf = deq(oracle, w, bits)
+    assert_close_dot(y, xa.astype(np.float64) @ wf.astype(np.float64), xa, wf)
+
+
+def test_gemm_f16_input_and_store_f16_resid(ti, oracle):
+    M, K, N = 2, 512, 48
+    rng = np.random.RandomState(11)
+    w = (rng.standard_normal((K, N)) * 0.05).astype(f32)
+    x = rng.standard_normal((M, K)).astype(f16)
+    tiles, scales = ti.wpack_host(w, 4)
+    td, sd, xd = dev(ti, tiles), dev(ti, scales), dev(ti, x)
+    wf = deq(oracle, w, 4)
+    ref = x.astype(np.float64) @ wf.astype(np.float64)
+    # fp16 store
+    yd = ti.DeviceBuffer(M * N * 2)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F16, N, yd.ptr
+    gemm(ti, td, sd, 4, xd, ti.X_F16, K, M, N, K, ep)
+    y = yd.download(f16, (M, N)).astype(np.float64)
+    np.testing.assert_allclose(y, ref, rtol=2e-3, atol=2e-3)
+    # residual add in place
+    r = rng.standard_normal((M, N)).astype(f32)
+    rd = dev(ti, r)
+    ep.kind, ep.out = ti.EPI_RESID_F32, rd.ptr
+    gemm(ti, td, sd, 4, xd, ti.X_F16, K, M, N, K, ep)
+    assert_close_dot(rd.download(f32, (M, N)) - r, ref, x.astype(f32), wf, rel=5e-5)
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+def test_gemm_rmsnorm_prologue(ti, oracle, bits):
+    M, K, N = 3, 2048, 64
+    rng = np.random.RandomState(21)
+    w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
+    x = (rng.standard_normal((M, K)) * 3).astype(f32)
+    nw = (1 + 0.1 * rng.standard_normal(K)).astype(f32)
+    tiles, scales = ti.wpack_host(w, bits)
+    yd = ti.DeviceBuffer(M * N * 4)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F32, N, yd.ptr
+    gemm(ti, dev(ti, tiles), dev(ti, scales), bits, dev(ti, x), ti.X_F32_RMSNORM, K, M, N, K, ep,
+         norm_d=dev(ti, nw))
+    xn = oracle.rms_norm(x, nw)              # reference rms_norm, fp32
+    xa = xn.astype(f16).astype(f32)
+    wf = deq(oracle, w, bits)
+    y = yd.download(f32, (M, N))
+    # the device's rms differs from the reference's by fp32 reduction order (<1e-6 rel), which
+    # can move an activation across an fp16 rounding boundary: allow one fp16 ulp per element.
+    bound = (2e-5 + 1e-3) * (np.abs(xa) @ np.abs(wf)) + 1e-6
+    assert np.all(np.abs(y - xa.astype(np.float64) @ wf.astype(np.float64)) <= bound)
+
+
+def test_gemm_silu_mul_interleaved(ti, oracle):
+    M, K, I = 2, 256, 48
+    rng = np.random.RandomState(31)
+    g = (rng.standard_normal((K, I)) * 0.1).astype(f32)
+    u = (rng.standard_normal((K, I)) * 0.1).astype(f32)
+    x = rng.standard_normal((M, K)).astype(f32)
+    tiles, scales = ti.wpack_host(g, 4, n_total=2 * I, row_map=ti.ROWS_INTERLEAVE8, row_offset=0)
+    ti.wpack_host(u, 4, n_total=2 * I, row_map=ti.ROWS_INTERLEAVE8, row_offset=8, tiles=tiles, scales=scales)
+    yd = ti.DeviceBuffer(M * I * 2)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_SILU_MUL_F16, I, yd.ptr
+    gemm(ti, dev(ti, tiles), dev(ti, scales), 4, dev(ti, x), ti.X_F32, K, M, 2 * I, K, ep)
+    xa = x.astype(f16).astype(np.float64)
+    gg = xa @ deq(oracle, g, 4).astype(np.float64)
+    uu = xa @ deq(oracle, u, 4).astype(np.float64)
+    ref = uu * (gg / (1 + np.exp(-gg)))
+    np.testing.assert_allclose(yd.download(f16, (M, I)).astype(np.float64), ref, rtol=3e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("hd,nh,nkv", [(64, 4, 2), (128, 4, 4), (128, 8, 1)])
+def test_gemm_qkv_rope_kv_append(ti, oracle, hd, nh, nkv):
+    M, H, max_seq, theta = 2, 256, 32, 10000.0
+    qd, kvd = nh * hd, nkv * hd
+    N = qd + 2 * kvd
+    rng = np.random.RandomState(41 + hd + nh)
+    ws = [(rng.standard_normal((H, n)) * 0.05).astype(f32) for n in (qd, kvd, kvd)]
+    tiles = scales = None
+    for w, off in zip(ws, (0, qd, qd + kvd)):
+        tiles, scales = ti.wpack_host(w, 4, n_total=N, row_offset=off, tiles=tiles, scales=scales)
+    x = rng.standard_normal((M, H)).astype(f32)
+    pos = np.array([5, 17], np.int32)
+    cs = ti.rope_table(np.arange(max_seq, dtype=f32), hd, theta)
+    qd_buf = ti.DeviceBuffer(M * qd * 4)
+    stride = nkv * max_seq * hd
+    kc = ti.DeviceBuffer(M * stride * 2)
+    vc = ti.DeviceBuffer(M * stride * 2)
+    kc.zero(), vc.zero()
+    posd, csd = dev(ti, pos), dev(ti, cs)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_QKV_ROPE_KV, qd, qd_buf.ptr
+    ep.q_dim, ep.kv_dim, ep.head_dim, ep.max_seq = qd, kvd, hd, max_seq
+    ep.pos, ep.rope_cs, ep.k_cache, ep.v_cache, ep.kv_stream_stride = posd.ptr, csd.ptr, kc.ptr, vc.ptr, stride
+    gemm(ti, dev(ti, tiles), dev(ti, scales), 4, dev(ti, x), ti.X_F32, H, M, N, H, ep)
+    xa = x.astype(f16).astype(f32)
+    q, k, v = (xa.astype(np.float64) @ deq(oracle, w, 4).astype(np.float64) for w in ws)
+    kcache = kc.download(f16, (M, nkv, max_seq, hd)).astype(f32)
+    vcache = vc.download(f16, (M, nkv, max_seq, hd)).astype(f32)
+    qgot = qd_buf.download(f32, (M, qd))
+    for m in range(M):
+        p = np.array([pos[m]], f32)
+        qr = oracle.apply_rope(q[m].astype(f32).reshape(1, nh, 1, hd), p, theta).reshape(-1)
+        kr = oracle.apply_rope(k[m].astype(f32).reshape(1, nkv, 1, hd), p, theta).reshape(nkv, hd)
+        np.testing.assert_allclose(qgot[m], qr, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(kcache[m, :, pos[m]], kr, rtol=2e-3, atol=2e-3)
+        np.testing.assert_allclose(vcache[m, :, pos[m]], v[m].reshape(nkv, hd), rtol=2e-3, atol=2e-3)
+        other = [s for s in range(max_seq) if s != pos[m]]
+        assert not kcache[m][:, other].any() and not vcache[m][:, other].any()
+
+
+def test_gemm_logits_argmax(ti, oracle):
+    M, K, V = 3, 256, 4096
+    rng = np.random.RandomState(51)
+    w = (rng.standard_normal((K, V)) * 0.05).astype(f32)
+    x = rng.standard_normal((M, K)).astype(f32)
+    tiles, scales = ti.wpack_host(w, 4)
+    ld, am = ti.DeviceBuffer(M * V * 4), ti.DeviceBuffer(M * 8)
+    am.zero()
+    ctr = dev(ti, np.array([7], np.int32))
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out, ep.argmax, ep.step_ctr, ep.advance = ti.EPI_LOGITS_ARGMAX, V, ld.ptr, am.ptr, ctr.ptr, 1
+    gemm(ti, dev(ti, tiles), dev(ti, scales), 4, dev(ti, x), ti.X_F32, K, M, V, K, ep)
+    logits = ld.download(f32, (M, V))
+    keys = am.download(np.uint64, (M,))
+    idx = (0xFFFFFFFF - (keys & 0xFFFFFFFF)).astype(np.int64)
+    np.testing.assert_array_equal(idx, np.argmax(logits, axis=1))
+    assert ctr.download(np.int32, (1,))[0] == 8
+    ref = x.astype(f16).astype(np.float64) @ deq(oracle, w, 4).astype(np.float64)
+    np.testing.assert_allclose(logits, ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("bits", [4, 8, 16])
+def test_device_synth_matches_host_packer(ti, oracle, bits):
+    """ti_wsynth_device generates exactly the bytes the host packer makes from the oracle's weights."""
+    K, N, seed, tid = 256, 96, 1234, 77
+    w = oracle.synth_linear(seed, tid, K, N)
+    tiles, scales = ti.wpack_host(w, bits)
+    td = ti.DeviceBuffer(tiles.nbytes)
+    sd = ti.DeviceBuffer(max(scales.nbytes, 16))
+    L = ti.lib()
+    ti.check(L.ti_wsynth_device(seed, tid, K, N, N, bits, 0, 0, td.ptr, sd.ptr if bits != 16 else None, None))
+    ti.sync()
+    np.testing.assert_array_equal(td.download(np.uint8, tiles.shape), tiles)
+    if bits != 16:
+        np.testing.assert_array_equal(sd.download(np.uint16, scales.shape), scales)
+
+
+def _attn_case(ti, oracle, M, nh, nkv, hd, L_list, splits, max_seq=256, seed=0):
+    rng = np.random.RandomState(seed)
+    stride = nkv * max_seq * hd
+    kc = rng.standard_normal((M, nkv, max_seq, hd)).astype(f16)
+    vc = rng.standard_normal((M, nkv, max_seq, hd)).astype(f16)
+    q = rng.standard_normal((M, nh * hd)).astype(f32)
+    pos = np.array([l - 1 for l in L_list], np.int32)
+    out = ti.DeviceBuffer(M * nh * hd * 2)
+    ws = ti.DeviceBuffer(ti.lib().ti_attn_workspace_bytes(M, nh, hd, splits))
+    kd, vd, qd_, pd = dev(ti, kc), dev(ti, vc), dev(ti, q), dev(ti, pos)
+    ti.check(ti.lib().ti_attn_decode(qd_.ptr, kd.ptr, vd.ptr, stride, max_seq, pd.ptr, M, nh, nkv, hd, splits,
+                                     ws.ptr, out.ptr, None))
+    ti.sync()
+    got = out.download(f16, (M, nh * hd)).astype(f32)
+    grp = nh // nkv
+    for m in range(M):
+        S = L_list[m]
+        kx = np.repeat(kc[m, :, :S].astype(f32).transpose(1, 0, 2), grp, axis=1).reshape(1, S, nh * hd)
+        vx = np.repeat(vc[m, :, :S].astype(f32).transpose(1, 0, 2), grp, axis=1).reshape(1, S, nh * hd)
+        ref = oracle.multi_head_attention(q[m].reshape(1, 1, -1), kx, vx, nh).reshape(-1)
+        np.testing.assert_allclose(got[m], ref, rtol=4e-3, atol=4e-3)
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+@pytest.mark.parametrize("nh,nkv", [(4, 4), (8, 4), (8, 2), (8, 1)])
+def test_attention_decode(ti, oracle, hd, nh, nkv):
+    _attn_case(ti, oracle, 2, nh, nkv, hd, [1, 200], splits=4, seed=hd + nh + nkv)
+
+
+@pytest.mark.parametrize("splits", [1, 3, 16, 64])
+def test_attention_splits_and_lengths(ti, oracle, splits):
+    _attn_case(ti, oracle, 3, 4, 4, 128, [7, 64, 256], splits=splits, seed=splits)
+
+
+def test_attention_long_context(ti, oracle):
+    _attn_case(ti, oracle, 1, 8, 2, 128, [2048], splits=16, max_seq=2048, seed=9)
+
+
+# ------------------------------------------------------- fp32 op level (TensorEngine)
+def _same_bits(y, exp):
+    np.testing.assert_array_equal(np.ascontiguousarray(y, f32).view(np.uint32).reshape(-1),
+                                  np.ascontiguousarray(exp, f32).view(np.uint32).reshape(-1))
+
+
+def test_matmul_f32_bit_exact(ti, golden):
+    d = golden("matmul")
+    for i in range(len([k for k in d.files if k.startswith("shape")])):
+        B, M, K, N = (int(v) for v in d[f"shape{i}"])
+        sa, sb = d[f"seeds{i}"]
+        a, b = inp(int(sa), (B, M, K)), inp(int(sb), (K, N), 0.05)
+        yd = ti.DeviceBuffer(B * M * N * 4)
+        ad, bd = dev(ti, a), dev(ti, b)
+        ti.check(ti.lib().ti_matmul_f32(ad.ptr, bd.ptr, yd.ptr, None, B * M, K, N, 0, None))
+        ti.sync()
+        y = yd.download(f32, (B, M, N))
+        if f"y{i}" in d:
+            _same_bits(y, d[f"y{i}"])
+        else:
+            _same_bits(y.reshape(-1)[:512], d[f"y{i}_head"])
+
+
+def test_rms_norm_f32_bit_exact(ti, golden):
+    d = golden("rms_norm")
+    for i in range(len([k for k in d.files if k.startswith("shape")])):
+        rows, n = (int(v) for v in d[f"shape{i}"])
+        x = inp(200 + i, (rows, n))
+        w = (f32(1.0) + inp(300 + i, (n,), 0.1)).astype(f32)
+        yd = ti.DeviceBuffer(x.nbytes)
+        xd, wd = dev(ti, x), dev(ti, w)
+        ti.check(ti.lib().ti_rms_norm_f32(xd.ptr, wd.ptr, yd.ptr, rows, n, 1e-5, None))
+        ti.sync()
+        y = yd.download(f32, x.shape)
+        if f"y{i}" in d:
+            _same_bits(y, d[f"y{i}"])
+        else:
+            _same_bits(y.reshape(-1)[:512], d[f"y{i}_head"])
+
+
+def test_rope_f32_bit_exact(ti, golden):
+    d = golden("rope")
+    for i in range(len([k for k in d.files if k.startswith("shape")])):
+        shape = tuple(int(s) for s in d[f"shape{i}"])
+        x = inp(400 + i, shape)
+        pos = d[f"pos{i}"]
+        theta = float(d[f"theta{i}"][0])
+        if len(shape) == 3:
+            B, S, D = shape
+            heads = 1
+        else:
+            B, heads, S, D = shape
+        cs = ti.rope_table(pos, D, theta)
+        yd = ti.DeviceBuffer(x.nbytes)
+        xd, csd = dev(ti, x), dev(ti, cs)
+        ti.check(ti.lib().ti_rope_f32(xd.ptr, yd.ptr, csd.ptr, B, heads, S, D, 0, None))
+        ti.sync()
+        _same_bits(yd.download(f32, x.shape), d[f"y{i}"])
+
+
+def test_eltwise_f32(ti, golden):
+    d = golden("eltwise")
+    x, x2 = inp(500, (1001,), 4.0), inp(501, (1001,))
+    xd, x2d, yd = dev(ti, x), dev(ti, x2), ti.DeviceBuffer(x.nbytes)
+    L = ti.lib()
+    for name, call, exact in (("relu", lambda: L.ti_relu_f32(xd.ptr, yd.ptr, x.size, None), True),
+                              ("add", lambda: L.ti_add_f32(xd.ptr, x2d.ptr, yd.ptr, x.size, None), True),
+                              ("mul", lambda: L.ti_mul_f32(xd.ptr, x2d.ptr, yd.ptr, x.size, None), True),
+                              ("silu", lambda: L.ti_silu_f32(xd.ptr, yd.ptr, x.size, None), False)):
+        ti.check(call())
+        ti.sync()
+        y = yd.download(f32, x.shape)
+        if exact:
+            _same_bits(y, d[name])
+        else:   # device expf vs glibc expf: <= 2 ulp
+            np.testing.assert_allclose(y, d[name], rtol=1e-6, atol=1e-30)
+
+
+def test_softmax_f32(ti, golden):
+    d = golden("softmax")
+    for i in range(len([k for k in d.files if k.startswith("shape")])):
+        rows, n = (int(v) for v in d[f"shape{i}"])
+        T = float(d[f"T{i}"][0])
+        x = inp(600 + i, (rows, n), 5.0)
+        yd = ti.DeviceBuffer(x.nbytes)
+        xd = dev(ti, x)
+        ti.check(ti.lib().ti_softmax_f32(xd.ptr, yd.ptr, rows, n, T, None))
+        ti.sync()
+        y = yd.download(f32, x.shape)
+        exp = d[f"y{i}"] if f"y{i}" in d else d[f"y{i}_head"]
+        got = y if f"y{i}" in d else y.reshape(-1)[: exp.size]
+        if n >= 16 and n % 8 == 0:      # fast_exp path only: bit-identical
+            _same_bits(got, exp)
+        else:                            # std::exp terms: device expf
+            np.testing.assert_allclose(got.reshape(exp.shape), exp, rtol=2e-6, atol=1e-30)
+
+
+def test_argmax_lowest_index(ti):
+    x = np.random.RandomState(3).standard_normal((4, 5000)).astype(f32)
+    x[1, 100] = x[1, 4000] = 50.0     # tie -> lowest index
+    od = ti.DeviceBuffer(16)
+    xd = dev(ti, x)
+    ti.check(ti.lib().ti_argmax_f32(xd.ptr, od.ptr, 4, 5000, None))
+    ti.sync()
+    got = od.download(np.int32, (4,))
+    exp = np.argmax(x, axis=1)
+    np.testing.assert_array_equal(got, exp)
+    assert got[1] == 100

@@ -1,0 +1,697 @@
+// engine.cpp -- the device-resident decode engine (ti_engine.h).
+//
+// State per engine (one device, one HIP stream):
+//   * packed weights: per layer one fused [q|k|v] linear, o, one gate/up linear with rows
+//     interleaved by 8 (so the SiLU*up epilogue sees both halves in one 16-row tile), down;
+//     lm_head; fp16 embedding table; fp32 norm weights; RoPE (cos, sin) table computed on
+//     the host with the reference formula (tensor_engine.cpp:1561-1566, 1595-1597).
+//   * per stream fp16 K/V caches [layer][stream][kv_head][max_seq][head_dim].
+//   * a device-side decode loop: step counter, positions, argmax feedback -- one decode
+//     step is a fixed launch sequence captured once into a hipGraph and replayed, so the
+//     host never waits inside generate().
+// Reference counterparts: InferenceEngineImpl (src/model/inference_engine.cpp:446-693),
+// KVCache (:25-172), forward_pass_incremental (:1493-1552), generate (:734-802).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <utility>
+#include <vector>
+
+#include "ti_engine.h"
+#include "ti_hip.h"
+
+int ti_set_error(int code, const char* fmt, ...);
+int ti_check_hip(hipError_t e, const char* what);
+
+#define E_CHECK(expr, what)                                \
+  do {                                                     \
+    hipError_t _e = (expr);                                \
+    if (_e != hipSuccess) return ti_check_hip(_e, what);   \
+  } while (0)
+#define TI_TRY(expr)                 \
+  do {                               \
+    const int _rc = (expr);          \
+    if (_rc != TI_OK) return _rc;    \
+  } while (0)
+
+namespace {
+
+// tensor ids of the synthetic model: identical to oracle/ti_oracle.c
+constexpr uint32_t kTidEmb = 1, kTidOutNorm = 2, kTidLmHead = 3, kTidLayer0 = 16;
+enum { TL_ATTN_NORM = 0, TL_FFN_NORM, TL_Q, TL_K, TL_V, TL_O, TL_G, TL_U, TL_D };
+inline uint32_t tid_layer(int l, int t) { return kTidLayer0 + 16u * (uint32_t)l + (uint32_t)t; }
+inline uint32_t tid_kv(int l, int v) { return 0x100000u + 2u * (uint32_t)l + (uint32_t)v; }
+
+struct DevLinear {
+  void* tiles = nullptr;
+  uint16_t* scales = nullptr;
+  float* f32 = nullptr;     // compat: reference-layout fp32 [K][N]
+  int K = 0, N = 0;
+};
+
+struct DevLayer {
+  DevLinear qkv, o, gu, down;
+  float* attn_norm = nullptr;
+  float* ffn_norm = nullptr;
+  uint16_t* kc = nullptr;
+  uint16_t* vc = nullptr;
+};
+
+uint16_t host_half(float f) {
+  const _Float16 h = (_Float16)f;
+  uint16_t u;
+  std::memcpy(&u, &h, 2);
+  return u;
+}
+
+}  // namespace
+
+struct ti_engine {
+  ti_engine_config c{};
+  hipStream_t s = nullptr;
+  std::vector<void*> allocs;
+  std::vector<DevLayer> layer;
+  DevLinear lm;
+  uint16_t* emb = nullptr;
+  float* out_norm = nullptr;
+  float* rope_cs = nullptr;
+  // step buffers
+  float* h = nullptr;
+  float* q = nullptr;
+  float* tmp = nullptr;        // compat FFN activations (fp32)
+  float* logits = nullptr;
+  float* ws = nullptr;
+  uint16_t* attn = nullptr;
+  uint16_t* act = nullptr;
+  unsigned long long* argmax = nullptr;
+  int32_t* pos = nullptr;
+  int32_t* base_pos = nullptr;
+  int32_t* step_ctr = nullptr;
+  int32_t* n_in = nullptr;
+  int32_t* in_tokens = nullptr;
+  int32_t* out_tokens = nullptr;
+  int in_cap = 0, out_cap = 0;
+  int splits_max = 1;
+  int64_t kv_stride = 0;
+  size_t weight_bytes = 0, kv_bytes = 0;
+  std::map<std::pair<int, int>, hipGraphExec_t> graphs;  // (M, advance)
+  int replay_M = 0;
+
+  int qd() const { return c.heads * c.head_dim; }
+  int kvd() const { return c.kv_heads * c.head_dim; }
+
+  int alloc(void** p, size_t bytes) {
+    TI_TRY(ti_malloc(p, bytes));
+    allocs.push_back(*p);
+    E_CHECK(hipMemsetAsync(*p, 0, bytes, s), "hipMemsetAsync(alloc)");
+    return TI_OK;
+  }
+  template <class T>
+  int alloc_t(T** p, size_t count) {
+    void* v = nullptr;
+    TI_TRY(alloc(&v, count * sizeof(T)));
+    *p = static_cast<T*>(v);
+    return TI_OK;
+  }
+  int alloc_linear(DevLinear& L, int K, int N) {
+    L.K = K;
+    L.N = N;
+    if (c.compat) {
+      TI_TRY(alloc_t(&L.f32, (size_t)K * N));
+      weight_bytes += (size_t)K * N * 4;
+      return TI_OK;
+    }
+    const size_t tb = ti_wpack_tile_bytes(c.bits, K, N), sb = ti_wpack_scale_bytes(c.bits, K, N);
+    TI_TRY(alloc(&L.tiles, tb));
+    if (sb) {
+      void* p = nullptr;
+      TI_TRY(alloc(&p, sb));
+      L.scales = static_cast<uint16_t*>(p);
+    }
+    weight_bytes += tb + sb;
+    return TI_OK;
+  }
+  int splits_for(int M) const {
+    if (c.attn_splits > 0) return c.attn_splits;
+    const int target = 512;
+    int sp = (target + c.kv_heads * M - 1) / (c.kv_heads * M);
+    const int cap = std::max(1, c.max_seq / 64);
+    return std::max(1, std::min(sp, std::min(cap, 64)));
+  }
+  int mchunk(int K) const {
+    int m = 16;
+    while (m > 1 && ti_gemm_lds_bytes(m, K) > 96 * 1024) --m;
+    return m;
+  }
+
+  ~ti_engine() {
+    for (auto& g : graphs) hipGraphExecDestroy(g.second);
+    for (void* p : allocs) hipFree(p);
+    if (s) hipStreamDestroy(s);
+  }
+};
+
+namespace {
+
+int validate(const ti_engine_config& c) {
+  if (c.vocab < 1 || c.hidden < 1 || c.layers < 0 || c.inter < 1 || c.max_seq < 1 || c.max_batch < 1)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_create: non-positive size in config");
+  if (c.compat) return TI_OK;
+  if (c.heads < 1 || c.kv_heads < 1 || c.heads % c.kv_heads)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_create: heads %d / kv_heads %d", c.heads, c.kv_heads);
+  const int G = c.heads / c.kv_heads;
+  if (G != 1 && G != 2 && G != 4 && G != 8) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_create: GQA group %d", G);
+  if (c.head_dim != 64 && c.head_dim != 128) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_create: head_dim %d", c.head_dim);
+  if (c.bits != 4 && c.bits != 8 && c.bits != 16) return ti_set_error(TI_ERR_ARG, "ti_engine_create: bits %d", c.bits);
+  const int qd = c.heads * c.head_dim, kvd = c.kv_heads * c.head_dim;
+  if (c.hidden % 128 || qd % 128 || c.inter % 128)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_create: hidden, heads*head_dim and inter must be multiples of 128");
+  if (kvd % 16 || c.vocab % 16)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_create: kv_heads*head_dim and vocab must be multiples of 16");
+  return TI_OK;
+}
+
+// One decode step for streams [0, M) on e->s.  Graph-capturable (no host sync / alloc).
+int enqueue_step(ti_engine* e, int M, int advance) {
+  const ti_engine_config& c = e->c;
+  ti_step_args sa{};
+  sa.emb = e->emb;
+  sa.h = e->h;
+  sa.hidden = c.hidden;
+  sa.M = M;
+  sa.vocab = c.vocab;
+  sa.in_stride = e->in_cap;
+  sa.out_stride = e->out_cap;
+  sa.placeholder_first = -1;
+  sa.in_tokens = e->in_tokens;
+  sa.n_in = e->n_in;
+  sa.argmax = e->argmax;
+  sa.out_tokens = e->out_tokens;
+  sa.pos = e->pos;
+  sa.base_pos = e->base_pos;
+  sa.step_ctr = e->step_ctr;
+  TI_TRY(ti_step_begin(&sa, e->s));
+
+  const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
+  auto gemm = [&](const DevLinear& W, const void* x, int x_kind, int ldx, size_t x_elem, const float* nw,
+                  ti_epilogue epi, size_t out_elem, bool last_gets_ctr) -> int {
+    const int mc = e->mchunk(W.K);
+    for (int m0 = 0; m0 < M; m0 += mc) {
+      const int mm = std::min(mc, M - m0);
+      ti_epilogue ep = epi;
+      ep.out = static_cast<char*>(epi.out) + (size_t)m0 * epi.ldo * out_elem;
+      if (ep.pos) ep.pos += m0;
+      if (ep.k_cache) ep.k_cache += (size_t)m0 * ep.kv_stream_stride;
+      if (ep.v_cache) ep.v_cache += (size_t)m0 * ep.kv_stream_stride;
+      if (ep.argmax) ep.argmax += m0;
+      if (!(last_gets_ctr && m0 + mm >= M)) ep.step_ctr = nullptr;
+      const void* xm = static_cast<const char*>(x) + (size_t)m0 * ldx * x_elem;
+      TI_TRY(ti_gemm_wq_a16(W.tiles, W.scales, c.bits, xm, x_kind, ldx, nw, c.eps, mm, W.N, W.K, &ep, e->s));
+    }
+    return TI_OK;
+  };
+
+  for (int l = 0; l < c.layers; ++l) {
+    DevLayer& L = e->layer[l];
+    ti_epilogue ep{};
+    ep.kind = TI_EPI_QKV_ROPE_KV;
+    ep.ldo = qd;
+    ep.out = e->q;
+    ep.q_dim = qd;
+    ep.kv_dim = kvd;
+    ep.head_dim = c.head_dim;
+    ep.max_seq = c.max_seq;
+    ep.pos = e->pos;
+    ep.rope_cs = e->rope_cs;
+    ep.k_cache = L.kc;
+    ep.v_cache = L.vc;
+    ep.kv_stream_stride = e->kv_stride;
+    TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));
+
+    TI_TRY(ti_attn_decode(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M, c.heads, c.kv_heads, c.head_dim,
+                          e->splits_for(M), e->ws, e->attn, e->s));
+
+    ti_epilogue eo{};
+    eo.kind = TI_EPI_RESID_F32;
+    eo.ldo = H;
+    eo.out = e->h;
+    TI_TRY(gemm(L.o, e->attn, TI_X_F16, qd, 2, nullptr, eo, 4, false));
+
+    ti_epilogue eg{};
+    eg.kind = TI_EPI_SILU_MUL_F16;
+    eg.ldo = I;
+    eg.out = e->act;
+    TI_TRY(gemm(L.gu, e->h, TI_X_F32_RMSNORM, H, 4, L.ffn_norm, eg, 2, false));
+
+    ti_epilogue ed{};
+    ed.kind = TI_EPI_RESID_F32;
+    ed.ldo = H;
+    ed.out = e->h;
+    TI_TRY(gemm(L.down, e->act, TI_X_F16, I, 2, nullptr, ed, 4, false));
+  }
+  ti_epilogue el{};
+  el.kind = TI_EPI_LOGITS_ARGMAX;
+  el.ldo = V;
+  el.out = e->logits;
+  el.argmax = e->argmax;
+  el.step_ctr = e->step_ctr;
+  el.advance = advance;
+  return gemm(e->lm, e->h, TI_X_F32_RMSNORM, H, 4, e->out_norm, el, 4, true);
+}
+
+int get_graph(ti_engine* e, int M, int advance, hipGraphExec_t* out) {
+  auto key = std::make_pair(M, advance);
+  auto it = e->graphs.find(key);
+  if (it != e->graphs.end()) {
+    *out = it->second;
+    return TI_OK;
+  }
+  TI_TRY(ti_gemm_prepare());
+  E_CHECK(hipStreamBeginCapture(e->s, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+  const int rc = enqueue_step(e, M, advance);
+  hipGraph_t g = nullptr;
+  const hipError_t ec = hipStreamEndCapture(e->s, &g);
+  if (rc != TI_OK) {
+    if (g) hipGraphDestroy(g);
+    return rc;
+  }
+  E_CHECK(ec, "hipStreamEndCapture");
+  hipGraphExec_t ex = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  E_CHECK(ei, "hipGraphInstantiate");
+  e->graphs[key] = ex;
+  *out = ex;
+  return TI_OK;
+}
+
+int ensure_io(ti_engine* e, int in_cap, int out_cap) {
+  const int B = e->c.max_batch;
+  if (in_cap > e->in_cap) {
+    // graphs bake the buffers in: drop them
+    for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
+    e->graphs.clear();
+    void* p = nullptr;
+    TI_TRY(e->alloc(&p, (size_t)B * in_cap * sizeof(int32_t)));
+    e->in_tokens = static_cast<int32_t*>(p);
+    e->in_cap = in_cap;
+  }
+  if (out_cap > e->out_cap) {
+    for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
+    e->graphs.clear();
+    void* p = nullptr;
+    TI_TRY(e->alloc(&p, (size_t)B * out_cap * sizeof(int32_t)));
+    e->out_tokens = static_cast<int32_t*>(p);
+    e->out_cap = out_cap;
+  }
+  return TI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
+  if (!cfg || !out) return ti_set_error(TI_ERR_ARG, "ti_engine_create: null");
+  *out = nullptr;
+  TI_TRY(validate(*cfg));
+  TI_TRY(ti_init(cfg->device));
+  ti_engine* e = new ti_engine();
+  e->c = *cfg;
+  const ti_engine_config& c = e->c;
+  auto fail = [&](int rc) { delete e; return rc; };
+  if (hipStreamCreateWithFlags(&e->s, hipStreamNonBlocking) != hipSuccess)
+    return fail(ti_check_hip(hipErrorUnknown, "hipStreamCreate"));
+  const int B = c.max_batch, H = c.hidden, I = c.inter, V = c.vocab;
+  int rc = TI_OK;
+  e->layer.resize((size_t)c.layers);
+  if (c.compat) {
+    for (auto& L : e->layer) {
+      if ((rc = e->alloc_linear(L.gu, H, I)) || (rc = e->alloc_linear(L.down, I, H))) return fail(rc);
+    }
+    if ((rc = e->alloc_linear(e->lm, H, V))) return fail(rc);
+    if ((rc = e->alloc_t(&e->tmp, (size_t)B * I))) return fail(rc);
+  } else {
+    const int qd = e->qd(), kvd = e->kvd(), hd = c.head_dim;
+    e->kv_stride = (int64_t)c.kv_heads * c.max_seq * hd;
+    for (auto& L : e->layer) {
+      if ((rc = e->alloc_linear(L.qkv, H, qd + 2 * kvd)) || (rc = e->alloc_linear(L.o, qd, H)) ||
+          (rc = e->alloc_linear(L.gu, H, 2 * I)) || (rc = e->alloc_linear(L.down, I, H)) ||
+          (rc = e->alloc_t(&L.attn_norm, (size_t)H)) || (rc = e->alloc_t(&L.ffn_norm, (size_t)H)) ||
+          (rc = e->alloc_t(&L.kc, (size_t)B * e->kv_stride)) || (rc = e->alloc_t(&L.vc, (size_t)B * e->kv_stride)))
+        return fail(rc);
+      e->kv_bytes += (size_t)2 * B * e->kv_stride * 2;
+    }
+    if ((rc = e->alloc_linear(e->lm, H, V)) || (rc = e->alloc_t(&e->emb, (size_t)V * H)) ||
+        (rc = e->alloc_t(&e->out_norm, (size_t)H)) || (rc = e->alloc_t(&e->rope_cs, (size_t)c.max_seq * hd)))
+      return fail(rc);
+    e->weight_bytes += (size_t)V * H * 2 + (size_t)H * 4 * (2 * c.layers + 1);
+    // RoPE table with the reference formula: freq_i = 1 / theta^(2i/d), angle = pos * freq_i.
+    std::vector<float> cs((size_t)c.max_seq * hd), pv((size_t)c.max_seq);
+    for (int p = 0; p < c.max_seq; ++p) pv[p] = (float)p;
+    if ((rc = ti_rope_table(pv.data(), c.max_seq, hd, c.rope_theta, cs.data()))) return fail(rc);
+    if ((rc = ti_memcpy_h2d(e->rope_cs, cs.data(), cs.size() * 4, e->s))) return fail(rc);
+    e->splits_max = e->splits_for(1);
+    if ((rc = e->alloc_t(&e->q, (size_t)B * qd)) || (rc = e->alloc_t(&e->attn, (size_t)B * qd)) ||
+        (rc = e->alloc_t(&e->act, (size_t)B * I)) ||
+        (rc = e->alloc(reinterpret_cast<void**>(&e->ws), ti_attn_workspace_bytes(B, c.heads, hd, e->splits_max))))
+      return fail(rc);
+  }
+  if ((rc = e->alloc_t(&e->h, (size_t)B * H)) || (rc = e->alloc_t(&e->logits, (size_t)B * V)) ||
+      (rc = e->alloc_t(&e->argmax, (size_t)B)) || (rc = e->alloc_t(&e->pos, (size_t)B)) ||
+      (rc = e->alloc_t(&e->base_pos, (size_t)B)) || (rc = e->alloc_t(&e->step_ctr, (size_t)1)) ||
+      (rc = e->alloc_t(&e->n_in, (size_t)B)) || (rc = ensure_io(e, 8, 8)))
+    return fail(rc);
+  if (hipStreamSynchronize(e->s) != hipSuccess) return fail(ti_check_hip(hipErrorUnknown, "hipStreamSynchronize"));
+  *out = e;
+  return TI_OK;
+}
+
+int ti_engine_destroy(ti_engine* e) {
+  if (e) {
+    hipStreamSynchronize(e->s);
+    delete e;
+  }
+  return TI_OK;
+}
+
+int ti_engine_get_stream(ti_engine* e, void** stream) {
+  if (!e || !stream) return ti_set_error(TI_ERR_ARG, "ti_engine_get_stream: null");
+  *stream = (void*)e->s;
+  return TI_OK;
+}
+
+int ti_engine_memory(ti_engine* e, size_t* wb, size_t* kb) {
+  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_memory: null");
+  if (wb) *wb = e->weight_bytes;
+  if (kb) *kb = e->kv_bytes;
+  return TI_OK;
+}
+
+int ti_engine_set_tensor(ti_engine* e, int slot, int layer, const float* data, int scale_mode) {
+  if (!e || !data) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor: null");
+  const ti_engine_config& c = e->c;
+  const int H = c.hidden, I = c.inter, V = c.vocab;
+  const bool per_layer = slot <= TI_W_DOWN || slot == TI_V_ATTN_NORM || slot == TI_V_FFN_NORM;
+  if (per_layer && (layer < 0 || layer >= c.layers))
+    return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor: layer %d of %d", layer, c.layers);
+
+  if (c.compat) {
+    DevLinear* L = nullptr;
+    size_t n = 0;
+    switch (slot) {
+      case TI_W_UP: L = &e->layer[layer].gu; n = (size_t)H * I; break;
+      case TI_W_DOWN: L = &e->layer[layer].down; n = (size_t)I * H; break;
+      case TI_W_LM_HEAD: L = &e->lm; n = (size_t)H * V; break;
+      case TI_W_Q: case TI_W_K: case TI_W_V: case TI_E_EMBED: return TI_OK;  // unused by the compat path
+      default: return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_set_tensor: slot %d not part of the compat model", slot);
+    }
+    return ti_memcpy_h2d(L->f32, data, n * 4, e->s);
+  }
+
+  if (slot == TI_V_ATTN_NORM || slot == TI_V_FFN_NORM || slot == TI_V_OUT_NORM) {
+    float* dst = slot == TI_V_OUT_NORM ? e->out_norm
+                                       : (slot == TI_V_ATTN_NORM ? e->layer[layer].attn_norm : e->layer[layer].ffn_norm);
+    return ti_memcpy_h2d(dst, data, (size_t)H * 4, e->s);
+  }
+  if (slot == TI_E_EMBED) {
+    std::vector<uint16_t> hb((size_t)V * H);
+    for (size_t i = 0; i < hb.size(); ++i) hb[i] = host_half(data[i]);
+    return ti_memcpy_h2d(e->emb, hb.data(), hb.size() * 2, e->s);
+  }
+  const int qd = e->qd(), kvd = e->kvd();
+  DevLinear* L = nullptr;
+  int K = 0, Nsrc = 0, map = TI_ROWS_CONCAT, off = 0;
+  switch (slot) {
+    case TI_W_Q: L = &e->layer[layer].qkv; K = H; Nsrc = qd; off = 0; break;
+    case TI_W_K: L = &e->layer[layer].qkv; K = H; Nsrc = kvd; off = qd; break;
+    case TI_W_V: L = &e->layer[layer].qkv; K = H; Nsrc = kvd; off = qd + kvd; break;
+    case TI_W_O: L = &e->layer[layer].o; K = qd; Nsrc = H; break;
+    case TI_W_GATE: L = &e->layer[layer].gu; K = H; Nsrc = I; map = TI_ROWS_INTERLEAVE8; off = 0; break;
+    case TI_W_UP: L = &e->layer[layer].gu; K = H; Nsrc = I; map = TI_ROWS_INTERLEAVE8; off = 8; break;
+    case TI_W_DOWN: L = &e->layer[layer].down; K = I; Nsrc = H; break;
+    case TI_W_LM_HEAD: L = &e->lm; K = H; Nsrc = V; break;
+    default: return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor: slot %d", slot);
+  }
+  // read-modify-write of the fused buffer: the packer only touches this part's rows
+  const size_t tb = ti_wpack_tile_bytes(c.bits, L->K, L->N), sb = ti_wpack_scale_bytes(c.bits, L->K, L->N);
+  std::vector<uint8_t> th(tb);
+  std::vector<uint16_t> sh(sb / 2 + 1);
+  TI_TRY(ti_memcpy_d2h(th.data(), L->tiles, tb, e->s));
+  if (sb) TI_TRY(ti_memcpy_d2h(sh.data(), L->scales, sb, e->s));
+  TI_TRY(ti_wpack_host(data, K, Nsrc, L->N, c.bits, scale_mode, map, off, th.data(), sb ? sh.data() : nullptr));
+  TI_TRY(ti_memcpy_h2d(L->tiles, th.data(), tb, e->s));
+  if (sb) TI_TRY(ti_memcpy_h2d(L->scales, sh.data(), sb, e->s));
+  return TI_OK;
+}
+
+int ti_engine_synth(ti_engine* e, uint64_t seed, float norm_jitter) {
+  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_synth: null");
+  const ti_engine_config& c = e->c;
+  if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_synth: compat engines take the reference model");
+  const int H = c.hidden, I = c.inter, V = c.vocab, qd = e->qd(), kvd = e->kvd(), b = c.bits;
+  for (int l = 0; l < c.layers; ++l) {
+    DevLayer& L = e->layer[l];
+    const int nq = qd + 2 * kvd;
+    TI_TRY(ti_wsynth_device(seed, tid_layer(l, TL_Q), H, qd, nq, b, TI_ROWS_CONCAT, 0, L.qkv.tiles, L.qkv.scales, e->s));
+    TI_TRY(ti_wsynth_device(seed, tid_layer(l, TL_K), H, kvd, nq, b, TI_ROWS_CONCAT, qd, L.qkv.tiles, L.qkv.scales, e->s));
+    TI_TRY(ti_wsynth_device(seed, tid_layer(l, TL_V), H, kvd, nq, b, TI_ROWS_CONCAT, qd + kvd, L.qkv.tiles, L.qkv.scales, e->s));
+    TI_TRY(ti_wsynth_device(seed, tid_layer(l, TL_O), qd, H, H, b, TI_ROWS_CONCAT, 0, L.o.tiles, L.o.scales, e->s));
+    TI_TRY(ti_wsynth_device(seed, tid_layer(l, TL_G), H, I, 2 * I, b, TI_ROWS_INTERLEAVE8, 0, L.gu.tiles, L.gu.scales, e->s));
+    TI_TRY(ti_wsynth_device(seed, tid_layer(l, TL_U), H, I, 2 * I, b, TI_ROWS_INTERLEAVE8, 8, L.gu.tiles, L.gu.scales, e->s));
+    TI_TRY(ti_wsynth_device(seed, tid_layer(l, TL_D), I, H, H, b, TI_ROWS_CONCAT, 0, L.down.tiles, L.down.scales, e->s));
+    TI_TRY(ti_fill_uniform_f32(seed, tid_layer(l, TL_ATTN_NORM), (uint64_t)H, norm_jitter, 1.0f, L.attn_norm, e->s));
+    TI_TRY(ti_fill_uniform_f32(seed, tid_layer(l, TL_FFN_NORM), (uint64_t)H, norm_jitter, 1.0f, L.ffn_norm, e->s));
+  }
+  TI_TRY(ti_wsynth_device(seed, kTidLmHead, H, V, V, b, TI_ROWS_CONCAT, 0, e->lm.tiles, e->lm.scales, e->s));
+  TI_TRY(ti_fill_uniform_f32(seed, kTidOutNorm, (uint64_t)H, norm_jitter, 1.0f, e->out_norm, e->s));
+  TI_TRY(ti_fill_uniform_f16(seed, kTidEmb, (uint64_t)V * H, 0.02f, e->emb, e->s));
+  return ti_stream_sync(e->s);
+}
+
+int ti_engine_fill_kv(ti_engine* e, int stream, int n, uint64_t seed) {
+  if (!e || e->c.compat) return ti_set_error(TI_ERR_ARG, "ti_engine_fill_kv: no KV cache");
+  if (stream < 0 || stream >= e->c.max_batch || n < 0 || n > e->c.max_seq)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_fill_kv: stream %d n %d", stream, n);
+  for (int l = 0; l < e->c.layers; ++l) {
+    DevLayer& L = e->layer[l];
+    TI_TRY(ti_fill_kv_uniform(seed, tid_kv(l, 0), n, e->c.kv_heads, e->c.head_dim, e->c.max_seq,
+                              L.kc + (size_t)stream * e->kv_stride, e->s));
+    TI_TRY(ti_fill_kv_uniform(seed, tid_kv(l, 1), n, e->c.kv_heads, e->c.head_dim, e->c.max_seq,
+                              L.vc + (size_t)stream * e->kv_stride, e->s));
+  }
+  return ti_stream_sync(e->s);
+}
+
+int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_t* lens, int stride,
+                       const int32_t* start_pos, int max_new, int32_t* out_tokens, float* last_logits) {
+  if (!e || !prompts || !lens || !out_tokens) return ti_set_error(TI_ERR_ARG, "ti_engine_generate: null");
+  const ti_engine_config& c = e->c;
+  if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_generate: use ti_engine_compat_step for compat engines");
+  if (n < 1 || n > c.max_batch || max_new < 1) return ti_set_error(TI_ERR_ARG, "ti_engine_generate: n=%d max_new=%d", n, max_new);
+  int nin_max = 0;
+  std::vector<int32_t> nin(n), base(n, 0);
+  for (int m = 0; m < n; ++m) {
+    if (lens[m] < 1 || lens[m] > stride) return ti_set_error(TI_ERR_ARG, "ti_engine_generate: prompt length %d", lens[m]);
+    nin[m] = lens[m];
+    nin_max = std::max(nin_max, lens[m]);
+    if (start_pos) base[m] = start_pos[m];
+  }
+  const int steps = nin_max + max_new - 1;
+  for (int m = 0; m < n; ++m)
+    if (base[m] < 0 || base[m] + steps > c.max_seq)
+      return ti_set_error(TI_ERR_ARG, "ti_engine_generate: stream %d needs %d KV slots > max_seq %d", m, base[m] + steps,
+                          c.max_seq);
+  TI_TRY(ensure_io(e, stride, std::max(steps, 1)));
+  std::vector<int32_t> in((size_t)n * e->in_cap, 0);
+  for (int m = 0; m < n; ++m) std::memcpy(&in[(size_t)m * e->in_cap], prompts + (size_t)m * stride, (size_t)lens[m] * 4);
+  TI_TRY(ti_memcpy_h2d(e->in_tokens, in.data(), in.size() * 4, e->s));
+  TI_TRY(ti_memcpy_h2d(e->n_in, nin.data(), (size_t)n * 4, e->s));
+  TI_TRY(ti_memcpy_h2d(e->base_pos, base.data(), (size_t)n * 4, e->s));
+  TI_TRY(ti_memset(e->step_ctr, 0, 4, e->s));
+  hipGraphExec_t g = nullptr;
+  TI_TRY(get_graph(e, n, 1, &g));
+  for (int s = 0; s < steps; ++s) E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
+  TI_TRY(ti_stream_sync(e->s));
+  std::vector<int32_t> outd((size_t)n * e->out_cap);
+  std::vector<unsigned long long> am((size_t)n);
+  TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
+  TI_TRY(ti_memcpy_d2h(am.data(), e->argmax, am.size() * 8, e->s));
+  for (int m = 0; m < n; ++m) {
+    const int produced = steps - nin[m] + 1;   // generated tokens of stream m
+    for (int t = 0; t < max_new; ++t) {
+      int32_t tok;
+      if (t < produced - 1) tok = outd[(size_t)m * e->out_cap + t];
+      else if (t == produced - 1) tok = (int32_t)(0xFFFFFFFFu - (uint32_t)(am[m] & 0xFFFFFFFFull));
+      else tok = -1;
+      out_tokens[(size_t)m * max_new + t] = tok;
+    }
+  }
+  if (last_logits) TI_TRY(ti_memcpy_d2h(last_logits, e->logits, (size_t)n * c.vocab * 4, e->s));
+  return TI_OK;
+}
+
+int ti_engine_step(ti_engine* e, int n, const int32_t* tokens, const int32_t* pos, float* logits) {
+  if (!e || !tokens || !pos) return ti_set_error(TI_ERR_ARG, "ti_engine_step: null");
+  const ti_engine_config& c = e->c;
+  if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_step: compat engine");
+  if (n < 1 || n > c.max_batch) return ti_set_error(TI_ERR_ARG, "ti_engine_step: n=%d", n);
+  for (int m = 0; m < n; ++m)
+    if (pos[m] < 0 || pos[m] >= c.max_seq) return ti_set_error(TI_ERR_ARG, "ti_engine_step: pos %d", pos[m]);
+  TI_TRY(ensure_io(e, 1, 1));
+  std::vector<int32_t> in((size_t)n * e->in_cap, 0), one(n, 1);
+  for (int m = 0; m < n; ++m) in[(size_t)m * e->in_cap] = tokens[m];
+  TI_TRY(ti_memcpy_h2d(e->in_tokens, in.data(), in.size() * 4, e->s));
+  TI_TRY(ti_memcpy_h2d(e->n_in, one.data(), (size_t)n * 4, e->s));
+  TI_TRY(ti_memcpy_h2d(e->base_pos, pos, (size_t)n * 4, e->s));
+  TI_TRY(ti_memset(e->step_ctr, 0, 4, e->s));
+  hipGraphExec_t g = nullptr;
+  TI_TRY(get_graph(e, n, 1, &g));
+  E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
+  TI_TRY(ti_stream_sync(e->s));
+  if (logits) TI_TRY(ti_memcpy_d2h(logits, e->logits, (size_t)n * c.vocab * 4, e->s));
+  return TI_OK;
+}
+
+int ti_engine_compat_step(ti_engine* e, int placeholder_offset, float* logits) {
+  if (!e || !e->c.compat) return ti_set_error(TI_ERR_ARG, "ti_engine_compat_step: not a compat engine");
+  const ti_engine_config& c = e->c;
+  const int H = c.hidden, I = c.inter, V = c.vocab;
+  std::vector<int32_t> zero(1, 0);
+  TI_TRY(ti_memset(e->step_ctr, 0, 4, e->s));
+  ti_step_args sa{};
+  sa.h = e->h;
+  sa.hidden = H;
+  sa.M = 1;
+  sa.vocab = V;
+  sa.placeholder_first = placeholder_offset;
+  sa.argmax = e->argmax;
+  sa.pos = e->pos;
+  sa.base_pos = e->base_pos;
+  sa.step_ctr = e->step_ctr;
+  TI_TRY(ti_step_begin(&sa, e->s));
+  for (int l = 0; l < c.layers; ++l) {
+    DevLayer& L = e->layer[l];
+    // TransformerLayer::forward without attention weights (inference_engine.cpp:293-296):
+    // post_attn = add(x, x); ffn = relu(post_attn @ up) @ down (:392-398); out = add(post_attn, ffn).
+    TI_TRY(ti_add_f32(e->h, e->h, e->h, H, e->s));
+    TI_TRY(ti_matmul_f32(e->h, L.gu.f32, e->tmp, nullptr, 1, H, I, 1, e->s));
+    TI_TRY(ti_matmul_f32(e->tmp, L.down.f32, e->h, e->h, 1, I, H, 2, e->s));
+  }
+  TI_TRY(ti_matmul_f32(e->h, e->lm.f32, e->logits, nullptr, 1, H, V, 0, e->s));
+  TI_TRY(ti_stream_sync(e->s));
+  if (logits) TI_TRY(ti_memcpy_d2h(logits, e->logits, (size_t)V * 4, e->s));
+  return TI_OK;
+}
+
+int ti_engine_replay_prepare(ti_engine* e, int n, int kv_len, int start_token) {
+  if (!e || e->c.compat) return ti_set_error(TI_ERR_ARG, "ti_engine_replay_prepare: bad engine");
+  const ti_engine_config& c = e->c;
+  if (n < 1 || n > c.max_batch || kv_len < 1 || kv_len > c.max_seq || start_token < 0 || start_token >= c.vocab)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_replay_prepare: n=%d kv_len=%d", n, kv_len);
+  TI_TRY(ensure_io(e, 1, 1));
+  std::vector<int32_t> base(n, kv_len - 1), zero(n, 0);
+  std::vector<unsigned long long> am(n, (unsigned long long)(0xFFFFFFFFu - (uint32_t)start_token));
+  TI_TRY(ti_memcpy_h2d(e->base_pos, base.data(), (size_t)n * 4, e->s));
+  TI_TRY(ti_memcpy_h2d(e->n_in, zero.data(), (size_t)n * 4, e->s));
+  TI_TRY(ti_memcpy_h2d(e->argmax, am.data(), (size_t)n * 8, e->s));
+  TI_TRY(ti_memset(e->step_ctr, 0, 4, e->s));
+  hipGraphExec_t g = nullptr;
+  TI_TRY(get_graph(e, n, 0, &g));
+  e->replay_M = n;
+  return ti_stream_sync(e->s);
+}
+
+int ti_engine_replay_run(ti_engine* e, int steps) {
+  if (!e || e->replay_M < 1) return ti_set_error(TI_ERR_ARG, "ti_engine_replay_run: call ti_engine_replay_prepare first");
+  hipGraphExec_t g = e->graphs.at(std::make_pair(e->replay_M, 0));
+  for (int s = 0; s < steps; ++s) E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
+  return TI_OK;
+}
+
+int ti_engine_sync(ti_engine* e) {
+  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_sync: null");
+  return ti_stream_sync(e->s);
+}
+
+int ti_engine_last_tokens(ti_engine* e, int n, int32_t* tokens) {
+  if (!e || !tokens || n < 1 || n > e->c.max_batch) return ti_set_error(TI_ERR_ARG, "ti_engine_last_tokens");
+  std::vector<unsigned long long> am((size_t)n);
+  TI_TRY(ti_memcpy_d2h(am.data(), e->argmax, am.size() * 8, e->s));
+  for (int m = 0; m < n; ++m) tokens[m] = (int32_t)(0xFFFFFFFFu - (uint32_t)(am[m] & 0xFFFFFFFFull));
+  return TI_OK;
+}
+
+int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, double* avg_us, double* bytes) {
+  if (!e || e->c.compat || !avg_us || !bytes || reps < 1 || n < 1 || n > e->c.max_batch || e->c.layers < 1)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_time_kernel: bad arguments");
+  const ti_engine_config& c = e->c;
+  DevLayer& L = e->layer[0];
+  const int H = c.hidden, I = c.inter, qd = e->qd(), kvd = e->kvd();
+  const DevLinear* W = nullptr;
+  const void* x = nullptr;
+  int xk = TI_X_F16, ldx = 0;
+  const float* nw = nullptr;
+  ti_epilogue ep{};
+  switch (which) {
+    case 0: W = &L.qkv; x = e->h; xk = TI_X_F32_RMSNORM; ldx = H; nw = L.attn_norm;
+      ep.kind = TI_EPI_QKV_ROPE_KV; ep.ldo = qd; ep.out = e->q; ep.q_dim = qd; ep.kv_dim = kvd; ep.head_dim = c.head_dim;
+      ep.max_seq = c.max_seq; ep.pos = e->pos; ep.rope_cs = e->rope_cs; ep.k_cache = L.kc; ep.v_cache = L.vc;
+      ep.kv_stream_stride = e->kv_stride; break;
+    case 1: W = &L.o; x = e->attn; ldx = qd; ep.kind = TI_EPI_STORE_F32; ep.ldo = H; ep.out = e->tmp ? e->tmp : e->q; break;
+    case 2: W = &L.gu; x = e->h; xk = TI_X_F32_RMSNORM; ldx = H; nw = L.ffn_norm;
+      ep.kind = TI_EPI_SILU_MUL_F16; ep.ldo = I; ep.out = e->act; break;
+    case 3: W = &L.down; x = e->act; ldx = I; ep.kind = TI_EPI_STORE_F32; ep.ldo = H; ep.out = e->q; break;
+    case 4: W = &e->lm; x = e->h; xk = TI_X_F32_RMSNORM; ldx = H; nw = e->out_norm;
+      ep.kind = TI_EPI_LOGITS_ARGMAX; ep.ldo = c.vocab; ep.out = e->logits; ep.argmax = e->argmax; break;
+    case 5: break;
+    default: return ti_set_error(TI_ERR_ARG, "ti_engine_time_kernel: which=%d", which);
+  }
+  if (which == 1 || which == 3) {
+    // STORE_F32 into a scratch of n*H floats: q holds n*qd >= n*H only if qd >= H
+    if ((size_t)qd < (size_t)H) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_time_kernel: scratch too small");
+    ep.out = e->q;
+  }
+  std::vector<int32_t> base(n, kv_len - 1);
+  TI_TRY(ti_memcpy_h2d(e->pos, base.data(), (size_t)n * 4, e->s));
+  hipEvent_t a, b;
+  E_CHECK(hipEventCreate(&a), "hipEventCreate");
+  E_CHECK(hipEventCreate(&b), "hipEventCreate");
+  auto launch = [&]() -> int {
+    if (which == 5)
+      return ti_attn_decode(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, n, c.heads, c.kv_heads, c.head_dim,
+                            e->splits_for(n), e->ws, e->attn, e->s);
+    const int mc = e->mchunk(W->K);
+    for (int m0 = 0; m0 < n; m0 += mc) {
+      const int mm = std::min(mc, n - m0);
+      TI_TRY(ti_gemm_wq_a16(W->tiles, W->scales, c.bits, x, xk, ldx, nw, c.eps, mm, W->N, W->K, &ep, e->s));
+    }
+    return TI_OK;
+  };
+  int rc = launch();   // warm
+  if (rc == TI_OK) {
+    hipEventRecord(a, e->s);
+    for (int r = 0; r < reps && rc == TI_OK; ++r) rc = launch();
+    hipEventRecord(b, e->s);
+    hipEventSynchronize(b);
+  }
+  float ms = 0.0f;
+  hipEventElapsedTime(&ms, a, b);
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  TI_TRY(rc);
+  const int launches_per = which == 5 ? 1 : (n + e->mchunk(W->K) - 1) / e->mchunk(W->K);
+  *avg_us = (double)ms * 1000.0 / (double)(reps * launches_per);
+  if (which == 5) {
+    *bytes = 2.0 * n * (double)kvd * kv_len * 2.0 + (double)n * qd * (4 + 2);
+  } else {
+    const double wbytes = (double)ti_wpack_tile_bytes(c.bits, W->K, W->N) + (double)ti_wpack_scale_bytes(c.bits, W->K, W->N);
+    *bytes = wbytes / launches_per + (double)n / launches_per * W->K * (xk == TI_X_F16 ? 2 : 4);
+  }
+  return TI_OK;
+}
+
+}  // extern "C"

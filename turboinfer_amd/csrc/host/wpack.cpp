@@ -1,0 +1,121 @@
+// wpack.cpp -- host-side quantize + pack of linear weights into the gfx950 tile format.
+//
+// The reference Quantizer (src/optimize/quantization.cpp) quantizes a whole tensor with one
+// symmetric scale (calculate_quantization_info :355-360, 375-378), stores INT4 unpacked in
+// int32 (:45-46) and drops the scale (quantize_model :89-118).  Here the same symmetric
+// formula -- scale = absmax / 7 (int4) or / 127 (int8), q = clamp(round(x / scale)) with
+// std::round (half away from zero) -- is applied per group of 128 k of one output column,
+// and the result is packed two nibbles per byte with an fp16 scale per group.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "ti_hip.h"
+
+int ti_set_error(int code, const char* fmt, ...);
+
+namespace {
+
+inline int map_row(int c, int row_map, int row_offset) {
+  return row_map == TI_ROWS_INTERLEAVE8 ? 16 * (c >> 3) + (c & 7) + row_offset : row_offset + c;
+}
+
+inline float clamp_ref(float v, float lo, float hi) {   // std::max(lo, std::min(hi, v))
+  const float t = (v < hi) ? v : hi;
+  return (lo < t) ? t : lo;
+}
+
+inline uint16_t to_half(float f) {
+  const _Float16 h = (_Float16)f;                         // round to nearest even
+  uint16_t u;
+  std::memcpy(&u, &h, 2);
+  return u;
+}
+
+}  // namespace
+
+extern "C" size_t ti_wpack_tile_bytes(int bits, int K, int N) {
+  if (K <= 0 || N <= 0) return 0;
+  return (size_t)(N / 16) * (size_t)(K / 128) * 256u * (size_t)bits;
+}
+
+extern "C" size_t ti_wpack_scale_bytes(int bits, int K, int N) {
+  if (bits == 16 || K <= 0 || N <= 0) return 0;
+  return (size_t)(N / 16) * (size_t)(K / 128) * 16u * sizeof(uint16_t);
+}
+
+extern "C" int ti_wpack_host(const float* w, int K, int N_src, int N_total, int bits, int scale_mode, int row_map,
+                             int row_offset, void* tiles, uint16_t* scales) {
+  if (!w || !tiles) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: null pointer");
+  if (bits != 4 && bits != 8 && bits != 16) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: bits %d", bits);
+  if (K <= 0 || (K & 127) || N_total <= 0 || (N_total & 15) || N_src <= 0)
+    return ti_set_error(TI_ERR_ARG, "ti_wpack_host: K %% 128 / N %% 16 (K=%d N_total=%d)", K, N_total);
+  if (row_map == TI_ROWS_INTERLEAVE8 && (N_src & 7)) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: interleave needs N %% 8 == 0");
+  if (map_row(N_src - 1, row_map, row_offset) >= N_total || row_offset < 0)
+    return ti_set_error(TI_ERR_ARG, "ti_wpack_host: rows do not fit N_total");
+  if (bits != 16 && !scales) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: scales required");
+  if (scale_mode < TI_SCALE_GROUP || scale_mode > TI_SCALE_UNIT) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: scale_mode");
+  const int KT = K / 128;
+  uint8_t* tb = static_cast<uint8_t*>(tiles);
+
+  if (bits == 16) {
+    for (int c = 0; c < N_src; ++c) {
+      const int n = map_row(c, row_map, row_offset), nt = n >> 4, r = n & 15;
+      for (int k = 0; k < K; ++k) {
+        const int kt = k >> 7, kk = k & 127, kq = kk >> 5, ch = (kk & 31) >> 3, e = kk & 7;
+        const size_t off = ((size_t)nt * KT + kt) * 2048 + (size_t)ch * 512 + (size_t)(kq * 16 + r) * 8 + e;
+        reinterpret_cast<uint16_t*>(tb)[off] = to_half(w[(size_t)k * N_src + c]);
+      }
+    }
+    return TI_OK;
+  }
+
+  const float qmax = bits == 4 ? 7.0f : 127.0f, qlo = bits == 4 ? -7.0f : -128.0f;
+  float tensor_scale = 1.0f;
+  if (scale_mode == TI_SCALE_TENSOR) {
+    float amax = 0.0f;
+    for (size_t i = 0; i < (size_t)K * N_src; ++i) amax = std::max(amax, std::fabs(w[i]));
+    tensor_scale = amax / qmax;
+  }
+  const size_t tile_bytes = (size_t)256 * bits;
+  float col[128];
+  for (int c = 0; c < N_src; ++c) {
+    const int n = map_row(c, row_map, row_offset), nt = n >> 4, r = n & 15;
+    for (int g = 0; g < KT; ++g) {
+      float amax = 0.0f;
+      for (int i = 0; i < 128; ++i) {
+        col[i] = w[(size_t)(g * 128 + i) * N_src + c];
+        amax = std::max(amax, std::fabs(col[i]));
+      }
+      const float sc = scale_mode == TI_SCALE_GROUP ? amax / qmax : tensor_scale;
+      scales[((size_t)nt * KT + g) * 16 + r] = to_half(scale_mode == TI_SCALE_UNIT ? 1.0f : sc);
+      int8_t q[128];
+      for (int i = 0; i < 128; ++i) {
+        const float v = scale_mode == TI_SCALE_UNIT ? std::round(col[i]) : std::round(col[i] / sc);
+        q[i] = (int8_t)clamp_ref(v, qlo, qmax);
+      }
+      uint8_t* tile = tb + ((size_t)nt * KT + g) * tile_bytes;
+      for (int kq = 0; kq < 4; ++kq) {
+        const int lane = kq * 16 + r;
+        if (bits == 4) {
+          uint32_t words[4];
+          for (int s4 = 0; s4 < 4; ++s4) {
+            uint32_t wd = 0;
+            for (int e = 0; e < 8; ++e) {
+              const uint32_t nib = (uint32_t)(q[kq * 32 + s4 * 8 + e] + 8) & 0xF;
+              wd |= nib << ((e & 1) ? (16 + 4 * (e >> 1)) : (4 * (e >> 1)));
+            }
+            words[s4] = wd;
+          }
+          std::memcpy(tile + lane * 16, words, 16);
+        } else {
+          for (int ch = 0; ch < 2; ++ch) std::memcpy(tile + ch * 1024 + lane * 16, q + kq * 32 + ch * 16, 16);
+        }
+      }
+    }
+  }
+  return TI_OK;
+}

@@ -1,0 +1,98 @@
+// common.hpp -- shared device helpers for the gfx950 kernels (wave64, CDNA4).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ti_hip.h"
+
+namespace ti {
+
+typedef _Float16 f16;
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------- fp16 helpers
+__device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(f16, h); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (f16)f); }
+
+// fp32 -> fp16 bits, round to nearest even with subnormals, in integer arithmetic: used where
+// device output must be bit-identical to the host / oracle (or_float_to_half); the hardware
+// conversion rounds some fp16-subnormal results differently.
+__device__ inline uint16_t f2h_soft(float f) {
+  const uint32_t x = __builtin_bit_cast(uint32_t, f);
+  const uint16_t s = (uint16_t)((x >> 16) & 0x8000u);
+  const uint32_t ax = x & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return s | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0u);
+  if (ax >= 0x477ff000u) return s | 0x7c00u;
+  if (ax < 0x38800000u) {
+    if (ax < 0x33000000u) return s;
+    const uint32_t e = ax >> 23, m = (ax & 0x7fffffu) | 0x800000u, sh = 126u - e;
+    const uint32_t hm = m >> sh, rem = m & ((1u << sh) - 1u), half = 1u << (sh - 1u);
+    return s | (uint16_t)(hm + ((rem > half || (rem == half && (hm & 1u))) ? 1u : 0u));
+  }
+  uint32_t hb = (ax >> 13) - (112u << 10);
+  const uint32_t rem = ax & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (hb & 1u))) ++hb;
+  return s | (uint16_t)hb;
+}
+
+// ------------------------------------------------------------ wave reductions
+template <int WIDTH>
+__device__ __forceinline__ float wave_sum_xor(float v) {
+#pragma unroll
+  for (int o = WIDTH / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+template <int WIDTH>
+__device__ __forceinline__ float wave_max_xor(float v) {
+#pragma unroll
+  for (int o = WIDTH / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// ----------------------------------------------------- synthetic model stream
+// Bit-identical to or_splitmix64 / or_synth_unit in oracle/ti_oracle.c.
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t synth_stream(uint64_t seed, uint32_t tid) {
+  return splitmix64(seed ^ ((uint64_t)tid * 0xD1B54A32D192ED03ULL));
+}
+__host__ __device__ __forceinline__ float synth_unit(uint64_t stream, uint64_t idx) {
+  const uint64_t h = splitmix64(stream + idx);
+  const int32_t m = (int32_t)(h >> 40);
+  return (float)(2 * m - (1 << 24)) * (1.0f / 16777216.0f);
+}
+
+// ---------------------------------------------------------------- tile layout
+// See ti_hip.h: a tile is 16 output rows x 128 k; chunk c (1 KiB) holds, for lane l,
+// 16 bytes of row (l & 15) starting at k = 32*(l>>4) + c*(32/chunks).
+template <int BITS>
+struct TileFmt {
+  static constexpr int kChunks = BITS / 4;           // 1, 2, 4 dwordx4 per lane
+  static constexpr int kBytes = 1024 * kChunks;
+  static constexpr int kKPerChunk = 32 / kChunks;    // k values per lane per chunk
+};
+
+__host__ __device__ __forceinline__ size_t tile_index(int nt, int kt, int KT) {
+  return (size_t)nt * KT + kt;
+}
+
+}  // namespace ti
+
+// error helper shared by the launchers (defined in host/capi.cpp)
+extern "C++" int ti_set_error(int code, const char* fmt, ...);
+extern "C++" int ti_check_hip(hipError_t e, const char* what);
+#define TI_HIP_CHECK(expr, what)                         \
+  do {                                                   \
+    hipError_t _e = (expr);                              \
+    if (_e != hipSuccess) return ti_check_hip(_e, what); \
+  } while (0)
+#define TI_LAUNCH_CHECK(what) TI_HIP_CHECK(hipGetLastError(), what)

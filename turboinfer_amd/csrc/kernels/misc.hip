@@ -1,0 +1,226 @@
+// misc.hip -- device-side decode loop step, synthetic weight / KV generation.
+#include <math.h>
+
+#include "common.hpp"
+
+namespace ti {
+
+// --------------------------------------------------------------- step begin
+// One block per stream m.  The decode loop runs entirely on the device: the token of
+// step s is the prompt token while s < n_in[m], else the previous step's greedy argmax
+// (the key packs (value, 0xFFFFFFFF - index), so the max is the lowest-index maximum).
+__global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a) {
+  __shared__ int s_tok;
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const int s = *a.step_ctr;
+  const int nin = a.n_in ? a.n_in[m] : 0;
+  if (tid == 0) {
+    int tok;
+    if (s < nin) {
+      tok = a.in_tokens[(size_t)m * a.in_stride + s];
+    } else {
+      tok = (int)(0xFFFFFFFFu - (uint32_t)(a.argmax[m] & 0xFFFFFFFFull));
+      if (a.out_tokens && s - nin < a.out_stride) a.out_tokens[(size_t)m * a.out_stride + (s - nin)] = tok;
+    }
+    if (tok < 0 || tok >= a.vocab) tok = 0;     // never index outside the table
+    s_tok = tok;
+    a.pos[m] = a.base_pos[m] + s;
+    a.argmax[m] = 0ull;
+  }
+  __syncthreads();
+  float* h = a.h + (size_t)m * a.hidden;
+  if (a.placeholder_first >= 0) {
+    // forward_pass / forward_pass_incremental placeholder rows (inference_engine.cpp:1444-1448,
+    // 1509-1512): 0.1f * (flat_index % 100).
+    const size_t off = s == 0 ? (size_t)a.placeholder_first : 0;
+    for (int i = tid; i < a.hidden; i += 256) h[i] = 0.1f * (float)((off + (size_t)i) % 100);
+  } else {
+    const uint16_t* e = a.emb + (size_t)s_tok * a.hidden;
+    for (int i = tid; i < a.hidden; i += 256) h[i] = h2f(e[i]);
+  }
+}
+
+// ---------------------------------------------------------- synthetic weights
+__host__ __device__ inline int map_row(int c, int row_map, int row_offset) {
+  return row_map == TI_ROWS_INTERLEAVE8 ? 16 * (c >> 3) + (c & 7) + row_offset : row_offset + c;
+}
+
+// One thread per (source column c, k-group g): 128 seeded values -> per-group symmetric
+// scale (absmax / 7 or / 127) -> q = clamp(round(w / s)) -> packed tile bytes + fp16 scale.
+template <int BITS>
+__global__ __launch_bounds__(128) void wsynth_kernel(uint64_t stream, int K, int N_src, int row_map,
+                                                     int row_offset, float amp, uint8_t* tiles,
+                                                     uint16_t* scales) {
+  const int KT = K >> 7;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N_src * KT) return;
+  const int c = (int)(t % N_src), g = (int)(t / N_src);
+  float w[128];
+  float amax = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 128; ++i) {
+    w[i] = synth_unit(stream, (uint64_t)(g * 128 + i) * (uint64_t)N_src + (uint64_t)c) * amp;
+    amax = fmaxf(amax, fabsf(w[i]));
+  }
+  const float qmax = BITS == 4 ? 7.0f : 127.0f, qlo = BITS == 4 ? -7.0f : -128.0f;
+  const float sc = amax / qmax;
+  const int n = map_row(c, row_map, row_offset), nt = n >> 4, r = n & 15;
+  scales[((size_t)nt * KT + g) * 16 + r] = f2h_soft(sc);
+  uint8_t* tile = tiles + ((size_t)nt * KT + g) * (size_t)TileFmt<BITS>::kBytes;
+#pragma unroll
+  for (int kq = 0; kq < 4; ++kq) {
+    const int lane = kq * 16 + r;
+    if constexpr (BITS == 4) {
+      uint32_t words[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        uint32_t wd = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float q = roundf(w[kq * 32 + s4 * 8 + e] / sc);
+          q = fmaxf(qlo, fminf(qmax, q));
+          const uint32_t nib = (uint32_t)((int)q + 8) & 0xF;
+          const int p = e >> 1;
+          wd |= nib << ((e & 1) ? (16 + 4 * p) : (4 * p));
+        }
+        words[s4] = wd;
+      }
+      *(uint4*)(tile + lane * 16) = make_uint4(words[0], words[1], words[2], words[3]);
+    } else {
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) {
+        uint32_t words[4];
+#pragma unroll
+        for (int wi = 0; wi < 4; ++wi) {
+          uint32_t wd = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            float q = roundf(w[kq * 32 + ch * 16 + wi * 4 + b] / sc);
+            q = fmaxf(qlo, fminf(qmax, q));
+            wd |= ((uint32_t)(int)q & 0xFFu) << (8 * b);
+          }
+          words[wi] = wd;
+        }
+        *(uint4*)(tile + ch * 1024 + lane * 16) = make_uint4(words[0], words[1], words[2], words[3]);
+      }
+    }
+  }
+}
+
+// fp16 weights: element-parallel, no scale.
+__global__ void wsynth_f16_kernel(uint64_t stream, int K, int N_src, int row_map, int row_offset, float amp,
+                                  uint16_t* tiles) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)K * N_src) return;
+  const int k = (int)(t / N_src), c = (int)(t % N_src);
+  const float v = synth_unit(stream, (uint64_t)t) * amp;
+  const int KT = K >> 7, n = map_row(c, row_map, row_offset), nt = n >> 4, r = n & 15;
+  const int kt = k >> 7, kk = k & 127, kq = kk >> 5, ch = (kk & 31) >> 3, e = kk & 7;
+  const size_t off = ((size_t)nt * KT + kt) * 2048 + (size_t)ch * 512 + (size_t)(kq * 16 + r) * 8 + e;
+  tiles[off] = f2h_soft(v);
+}
+
+__global__ void fill_uniform_f16_kernel(uint64_t stream, uint64_t n, float mul, uint16_t* dst) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = f2h_soft(synth_unit(stream, i) * mul);
+}
+__global__ void fill_uniform_f32_kernel(uint64_t stream, uint64_t n, float mul, float add, float* dst) {
+  // add + mul*u with two roundings, as the oracle's `1.0f + jitter * u` (no contraction)
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = __fadd_rn(add, __fmul_rn(mul, synth_unit(stream, i)));
+}
+
+// Synthetic KV (or_model_fill_kv): slot p of kv-head kvh, dim d takes element
+// p*(kv_heads*hd) + kvh*hd + d of the oracle's [pos][kv*hd] stream.
+__global__ void fill_kv_kernel(uint64_t stream, int n, int kv_heads, int hd, int max_seq, uint16_t* dst) {
+  const int64_t total = (int64_t)n * kv_heads * hd;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(i / (kv_heads * hd));
+    const int c = (int)(i - (int64_t)p * kv_heads * hd);
+    const int kvh = c / hd, d = c - kvh * hd;
+    dst[((size_t)kvh * max_seq + p) * hd + d] = f2h_soft(synth_unit(stream, (uint64_t)i));
+  }
+}
+
+}  // namespace ti
+
+extern "C" int ti_step_begin(const ti_step_args* a, ti_stream_t stream) {
+  using namespace ti;
+  if (!a || !a->h || !a->argmax || !a->pos || !a->base_pos || !a->step_ctr || a->M < 1 || a->hidden < 1)
+    return ti_set_error(TI_ERR_ARG, "ti_step_begin: bad arguments");
+  if (a->placeholder_first < 0 && !a->emb) return ti_set_error(TI_ERR_ARG, "ti_step_begin: emb required");
+  if (a->n_in && !a->in_tokens) return ti_set_error(TI_ERR_ARG, "ti_step_begin: in_tokens required");
+  hipLaunchKernelGGL(step_begin_kernel, dim3(a->M), dim3(256), 0, (hipStream_t)stream, *a);
+  TI_LAUNCH_CHECK("step_begin_kernel");
+  return TI_OK;
+}
+
+extern "C" int ti_wsynth_device(uint64_t seed, uint32_t tensor_id, int K, int N_src, int N_total, int bits,
+                                int row_map, int row_offset, void* tiles, uint16_t* scales, ti_stream_t stream) {
+  using namespace ti;
+  if (!tiles || K <= 0 || (K & 127) || N_total <= 0 || (N_total & 15) || N_src <= 0)
+    return ti_set_error(TI_ERR_ARG, "ti_wsynth_device: bad shape K=%d N_src=%d N_total=%d", K, N_src, N_total);
+  if (map_row(N_src - 1, row_map, row_offset) >= N_total || (row_map == TI_ROWS_INTERLEAVE8 && (N_src & 7)))
+    return ti_set_error(TI_ERR_ARG, "ti_wsynth_device: rows do not fit N_total");
+  const float amp = sqrtf(3.0f) / sqrtf((float)K);
+  const uint64_t stream_id = synth_stream(seed, tensor_id);
+  hipStream_t s = (hipStream_t)stream;
+  if (bits == 16) {
+    const int64_t n = (int64_t)K * N_src;
+    hipLaunchKernelGGL(wsynth_f16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, stream_id, K, N_src,
+                       row_map, row_offset, amp, (uint16_t*)tiles);
+    TI_LAUNCH_CHECK("wsynth_f16_kernel");
+    return TI_OK;
+  }
+  if (!scales) return ti_set_error(TI_ERR_ARG, "ti_wsynth_device: scales required");
+  const int64_t n = (int64_t)N_src * (K >> 7);
+  const dim3 grid((unsigned)((n + 127) / 128));
+  if (bits == 4)
+    hipLaunchKernelGGL(wsynth_kernel<4>, grid, dim3(128), 0, s, stream_id, K, N_src, row_map, row_offset, amp,
+                       (uint8_t*)tiles, scales);
+  else if (bits == 8)
+    hipLaunchKernelGGL(wsynth_kernel<8>, grid, dim3(128), 0, s, stream_id, K, N_src, row_map, row_offset, amp,
+                       (uint8_t*)tiles, scales);
+  else
+    return ti_set_error(TI_ERR_ARG, "ti_wsynth_device: bits %d", bits);
+  TI_LAUNCH_CHECK("wsynth_kernel");
+  return TI_OK;
+}
+
+extern "C" int ti_fill_uniform_f16(uint64_t seed, uint32_t tensor_id, uint64_t n, float mul, uint16_t* dst,
+                                   ti_stream_t stream) {
+  using namespace ti;
+  if (!dst) return ti_set_error(TI_ERR_ARG, "ti_fill_uniform_f16: null");
+  if (n == 0) return TI_OK;
+  const unsigned blocks = (unsigned)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536);
+  hipLaunchKernelGGL(fill_uniform_f16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     synth_stream(seed, tensor_id), n, mul, dst);
+  TI_LAUNCH_CHECK("fill_uniform_f16_kernel");
+  return TI_OK;
+}
+
+extern "C" int ti_fill_kv_uniform(uint64_t seed, uint32_t tensor_id, int n, int kv_heads, int head_dim,
+                                  int max_seq, uint16_t* dst, ti_stream_t stream) {
+  using namespace ti;
+  if (!dst || n < 0 || n > max_seq || kv_heads < 1 || head_dim < 1)
+    return ti_set_error(TI_ERR_ARG, "ti_fill_kv_uniform: bad arguments");
+  if (n == 0) return TI_OK;
+  const int64_t total = (int64_t)n * kv_heads * head_dim;
+  const unsigned blocks = (unsigned)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  hipLaunchKernelGGL(fill_kv_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, synth_stream(seed, tensor_id),
+                     n, kv_heads, head_dim, max_seq, dst);
+  TI_LAUNCH_CHECK("fill_kv_kernel");
+  return TI_OK;
+}
+
+extern "C" int ti_fill_uniform_f32(uint64_t seed, uint32_t tensor_id, uint64_t n, float mul, float add, float* dst,
+                                   ti_stream_t stream) {
+  using namespace ti;
+  if (!dst) return ti_set_error(TI_ERR_ARG, "ti_fill_uniform_f32: null");
+  if (n == 0) return TI_OK;
+  const unsigned blocks = (unsigned)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536);
+  hipLaunchKernelGGL(fill_uniform_f32_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     synth_stream(seed, tensor_id), n, mul, add, dst);
+  TI_LAUNCH_CHECK("fill_uniform_f32_kernel");
+  return TI_OK;
+}
