@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""bench.py -- decode tokens/s per GPU, Llama-2-7B-shape INT4 (group 128) at 2048-token KV,
+and the achieved fraction of the HBM-read roofline (BASELINE.json `metric`, configs[2]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--kv L] [--model llama2-7b]
+
+One process per GPU (torchrun for N > 1).  Each rank holds an independent replica of the
+model with B decode streams (requests) and their fp16 KV caches in its own HBM: the path
+shards by request, there is no collective on the data path (torch.distributed/gloo only
+carries the barrier and the max-over-ranks of the timing).  A step = one decode token for
+each of the rank's B streams, replayed at position L-1 so every step reads exactly L cache
+slots (SURVEY 8(d) replay mode), greedy feedback on the device.  Synthetic random weights of
+the named architecture (no checkpoints are reachable); `data` says so.
+
+rank 0 prints ONE JSON line with the contract fields plus `roofline` (dominant kernel:
+the W4 decode GEMM, live HIP-event timing on the engine stream) and `cpu_baseline` (the
+compiled reference's own CPU decode ops timed on this host, rank 0 / N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MODELS = {
+    # name: (vocab, hidden, layers, heads, kv_heads, head_dim, inter, bits, rope_theta)
+    "llama2-7b": (32000, 4096, 32, 32, 32, 128, 11008, 4, 10000.0),
+    "tinyllama-1.1b": (32000, 2048, 22, 32, 4, 64, 5632, 8, 10000.0),
+    "llama3-8b": (128256, 4096, 32, 32, 8, 128, 14336, 4, 500000.0),
+}
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def step_bytes(m, B, L):
+    """Algorithmic HBM bytes of one decode step: weights once + B streams' KV."""
+    import turboinfer_amd as T
+    V, H, layers, nh, nkv, hd, I, bits, _ = m
+    lib = T.lib()
+
+    def lin(K, N):
+        return lib.ti_wpack_tile_bytes(bits, K, N) + lib.ti_wpack_scale_bytes(bits, K, N)
+
+    w = layers * (lin(H, nh * hd + 2 * nkv * hd) + lin(nh * hd, H) + lin(H, 2 * I) + lin(I, H))
+    w += lin(H, V) + (2 * layers + 1) * H * 4 + B * H * 2          # lm_head, norms (fp32), embedding rows
+    kv_read = 2 * layers * nkv * hd * 2 * L
+    kv_write = 2 * layers * nkv * hd * 2
+    return w + B * (kv_read + kv_write), w
+
+
+class Group:
+    """Barrier / max over ranks.  World 1: trivial; otherwise torch.distributed over gloo
+    (CPU-side only: nothing of the decode path goes through it)."""
+
+    def __init__(self):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, v: float) -> float:
+        if not self.dist:
+            return v
+        import torch
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def cpu_baseline(m, L):
+    """The reference's own CPU decode (oracle/_ref: unmodified sources, g++ -O3 -mavx2 -mfma):
+    one layer of the reference-composed decode step (rms_norm, q/k/v/o matmul_3d_2d, apply_rope,
+    multi_head_attention over L cached tokens, SwiGLU FFN) with int32-stored INT4 weights as
+    Quantizer::quantize_model hands them to the engine, plus the lm_head matmul; token time =
+    layers * layer + lm_head.  Bounded sample (~5-10 s of CPU work)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        from pyoracle import Reference
+        ref = Reference()
+    except Exception as exc:  # reference library not shipped with this checkout
+        return {"value": None, "unit": "tokens/s", "cores": 1, "kind": "reference",
+                "sample": f"unavailable: {exc}"}
+    V, H, layers, nh, nkv, hd, I, bits, _ = m
+    layer_s, head_s = ref.time_decode(H, nh, I, V, L, weight_kind=1, n_layers=1)
+    tok_s = layers * layer_s + head_s
+    return {"value": round(1.0 / tok_s, 6), "unit": "tokens/s", "cores": 1, "kind": "reference",
+            "sample": f"1 decode layer ({layer_s:.2f} s) x {layers} + lm_head ({head_s:.2f} s) at L={L}, "
+                      f"INT4 held as int32 (reference quantized path), 1 stream; matmul_3d_2d is single-threaded "
+                      f"(tensor_engine.cpp:620-633); host {os.uname().machine}, {os.cpu_count()} logical CPUs"}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=256)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=1, help="decode streams per GPU")
+    ap.add_argument("--kv", type=int, default=2048, help="KV length read per step")
+    ap.add_argument("--model", default="llama2-7b", choices=sorted(MODELS))
+    ap.add_argument("--seed", type=int, default=0x7157)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-reps", type=int, default=50)
+    args = ap.parse_args()
+
+    import turboinfer_amd as T
+
+    g = Group()
+    T.init(g.local_rank)
+    m = MODELS[args.model]
+    V, H, layers, nh, nkv, hd, I, bits, theta = m
+    B, L = args.batch, args.kv
+    e = T.Engine(V, H, layers, nh, nkv, hd, I, bits=bits, max_seq=L, max_batch=B, rope_theta=theta,
+                 device=g.local_rank)
+    e.synth(args.seed + g.rank, 0.0)
+    for s in range(B):
+        e.fill_kv(s, L - 1, args.seed + 1000 * g.rank + s)
+    e.replay_prepare(B, L, (args.seed + g.rank) % V)
+
+    e.replay_run(args.warmup)
+    e.sync()
+    g.barrier()
+    e.sync()
+    t0 = time.perf_counter()
+    e.replay_run(args.steps)
+    e.sync()
+    t1 = time.perf_counter()
+    g.barrier()
+    dt = g.max(t1 - t0)
+
+    tokens = B * args.steps * g.world
+    value = tokens / dt
+    ms_per_step = dt / args.steps * 1000.0
+    sb, wb = step_bytes(m, B, L)
+
+    # Dominant kernel: the W4 decode GEMM (gemv_wq_kernel<4>), ~76 % of a step's bytes.
+    # Live timing: each linear class of layer 0 launched back to back between two HIP events
+    # on the engine stream; a step issues layers x (qkv, o, gate/up, down) + lm_head launches.
+    names = ["qkv", "o", "gate_up", "down", "lm_head"]
+    per = {}
+    gemv_bytes = gemv_us = 0.0
+    n_launch = 0
+    for w, name in enumerate(names):
+        us, by = e.time_kernel(w, B, L, args.kernel_reps)
+        cnt = 1 if name == "lm_head" else layers
+        per[name] = {"avg_us": round(us, 3), "bytes": int(by), "GBps": round(by / us / 1e3, 1)}
+        gemv_bytes += by * cnt
+        gemv_us += us * cnt
+        n_launch += cnt
+    att_us, att_bytes = e.time_kernel(5, B, L, args.kernel_reps)
+    per["attention"] = {"avg_us": round(att_us, 3), "bytes": int(att_bytes), "GBps": round(att_bytes / att_us / 1e3, 1)}
+    achieved = gemv_bytes / gemv_us / 1e3   # GB/s
+    e.close()
+
+    result = None
+    if g.rank == 0:
+        result = {
+            "metric": "decode tokens/s/GPU, Llama-7B-shape INT4 @2048 ctx; % HBM-read roofline",
+            "value": round(value, 3),
+            "unit": "tokens/s",
+            "n_gpus": g.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "w4a16" if bits == 4 else ("w8a16" if bits == 8 else "f16"),
+            "data": "synthetic (seeded random weights of the named architecture, quantized per group of 128; "
+                    "synthetic fp16 KV cache)",
+            "config": {"workload": f"{args.model} INT{bits} g128 decode, {B} stream(s)/GPU, KV {L}, replay at pos {L - 1}",
+                       "model": args.model, "global_batch": B * g.world, "seq_len": L,
+                       "parallelism": f"replicas{g.world} (request-sharded, no collectives)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "gemv_wq_kernel<4>",
+                         "bytes_per_launch": int(gemv_bytes / n_launch), "avg_launch_us": round(gemv_us / n_launch, 3)},
+            "step_roofline": {"bytes_per_step": int(sb), "weight_bytes": int(wb),
+                              "achieved_GBps": round(sb / (ms_per_step * 1e-3) / 1e9, 1),
+                              "frac": round(sb / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "roofline_tokens_per_s_per_gpu": round(B * HBM_PEAK_GBS * 1e9 / sb, 1)},
+            "kernels": per,
+        }
+        if g.world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(m, L)
+        else:
+            result["cpu_baseline"] = None
+    g.barrier()
+    g.close()
+    if result is not None:
+        print(json.dumps(result))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

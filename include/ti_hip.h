@@ -122,8 +122,15 @@ enum ti_epilogue_kind {
                                 fp16(up_j * silu(gate_j)), N/2 outputs                   */
   TI_EPI_QKV_ROPE_KV = 4,    /* rows [q | k | v]: RoPE(pos[m]) on q and k, q -> out_f32,
                                 k, v -> fp16 KV cache slot pos[m]                        */
-  TI_EPI_LOGITS_ARGMAX = 5   /* out_f32 logits + atomicMax of (value, -index) into argmax[m] */
+  TI_EPI_LOGITS_ARGMAX = 5   /* out_f32 logits + greedy argmax keys (see below)            */
 };
+
+/* Greedy argmax keys: key = (order-preserving bits of the logit) << 32 | (0xFFFFFFFF - n), so
+ * the max key is the largest logit at the lowest index.  Each workgroup folds its tiles into
+ * one key per row and atomicMax-es it into one of TI_ARGMAX_SLOTS slots (no single hot word);
+ * row m's key is the max over argmax[m*TI_ARGMAX_SLOTS + 0 .. SLOTS-1], its token
+ * 0xFFFFFFFF - (key & 0xFFFFFFFF). */
+#define TI_ARGMAX_SLOTS 32
 
 typedef struct ti_epilogue {
   int32_t kind;
@@ -137,7 +144,7 @@ typedef struct ti_epilogue {
   uint16_t* v_cache;
   int64_t kv_stream_stride;          /* elements between streams */
   /* TI_EPI_LOGITS_ARGMAX */
-  unsigned long long* argmax;        /* device [M] keys, zeroed before the call */
+  unsigned long long* argmax;        /* device [M][TI_ARGMAX_SLOTS] keys, zeroed before the call */
   int32_t* step_ctr;                 /* device counter += advance by one thread (nullable) */
   int32_t advance;
   int32_t _pad;
@@ -146,8 +153,8 @@ typedef struct ti_epilogue {
 int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind,
                    int ldx, const float* norm_w, float eps, int M, int N, int K,
                    const ti_epilogue* epi, ti_stream_t s);
-/* LDS bytes one workgroup of ti_gemm_wq_a16 needs for M rows of K (<= 160 KiB). */
-int ti_gemm_lds_bytes(int M, int K);
+/* LDS bytes one workgroup of ti_gemm_wq_a16 needs for an M x N x K call (<= 160 KiB). */
+int ti_gemm_lds_bytes(int M, int N, int K);
 /* One-time kernel attribute setup; call before capturing ti_gemm_wq_a16 into a graph. */
 int ti_gemm_prepare(void);
 
@@ -167,7 +174,7 @@ int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_ca
 /* ------------------------------------------------------- step begin (device loop)
  * One block per stream: picks the token of this step (prompt token while step < n_in[m],
  * else the previous step's argmax), records fed-back tokens, gathers the fp16 embedding row
- * into h (fp32), sets pos[m] = base_pos[m] + *step_ctr, clears argmax[m].
+ * into h (fp32), sets pos[m] = base_pos[m] + *step_ctr, clears argmax row m (all slots).
  * placeholder_first >= 0 selects the reference_compat placeholder embedding
  * 0.1f*((offset + i) % 100) (inference_engine.cpp:1444-1448, 1509-1512) with offset
  * placeholder_first on step 0 and 0 afterwards. */
@@ -177,7 +184,7 @@ typedef struct ti_step_args {
   int32_t hidden, M, vocab, in_stride, out_stride, placeholder_first;
   const int32_t* in_tokens;          /* [M][in_stride] */
   const int32_t* n_in;               /* [M] */
-  unsigned long long* argmax;        /* [M] */
+  unsigned long long* argmax;        /* [M][TI_ARGMAX_SLOTS] */
   int32_t* out_tokens;               /* [M][out_stride] generated tokens */
   int32_t* pos;                      /* [M] */
   const int32_t* base_pos;           /* [M] */

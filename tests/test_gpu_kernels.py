@@ -184,14 +184,14 @@ def test_gemm_logits_argmax(ti, oracle):
     w = (rng.standard_normal((K, V)) * 0.05).astype(f32)
     x = rng.standard_normal((M, K)).astype(f32)
     tiles, scales = ti.wpack_host(w, 4)
-    ld, am = ti.DeviceBuffer(M * V * 4), ti.DeviceBuffer(M * 8)
+    ld, am = ti.DeviceBuffer(M * V * 4), ti.DeviceBuffer(M * ti.ARGMAX_SLOTS * 8)
     am.zero()
     ctr = dev(ti, np.array([7], np.int32))
     ep = ti.Epilogue()
     ep.kind, ep.ldo, ep.out, ep.argmax, ep.step_ctr, ep.advance = ti.EPI_LOGITS_ARGMAX, V, ld.ptr, am.ptr, ctr.ptr, 1
     gemm(ti, dev(ti, tiles), dev(ti, scales), 4, dev(ti, x), ti.X_F32, K, M, V, K, ep)
     logits = ld.download(f32, (M, V))
-    keys = am.download(np.uint64, (M,))
+    keys = am.download(np.uint64, (M, ti.ARGMAX_SLOTS)).max(axis=1)
     idx = (0xFFFFFFFF - (keys & 0xFFFFFFFF)).astype(np.int64)
     np.testing.assert_array_equal(idx, np.argmax(logits, axis=1))
     assert ctr.download(np.int32, (1,))[0] == 8
@@ -224,6 +224,7 @@ def _attn_case(ti, oracle, M, nh, nkv, hd, L_list, splits, max_seq=256, seed=0):
     pos = np.array([l - 1 for l in L_list], np.int32)
     out = ti.DeviceBuffer(M * nh * hd * 2)
     ws = ti.DeviceBuffer(ti.lib().ti_attn_workspace_bytes(M, nh, hd, splits))
+    ws.zero()   # arrival tickets start at zero (re-armed by every call)
     kd, vd, qd_, pd = dev(ti, kc), dev(ti, vc), dev(ti, q), dev(ti, pos)
     ti.check(ti.lib().ti_attn_decode(qd_.ptr, kd.ptr, vd.ptr, stride, max_seq, pd.ptr, M, nh, nkv, hd, splits,
                                      ws.ptr, out.ptr, None))

@@ -24,6 +24,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libturboinfer_amd.so")
 TI_OK = 0
 X_F16, X_F32, X_F32_RMSNORM = 0, 1, 2
 EPI_STORE_F32, EPI_STORE_F16, EPI_RESID_F32, EPI_SILU_MUL_F16, EPI_QKV_ROPE_KV, EPI_LOGITS_ARGMAX = range(6)
+ARGMAX_SLOTS = 32   # TI_ARGMAX_SLOTS (include/ti_hip.h)
 SCALE_GROUP, SCALE_TENSOR, SCALE_UNIT = 0, 1, 2
 ROWS_CONCAT, ROWS_INTERLEAVE8 = 0, 1
 (W_Q, W_K, W_V, W_O, W_GATE, W_UP, W_DOWN, W_LM_HEAD, V_ATTN_NORM, V_FFN_NORM, V_OUT_NORM, E_EMBED) = range(12)
@@ -107,7 +108,7 @@ def lib() -> C.CDLL:
         L.ti_fill_uniform_f32.argtypes = [u64, C.c_uint32, u64, f32, f32, vp, vp]
         L.ti_fill_kv_uniform.argtypes = [u64, C.c_uint32, i32, i32, i32, i32, vp, vp]
         L.ti_gemm_wq_a16.argtypes = [vp, vp, i32, vp, i32, i32, vp, f32, i32, i32, i32, C.POINTER(Epilogue), vp]
-        L.ti_gemm_lds_bytes.argtypes = [i32, i32]
+        L.ti_gemm_lds_bytes.argtypes = [i32, i32, i32]
         L.ti_attn_workspace_bytes.argtypes = [i32, i32, i32, i32]
         L.ti_attn_workspace_bytes.restype = sz
         L.ti_attn_decode.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]

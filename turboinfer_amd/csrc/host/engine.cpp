@@ -141,9 +141,9 @@ struct ti_engine {
     const int cap = std::max(1, c.max_seq / 64);
     return std::max(1, std::min(sp, std::min(cap, 64)));
   }
-  int mchunk(int K) const {
+  int mchunk(int N, int K) const {
     int m = 16;
-    while (m > 1 && ti_gemm_lds_bytes(m, K) > 96 * 1024) --m;
+    while (m > 1 && ti_gemm_lds_bytes(m, N, K) > 160 * 1024) --m;
     return m;
   }
 
@@ -198,7 +198,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
   auto gemm = [&](const DevLinear& W, const void* x, int x_kind, int ldx, size_t x_elem, const float* nw,
                   ti_epilogue epi, size_t out_elem, bool last_gets_ctr) -> int {
-    const int mc = e->mchunk(W.K);
+    const int mc = e->mchunk(W.N, W.K);
     for (int m0 = 0; m0 < M; m0 += mc) {
       const int mm = std::min(mc, M - m0);
       ti_epilogue ep = epi;
@@ -206,7 +206,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
       if (ep.pos) ep.pos += m0;
       if (ep.k_cache) ep.k_cache += (size_t)m0 * ep.kv_stream_stride;
       if (ep.v_cache) ep.v_cache += (size_t)m0 * ep.kv_stream_stride;
-      if (ep.argmax) ep.argmax += m0;
+      if (ep.argmax) ep.argmax += (size_t)m0 * TI_ARGMAX_SLOTS;
       if (!(last_gets_ctr && m0 + mm >= M)) ep.step_ctr = nullptr;
       const void* xm = static_cast<const char*>(x) + (size_t)m0 * ldx * x_elem;
       TI_TRY(ti_gemm_wq_a16(W.tiles, W.scales, c.bits, xm, x_kind, ldx, nw, c.eps, mm, W.N, W.K, &ep, e->s));
@@ -310,6 +310,16 @@ int ensure_io(ti_engine* e, int in_cap, int out_cap) {
   return TI_OK;
 }
 
+// Row keys of the greedy argmax: max over each row's TI_ARGMAX_SLOTS slots.
+int read_argmax(ti_engine* e, int n, std::vector<unsigned long long>& keys) {
+  std::vector<unsigned long long> slots((size_t)n * TI_ARGMAX_SLOTS);
+  TI_TRY(ti_memcpy_d2h(slots.data(), e->argmax, slots.size() * 8, e->s));
+  keys.assign((size_t)n, 0ull);
+  for (int m = 0; m < n; ++m)
+    for (int j = 0; j < TI_ARGMAX_SLOTS; ++j) keys[m] = std::max(keys[m], slots[(size_t)m * TI_ARGMAX_SLOTS + j]);
+  return TI_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -361,7 +371,7 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
       return fail(rc);
   }
   if ((rc = e->alloc_t(&e->h, (size_t)B * H)) || (rc = e->alloc_t(&e->logits, (size_t)B * V)) ||
-      (rc = e->alloc_t(&e->argmax, (size_t)B)) || (rc = e->alloc_t(&e->pos, (size_t)B)) ||
+      (rc = e->alloc_t(&e->argmax, (size_t)B * TI_ARGMAX_SLOTS)) || (rc = e->alloc_t(&e->pos, (size_t)B)) ||
       (rc = e->alloc_t(&e->base_pos, (size_t)B)) || (rc = e->alloc_t(&e->step_ctr, (size_t)1)) ||
       (rc = e->alloc_t(&e->n_in, (size_t)B)) || (rc = ensure_io(e, 8, 8)))
     return fail(rc);
@@ -517,9 +527,9 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
   for (int s = 0; s < steps; ++s) E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
   TI_TRY(ti_stream_sync(e->s));
   std::vector<int32_t> outd((size_t)n * e->out_cap);
-  std::vector<unsigned long long> am((size_t)n);
+  std::vector<unsigned long long> am;
   TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
-  TI_TRY(ti_memcpy_d2h(am.data(), e->argmax, am.size() * 8, e->s));
+  TI_TRY(read_argmax(e, n, am));
   for (int m = 0; m < n; ++m) {
     const int produced = steps - nin[m] + 1;   // generated tokens of stream m
     for (int t = 0; t < max_new; ++t) {
@@ -594,10 +604,11 @@ int ti_engine_replay_prepare(ti_engine* e, int n, int kv_len, int start_token) {
     return ti_set_error(TI_ERR_ARG, "ti_engine_replay_prepare: n=%d kv_len=%d", n, kv_len);
   TI_TRY(ensure_io(e, 1, 1));
   std::vector<int32_t> base(n, kv_len - 1), zero(n, 0);
-  std::vector<unsigned long long> am(n, (unsigned long long)(0xFFFFFFFFu - (uint32_t)start_token));
+  std::vector<unsigned long long> am((size_t)n * TI_ARGMAX_SLOTS, 0ull);
+  for (int m = 0; m < n; ++m) am[(size_t)m * TI_ARGMAX_SLOTS] = 0xFFFFFFFFu - (uint32_t)start_token;
   TI_TRY(ti_memcpy_h2d(e->base_pos, base.data(), (size_t)n * 4, e->s));
   TI_TRY(ti_memcpy_h2d(e->n_in, zero.data(), (size_t)n * 4, e->s));
-  TI_TRY(ti_memcpy_h2d(e->argmax, am.data(), (size_t)n * 8, e->s));
+  TI_TRY(ti_memcpy_h2d(e->argmax, am.data(), am.size() * 8, e->s));
   TI_TRY(ti_memset(e->step_ctr, 0, 4, e->s));
   hipGraphExec_t g = nullptr;
   TI_TRY(get_graph(e, n, 0, &g));
@@ -619,8 +630,8 @@ int ti_engine_sync(ti_engine* e) {
 
 int ti_engine_last_tokens(ti_engine* e, int n, int32_t* tokens) {
   if (!e || !tokens || n < 1 || n > e->c.max_batch) return ti_set_error(TI_ERR_ARG, "ti_engine_last_tokens");
-  std::vector<unsigned long long> am((size_t)n);
-  TI_TRY(ti_memcpy_d2h(am.data(), e->argmax, am.size() * 8, e->s));
+  std::vector<unsigned long long> am;
+  TI_TRY(read_argmax(e, n, am));
   for (int m = 0; m < n; ++m) tokens[m] = (int32_t)(0xFFFFFFFFu - (uint32_t)(am[m] & 0xFFFFFFFFull));
   return TI_OK;
 }
@@ -664,7 +675,7 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
     if (which == 5)
       return ti_attn_decode(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, n, c.heads, c.kv_heads, c.head_dim,
                             e->splits_for(n), e->ws, e->attn, e->s);
-    const int mc = e->mchunk(W->K);
+    const int mc = e->mchunk(W->N, W->K);
     for (int m0 = 0; m0 < n; m0 += mc) {
       const int mm = std::min(mc, n - m0);
       TI_TRY(ti_gemm_wq_a16(W->tiles, W->scales, c.bits, x, xk, ldx, nw, c.eps, mm, W->N, W->K, &ep, e->s));
@@ -683,7 +694,7 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
   hipEventDestroy(a);
   hipEventDestroy(b);
   TI_TRY(rc);
-  const int launches_per = which == 5 ? 1 : (n + e->mchunk(W->K) - 1) / e->mchunk(W->K);
+  const int launches_per = which == 5 ? 1 : (n + e->mchunk(W->N, W->K) - 1) / e->mchunk(W->N, W->K);
   *avg_us = (double)ms * 1000.0 / (double)(reps * launches_per);
   if (which == 5) {
     *bytes = 2.0 * n * (double)kvd * kv_len * 2.0 + (double)n * qd * (4 + 2);

@@ -11,7 +11,8 @@
 //   hd/8 lanes hold one key row (8 fp16 = one dwordx4 each); a wave-load covers
 //   64/(hd/8) keys; every wave keeps R = 4 K loads and 4 V loads in flight.
 //   Per wave: online softmax (running max / sum, rescale by exp(m_old - m_new) once per
-//   block); waves combined through LDS; splits combined by attn_combine_kernel.
+//   block); waves combined through LDS; the splits of a (stream, kv-head) are combined
+//   in the same launch by whichever workgroup arrives last (agent-scope ticket).
 #include <math.h>
 
 #include "common.hpp"
@@ -26,6 +27,7 @@ struct AttnArgs {
   const uint16_t* vc;
   const int32_t* pos;
   float* ws;
+  int32_t* counters;
   uint16_t* out;
   int64_t stride;
   int32_t max_seq, M, heads, kv_heads, splits;
@@ -175,6 +177,10 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const AttnArgs a) {
       }
     }
     const int h = kvh * G + g;
+    if (a.splits == 1) {     // the whole sequence is ours: normalise and write out directly
+      a.out[(size_t)m * a.heads * HD + (size_t)h * HD + d] = f2h(l > 0.0f ? o / l : 0.0f);
+      continue;
+    }
     float* dst = a.ws + ((size_t)(m * a.heads + h) * a.splits + split) * row;
     dst[d] = o;
     if (d == 0) {
@@ -182,38 +188,51 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const AttnArgs a) {
       dst[HD + 1] = l;
     }
   }
-}
+  if (a.splits == 1) return;
 
-template <int HD>
-__global__ __launch_bounds__(64) void attn_combine_kernel(const AttnArgs a) {
-  constexpr int PER = HD / 64;
-  const int h = blockIdx.x, m = blockIdx.y, lane = threadIdx.x;
-  const int row = ws_row(HD);
-  const float* base = a.ws + (size_t)(m * a.heads + h) * a.splits * row;
-  float mx = -INFINITY;
-  for (int s = 0; s < a.splits; ++s) mx = fmaxf(mx, base[s * row + HD]);
-  float num[PER], den = 0.0f;
-#pragma unroll
-  for (int e = 0; e < PER; ++e) num[e] = 0.0f;
-  for (int s = 0; s < a.splits; ++s) {
-    const float ms = base[s * row + HD];
-    if (ms == -INFINITY) continue;
-    const float f = __expf(ms - mx);
-    den = fmaf(f, base[s * row + HD + 1], den);
-#pragma unroll
-    for (int e = 0; e < PER; ++e) num[e] = fmaf(f, base[s * row + lane + 64 * e], num[e]);
+  // ---- split combine, inside the launch: the last of the `splits` workgroups of this
+  // (stream, kv-head) to arrive merges all partials.  Hand-off per MI355X_MICROARCH.md
+  // "inter-workgroup visibility": every storing wave drains its stores, workgroup barrier,
+  // one lane agent-release + relaxed ticket; the last arriver agent-acquires before reading.
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int32_t* ticket = a.counters + (size_t)m * a.kv_heads + kvh;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == a.splits - 1);
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
-#pragma unroll
-  for (int e = 0; e < PER; ++e)
-    a.out[(size_t)m * a.heads * HD + (size_t)h * HD + lane + 64 * e] = f2h(num[e] / den);
+  __syncthreads();
+  if (!s_last) return;
+  for (int idx = tid; idx < G * HD; idx += 256) {
+    const int g = idx / HD, d = idx - g * HD, h = kvh * G + g;
+    const float* base = a.ws + (size_t)(m * a.heads + h) * a.splits * row;
+    float mx = -INFINITY;
+#pragma unroll 8
+    for (int s = 0; s < a.splits; ++s) mx = fmaxf(mx, base[s * row + HD]);
+    float num = 0.0f, den = 0.0f;
+#pragma unroll 8
+    for (int s = 0; s < a.splits; ++s) {
+      const float ms = base[s * row + HD];
+      const float f = ms == -INFINITY ? 0.0f : __expf(ms - mx);   // empty split: weight 0
+      den = fmaf(f, base[s * row + HD + 1], den);
+      num = fmaf(f, base[s * row + d], num);
+    }
+    a.out[(size_t)m * a.heads * HD + (size_t)h * HD + d] = f2h(num / den);
+  }
+  if (tid == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
 }
 
 template <int HD, int G>
 static int launch_attn(const AttnArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((attn_split_kernel<HD, G>), dim3(a.splits, a.kv_heads, a.M), dim3(256), 0, s, a);
   TI_LAUNCH_CHECK("attn_split_kernel");
-  hipLaunchKernelGGL(attn_combine_kernel<HD>, dim3(a.heads, a.M), dim3(64), 0, s, a);
-  TI_LAUNCH_CHECK("attn_combine_kernel");
   return TI_OK;
 }
 
@@ -230,8 +249,15 @@ static int dispatch_group(const AttnArgs& a, int G, hipStream_t s) {
 
 }  // namespace ti
 
+static size_t partial_bytes(int M, int heads, int head_dim, int splits) {
+  return ((size_t)M * heads * splits * ti::ws_row(head_dim) * sizeof(float) + 255) & ~(size_t)255;
+}
+
+// partials [M][heads][splits][head_dim + 4] fp32, then the arrival tickets [M][heads] int32
+// (sized for heads >= kv_heads); the tickets must be zero before the first call and are
+// re-armed by every call.
 extern "C" size_t ti_attn_workspace_bytes(int M, int heads, int head_dim, int splits) {
-  return (size_t)M * heads * splits * ti::ws_row(head_dim) * sizeof(float);
+  return partial_bytes(M, heads, head_dim, splits) + (size_t)M * heads * sizeof(int32_t);
 }
 
 extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
@@ -254,6 +280,7 @@ extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uin
   a.vc = v_cache;
   a.pos = pos;
   a.ws = workspace;
+  a.counters = (int32_t*)((char*)workspace + partial_bytes(M, heads, head_dim, splits));
   a.out = out;
   a.stride = kv_stream_stride;
   a.max_seq = max_seq;

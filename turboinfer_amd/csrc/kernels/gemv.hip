@@ -5,26 +5,43 @@
 // int weights' convert_dtype (:2218-2284), plus the neighbouring element-wise ops of
 // TransformerLayer::forward (src/model/inference_engine.cpp:203-233, 376-401).
 //
-// Shape of the work (M <= 16 decode rows, N outputs, K inputs):
-//   * one workgroup = 8 waves = one 16-row output tile; the waves interleave over the
-//     K/128 k-tiles (wave w takes k-tiles w, w+8, ...), each wave keeping B k-tiles of
-//     packed weights in flight as plain dwordx4 loads straight into VGPRs (weights are
-//     streamed once -- no LDS round trip, cdna_hip_programming.md "GEMV / M <= 16").
-//   * the activation row(s) are staged once per workgroup in LDS as fp16 (the rms_norm
-//     prologue is fused here), read back as MFMA A fragments with ds_read_b128.
-//   * per k-tile: 4 x v_mfma_f32_16x16x32_f16 on (x, dequantized W) then one fp32 FMA by
-//     the group scale; int4 nibbles -> fp16 with the 0x6400 magic (exact), int8 with
-//     v_perm_b32 + the same magic.
-//   * the 8 waves' partial tiles are summed in LDS in a fixed order (deterministic) and
-//     the epilogue (residual add, SiLU*up, RoPE + KV append, logits + argmax) runs on the
-//     16 x M results of the tile.
+// Shape of the work (M <= 16 decode rows, N outputs, K inputs), one launch per projection:
+//   * one 8-wave workgroup per CU streams a contiguous run of 16-row tiles; wave w owns
+//     k-tiles w, w+8, ... of every tile and keeps R items (1 KiB each for int4) of packed
+//     weights in flight as dwordx4 loads straight into VGPRs, refilled R items ahead across
+//     tile boundaries (weights are read once: no LDS round trip, cdna_hip_programming.md
+//     "GEMV / M <= 16").
+//   * everything small the workgroup needs (group scales, the activation rows, the
+//     epilogue's residual / position inputs) is loaded BEFORE the weight ring is issued,
+//     so waiting for it never drains the ring (vmcnt retires in issue order).
+//   * the activation row(s) are staged in LDS as fp16 (rms_norm fused), read back as MFMA
+//     A fragments; per item 4 x v_mfma_f32_16x16x32_f16 on (x, dequantized W) then one
+//     fp32 FMA by the group scale; int4 nibbles -> fp16 with the 0x6400 magic (exact), int8
+//     with v_perm_b32 + the same magic.
+//   * the stream loop has no branches and no barriers: each item's running partial is
+//     written to its tile's LDS slab (or a dummy slab), so the compiler schedules R items
+//     as one block; after the stream the 8 waves' partials are summed in a fixed order
+//     (deterministic) and the epilogue (residual add, SiLU*up, RoPE + KV append, logits +
+//     argmax) runs on the 16 x M results of each tile.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.hpp"
 
 namespace ti {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef TI_GEMV_EXP
+#define TI_GEMV_EXP 0   // product build; tools/probe_gemv.hip compiles diagnostic variants
+#endif
+#if TI_GEMV_EXP & 4   // diagnostic: per-workgroup phase timestamps (s_memrealtime, 100 MHz)
+__device__ unsigned long long g_gemv_ts[4096 * 8];
+#define GEMV_TS(k) \
+  do { if (threadIdx.x == 0) g_gemv_ts[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define GEMV_TS(k) do { } while (0)
+#endif
 
 constexpr int kGemvWaves = 8;
 constexpr int kGemvThreads = kGemvWaves * kWave;
@@ -41,23 +58,60 @@ struct GemvArgs {
 
 __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
 
-__host__ __device__ inline int gemv_lds_bytes(int M, int K) {
-  const int KT = K >> 7;
-  return align16(M * (K + 8) * 2) + align16(KT * 32) + kGemvWaves * kWave * 4 * 4;
+// Workgroups per launch: one 8-wave workgroup per CU (each wave keeps 64 VGPRs of packed
+// weights in flight), never more than there are 16-row tiles.
+static int g_wg_per_cu = 0;   // TI_GEMV_WG_PER_CU (tuning knob), default 1
+
+__host__ inline int gemv_grid(int N, int num_cus) {
+  if (g_wg_per_cu <= 0) {
+    const char* s = getenv("TI_GEMV_WG_PER_CU");
+    g_wg_per_cu = s && atoi(s) > 0 ? atoi(s) : 1;
+  }
+  const int NT = N >> 4;
+  const int g = g_wg_per_cu * (num_cus > 0 ? num_cus : 256);
+  return NT < g ? NT : g;
+}
+
+// LDS image of one workgroup (bytes, each region 16-aligned):
+//   x      [M][K + 8] fp16            activation rows (row pad breaks bank aliasing)
+//   scales [ntl][K/128][16] fp16      group scales of the workgroup's tiles
+//   slab   [ntl + 1][8][64] f32x4     per-wave partial tiles (+ one dummy slab)
+//   es     epilogue inputs: residual [ntl][M][16] f32, or RoPE (cos, sin) [M][hd] + pos [M]
+//   best   [16] u64                   argmax keys of the workgroup
+struct GemvLds {
+  int x, sc, slab, es, best, total;
+};
+__host__ __device__ inline GemvLds gemv_lds_layout(int M, int K, int ntl) {
+  GemvLds l;
+  l.x = 0;
+  l.sc = l.x + align16(M * (K + 8) * 2);
+  l.slab = l.sc + align16(ntl * (K >> 7) * 32);
+  l.es = l.slab + (ntl + 1) * kGemvWaves * kWave * 16;
+  const int es_bytes = ntl * M * 16 * 4 > M * 128 * 4 + 64 ? ntl * M * 16 * 4 : M * 128 * 4 + 64;
+  l.best = l.es + align16(es_bytes);
+  l.total = l.best + 16 * 8;
+  return l;
+}
+__host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_wg) {
+  return gemv_lds_layout(M, K, tiles_per_wg).total;
 }
 
 // ------------------------------------------------------------------- dequant
 // int4: word of 8 nibbles, nibble p holds element 2p, nibble p+4 element 2p+1, value q+8.
-__device__ __forceinline__ f16x8 deq_int4_word(uint32_t w) {
-  f16x8 r;
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const uint32_t t = ((w >> (4 * p)) & 0x000F000Fu) | 0x64006400u;   // fp16 1024+n, exact
-    const f16x2 h = __builtin_bit_cast(f16x2, t) - (f16x2){(f16)1032.0f, (f16)1032.0f};
-    r[2 * p] = h[0];
-    r[2 * p + 1] = h[1];
-  }
-  return r;
+// Low nibbles of each byte: (w & 0x000F000F) | 0x6400 = fp16 1024 + n, minus 1032.
+// High nibbles are used in place: (w & 0x00F000F0) | 0x6400 = fp16 1024 + 16 n, times 1/16
+// minus 72 (one fused v_pk_fma_f16).  All values are small integers: every step is exact.
+// 9 VALU ops per 8 weights (v_and_or_b32 x4, v_lshrrev x1, v_pk_add x2, v_pk_fma x2); the
+// caller keeps `magic` = 0x64006400 in a VGPR so v_and_or_b32 needs only one literal.
+__device__ __forceinline__ f16x8 deq_int4_word(uint32_t w, uint32_t magic) {
+  const f16x2 k_lo = {(f16)-1032.0f, (f16)-1032.0f}, k_sc = {(f16)0.0625f, (f16)0.0625f},
+              k_hi = {(f16)-72.0f, (f16)-72.0f};
+  const uint32_t w8 = w >> 8;
+  const f16x2 e01 = __builtin_bit_cast(f16x2, (w & 0x000F000Fu) | magic) + k_lo;
+  const f16x2 e23 = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, (w & 0x00F000F0u) | magic), k_sc, k_hi);
+  const f16x2 e45 = __builtin_bit_cast(f16x2, (w8 & 0x000F000Fu) | magic) + k_lo;
+  const f16x2 e67 = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, (w8 & 0x00F000F0u) | magic), k_sc, k_hi);
+  return (f16x8){e01[0], e01[1], e23[0], e23[1], e45[0], e45[1], e67[0], e67[1]};
 }
 // int8: 4 signed bytes in k order; (b ^ 0x80) = b + 128 -> fp16 1024 + b + 128 - 1152.
 __device__ __forceinline__ f16x2 deq_int8_pair(uint32_t t, uint32_t sel) {
@@ -74,9 +128,9 @@ __device__ __forceinline__ void deq_int8_word(uint32_t w, f16x8& r, int o) {
 }
 
 template <int BITS>
-__device__ __forceinline__ f16x8 dequant_step(const u32x4 (&w)[BITS / 4], int s4) {
+__device__ __forceinline__ f16x8 dequant_step(const u32x4 (&w)[BITS / 4], int s4, uint32_t magic) {
   if constexpr (BITS == 4) {
-    return deq_int4_word(w[0][s4]);
+    return deq_int4_word(w[0][s4], magic);
   } else if constexpr (BITS == 8) {
     f16x8 r;
     const u32x4 c = w[s4 >> 1];
@@ -89,9 +143,16 @@ __device__ __forceinline__ f16x8 dequant_step(const u32x4 (&w)[BITS / 4], int s4
 }
 
 // ------------------------------------------------------------- x staging (LDS)
-__device__ __forceinline__ void stage_x(const GemvArgs& a, f16* xl, float* red) {
+// x staging modes (chosen on the host): fp16 rows prefetched into registers; fp32 rows;
+// rms_norm of ONE row of K <= 4096 held in registers; rms_norm of several / longer rows.
+enum { XM_F16 = 0, XM_F32 = 1, XM_NORM1 = 2, XM_NORM = 3 };
+
+// Generic staging (M > 1 with rms_norm, f32 rows, or rows longer than the register
+// prefetch covers).  Runs after the ring is issued, so its loads wait behind the ring.
+template <int XM>
+__device__ __forceinline__ void stage_x_generic(const GemvArgs& a, f16* xl, float* red, int k8_from) {
   const int tid = threadIdx.x, K = a.K, xs = K + 8, K8 = K >> 3;
-  if (a.x_kind == TI_X_F32_RMSNORM) {
+  if constexpr (XM == XM_NORM || XM == XM_NORM1) {
     // rms_norm (tensor_engine.cpp:1488-1505): y = (x / sqrt(sum(x^2)/K + eps)) * w.
     for (int m = 0; m < a.M; ++m) {
       const float* xr = (const float*)a.x + (size_t)m * a.ldx;
@@ -120,7 +181,7 @@ __device__ __forceinline__ void stage_x(const GemvArgs& a, f16* xl, float* red) 
       }
       __syncthreads();   // red reused by the next row
     }
-  } else if (a.x_kind == TI_X_F32) {
+  } else if constexpr (XM == XM_F32) {
     for (int i = tid; i < a.M * K8; i += kGemvThreads) {
       const int m = i / K8, k8 = i - m * K8;
       const float* xr = (const float*)a.x + (size_t)m * a.ldx + 8 * k8;
@@ -131,7 +192,7 @@ __device__ __forceinline__ void stage_x(const GemvArgs& a, f16* xl, float* red) 
       *(f16x8*)(xl + m * xs + 8 * k8) = h;
     }
   } else {
-    for (int i = tid; i < a.M * K8; i += kGemvThreads) {
+    for (int i = tid + k8_from; i < a.M * K8; i += kGemvThreads) {
       const int m = i / K8, k8 = i - m * K8;
       *(u32x4*)(xl + m * xs + 8 * k8) = *(const u32x4*)((const f16*)a.x + (size_t)m * a.ldx + 8 * k8);
     }
@@ -144,9 +205,11 @@ __device__ __forceinline__ uint32_t float_order_key(float v) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-// Runs in waves 0..3: thread t holds y[m][n] of tile nt with l = t & 63, i = t >> 6,
-// m = 4*(l>>4) + i, n = l & 15 (the v_mfma_f32_16x16x32 C layout, reduced over waves).
-__device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int l, int i, float v) {
+// Thread (l = lane, i = wave & 3) holds y[m][n] of tile nt with m = 4*(l>>4) + i,
+// n = l & 15 (the v_mfma_f32_16x16x32 C layout, reduced over the 8 waves).  `best` is the
+// thread's running argmax key for LOGITS_ARGMAX.
+__device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int l, int i, float v, const float* es,
+                                         unsigned long long& best) {
   const ti_epilogue& e = a.epi;
   const int m = 4 * (l >> 4) + i, n = l & 15, ng = nt * 16 + n;
   const bool live = m < a.M;
@@ -157,8 +220,8 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int l, int i
     case TI_EPI_STORE_F16:
       if (live) ((uint16_t*)e.out)[(size_t)m * e.ldo + ng] = f2h(v);
       break;
-    case TI_EPI_RESID_F32:
-      if (live) ((float*)e.out)[(size_t)m * e.ldo + ng] += v;   // add(residual, y), :1626-1678
+    case TI_EPI_RESID_F32:   // add(residual, y), tensor_engine.cpp:1626-1678; residual pre-staged in LDS
+      if (live) ((float*)e.out)[(size_t)m * e.ldo + ng] = es[(tl * a.M + m) * 16 + n] + v;
       break;
     case TI_EPI_SILU_MUL_F16: {
       // compute_ffn (inference_engine.cpp:386-391): multiply(up, silu(gate)).
@@ -172,12 +235,12 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int l, int i
     case TI_EPI_QKV_ROPE_KV: {
       const float partner = __shfl_xor(v, 1, kWave);
       if (!live) break;
-      const int p = e.pos[m];
       const int hd = e.head_dim;
+      const int p = ((const int*)(es + a.M * hd))[m];
       if (ng < e.q_dim + e.kv_dim) {
         const int base = ng < e.q_dim ? 0 : e.q_dim;
         const int d = (ng - base) % hd;
-        const float2 cs = *(const float2*)(e.rope_cs + ((size_t)p * (hd >> 1) + (d >> 1)) * 2);
+        const float2 cs = *(const float2*)(es + m * hd + (d & ~1));   // (cos, sin) of pos[m], staged
         // apply_rope (tensor_engine.cpp:1602-1612): even = x*c - y*s, odd = x*s + y*c,
         // evaluated with the reference build's contraction pattern.
         const float r = (d & 1) == 0 ? fmaf(-partner, cs.y, v * cs.x) : fmaf(v, cs.x, partner * cs.y);
@@ -195,17 +258,12 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int l, int i
       break;
     }
     case TI_EPI_LOGITS_ARGMAX: {
-      if (live) ((float*)e.out)[(size_t)m * e.ldo + ng] = v;
-      unsigned long long key = live ? (((unsigned long long)float_order_key(v) << 32) |
-                                       (unsigned long long)(0xFFFFFFFFu - (uint32_t)ng))
-                                    : 0ull;
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        const unsigned long long other = __shfl_xor(key, o, kWave);
-        key = other > key ? other : key;
+      if (live) {
+        ((float*)e.out)[(size_t)m * e.ldo + ng] = v;
+        const unsigned long long key = ((unsigned long long)float_order_key(v) << 32) |
+                                       (unsigned long long)(0xFFFFFFFFu - (uint32_t)ng);
+        best = key > best ? key : best;
       }
-      if (live && n == 0) atomicMax(e.argmax + m, key);
-      if (e.step_ctr && blockIdx.x == 0 && threadIdx.x == 0) *e.step_ctr += e.advance;
       break;
     }
     default:
@@ -214,99 +272,255 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int l, int i
 }
 
 // --------------------------------------------------------------------- kernel
-template <int BITS>
-__global__ __launch_bounds__(kGemvThreads, 2) void gemv_wq_kernel(const GemvArgs a) {
+// LDS barrier that leaves the wave's outstanding global loads in flight (a plain
+// __syncthreads() may drain vmcnt): LDS writes retired, then s_barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BITS, int XM>
+__global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs a) {
   constexpr int C = TileFmt<BITS>::kChunks;
-  constexpr int B = (BITS == 16) ? 2 : 4;                      // k-tiles per wave in flight
-  constexpr int S = kGemvWaves;                                // k-tile stride between a wave's tiles
+  constexpr int R = 64 / (4 * C);                  // ring depth: 16 / 8 / 4 items (64 VGPRs of weights)
+  constexpr int XPF = 3;                           // fp16 x: 16-byte pieces prefetched per thread
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int KT = a.K >> 7, xs = a.K + 8;
-  const int nt = blockIdx.x;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  f16* xl = (f16*)smem;
-  uint16_t* sl = (uint16_t*)(smem + align16(a.M * xs * 2));
-  float* red = (float*)(smem + align16(a.M * xs * 2) + align16(KT * 32));
+  GEMV_TS(0);
+  const int KT = a.K >> 7, xs = a.K + 8, NT = a.N >> 4, K8 = a.K >> 3;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: counters live in SGPRs
+  const int t0 = (int)((int64_t)blockIdx.x * NT / gridDim.x);
+  const int t1 = (int)((int64_t)(blockIdx.x + 1) * NT / gridDim.x);
+  const int ntl = t1 - t0;
+  const int KW = wave < KT ? (KT - wave + kGemvWaves - 1) / kGemvWaves : 0;   // k-tiles per tile, this wave
+  const int total = ntl * KW;
+  const GemvLds L = gemv_lds_layout(a.M, a.K, ntl);
+  f16* xl = (f16*)(smem + L.x);
+  uint16_t* sl = (uint16_t*)(smem + L.sc);
+  f32x4* slab = (f32x4*)(smem + L.slab);           // [ntl + 1][8][64]
+  float* es = (float*)(smem + L.es);
+  unsigned long long* best_l = (unsigned long long*)(smem + L.best);
+  float* red = (float*)(smem + L.slab);            // norm reduction scratch (before the stream)
 
-  // Issue the first weight batch before anything else so HBM latency overlaps the
-  // x / scale staging.  Out-of-range k-tiles re-load the last tile (no branch around
-  // the loads; their compute is skipped).
-  const u32x4* tb = a.tiles + (size_t)nt * KT * (kWave * C);
-  u32x4 cur[B][C];
+  // ---- 1. small inputs into registers, ahead of the ring
+  const int n_sc = BITS == 16 ? 0 : ntl * KT * 2;  // u32x4 pieces of scales
+  const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16);
+  u32x4 sc_reg = {0u, 0u, 0u, 0u};
+  if constexpr (BITS != 16) sc_reg = sg[tid < n_sc ? tid : 0];
+
+  const int nx16 = a.M * K8;
+  float4 v0, v1, w0, w1;
+  u32x4 xr16[XPF];
+  if constexpr (XM == XM_NORM1) {
+    const int k8 = tid < K8 ? tid : K8 - 1;
+    const float* xr = (const float*)a.x;
+    v0 = *(const float4*)(xr + 8 * k8);
+    v1 = *(const float4*)(xr + 8 * k8 + 4);
+    w0 = *(const float4*)(a.norm_w + 8 * k8);
+    w1 = *(const float4*)(a.norm_w + 8 * k8 + 4);
+  } else if constexpr (XM == XM_F16) {
 #pragma unroll
-  for (int i = 0; i < B; ++i) {
-    const int kt = min(wave + i * S, KT - 1);
+    for (int q = 0; q < XPF; ++q) {
+      const int i = tid + q * kGemvThreads < nx16 ? tid + q * kGemvThreads : nx16 - 1;
+      const int m = i / K8, k8 = i - m * K8;
+      xr16[q] = *(const u32x4*)((const f16*)a.x + (size_t)m * a.ldx + 8 * k8);
+    }
+  }
+  // Epilogue input, one word per thread, loaded unconditionally (a branch here would make
+  // the compiler wait at the join): a residual element of our tiles, this step's position
+  // of row tid, or a dummy word of x.
+  const int n_res = a.epi.kind == TI_EPI_RESID_F32 ? ntl * a.M * 16 : 0;
+  const float* pre_p;
+  {
+    const int idx = tid < n_res ? tid : 0;
+    const int tl = idx / (a.M * 16), rem = idx - tl * a.M * 16, m = rem >> 4, n = rem & 15;
+    const float* rp = (const float*)a.epi.out + (size_t)m * a.epi.ldo + (t0 + tl) * 16 + n;
+    const float* pp = (const float*)a.epi.pos + (tid < a.M ? tid : 0);
+    pre_p = a.epi.kind == TI_EPI_RESID_F32 ? rp : a.epi.kind == TI_EPI_QKV_ROPE_KV ? pp : (const float*)a.x;
+  }
+  const float pre = *pre_p;
+
+  // ---- 2. the weight ring.  Item j of this wave = (tile j / KW, k-tile wave + 8 * (j % KW));
+  // items past the end re-load the last item (no branch around loads); coordinates advance
+  // by counters (no integer division in the stream).
+  const u32x4* tb = a.tiles + (size_t)t0 * KT * (kWave * C) + lane;
+  const size_t last_off = total > 0 ? ((size_t)(ntl - 1) * KT + wave + kGemvWaves * (KW - 1)) * (kWave * C) : 0;
+  int rt = 0, rk = 0, rj = 0;                      // refill cursor: tile, k index, item
+  auto refill_off = [&]() -> size_t {
+    const size_t o = rj < total ? ((size_t)rt * KT + wave + kGemvWaves * rk) * (kWave * C) : last_off;
+    ++rj;
+    if (++rk == KW) { rk = 0; ++rt; }
+    return o;
+  };
+  u32x4 ring[R][C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) cur[i][c] = tb[((size_t)kt * C + c) * kWave + lane];
+  for (int s = 0; s < R; ++s) {
+    const size_t o = refill_off();
+#pragma unroll
+    for (int c = 0; c < C; ++c) ring[s][c] = tb[o + c * kWave];
   }
 
+  GEMV_TS(1);
+  // ---- 3. stage scales and x in LDS (waits only for the loads of step 1)
   if constexpr (BITS != 16) {
-    const u32x4* sg = (const u32x4*)(a.scales + (size_t)nt * KT * 16);
-    for (int i = tid; i < KT * 2; i += kGemvThreads) ((u32x4*)sl)[i] = sg[i];
+    if (tid < n_sc) ((u32x4*)sl)[tid] = sc_reg;
   }
-  stage_x(a, xl, red);
-  __syncthreads();
+  if constexpr (XM == XM_NORM1) {
+    // rms_norm (tensor_engine.cpp:1488-1505) of the single row, x and w held in registers.
+    float ss = 0.0f;
+    if (tid < K8) {
+      ss = fmaf(v0.x, v0.x, ss); ss = fmaf(v0.y, v0.y, ss); ss = fmaf(v0.z, v0.z, ss); ss = fmaf(v0.w, v0.w, ss);
+      ss = fmaf(v1.x, v1.x, ss); ss = fmaf(v1.y, v1.y, ss); ss = fmaf(v1.z, v1.z, ss); ss = fmaf(v1.w, v1.w, ss);
+    }
+    ss = wave_sum_xor<kWave>(ss);
+    if (lane == 0) red[wave] = ss;
+    lds_barrier();
+    float tot = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kGemvWaves; ++w) tot += red[w];
+    const float rms = sqrtf(tot / (float)a.K + a.eps);
+    if (tid < K8) {
+      f16x8 h;
+      h[0] = (f16)((v0.x / rms) * w0.x); h[1] = (f16)((v0.y / rms) * w0.y);
+      h[2] = (f16)((v0.z / rms) * w0.z); h[3] = (f16)((v0.w / rms) * w0.w);
+      h[4] = (f16)((v1.x / rms) * w1.x); h[5] = (f16)((v1.y / rms) * w1.y);
+      h[6] = (f16)((v1.z / rms) * w1.z); h[7] = (f16)((v1.w / rms) * w1.w);
+      *(f16x8*)(xl + 8 * tid) = h;
+    }
+  } else if constexpr (XM == XM_F16) {
+#pragma unroll
+    for (int q = 0; q < XPF; ++q) {
+      const int i = tid + q * kGemvThreads;
+      if (i < nx16) {
+        const int m = i / K8, k8 = i - m * K8;
+        *(u32x4*)(xl + m * xs + 8 * k8) = xr16[q];
+      }
+    }
+  }
+  // rare shapes: what the register prefetch did not cover (these loads wait behind the ring)
+  if constexpr (BITS != 16) {
+    for (int i = tid + kGemvThreads; i < n_sc; i += kGemvThreads) ((u32x4*)sl)[i] = sg[i];
+  }
+  if constexpr (XM == XM_F16) {
+    if (nx16 > XPF * kGemvThreads) stage_x_generic<XM>(a, xl, red, XPF * kGemvThreads);
+  } else if constexpr (XM != XM_NORM1) {
+    stage_x_generic<XM>(a, xl, red, 0);
+  }
+  if (a.epi.kind == TI_EPI_QKV_ROPE_KV && tid < a.M) ((int*)(es + a.M * a.epi.head_dim))[tid] = __builtin_bit_cast(int, pre);
+  if (tid < 16) best_l[tid] = 0ull;
+  lds_barrier();
 
+  // RoPE (cos, sin) of each row's position: issued now, consumed after the stream.
+  float cs_reg = 0.0f;
+  const int n_cs = a.epi.kind == TI_EPI_QKV_ROPE_KV ? a.M * a.epi.head_dim : 0;
+  if (n_cs > 0) {
+    const int hd = a.epi.head_dim, idx = tid < n_cs ? tid : 0, m = idx / hd, j = idx - m * hd;
+    cs_reg = a.epi.rope_cs[(size_t)((const int*)(es + a.M * hd))[m] * hd + j];
+  }
+
+  GEMV_TS(2);
+  // ---- 4. the stream: branch-free, R items per block
   const int r = lane & 15, kq = lane >> 4;
   const f16* xrow = xl + (r < a.M ? r : a.M - 1) * xs + kq * 32;
   f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int kb = wave; kb < KT; kb += B * S) {
-    const int kn = kb + B * S;
-    const bool more = kn < KT;
-    u32x4 nxt[B][C];
-    if (more) {
+  uint32_t magic;   // 0x64006400 in a VGPR (see deq_int4_word)
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
+  f32x4* my_slab = slab + wave * kWave + lane;     // + tile * 8 * 64
+  constexpr int kSlabStride = kGemvWaves * kWave;
+  int ct = 0, ck = 0;                              // compute cursor: tile, k index
+  auto item = [&](const u32x4 (&w)[C]) {
+    const int kt = wave + kGemvWaves * ck;
+    f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
+    if constexpr (BITS == 16) t = acc;
+#if TI_GEMV_EXP & 1   // diagnostic build (tools/probe_gemv.hip): stream only, no dequant / MFMA
+    t[0] += __builtin_bit_cast(float, w[0][0] ^ w[0][1] ^ w[0][2] ^ w[0][3]) + (float)xrow[kt];
+#else
 #pragma unroll
-      for (int i = 0; i < B; ++i) {
-        const int kt = min(kn + i * S, KT - 1);
-#pragma unroll
-        for (int c = 0; c < C; ++c) nxt[i][c] = tb[((size_t)kt * C + c) * kWave + lane];
-      }
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const f16x8 bf = dequant_step<BITS>(w, s4, magic);
+      const f16x8 af = *(const f16x8*)(xrow + kt * 128 + s4 * 8);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, t, 0, 0, 0);
     }
-#pragma unroll
-    for (int i = 0; i < B; ++i) {
-      const int kt = kb + i * S;
-      if (kt < KT) {
-        f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
-        if constexpr (BITS == 16) t = acc;
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const f16x8 bf = dequant_step<BITS>(cur[i], s4);
-          const f16x8 af = *(const f16x8*)(xrow + kt * 128 + s4 * 8);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, t, 0, 0, 0);
-        }
-        if constexpr (BITS == 16) {
-          acc = t;
-        } else {
-          const float sc = h2f(sl[kt * 16 + r]);
-          acc[0] = fmaf(sc, t[0], acc[0]);
-          acc[1] = fmaf(sc, t[1], acc[1]);
-          acc[2] = fmaf(sc, t[2], acc[2]);
-          acc[3] = fmaf(sc, t[3], acc[3]);
-        }
-      }
+#endif
+    if constexpr (BITS == 16) {
+      acc = t;
+    } else {
+      const float sc = h2f(sl[(ct * KT + kt) * 16 + r]);
+      acc[0] = fmaf(sc, t[0], acc[0]);
+      acc[1] = fmaf(sc, t[1], acc[1]);
+      acc[2] = fmaf(sc, t[2], acc[2]);
+      acc[3] = fmaf(sc, t[3], acc[3]);
     }
-    if (more) {
+    // the tile's last item lands in its slab, every other item in the dummy slab
+    const bool last = ++ck == KW;
+    my_slab[(last ? ct : ntl) * kSlabStride] = acc;
+    if (last) acc = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    ck = last ? 0 : ck;
+    ct += last ? 1 : 0;
+  };
+  int j0 = 0;
+  for (; j0 + R <= total; j0 += R) {   // full blocks: no branches, R items scheduled together
 #pragma unroll
-      for (int i = 0; i < B; ++i)
+    for (int s = 0; s < R; ++s) {
+      item(ring[s]);
+      const size_t o = refill_off();   // refill this slot R items ahead (clamped past the end)
 #pragma unroll
-        for (int c = 0; c < C; ++c) cur[i][c] = nxt[i][c];
+      for (int c = 0; c < C; ++c) ring[s][c] = tb[o + c * kWave];
     }
   }
+#pragma unroll
+  for (int s = 0; s < R; ++s)          // tail: the last total % R items, nothing refilled
+    if (j0 + s < total) item(ring[s]);
+  if (KW == 0)   // K < 8*128: this wave owns no k-tiles; its partials are zero
+    for (int tl = 0; tl < ntl; ++tl) my_slab[tl * kSlabStride] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 
-  // Cross-wave reduction in a fixed order, then the epilogue on waves 0..3.
-  *(f32x4*)(red + (wave * kWave + lane) * 4) = acc;
-  __syncthreads();
-  if (tid < 4 * kWave) {
-    const int l = tid & 63, i = tid >> 6;
+  GEMV_TS(3);
+  // ---- 5. epilogue inputs into LDS, reduce the 8 partials per tile, epilogue
+  if (tid < n_res) es[tid] = pre;
+  if (tid < n_cs) es[tid] = cs_reg;
+  lds_barrier();
+  unsigned long long best = 0ull;
+  const int i4 = wave & 3;
+  for (int tl = wave >> 2; tl < ntl; tl += 2) {
+    const float* sp = (const float*)(slab + tl * kSlabStride + lane) + i4;
     float v = 0.0f;
 #pragma unroll
-    for (int w = 0; w < kGemvWaves; ++w) v += red[(w * kWave + l) * 4 + i];
-    epilogue(a, nt, l, i, v);
+    for (int w = 0; w < kGemvWaves; ++w) v += sp[w * kWave * 4];
+    epilogue(a, t0 + tl, tl, lane, i4, v, es, best);
   }
+  if (a.epi.kind == TI_EPI_LOGITS_ARGMAX) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const unsigned long long other = __shfl_xor(best, o, kWave);
+      best = other > best ? other : best;
+    }
+    const int m = 4 * (lane >> 4) + i4;
+    if ((lane & 15) == 0 && m < a.M && best) atomicMax(best_l + m, best);
+    lds_barrier();
+    if (tid < a.M && best_l[tid])
+      atomicMax(a.epi.argmax + (size_t)tid * TI_ARGMAX_SLOTS + (blockIdx.x & (TI_ARGMAX_SLOTS - 1)), best_l[tid]);
+    if (a.epi.step_ctr && blockIdx.x == 0 && tid == 0) *a.epi.step_ctr += a.epi.advance;
+  }
+  GEMV_TS(4);
+}
+
+static int g_num_cus = 0;
+
+__host__ inline int gemv_xmode(int x_kind, int M, int K) {
+  if (x_kind == TI_X_F16) return XM_F16;
+  if (x_kind == TI_X_F32) return XM_F32;
+  return M == 1 && (K >> 3) <= kGemvThreads ? XM_NORM1 : XM_NORM;
 }
 
 template <int BITS>
-static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s) {
-  hipLaunchKernelGGL(gemv_wq_kernel<BITS>, dim3(a.N / 16), dim3(kGemvThreads), lds, s, a);
+static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid) {
+  switch (gemv_xmode(a.x_kind, a.M, a.K)) {
+    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16>), dim3(grid), dim3(kGemvThreads), lds, s, a); break;
+    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32>), dim3(grid), dim3(kGemvThreads), lds, s, a); break;
+    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1>), dim3(grid), dim3(kGemvThreads), lds, s, a); break;
+    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM>), dim3(grid), dim3(kGemvThreads), lds, s, a); break;
+  }
   TI_LAUNCH_CHECK("gemv_wq_kernel");
   return TI_OK;
 }
@@ -316,20 +530,41 @@ static bool g_prepared = false;
 }  // namespace ti
 
 // Raise the dynamic-LDS cap of the GEMM instantiations (call before any stream capture).
+static int query_cus() {
+  if (ti::g_num_cus <= 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      ti::g_num_cus = n;
+    else
+      ti::g_num_cus = 256;
+  }
+  return ti::g_num_cus;
+}
+
 extern "C" int ti_gemm_prepare(void) {
   using namespace ti;
+  query_cus();
   if (g_prepared) return TI_OK;
-  TI_HIP_CHECK(hipFuncSetAttribute((const void*)gemv_wq_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   160 * 1024), "hipFuncSetAttribute(gemv<4>)");
-  TI_HIP_CHECK(hipFuncSetAttribute((const void*)gemv_wq_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   160 * 1024), "hipFuncSetAttribute(gemv<8>)");
-  TI_HIP_CHECK(hipFuncSetAttribute((const void*)gemv_wq_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   160 * 1024), "hipFuncSetAttribute(gemv<16>)");
+  const void* fns[] = {
+      (const void*)gemv_wq_kernel<4, XM_F16>,  (const void*)gemv_wq_kernel<4, XM_F32>,
+      (const void*)gemv_wq_kernel<4, XM_NORM1>, (const void*)gemv_wq_kernel<4, XM_NORM>,
+      (const void*)gemv_wq_kernel<8, XM_F16>,  (const void*)gemv_wq_kernel<8, XM_F32>,
+      (const void*)gemv_wq_kernel<8, XM_NORM1>, (const void*)gemv_wq_kernel<8, XM_NORM>,
+      (const void*)gemv_wq_kernel<16, XM_F16>, (const void*)gemv_wq_kernel<16, XM_F32>,
+      (const void*)gemv_wq_kernel<16, XM_NORM1>, (const void*)gemv_wq_kernel<16, XM_NORM>};
+  for (const void* f : fns)
+    TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
+                 "hipFuncSetAttribute(gemv_wq_kernel)");
   g_prepared = true;
   return TI_OK;
 }
 
-extern "C" int ti_gemm_lds_bytes(int M, int K) { return ti::gemv_lds_bytes(M, K); }
+extern "C" int ti_gemm_lds_bytes(int M, int N, int K) {
+  if (M < 1 || N < 16 || K < 128) return 0;
+  const int NT = N >> 4, grid = ti::gemv_grid(N, query_cus());
+  return ti::gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid);
+}
 
 extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x,
                               int x_kind, int ldx, const float* norm_w, float eps, int M, int N, int K,
@@ -354,7 +589,7 @@ extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bit
       if (epi->ldo < N / 2) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: ldo < N/2");
       break;
     case TI_EPI_QKV_ROPE_KV:
-      if (!epi->pos || !epi->rope_cs || !epi->k_cache || !epi->v_cache || epi->head_dim <= 0 ||
+      if (!epi->pos || !epi->rope_cs || !epi->k_cache || !epi->v_cache || epi->head_dim <= 0 || epi->head_dim > 128 ||
           (epi->head_dim & 1) || epi->q_dim + 2 * epi->kv_dim != N || epi->q_dim % epi->head_dim ||
           epi->kv_dim % epi->head_dim || epi->ldo < epi->q_dim)
         return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: inconsistent QKV epilogue");
@@ -365,7 +600,8 @@ extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bit
     default:
       return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: unknown epilogue %d", epi->kind);
   }
-  const int lds = gemv_lds_bytes(M, K);
+  const int grid = gemv_grid(N, query_cus());
+  const int lds = gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid);
   if (lds > 160 * 1024)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: M*K too large for one LDS stage (M=%d K=%d)", M, K);
   if (lds > 64 * 1024 && !g_prepared) {
@@ -385,7 +621,7 @@ extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bit
   a.K = K;
   a.epi = *epi;
   hipStream_t s = (hipStream_t)stream;
-  if (bits == 4) return launch_gemv<4>(a, lds, s);
-  if (bits == 8) return launch_gemv<8>(a, lds, s);
-  return launch_gemv<16>(a, lds, s);
+  if (bits == 4) return launch_gemv<4>(a, lds, s, grid);
+  if (bits == 8) return launch_gemv<8>(a, lds, s, grid);
+  return launch_gemv<16>(a, lds, s, grid);
 }

@@ -14,20 +14,30 @@ __global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a) {
   const int m = blockIdx.x, tid = threadIdx.x;
   const int s = *a.step_ctr;
   const int nin = a.n_in ? a.n_in[m] : 0;
+  unsigned long long* am = a.argmax + (size_t)m * TI_ARGMAX_SLOTS;
+  unsigned long long key = 0ull;
+  if (tid < 64) {   // row m's key = max over its slots (wave 0)
+    key = tid < TI_ARGMAX_SLOTS ? am[tid] : 0ull;
+#pragma unroll
+    for (int o = 1; o < TI_ARGMAX_SLOTS; o <<= 1) {
+      const unsigned long long other = __shfl_xor(key, o, 64);
+      key = other > key ? other : key;
+    }
+  }
   if (tid == 0) {
     int tok;
     if (s < nin) {
       tok = a.in_tokens[(size_t)m * a.in_stride + s];
     } else {
-      tok = (int)(0xFFFFFFFFu - (uint32_t)(a.argmax[m] & 0xFFFFFFFFull));
+      tok = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
       if (a.out_tokens && s - nin < a.out_stride) a.out_tokens[(size_t)m * a.out_stride + (s - nin)] = tok;
     }
     if (tok < 0 || tok >= a.vocab) tok = 0;     // never index outside the table
     s_tok = tok;
     a.pos[m] = a.base_pos[m] + s;
-    a.argmax[m] = 0ull;
   }
-  __syncthreads();
+  __syncthreads();   // every slot read before any is cleared
+  if (tid < TI_ARGMAX_SLOTS) am[tid] = 0ull;
   float* h = a.h + (size_t)m * a.hidden;
   if (a.placeholder_first >= 0) {
     // forward_pass / forward_pass_incremental placeholder rows (inference_engine.cpp:1444-1448,
