@@ -163,8 +163,14 @@ int ti_gemm_prepare(void);
  * q fp32 [M][heads*head_dim]; stream m attends to cache slots [0, pos[m]] of layer cache
  * k_cache/v_cache ([stream][kv_head][max_seq][head_dim], stream stride kv_stream_stride).
  * Split-K over the sequence (flash-decoding): `splits` partial (max, sum, o) per
- * (stream, head) in workspace, then a combine pass writes fp16 out [M][heads*head_dim].
- * head_dim 64 or 128; heads/kv_heads in {1, 2, 4, 8}. */
+ * (stream, head) in workspace, merged in the same launch by the last-arriving split, which
+ * writes fp16 out [M][heads*head_dim].
+ * head_dim 64 or 128; heads/kv_heads in {1, 2, 4, 8}; M <= TI_ATTN_MAX_M.
+ * The workspace (ti_attn_workspace_bytes, for the largest M and splits the caller will use)
+ * must be zeroed once before the first call; calls keep its ticket region re-armed.  splits
+ * only shapes the work (results agree to rounding) and is capped by what one workgroup can
+ * merge in LDS. */
+#define TI_ATTN_MAX_M 256
 size_t ti_attn_workspace_bytes(int M, int heads, int head_dim, int splits);
 int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
                    int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,

@@ -136,7 +136,9 @@ struct ti_engine {
   }
   int splits_for(int M) const {
     if (c.attn_splits > 0) return c.attn_splits;
-    const int target = 512;
+    // one 8-wave attention workgroup per CU: a second round of workgroups costs a whole
+    // workgroup latency (load, merge hand-off) for little bandwidth (tools/probe_attn.hip)
+    const int target = 256;
     int sp = (target + c.kv_heads * M - 1) / (c.kv_heads * M);
     const int cap = std::max(1, c.max_seq / 64);
     return std::max(1, std::min(sp, std::min(cap, 64)));

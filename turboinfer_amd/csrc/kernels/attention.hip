@@ -5,15 +5,22 @@
 // s_j = (q . k_j) / sqrt(hd), p = softmax(s), o = sum_j p_j v_j.  GQA maps q-head h to
 // kv-head h / (heads / kv_heads) (the reference has no GQA; the oracle expands heads).
 //
-// Bandwidth-bound (2 * L * hd * 2 bytes of K/V per kv-head per stream): no MFMA.
-//   grid (splits, kv_heads, M); a workgroup = 4 waves owns keys [s0, s1) of one
+// HBM-bound (2 * L * hd * 2 bytes of K/V per kv-head per stream), no MFMA:
+//   grid (splits, kv_heads, M); a workgroup = 8 waves owns keys [s0, s1) of one
 //   (stream, kv-head) and ALL q-heads of its group, so each K/V byte is read once.
-//   hd/8 lanes hold one key row (8 fp16 = one dwordx4 each); a wave-load covers
-//   64/(hd/8) keys; every wave keeps R = 4 K loads and 4 V loads in flight.
-//   Per wave: online softmax (running max / sum, rescale by exp(m_old - m_new) once per
-//   block); waves combined through LDS; the splits of a (stream, kv-head) are combined
-//   in the same launch by whichever workgroup arrives last (agent-scope ticket).
+//   hd/8 lanes hold one key row (8 fp16 = one dwordx4); a wave-load covers 64/(hd/8)
+//   keys ("slot"); wave w takes slots w, w+8, ... and keeps R of them (K and V) in flight
+//   in a register ring refilled R slots ahead (the GEMV's streaming scheme).
+//   Softmax is online PER LANE GROUP (one key row per group and slot): running max, sum
+//   and o-accumulator live in the group's lanes, so the stream needs no cross-group
+//   reduction; groups, then waves (LDS), then splits are merged at the end.
+//   Splits of a (stream, kv-head) are merged in the same launch by the workgroup that
+//   arrives last: partials are stored write-through (sc1) and drained, one lane adds to
+//   the arrival ticket, the last arriver reads them back with sc1 loads
+//   (MI355X_MICROARCH.md "Hand-offs measured with sc1 loads"; no L2 write-back fence).
 #include <math.h>
+
+#include <algorithm>
 
 #include "common.hpp"
 
@@ -34,6 +41,9 @@ struct AttnArgs {
   float scale;
 };
 
+constexpr int kAttnWaves = 8;
+constexpr int kAttnThreads = kAttnWaves * kWave;
+
 __host__ __device__ inline int ws_row(int hd) { return hd + 4; }
 
 __device__ __forceinline__ void unpack8(const u32x4 v, float (&f)[8]) {
@@ -48,31 +58,60 @@ __device__ __forceinline__ void unpack8(const u32x4 v, float (&f)[8]) {
   }
 }
 
+// Write-through (sc1) 16-byte buffer store / load for the split hand-off (aux bit 4 = sc1
+// on gfx950); builtins, so the compiler counts them for its waitcnts.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ws_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
+}
+constexpr int kAuxSc1 = 16;
+
+// Largest split count whose partials (splits x G rows of hd + 4 floats) the merging
+// workgroup can stage in its 48 KiB LDS buffer.
+__host__ __device__ constexpr int attn_max_splits(int G, int HD) { return (48 * 1024) / (G * (HD + 4) * 4); }
+
 template <int HD, int G>
-__global__ __launch_bounds__(256) void attn_split_kernel(const AttnArgs a) {
+__global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnArgs a) {
   constexpr int LPK = HD / 8;       // lanes per key row
-  constexpr int KPW = 64 / LPK;     // keys per wave-load
-  constexpr int R = 4;              // wave-loads in flight per operand
-  constexpr int KPB = 4 * KPW * R;  // keys per workgroup block
-  __shared__ float s_m[4][G], s_l[4][G];
-  __shared__ __attribute__((aligned(16))) float s_acc[4][G][HD];
+  constexpr int KPW = 64 / LPK;     // keys per slot (wave-load)
+  constexpr int R = 8;              // slots in flight per operand
+  __shared__ float s_m[kAttnWaves][G], s_l[kAttnWaves][G];
+  __shared__ __attribute__((aligned(16))) float s_acc[kAttnWaves][G][HD];
+  __shared__ __attribute__((aligned(16))) float s_part[48 * 1024 / 4];   // merged rows, then all partials
+  __shared__ int s_last;
 
   const int split = blockIdx.x, kvh = blockIdx.y, m = blockIdx.z;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int dl = lane % LPK, kg = lane / LPK;
   const int L = a.pos[m] + 1;
   const int chunk = (L + a.splits - 1) / a.splits;
   const int s0 = split * chunk, s1 = min(L, s0 + chunk);
-  const uint16_t* kb = a.kc + (int64_t)m * a.stride + (int64_t)kvh * a.max_seq * HD + dl * 8;
-  const uint16_t* vb = a.vc + (int64_t)m * a.stride + (int64_t)kvh * a.max_seq * HD + dl * 8;
+  const int nslot = s1 > s0 ? (s1 - s0 + KPW - 1) / KPW : 0;               // slots of the chunk
+  const int total = wave < nslot ? (nslot - wave + kAttnWaves - 1) / kAttnWaves : 0;   // this wave's
+  const int64_t base = (int64_t)m * a.stride + (int64_t)kvh * a.max_seq * HD + dl * 8;
+  const uint16_t* kb = a.kc + base;
+  const uint16_t* vb = a.vc + base;
+
+  // the K/V ring first (nothing else to wait for), then q
+  int rj = 0;
+  auto slot_key = [&](int i) { return s0 + (wave + kAttnWaves * i) * KPW + kg; };
+  u32x4 kr[R], vr[R];
+  auto refill = [&](int s) {
+    const int key = min(slot_key(rj < total ? rj : max(total - 1, 0)), max(s1 - 1, 0));
+    ++rj;
+    kr[s] = *(const u32x4*)(kb + (int64_t)key * HD);
+    vr[s] = *(const u32x4*)(vb + (int64_t)key * HD);
+  };
+#pragma unroll
+  for (int s = 0; s < R; ++s) refill(s);
 
   float q[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const float* qp = a.q + (size_t)m * a.heads * HD + (size_t)(kvh * G + g) * HD + dl * 8;
     const float4 q0 = *(const float4*)qp, q1 = *(const float4*)(qp + 4);
-    q[g][0] = q0.x; q[g][1] = q0.y; q[g][2] = q0.z; q[g][3] = q0.w;
-    q[g][4] = q1.x; q[g][5] = q1.y; q[g][6] = q1.z; q[g][7] = q1.w;
+    q[g][0] = q0.x * a.scale; q[g][1] = q0.y * a.scale; q[g][2] = q0.z * a.scale; q[g][3] = q0.w * a.scale;
+    q[g][4] = q1.x * a.scale; q[g][5] = q1.y * a.scale; q[g][6] = q1.z * a.scale; q[g][7] = q1.w * a.scale;
   }
   float mrun[G], lrun[G], acc[G][8];
 #pragma unroll
@@ -83,69 +122,61 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const AttnArgs a) {
     for (int e = 0; e < 8; ++e) acc[g][e] = 0.0f;
   }
 
-  for (int blk = s0; blk < s1; blk += KPB) {
-    u32x4 kr[R], vr[R];
-    int jr[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      jr[r] = blk + (r * 4 + wave) * KPW + kg;
-      const int jc = min(jr[r], s1 - 1);            // always a valid slot; masked below
-      kr[r] = *(const u32x4*)(kb + (int64_t)jc * HD);
-      vr[r] = *(const u32x4*)(vb + (int64_t)jc * HD);
-    }
-    float sc[G][R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      float kf[8];
-      unpack8(kr[r], kf);
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        float d = 0.0f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d = fmaf(q[g][e], kf[e], d);
-        d = wave_sum_xor<LPK>(d);
-        sc[g][r] = jr[r] < s1 ? d * a.scale : -INFINITY;
-      }
-    }
+  int ci = 0;   // compute cursor (slot index of this wave)
+  auto consume = [&](const u32x4& kv, const u32x4& vv) {
+    const bool valid = slot_key(ci) < s1;
+    ++ci;
+    float kf[8], vf[8];
+    unpack8(kv, kf);
+    unpack8(vv, vf);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      float bm = sc[g][0];
+      float d = 0.0f;
 #pragma unroll
-      for (int r = 1; r < R; ++r) bm = fmaxf(bm, sc[g][r]);
-#pragma unroll
-      for (int o = LPK; o < 64; o <<= 1) bm = fmaxf(bm, __shfl_xor(bm, o, kWave));
-      const float mn = fmaxf(mrun[g], bm);
-      if (mn == -INFINITY) continue;                 // wave-uniform: nothing valid yet
-      const float alpha = __expf(mrun[g] - mn);
-      float p[R], ps = 0.0f;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        p[r] = __expf(sc[g][r] - mn);
-        ps += p[r];
-      }
-#pragma unroll
-      for (int o = LPK; o < 64; o <<= 1) ps += __shfl_xor(ps, o, kWave);
-      lrun[g] = lrun[g] * alpha + ps;
+      for (int e = 0; e < 8; ++e) d = fmaf(q[g][e], kf[e], d);
+      d = wave_sum_xor<LPK>(d);
+      const float sc = valid ? d : -INFINITY;
+      const float mn = fmaxf(mrun[g], sc);
+      const float alpha = mrun[g] == mn ? 1.0f : __expf(mrun[g] - mn);
+      const float p = valid ? __expf(sc - mn) : 0.0f;
+      lrun[g] = fmaf(lrun[g], alpha, p);
       mrun[g] = mn;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[g][e] *= alpha;
+      for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(p, vf[e], acc[g][e] * alpha);
+    }
+  };
+  int j0 = 0;
+  for (; j0 + R <= total; j0 += R) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        float vf[8];
-        unpack8(vr[r], vf);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(p[r], vf[e], acc[g][e]);
-      }
+    for (int s = 0; s < R; ++s) {
+      consume(kr[s], vr[s]);
+      refill(s);
     }
   }
+#pragma unroll
+  for (int s = 0; s < R; ++s)
+    if (j0 + s < total) consume(kr[s], vr[s]);
 
-  // sum the per-lane partials over the key groups of the wave
+  // merge the lane groups of the wave (each holds its own max / sum / o)
 #pragma unroll
-  for (int g = 0; g < G; ++g)
+  for (int g = 0; g < G; ++g) {
+    float mx = mrun[g];
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
+    for (int o = LPK; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, kWave));
+    const float f = mrun[g] == -INFINITY ? 0.0f : __expf(mrun[g] - mx);
+    float l = lrun[g] * f;
 #pragma unroll
-      for (int o = LPK; o < 64; o <<= 1) acc[g][e] += __shfl_xor(acc[g][e], o, kWave);
+    for (int o = LPK; o < 64; o <<= 1) l += __shfl_xor(l, o, kWave);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = acc[g][e] * f;
+#pragma unroll
+      for (int o = LPK; o < 64; o <<= 1) v += __shfl_xor(v, o, kWave);
+      acc[g][e] = v;
+    }
+    mrun[g] = mx;
+    lrun[g] = l;
+  }
   if (lane < LPK) {
 #pragma unroll
     for (int g = 0; g < G; ++g)
@@ -160,18 +191,19 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const AttnArgs a) {
     }
   }
   __syncthreads();
+
+  // merge the waves; one thread per (q-head of the group, dim)
   const int row = ws_row(HD);
-  for (int idx = tid; idx < G * HD; idx += 256) {
+  for (int idx = tid; idx < G * HD; idx += kAttnThreads) {
     const int g = idx / HD, d = idx - g * HD;
     float mx = s_m[0][g];
 #pragma unroll
-    for (int w = 1; w < 4; ++w) mx = fmaxf(mx, s_m[w][g]);
+    for (int w = 1; w < kAttnWaves; ++w) mx = fmaxf(mx, s_m[w][g]);
     float o = 0.0f, l = 0.0f;
     if (mx != -INFINITY) {
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        if (s_m[w][g] == -INFINITY) continue;
-        const float f = __expf(s_m[w][g] - mx);
+      for (int w = 0; w < kAttnWaves; ++w) {
+        const float f = s_m[w][g] == -INFINITY ? 0.0f : __expf(s_m[w][g] - mx);
         o = fmaf(f, s_acc[w][g][d], o);
         l = fmaf(f, s_l[w][g], l);
       }
@@ -181,48 +213,58 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const AttnArgs a) {
       a.out[(size_t)m * a.heads * HD + (size_t)h * HD + d] = f2h(l > 0.0f ? o / l : 0.0f);
       continue;
     }
-    float* dst = a.ws + ((size_t)(m * a.heads + h) * a.splits + split) * row;
-    dst[d] = o;
+    s_part[g * row + d] = o;   // this split's row [o | max, sum, 0, 0]
     if (d == 0) {
-      dst[HD] = mx;
-      dst[HD + 1] = l;
+      s_part[g * row + HD] = mx;
+      s_part[g * row + HD + 1] = l;
+      s_part[g * row + HD + 2] = 0.0f;
+      s_part[g * row + HD + 3] = 0.0f;
     }
   }
   if (a.splits == 1) return;
+  __syncthreads();
 
-  // ---- split combine, inside the launch: the last of the `splits` workgroups of this
-  // (stream, kv-head) to arrive merges all partials.  Hand-off per MI355X_MICROARCH.md
-  // "inter-workgroup visibility": every storing wave drains its stores, workgroup barrier,
-  // one lane agent-release + relaxed ticket; the last arriver agent-acquires before reading.
-  __shared__ int s_last;
+  // ---- publish: the G rows of this split, write-through 16-byte stores.  Partials of
+  // (stream, head) are contiguous: [m][h][split][row].
+  constexpr int V4 = (HD + 4) / 4;
+  const __amdgpu_buffer_rsrc_t wsr = ws_rsrc(a.ws);
+  for (int i = tid; i < G * V4; i += kAttnThreads) {
+    const int g = i / V4, c = i - g * V4, h = kvh * G + g;
+    const int off = (((m * a.heads + h) * a.splits + split) * row + 4 * c) * 4;
+    __builtin_amdgcn_raw_buffer_store_b128(*(const f32x4*)(s_part + g * row + 4 * c), wsr, off, 0, kAuxSc1);
+  }
+  // ---- split merge by the last arriver: every storing wave drains its write-through
+  // stores, barrier, one lane adds to the ticket; its returned value names the last.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int32_t* ticket = a.counters + (size_t)m * a.kv_heads + kvh;
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (t == a.splits - 1);
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
   __syncthreads();
   if (!s_last) return;
-  for (int idx = tid; idx < G * HD; idx += 256) {
+  // all partials of the group's heads in one round trip: s_part[g][split][row]
+  const int nv = G * a.splits * V4;
+  for (int i = tid; i < nv; i += kAttnThreads) {
+    const int g = i / (a.splits * V4), rem = i - g * a.splits * V4;
+    const int h = kvh * G + g;
+    const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(wsr, ((m * a.heads + h) * a.splits * row + 4 * rem) * 4, 0,
+                                                          kAuxSc1);
+    *(f32x4*)(s_part + (size_t)g * a.splits * row + 4 * rem) = v;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < G * HD; idx += kAttnThreads) {
     const int g = idx / HD, d = idx - g * HD, h = kvh * G + g;
-    const float* base = a.ws + (size_t)(m * a.heads + h) * a.splits * row;
+    const float* pb = s_part + (size_t)g * a.splits * row;
     float mx = -INFINITY;
-#pragma unroll 8
-    for (int s = 0; s < a.splits; ++s) mx = fmaxf(mx, base[s * row + HD]);
+    for (int sp = 0; sp < a.splits; ++sp) mx = fmaxf(mx, pb[sp * row + HD]);
     float num = 0.0f, den = 0.0f;
-#pragma unroll 8
-    for (int s = 0; s < a.splits; ++s) {
-      const float ms = base[s * row + HD];
+    for (int sp = 0; sp < a.splits; ++sp) {
+      const float ms = pb[sp * row + HD];
       const float f = ms == -INFINITY ? 0.0f : __expf(ms - mx);   // empty split: weight 0
-      den = fmaf(f, base[s * row + HD + 1], den);
-      num = fmaf(f, base[s * row + d], num);
+      den = fmaf(f, pb[sp * row + HD + 1], den);
+      num = fmaf(f, pb[sp * row + d], num);
     }
     a.out[(size_t)m * a.heads * HD + (size_t)h * HD + d] = f2h(num / den);
   }
@@ -231,7 +273,7 @@ __global__ __launch_bounds__(256) void attn_split_kernel(const AttnArgs a) {
 
 template <int HD, int G>
 static int launch_attn(const AttnArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((attn_split_kernel<HD, G>), dim3(a.splits, a.kv_heads, a.M), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((attn_split_kernel<HD, G>), dim3(a.splits, a.kv_heads, a.M), dim3(kAttnThreads), 0, s, a);
   TI_LAUNCH_CHECK("attn_split_kernel");
   return TI_OK;
 }
@@ -249,15 +291,14 @@ static int dispatch_group(const AttnArgs& a, int G, hipStream_t s) {
 
 }  // namespace ti
 
-static size_t partial_bytes(int M, int heads, int head_dim, int splits) {
-  return ((size_t)M * heads * splits * ti::ws_row(head_dim) * sizeof(float) + 255) & ~(size_t)255;
-}
+// Workspace: the arrival tickets first, at a fixed place for every call ([TI_ATTN_MAX_M][heads]
+// int32, sized for heads >= kv_heads, zero before the first call and re-armed by every
+// call), then the partials [M][heads][splits][head_dim + 4] fp32.  A fixed ticket region
+// keeps calls with different M or splits from reading each other's partials as tickets.
+static size_t ticket_bytes(int heads) { return ((size_t)TI_ATTN_MAX_M * heads * sizeof(int32_t) + 255) & ~(size_t)255; }
 
-// partials [M][heads][splits][head_dim + 4] fp32, then the arrival tickets [M][heads] int32
-// (sized for heads >= kv_heads); the tickets must be zero before the first call and are
-// re-armed by every call.
 extern "C" size_t ti_attn_workspace_bytes(int M, int heads, int head_dim, int splits) {
-  return partial_bytes(M, heads, head_dim, splits) + (size_t)M * heads * sizeof(int32_t);
+  return ticket_bytes(heads) + (size_t)M * heads * splits * ti::ws_row(head_dim) * sizeof(float);
 }
 
 extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
@@ -267,20 +308,24 @@ extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uin
   using namespace ti;
   if (!q || !k_cache || !v_cache || !pos || !workspace || !out)
     return ti_set_error(TI_ERR_ARG, "ti_attn_decode: null pointer");
-  if (M < 1 || heads < 1 || kv_heads < 1 || heads % kv_heads || splits < 1 || max_seq < 1)
+  if (M < 1 || M > TI_ATTN_MAX_M || heads < 1 || kv_heads < 1 || heads % kv_heads || splits < 1 || max_seq < 1)
     return ti_set_error(TI_ERR_ARG, "ti_attn_decode: bad sizes M=%d heads=%d kv_heads=%d splits=%d", M, heads,
                         kv_heads, splits);
   if (head_dim != 64 && head_dim != 128)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_attn_decode: head_dim %d not in {64,128}", head_dim);
   if (kv_stream_stride < (int64_t)kv_heads * max_seq * head_dim)
     return ti_set_error(TI_ERR_ARG, "ti_attn_decode: kv_stream_stride too small");
+  const int G = heads / kv_heads;
+  // splits only shape the work (results agree to rounding); the merge stages all partials
+  // of a kv-head group in LDS, which bounds them.
+  splits = std::min(splits, std::max(1, ti::attn_max_splits(G, head_dim)));
   AttnArgs a;
   a.q = q;
   a.kc = k_cache;
   a.vc = v_cache;
   a.pos = pos;
-  a.ws = workspace;
-  a.counters = (int32_t*)((char*)workspace + partial_bytes(M, heads, head_dim, splits));
+  a.counters = (int32_t*)workspace;
+  a.ws = (float*)((char*)workspace + ticket_bytes(heads));
   a.out = out;
   a.stride = kv_stream_stride;
   a.max_seq = max_seq;
@@ -289,7 +334,6 @@ extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uin
   a.kv_heads = kv_heads;
   a.splits = splits;
   a.scale = 1.0f / sqrtf((float)head_dim);   // tensor_engine.cpp:1288 (hidden = head_dim per head)
-  const int G = heads / kv_heads;
   hipStream_t s = (hipStream_t)stream;
   return head_dim == 128 ? dispatch_group<128>(a, G, s) : dispatch_group<64>(a, G, s);
 }
