@@ -106,6 +106,21 @@ def cpu_baseline(m, L):
                       f"(tensor_engine.cpp:620-633); host {os.uname().machine}, {os.cpu_count()} logical CPUs"}
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed FETCH_SIZE pass
+    (profiles/r*_pmc_traffic.json, written by tools/pmc_traffic.py from a separate
+    `rocprofv3 --pmc FETCH_SIZE` run of this bench), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+        return int(d["kernels"][kernel]["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+    except (KeyError, ValueError, OSError):
+        return None, None
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -150,8 +165,10 @@ def main() -> int:
     sb, wb = step_bytes(m, B, L)
 
     # Dominant kernel: the W4 decode GEMM (gemv_wq_kernel<4>), ~76 % of a step's bytes.
-    # Live timing: each linear class of layer 0 launched back to back between two HIP events
-    # on the engine stream; a step issues layers x (qkv, o, gate/up, down) + lm_head launches.
+    # Live timing: each linear class launched back to back between two HIP events on the
+    # engine stream, cycling through the layers so the weights come from HBM as in a step
+    # (per-launch time includes the ~1.2-1.5 us dependent-launch boundary); a step issues
+    # layers x (qkv, o, gate/up, down) + lm_head launches, weighted accordingly.
     names = ["qkv", "o", "gate_up", "down", "lm_head"]
     per = {}
     gemv_bytes = gemv_us = 0.0
@@ -168,6 +185,7 @@ def main() -> int:
     achieved = gemv_bytes / gemv_us / 1e3   # GB/s
     e.close()
 
+    traffic, traffic_src = pmc_traffic("gemv_wq_kernel<4>") if bits == 4 and B == 1 else (None, None)
     result = None
     if g.rank == 0:
         result = {
@@ -188,7 +206,8 @@ def main() -> int:
                        "model": args.model, "global_batch": B * g.world, "seq_len": L,
                        "parallelism": f"replicas{g.world} (request-sharded, no collectives)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "gemv_wq_kernel<4>",
                          "bytes_per_launch": int(gemv_bytes / n_launch), "avg_launch_us": round(gemv_us / n_launch, 3)},
             "step_roofline": {"bytes_per_step": int(sb), "weight_bytes": int(wb),

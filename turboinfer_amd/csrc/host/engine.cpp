@@ -642,38 +642,50 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
   if (!e || e->c.compat || !avg_us || !bytes || reps < 1 || n < 1 || n > e->c.max_batch || e->c.layers < 1)
     return ti_set_error(TI_ERR_ARG, "ti_engine_time_kernel: bad arguments");
   const ti_engine_config& c = e->c;
-  DevLayer& L = e->layer[0];
   const int H = c.hidden, I = c.inter, qd = e->qd(), kvd = e->kvd();
+  // Launch r uses layer r % layers, so (as in a real step) its weights are not still in
+  // the 256 MB Infinity Cache from the previous launch.
+  int cur = 0;
+  auto setup = [&](DevLayer& L, const DevLinear*& W, const void*& x, int& xk, int& ldx, const float*& nw,
+                     ti_epilogue& ep) -> int {
+    W = nullptr; x = nullptr; xk = TI_X_F16; ldx = 0; nw = nullptr; ep = ti_epilogue{};
+    switch (which) {
+      case 0: W = &L.qkv; x = e->h; xk = TI_X_F32_RMSNORM; ldx = H; nw = L.attn_norm;
+        ep.kind = TI_EPI_QKV_ROPE_KV; ep.ldo = qd; ep.out = e->q; ep.q_dim = qd; ep.kv_dim = kvd; ep.head_dim = c.head_dim;
+        ep.max_seq = c.max_seq; ep.pos = e->pos; ep.rope_cs = e->rope_cs; ep.k_cache = L.kc; ep.v_cache = L.vc;
+        ep.kv_stream_stride = e->kv_stride; break;
+      case 1: W = &L.o; x = e->attn; ldx = qd; ep.kind = TI_EPI_STORE_F32; ep.ldo = H; ep.out = e->tmp ? e->tmp : e->q; break;
+      case 2: W = &L.gu; x = e->h; xk = TI_X_F32_RMSNORM; ldx = H; nw = L.ffn_norm;
+        ep.kind = TI_EPI_SILU_MUL_F16; ep.ldo = I; ep.out = e->act; break;
+      case 3: W = &L.down; x = e->act; ldx = I; ep.kind = TI_EPI_STORE_F32; ep.ldo = H; ep.out = e->q; break;
+      case 4: W = &e->lm; x = e->h; xk = TI_X_F32_RMSNORM; ldx = H; nw = e->out_norm;
+        ep.kind = TI_EPI_LOGITS_ARGMAX; ep.ldo = c.vocab; ep.out = e->logits; ep.argmax = e->argmax; break;
+      case 5: break;
+      default: return ti_set_error(TI_ERR_ARG, "ti_engine_time_kernel: which=%d", which);
+    }
+    if (which == 1 || which == 3) {
+      // STORE_F32 into a scratch of n*H floats: q holds n*qd >= n*H only if qd >= H
+      if ((size_t)qd < (size_t)H) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_time_kernel: scratch too small");
+      ep.out = e->q;
+    }
+    return TI_OK;
+  };
   const DevLinear* W = nullptr;
   const void* x = nullptr;
   int xk = TI_X_F16, ldx = 0;
   const float* nw = nullptr;
   ti_epilogue ep{};
-  switch (which) {
-    case 0: W = &L.qkv; x = e->h; xk = TI_X_F32_RMSNORM; ldx = H; nw = L.attn_norm;
-      ep.kind = TI_EPI_QKV_ROPE_KV; ep.ldo = qd; ep.out = e->q; ep.q_dim = qd; ep.kv_dim = kvd; ep.head_dim = c.head_dim;
-      ep.max_seq = c.max_seq; ep.pos = e->pos; ep.rope_cs = e->rope_cs; ep.k_cache = L.kc; ep.v_cache = L.vc;
-      ep.kv_stream_stride = e->kv_stride; break;
-    case 1: W = &L.o; x = e->attn; ldx = qd; ep.kind = TI_EPI_STORE_F32; ep.ldo = H; ep.out = e->tmp ? e->tmp : e->q; break;
-    case 2: W = &L.gu; x = e->h; xk = TI_X_F32_RMSNORM; ldx = H; nw = L.ffn_norm;
-      ep.kind = TI_EPI_SILU_MUL_F16; ep.ldo = I; ep.out = e->act; break;
-    case 3: W = &L.down; x = e->act; ldx = I; ep.kind = TI_EPI_STORE_F32; ep.ldo = H; ep.out = e->q; break;
-    case 4: W = &e->lm; x = e->h; xk = TI_X_F32_RMSNORM; ldx = H; nw = e->out_norm;
-      ep.kind = TI_EPI_LOGITS_ARGMAX; ep.ldo = c.vocab; ep.out = e->logits; ep.argmax = e->argmax; break;
-    case 5: break;
-    default: return ti_set_error(TI_ERR_ARG, "ti_engine_time_kernel: which=%d", which);
-  }
-  if (which == 1 || which == 3) {
-    // STORE_F32 into a scratch of n*H floats: q holds n*qd >= n*H only if qd >= H
-    if ((size_t)qd < (size_t)H) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_time_kernel: scratch too small");
-    ep.out = e->q;
-  }
+  TI_TRY(setup(e->layer[0], W, x, xk, ldx, nw, ep));
   std::vector<int32_t> base(n, kv_len - 1);
   TI_TRY(ti_memcpy_h2d(e->pos, base.data(), (size_t)n * 4, e->s));
   hipEvent_t a, b;
   E_CHECK(hipEventCreate(&a), "hipEventCreate");
   E_CHECK(hipEventCreate(&b), "hipEventCreate");
   auto launch = [&]() -> int {
+    DevLayer& L = e->layer[cur];
+    cur = (cur + 1) % c.layers;
+    TI_TRY(setup(L, W, x, xk, ldx, nw, ep));
+    // (the one lm_head, 68 MB at 7B, fits the Infinity Cache: back-to-back it runs warm)
     if (which == 5)
       return ti_attn_decode(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, n, c.heads, c.kv_heads, c.head_dim,
                             e->splits_for(n), e->ws, e->attn, e->s);
