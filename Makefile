@@ -15,10 +15,13 @@ DEVFLAGS:= $(COMMON) --offload-arch=$(ARCH) -fno-gpu-rdc
 
 KERN    := $(wildcard turboinfer_amd/csrc/kernels/*.hip)
 HOST    := $(wildcard turboinfer_amd/csrc/host/*.cpp)
+API     := $(wildcard turboinfer_amd/csrc/api/*.cpp)
 KOBJ    := $(patsubst turboinfer_amd/csrc/kernels/%.hip,$(BUILD)/k_%.o,$(KERN))
 HOBJ    := $(patsubst turboinfer_amd/csrc/host/%.cpp,$(BUILD)/h_%.o,$(HOST))
+AOBJ    := $(patsubst turboinfer_amd/csrc/api/%.cpp,$(BUILD)/a_%.o,$(API))
 HDRS    := $(wildcard include/*.h) $(wildcard include/turboinfer/*/*.hpp) $(wildcard include/turboinfer/*.hpp) \
-           $(wildcard turboinfer_amd/csrc/kernels/*.hpp) $(wildcard turboinfer_amd/csrc/host/*.hpp)
+           $(wildcard turboinfer_amd/csrc/kernels/*.hpp) $(wildcard turboinfer_amd/csrc/host/*.hpp) \
+           $(wildcard turboinfer_amd/csrc/api/*.hpp)
 
 all: $(LIB)
 
@@ -34,17 +37,20 @@ $(BUILD)/h_%.o: turboinfer_amd/csrc/host/%.cpp $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(COMMON) -ffp-contract=off -x hip --offload-arch=$(ARCH) -c $< -o $@
 
-$(LIB): $(KOBJ) $(HOBJ)
+# C++20 drop-in API (turboinfer::core / model / optimize): host code over the C-ABI only
+$(BUILD)/a_%.o: turboinfer_amd/csrc/api/%.cpp $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(COMMON) -ffp-contract=off -c $< -o $@
+
+$(LIB): $(KOBJ) $(HOBJ) $(AOBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(KOBJ) $(HOBJ) -Wl,-soname,libturboinfer_amd.so
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(KOBJ) $(HOBJ) $(AOBJ) -Wl,-soname,libturboinfer_amd.so
 
-CPPTESTS := $(patsubst tests/cpp/%.cpp,$(BUILD)/tests/%,$(wildcard tests/cpp/*.cpp))
+# C++ API test drivers (tests/cpp/*.cpp -> tests/cpp/bin/), linked against the in-tree library
+CPPTESTS := $(patsubst tests/cpp/%.cpp,tests/cpp/bin/%,$(wildcard tests/cpp/*.cpp))
 test-bins: $(CPPTESTS)
-$(BUILD)/tests/%: tests/cpp/%.cpp $(LIB)
-	@mkdir -p $(BUILD)/tests
-	$(HIPCC) -std=c++20 -O2 -Iinclude $< -o $@ -L$(LIBDIR) -lturboinfer_amd -Wl,-rpath,$(abspath $(LIBDIR))
-
-clean:
-	rm -rf $(BUILD) $(LIBDIR)
+tests/cpp/bin/%: tests/cpp/%.cpp $(HDRS) | $(LIB)
+	@mkdir -p tests/cpp/bin
+	$(HIPCC) -std=c++20 -O2 -Iinclude $< -o $@ -L$(LIBDIR) -lturboinfer_amd -Wl,-rpath,'$$ORIGIN/../../../$(LIBDIR)'
 
 .PHONY: all clean test-bins

@@ -22,6 +22,7 @@
  *   ti_rope_f32           TensorEngine::apply_rope :1510-1624 (host cos/sin table, same fma pattern)
  *   ti_silu_f32 / ti_add_f32 / ti_mul_f32 / ti_relu_f32   :900-923, :1626-1743, :828-869
  *   ti_softmax_f32        TensorEngine::softmax :925-1043 (same fast_exp_avx2 polynomial :262-302)
+ *   ti_attention_f32      TensorEngine::multi_head_attention / attention_fast_incremental (fp32 op level)
  *   ti_argmax_f32         greedy InferenceEngine::sample_next_token (top_k = 1) :1554-1673
  */
 #ifndef TI_HIP_H
@@ -215,6 +216,11 @@ int ti_relu_f32(const float* x, float* y, int64_t n, ti_stream_t s);
 int ti_add_f32(const float* a, const float* b, float* y, int64_t n, ti_stream_t s);
 int ti_mul_f32(const float* a, const float* b, float* y, int64_t n, ti_stream_t s);
 int ti_softmax_f32(const float* x, float* y, int rows, int n, float temperature, ti_stream_t s);
+/* multi_head_attention / attention_fast_incremental at op level: q [B][H], k, v [B][S][H]
+ * with `heads` heads of H/heads dims interleaved in H (heads = 1: a single head of H dims);
+ * out [B][H]; scratch B*heads*S floats (device). */
+int ti_attention_f32(const float* q, const float* k, const float* v, float* out, float* scratch, int B, int S,
+                     int H, int heads, ti_stream_t s);
 /* out[r] = argmax_n x[r][n], lowest index on ties. */
 int ti_argmax_f32(const float* x, int32_t* out, int rows, int n, ti_stream_t s);
 

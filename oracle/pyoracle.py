@@ -39,6 +39,17 @@ class ModelConfig(C.Structure):
                 ("group", C.c_int), ("max_seq", C.c_int)]
 
 
+_FP = C.POINTER(C.c_float)
+_FPP = C.POINTER(_FP)
+
+
+class _OrModel(C.Structure):
+    """Mirror of or_model (ti_oracle.h) -- read-only access to the materialised weights."""
+    _fields_ = [("cfg", ModelConfig), ("emb", _FP), ("attn_norm", _FPP), ("ffn_norm", _FPP), ("wq", _FPP),
+                ("wk", _FPP), ("wv", _FPP), ("wo", _FPP), ("wg", _FPP), ("wu", _FPP), ("wd", _FPP),
+                ("out_norm", _FP), ("lm_head", _FP), ("kc", _FPP), ("vc", _FPP), ("len", C.c_int)]
+
+
 class Oracle:
     """The plain-C restatement (ti_oracle.c)."""
 
@@ -225,6 +236,33 @@ class OracleModel:
 
     def fill_kv(self, n, seed):
         self.o.lib.or_model_fill_kv(self.ptr, n, seed)
+
+    def weights(self):
+        """The model's fp32 tensors under the reference's weight names
+        (inference_engine.cpp:483-563 "layers.N.attention.*" / "feed_forward.w1|w2|w3"),
+        [K][N] layout, copied out of the oracle."""
+        m = C.cast(self.ptr, C.POINTER(_OrModel)).contents
+        c = self.cfg
+        H, I, V = c["hidden"], c["inter"], c["vocab"]
+        qd, kvd = c["heads"] * c["head_dim"], c["kv_heads"] * c["head_dim"]
+
+        def arr(p, *shape):
+            return np.ctypeslib.as_array(p, shape=(int(np.prod(shape)),)).reshape(shape).copy()
+
+        out = {"token_embeddings.weight": arr(m.emb, V, H), "norm.weight": arr(m.out_norm, H),
+               "lm_head.weight": arr(m.lm_head, H, V)}
+        for l in range(c["layers"]):
+            p = f"layers.{l}."
+            out[p + "attention.q_proj.weight"] = arr(m.wq[l], H, qd)
+            out[p + "attention.k_proj.weight"] = arr(m.wk[l], H, kvd)
+            out[p + "attention.v_proj.weight"] = arr(m.wv[l], H, kvd)
+            out[p + "attention.o_proj.weight"] = arr(m.wo[l], qd, H)
+            out[p + "feed_forward.w3.weight"] = arr(m.wg[l], H, I)     # gate
+            out[p + "feed_forward.w1.weight"] = arr(m.wu[l], H, I)     # up
+            out[p + "feed_forward.w2.weight"] = arr(m.wd[l], I, H)     # down
+            out[p + "attention_norm.weight"] = arr(m.attn_norm[l], H)
+            out[p + "ffn_norm.weight"] = arr(m.ffn_norm[l], H)
+        return out
 
     def step(self, token, kv_round_f16=True):
         logits = np.empty(self.cfg["vocab"], np.float32)

@@ -1,0 +1,225 @@
+"""The drop-in C++20 API (include/turboinfer/*: Tensor, TensorEngine, Quantizer, ModelData,
+InferenceEngine) driven through tests/cpp/api_check, checked against the reference's golden
+vectors (tests/golden) and the oracle.
+
+CPU tests: Tensor / ModelData semantics and the host Quantizer (bit-exact against the
+reference's quantize_tensor / dequantize_tensor vectors).  GPU tests: TensorEngine ops
+(the same bars as the C-ABI op tests in test_gpu_kernels.py) and InferenceEngine generate()
+on the reference benchmark's plumbing model (exact tokens) and on mini Llama models built
+from the oracle's weights (greedy tokens of the reference-composed decode)."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, inp
+
+f32 = np.float32
+BIN = os.path.join(ROOT, "tests", "cpp", "bin", "api_check")
+LIB = os.path.join(ROOT, "turboinfer_amd", "lib", "libturboinfer_amd.so")
+CODES = {np.dtype(np.float32): 0, np.dtype(np.int32): 1, np.dtype(np.int8): 2}
+DTYPES = {0: np.float32, 1: np.int32, 2: np.int8}
+
+
+@pytest.fixture(scope="module")
+def api_check():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-C", ROOT, "-j8", "all"], check=True)
+    if not os.path.exists(BIN) or os.path.getmtime(BIN) < os.path.getmtime(os.path.join(ROOT, "tests", "cpp",
+                                                                                         "api_check.cpp")):
+        os.makedirs(os.path.dirname(BIN), exist_ok=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++20", "-O2", "-I" + os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "cpp", "api_check.cpp"), "-o", BIN,
+                        "-L" + os.path.dirname(LIB), "-lturboinfer_amd",
+                        "-Wl,-rpath,$ORIGIN/../../../turboinfer_amd/lib"], check=True)
+
+    def run(*args):
+        r = subprocess.run([BIN, *map(str, args)], capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, f"api_check {args[0]} failed:\n{r.stdout}\n{r.stderr}"
+        return r.stdout
+    return run
+
+
+def write(path, a):
+    a = np.ascontiguousarray(a)
+    with open(path, "wb") as f:
+        f.write(np.array([CODES[a.dtype], a.ndim], np.uint32).tobytes())
+        f.write(np.array(a.shape, np.uint64).tobytes())
+        f.write(a.tobytes())
+    return path
+
+
+def read(path):
+    with open(path, "rb") as f:
+        code, nd = np.frombuffer(f.read(8), np.uint32)
+        shape = tuple(int(v) for v in np.frombuffer(f.read(8 * int(nd)), np.uint64))
+        return np.frombuffer(f.read(), DTYPES[int(code)]).reshape(shape)
+
+
+def same_bits(a, b):
+    np.testing.assert_array_equal(np.asarray(a, f32).view(np.uint32), np.asarray(b, f32).view(np.uint32))
+
+
+# ---------------------------------------------------------------------------- CPU
+
+def test_tensor_and_model_data_semantics(api_check):
+    assert api_check("tensor").strip() == "ok"
+
+
+def test_quantizer_matches_reference_vectors(api_check, golden, tmp_path):
+    d = golden("quant")
+    for k in range(int(d["n"][0])):
+        x, bits, sym = d[f"x{k}"], int(d[f"bits{k}"][0]), int(d[f"sym{k}"][0])
+        out = tmp_path / f"q{k}.bin"
+        api_check("quant", write(tmp_path / f"x{k}.bin", x), bits, sym, out)
+        o = read(out)
+        n = x.size
+        same_bits(o[:1], d[f"scale{k}"])
+        same_bits(o[1:2], d[f"zp{k}"])
+        np.testing.assert_array_equal(o[2:2 + n].astype(np.int32), d[f"q{k}"])
+        same_bits(o[2 + n:], d[f"deq{k}"])
+
+
+# ---------------------------------------------------------------------------- GPU
+
+@pytest.mark.gpu
+def test_tensor_engine_ops_match_reference_vectors(api_check, golden, tmp_path):
+    t = tmp_path
+    # matmul (3D x 2D, matmul_3d_2d) -- bit-exact
+    d = golden("matmul")
+    for i in range(len([k for k in d.files if k.startswith("shape")])):
+        B, M, K, N = (int(v) for v in d[f"shape{i}"])
+        sa, sb = d[f"seeds{i}"]
+        a, b = inp(int(sa), (B, M, K)), inp(int(sb), (K, N), 0.05)
+        api_check("op", "matmul", t / "y.bin", write(t / "a.bin", a), write(t / "b.bin", b))
+        y = read(t / "y.bin")
+        assert y.shape == (B, M, N)
+        same_bits(y if f"y{i}" in d else y.reshape(-1)[:512], d[f"y{i}"] if f"y{i}" in d else d[f"y{i}_head"])
+    # rms_norm -- bit-exact
+    d = golden("rms_norm")
+    for i in range(len([k for k in d.files if k.startswith("shape")])):
+        rows, n = (int(v) for v in d[f"shape{i}"])
+        x, w = inp(200 + i, (rows, n)), (f32(1.0) + inp(300 + i, (n,), 0.1)).astype(f32)
+        api_check("op", "rms_norm", t / "y.bin", write(t / "x.bin", x), write(t / "w.bin", w), 1e-5)
+        y = read(t / "y.bin")
+        same_bits(y if f"y{i}" in d else y.reshape(-1)[:512], d[f"y{i}"] if f"y{i}" in d else d[f"y{i}_head"])
+    # apply_rope -- bit-exact
+    d = golden("rope")
+    for i in range(len([k for k in d.files if k.startswith("shape")])):
+        shape = tuple(int(s) for s in d[f"shape{i}"])
+        theta = float(d[f"theta{i}"][0])
+        api_check("op", "rope", t / "y.bin", write(t / "x.bin", inp(400 + i, shape)),
+                  write(t / "p.bin", d[f"pos{i}"].astype(f32)), repr(theta))
+        same_bits(read(t / "y.bin"), d[f"y{i}"])
+    # element-wise
+    d = golden("eltwise")
+    x, x2 = inp(500, (1001,), 4.0), inp(501, (1001,))
+    for name, ins, exact in (("relu", [x], True), ("add", [x, x2], True), ("mul", [x, x2], True),
+                             ("silu", [x], False)):
+        files = [write(t / f"e{j}.bin", v) for j, v in enumerate(ins)]
+        api_check("op", name, t / "y.bin", *files)
+        y = read(t / "y.bin")
+        ref = d["mul" if name == "mul" else name]
+        if exact:
+            same_bits(y, ref)
+        else:
+            np.testing.assert_allclose(y, ref, rtol=1e-6, atol=1e-30)
+    # softmax
+    d = golden("softmax")
+    for i in range(len([k for k in d.files if k.startswith("shape")])):
+        rows, n = (int(v) for v in d[f"shape{i}"])
+        T = float(d[f"T{i}"][0])
+        api_check("op", "softmax", t / "y.bin", write(t / "x.bin", inp(600 + i, (rows, n), 5.0)), repr(T))
+        y = read(t / "y.bin")
+        exp = d[f"y{i}"] if f"y{i}" in d else d[f"y{i}_head"]
+        got = y if f"y{i}" in d else y.reshape(-1)[: exp.size]
+        if n >= 16 and n % 8 == 0:
+            same_bits(got, exp)
+        else:
+            np.testing.assert_allclose(got.reshape(exp.shape), exp, rtol=2e-6, atol=1e-30)
+
+
+@pytest.mark.gpu
+def test_tensor_engine_attention_matches_reference_vectors(api_check, golden, tmp_path):
+    """attention_fast_incremental / multi_head_attention: same arithmetic sequence as the
+    reference except the device expf (an ulp from glibc's): rtol 1e-5."""
+    t = tmp_path
+    d = golden("attention")
+    for i in range(len([k for k in d.files if k.startswith("shape")])):
+        B, S, D = (int(v) for v in d[f"shape{i}"])
+        q, k, v = inp(700 + 3 * i, (B, 1, D)), inp(701 + 3 * i, (B, S, D)), inp(702 + 3 * i, (B, S, D))
+        api_check("op", "attention", t / "y.bin", write(t / "q.bin", q), write(t / "k.bin", k), write(t / "v.bin", v))
+        np.testing.assert_allclose(read(t / "y.bin"), d[f"y{i}"].reshape(B, 1, D), rtol=1e-5, atol=1e-6)
+    d = golden("mha")
+    for i in range(len([k for k in d.files if k.startswith("shape")])):
+        S, H, nh = (int(v) for v in d[f"shape{i}"])
+        q, k, v = inp(800 + 3 * i, (1, 1, H)), inp(801 + 3 * i, (1, S, H)), inp(802 + 3 * i, (1, S, H))
+        api_check("op", "mha", t / "y.bin", write(t / "q.bin", q), write(t / "k.bin", k), write(t / "v.bin", v), nh)
+        exp = d[f"y{i}"] if f"y{i}" in d else d[f"y{i}_head"]
+        got = read(t / "y.bin")
+        got = got if f"y{i}" in d else got.reshape(-1)[: exp.size]
+        np.testing.assert_allclose(got.reshape(exp.shape), exp, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_inference_engine_plumbing_generate_exact(api_check, golden, tmp_path):
+    """BASELINE config 1 through the C++ InferenceEngine: the reference benchmark's model
+    (benchmark_inference.cpp:145-225 fill patterns) -> reference_compat path, top_k = 1."""
+    d = golden("plumbing_generate")
+    V, H, layers, I = 1000, 256, 4, 1024
+    idx = np.arange(H * I)
+    up = ((((idx % 200).astype(f32) / f32(200.0)) - f32(0.5)) * f32(0.02)).astype(f32).reshape(H, I)
+    lm = ((((np.arange(H * V) % 500).astype(f32) / f32(500.0)) - f32(0.5)) * f32(0.01)).astype(f32).reshape(H, V)
+    mdir = tmp_path / "plumb"
+    mdir.mkdir()
+    lines = [f"meta {V} {H} {layers} 4 {I} 10000.0"]
+    write(mdir / "up.bin", up)
+    write(mdir / "down.bin", up.reshape(-1).reshape(I, H))
+    write(mdir / "lm.bin", lm)
+    for l in range(layers):
+        lines += [f"layers.{l}.feed_forward.w1.weight up.bin", f"layers.{l}.feed_forward.w2.weight down.bin"]
+    lines.append("lm_head.weight lm.bin")
+    (mdir / "manifest.txt").write_text("\n".join(lines) + "\n")
+    for i in range(3):
+        prompt = d[f"prompt{i}"].astype(np.int32)[None, :]
+        api_check("generate", mdir, write(tmp_path / "p.bin", prompt), 20, 1, 0, tmp_path / "o.bin")
+        got = [int(v) for v in read(tmp_path / "o.bin")[0] if v >= 0]
+        assert got == d[f"tokens{i}"].tolist()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["mini_gqa_w4", "mini_hd128_w8"])
+def test_inference_engine_llama_greedy_matches_reference(api_check, golden, oracle, tmp_path, name):
+    """A Llama-shape ModelData (the oracle's weights under the reference's names) through
+    InferenceEngine::generate_batch with top_k = 1 and group quantization on upload: the
+    greedy tokens of the reference-composed decode (golden), up to the first near-tie."""
+    from pyoracle import OracleModel
+    d = golden(f"decode_{name}")
+    cfg = json.loads(str(d["cfg"]))
+    m = OracleModel(oracle, cfg, int(d["seed"][0]), float(d["jitter"][0]))
+    w = m.weights()
+    m.close()
+    mdir = tmp_path / name
+    mdir.mkdir()
+    lines = [f"meta {cfg['vocab']} {cfg['hidden']} {cfg['layers']} {cfg['heads']} {cfg['inter']} {cfg['rope_theta']!r}"]
+    for j, (k, v) in enumerate(w.items()):
+        write(mdir / f"t{j}.bin", v.astype(f32))
+        lines.append(f"{k} t{j}.bin")
+    (mdir / "manifest.txt").write_text("\n".join(lines) + "\n")
+    prompt = d["prompt"].tolist()
+    ref_new = d["tokens"].tolist()[len(prompt):]
+    prompts = np.array([prompt, prompt], np.int32)        # two identical requests: batch path
+    api_check("generate", mdir, write(tmp_path / "p.bin", prompts), len(ref_new), 1, cfg["bits"], tmp_path / "o.bin")
+    out = read(tmp_path / "o.bin")
+    for row in out:
+        got = [int(v) for v in row[len(prompt):] if v >= 0]
+        for i, (g, r) in enumerate(zip(got, ref_new)):
+            lg = d["logits"][len(prompt) - 1 + i]
+            s = np.sort(lg)
+            if s[-1] - s[-2] <= 1e-2 * float(np.max(np.abs(lg))):
+                break                      # near-tie: later tokens may legitimately diverge
+            assert g == r, f"token {i}: C++ API {g} reference {r}"

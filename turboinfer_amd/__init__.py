@@ -66,8 +66,8 @@ EXPORTED = [
     "ti_wpack_tile_bytes", "ti_wpack_scale_bytes", "ti_wpack_host", "ti_wsynth_device", "ti_fill_uniform_f16",
     "ti_fill_uniform_f32", "ti_fill_kv_uniform", "ti_gemm_wq_a16", "ti_gemm_lds_bytes", "ti_gemm_prepare",
     "ti_attn_workspace_bytes", "ti_attn_decode", "ti_step_begin", "ti_matmul_f32", "ti_rms_norm_f32",
-    "ti_rope_f32", "ti_silu_f32", "ti_relu_f32", "ti_add_f32", "ti_mul_f32", "ti_softmax_f32", "ti_argmax_f32",
-    "ti_engine_create", "ti_engine_destroy", "ti_engine_get_stream", "ti_engine_memory", "ti_engine_set_tensor",
+    "ti_rope_f32", "ti_silu_f32", "ti_relu_f32", "ti_add_f32", "ti_mul_f32", "ti_softmax_f32", "ti_attention_f32",
+    "ti_argmax_f32", "ti_engine_create", "ti_engine_destroy", "ti_engine_get_stream", "ti_engine_memory", "ti_engine_set_tensor",
     "ti_engine_synth", "ti_engine_fill_kv", "ti_engine_generate", "ti_engine_step", "ti_engine_compat_step",
     "ti_engine_replay_prepare", "ti_engine_replay_run", "ti_engine_sync", "ti_engine_last_tokens",
     "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token",
@@ -121,6 +121,7 @@ def lib() -> C.CDLL:
         for n in ("ti_add_f32", "ti_mul_f32"):
             getattr(L, n).argtypes = [vp, vp, vp, i64, vp]
         L.ti_softmax_f32.argtypes = [vp, vp, i32, i32, f32, vp]
+        L.ti_attention_f32.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, vp]
         L.ti_argmax_f32.argtypes = [vp, vp, i32, i32, vp]
         L.ti_engine_create.argtypes = [C.POINTER(EngineConfig), C.POINTER(vp)]
         L.ti_engine_destroy.argtypes = [vp]

@@ -197,6 +197,64 @@ __global__ __launch_bounds__(256) void argmax_f32_kernel(const float* x, int32_t
 
 }  // namespace ti
 
+// attention_fast_incremental (tensor_engine.cpp:1254-1388) for one (batch row, head) per
+// block, heads addressed with strides so multi_head_attention's slicing (:1149-1252) needs
+// no copies.  Scores: 8 lane partial fmas over the 8-aligned prefix, lanes added in
+// order, then the ordered tail (as the reference's AVX2 loop + scalar remainder); softmax
+// with max / exp / sequential sum / divide; output: 8 lane partial fmas over the 8-aligned
+// key prefix, lanes added in order, fused tail.  exp is the device expf (glibc's expf may
+// differ by an ulp), so results match within rounding, not bitwise.
+__global__ __launch_bounds__(256) void attention_f32_kernel(const float* q, const float* k, const float* v,
+                                                            float* out, float* scratch, int S, int D, int heads,
+                                                            int64_t ldq, int64_t ldkv, int64_t ldo) {
+  const int b = blockIdx.x, h = blockIdx.y;
+  const float* qb = q + (size_t)b * ldq + (size_t)h * D;
+  const float* kb = k + (size_t)b * S * ldkv + (size_t)h * D;
+  const float* vb = v + (size_t)b * S * ldkv + (size_t)h * D;
+  float* sc = scratch + ((size_t)b * heads + h) * S;
+  const float scale = 1.0f / sqrtf((float)D);
+  const int de = (D / 8) * 8;
+  for (int j = threadIdx.x; j < S; j += 256) {
+    const float* kr = kb + (size_t)j * ldkv;
+    float lane[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < de; i += 8)
+      for (int l = 0; l < 8; ++l) lane[l] = fmaf(qb[i + l], kr[i + l], lane[l]);
+    float s = 0.0f;
+    for (int l = 0; l < 8; ++l) s = s + lane[l];
+    int i = de;
+    for (; i + 4 <= D; i += 4)
+      for (int l = 0; l < 4; ++l) s = s + qb[i + l] * kr[i + l];
+    for (; i < D; ++i) s = fmaf(qb[i], kr[i], s);
+    sc[j] = s * scale;
+  }
+  __syncthreads();
+  __shared__ float s_sum;
+  if (threadIdx.x == 0) {
+    float mx = sc[0];
+    for (int j = 1; j < S; ++j) mx = (mx < sc[j]) ? sc[j] : mx;
+    float se = 0.0f;
+    for (int j = 0; j < S; ++j) {
+      sc[j] = expf(sc[j] - mx);
+      se = se + sc[j];
+    }
+    s_sum = se;
+  }
+  __syncthreads();
+  const float se = s_sum;
+  for (int j = threadIdx.x; j < S; j += 256) sc[j] = sc[j] / se;
+  __syncthreads();
+  const int ke = (S / 8) * 8;
+  for (int d = threadIdx.x; d < D; d += 256) {
+    float lane[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < ke; j += 8)
+      for (int l = 0; l < 8; ++l) lane[l] = fmaf(sc[j + l], vb[(size_t)(j + l) * ldkv + d], lane[l]);
+    float o = 0.0f;
+    for (int l = 0; l < 8; ++l) o = o + lane[l];
+    for (int j = ke; j < S; ++j) o = fmaf(sc[j], vb[(size_t)j * ldkv + d], o);
+    out[(size_t)b * ldo + (size_t)h * D + d] = o;
+  }
+}
+
 static unsigned grid_for(int64_t n) {
   const int64_t b = (n + 255) / 256;
   return (unsigned)(b < 65536 ? (b > 0 ? b : 1) : 65536);
@@ -247,6 +305,17 @@ extern "C" int ti_softmax_f32(const float* x, float* y, int rows, int n, float t
   if (!x || !y || rows < 1 || n < 1) return ti_set_error(TI_ERR_ARG, "ti_softmax_f32: bad arguments");
   hipLaunchKernelGGL(ti::softmax_f32_kernel, dim3(rows), dim3(256), 0, (hipStream_t)s, x, y, n, temperature);
   TI_LAUNCH_CHECK("softmax_f32_kernel");
+  return TI_OK;
+}
+
+extern "C" int ti_attention_f32(const float* q, const float* k, const float* v, float* out, float* scratch, int B,
+                                int S, int H, int heads, ti_stream_t s) {
+  using namespace ti;
+  if (!q || !k || !v || !out || !scratch || B < 1 || S < 1 || heads < 1 || H < heads || H % heads)
+    return ti_set_error(TI_ERR_ARG, "ti_attention_f32: bad arguments B=%d S=%d H=%d heads=%d", B, S, H, heads);
+  hipLaunchKernelGGL(attention_f32_kernel, dim3(B, heads), dim3(256), 0, (hipStream_t)s, q, k, v, out, scratch, S,
+                     H / heads, heads, (int64_t)H, (int64_t)H, (int64_t)H);
+  TI_LAUNCH_CHECK("attention_f32_kernel");
   return TI_OK;
 }
 
