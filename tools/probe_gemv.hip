@@ -1,11 +1,12 @@
 // probe_gemv.hip -- per-launch timing of ti_gemm_wq_a16 on the Llama-2-7B INT4 decode shapes,
 // replayed from a hipGraph (GPU box, diagnostic only; not part of the product).
 //
-//   for e in 0 1 4 5; do hipcc -std=c++20 -O3 -Iinclude -Iturboinfer_amd/csrc/kernels --offload-arch=gfx950 \
+//   for e in 0 1 4 5 8 16 12 20; do hipcc -std=c++20 -O3 -Iinclude -Iturboinfer_amd/csrc/kernels --offload-arch=gfx950 \
 //     -DTI_GEMV_EXP=$e tools/probe_gemv.hip -o tools/probe_gemv_e$e; done
 //
 // The kernel source is compiled into this TU with TI_GEMV_EXP:
-//   0 product kernel, 1 stream only (no dequant/MFMA), +4 per-workgroup phase timestamps.
+//   0 product kernel, 1 stream only (no dequant/MFMA), +4 per-workgroup phase timestamps,
+//   +8 no x / scale dependency (constants), +16 non-temporal weight loads.
 // Weights are random bytes (timing does not depend on values); x is fp16 or f32+rmsnorm.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>

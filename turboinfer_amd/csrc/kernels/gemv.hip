@@ -75,17 +75,19 @@ __host__ inline int gemv_grid(int N, int num_cus) {
 // LDS image of one workgroup (bytes, each region 16-aligned):
 //   x      [M][K + 8] fp16            activation rows (row pad breaks bank aliasing)
 //   scales [ntl][K/128][16] fp16      group scales of the workgroup's tiles
+//   corr   [K/128][16] f32            int4: per (group, row) offset correction (see deq_int4_raw)
 //   slab   [ntl + 1][8][64] f32x4     per-wave partial tiles (+ one dummy slab)
 //   es     epilogue inputs: residual [ntl][M][16] f32, or RoPE (cos, sin) [M][hd] + pos [M]
 //   best   [16] u64                   argmax keys of the workgroup
 struct GemvLds {
-  int x, sc, slab, es, best, total;
+  int x, sc, corr, slab, es, best, total;
 };
 __host__ __device__ inline GemvLds gemv_lds_layout(int M, int K, int ntl) {
   GemvLds l;
   l.x = 0;
   l.sc = l.x + align16(M * (K + 8) * 2);
-  l.slab = l.sc + align16(ntl * (K >> 7) * 32);
+  l.corr = l.sc + align16(ntl * (K >> 7) * 32);
+  l.slab = l.corr + (K >> 7) * 16 * 4;         // int4 offset correction [K/128][16 rows] f32
   l.es = l.slab + (ntl + 1) * kGemvWaves * kWave * 16;
   const int es_bytes = ntl * M * 16 * 4 > M * 128 * 4 + 64 ? ntl * M * 16 * 4 : M * 128 * 4 + 64;
   l.best = l.es + align16(es_bytes);
@@ -98,21 +100,6 @@ __host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_
 
 // ------------------------------------------------------------------- dequant
 // int4: word of 8 nibbles, nibble p holds element 2p, nibble p+4 element 2p+1, value q+8.
-// Low nibbles of each byte: (w & 0x000F000F) | 0x6400 = fp16 1024 + n, minus 1032.
-// High nibbles are used in place: (w & 0x00F000F0) | 0x6400 = fp16 1024 + 16 n, times 1/16
-// minus 72 (one fused v_pk_fma_f16).  All values are small integers: every step is exact.
-// 9 VALU ops per 8 weights (v_and_or_b32 x4, v_lshrrev x1, v_pk_add x2, v_pk_fma x2); the
-// caller keeps `magic` = 0x64006400 in a VGPR so v_and_or_b32 needs only one literal.
-__device__ __forceinline__ f16x8 deq_int4_word(uint32_t w, uint32_t magic) {
-  const f16x2 k_lo = {(f16)-1032.0f, (f16)-1032.0f}, k_sc = {(f16)0.0625f, (f16)0.0625f},
-              k_hi = {(f16)-72.0f, (f16)-72.0f};
-  const uint32_t w8 = w >> 8;
-  const f16x2 e01 = __builtin_bit_cast(f16x2, (w & 0x000F000Fu) | magic) + k_lo;
-  const f16x2 e23 = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, (w & 0x00F000F0u) | magic), k_sc, k_hi);
-  const f16x2 e45 = __builtin_bit_cast(f16x2, (w8 & 0x000F000Fu) | magic) + k_lo;
-  const f16x2 e67 = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, (w8 & 0x00F000F0u) | magic), k_sc, k_hi);
-  return (f16x8){e01[0], e01[1], e23[0], e23[1], e45[0], e45[1], e67[0], e67[1]};
-}
 // int8: 4 signed bytes in k order; (b ^ 0x80) = b + 128 -> fp16 1024 + b + 128 - 1152.
 __device__ __forceinline__ f16x2 deq_int8_pair(uint32_t t, uint32_t sel) {
   const uint32_t v = __builtin_amdgcn_perm(0x64646464u, t, sel);
@@ -127,10 +114,28 @@ __device__ __forceinline__ void deq_int8_word(uint32_t w, f16x8& r, int o) {
   r[o + 3] = hi[1];
 }
 
+// int4, offset folded (5 VALU ops per 8 weights): fp16 lanes hold 1024 + n for the low
+// nibble of each byte and 1024 + 16 n for the high one -- the raw bit patterns after one
+// v_and_or_b32 each.  The activations are staged so that this is exact arithmetic: x at
+// k % 8 in {2,3,6,7} (high-nibble slots) is pre-scaled by 1/16, making a_k * (1024 + 16 n)
+// = 64 x_k + x_k n, and the MFMA sum t of one 128-k group then equals
+//   sum_k x_k (n_k - 8) + D,   D = 1032 * sum_lo a_k + 1152 * sum_hi a_k,
+// with D depending only on the activation row and the group: it is precomputed once per
+// workgroup (corr table) and subtracted before the group scale is applied.
+__device__ __forceinline__ f16x8 deq_int4_raw(uint32_t w, uint32_t magic) {
+  const uint32_t w8 = w >> 8;
+  u32x4 r;
+  r[0] = (w & 0x000F000Fu) | magic;
+  r[1] = (w & 0x00F000F0u) | magic;
+  r[2] = (w8 & 0x000F000Fu) | magic;
+  r[3] = (w8 & 0x00F000F0u) | magic;
+  return __builtin_bit_cast(f16x8, r);
+}
+
 template <int BITS>
 __device__ __forceinline__ f16x8 dequant_step(const u32x4 (&w)[BITS / 4], int s4, uint32_t magic) {
   if constexpr (BITS == 4) {
-    return deq_int4_word(w[0][s4], magic);
+    return deq_int4_raw(w[0][s4], magic);
   } else if constexpr (BITS == 8) {
     f16x8 r;
     const u32x4 c = w[s4 >> 1];
@@ -271,6 +276,18 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int 
   }
 }
 
+// Weight stream load: read once per launch, so non-temporal where that pays (TI_GEMV_NT).
+#ifndef TI_GEMV_NT
+#define TI_GEMV_NT 0
+#endif
+__device__ __forceinline__ u32x4 ld_w(const u32x4* p) {
+#if TI_GEMV_NT || (TI_GEMV_EXP & 16)
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 // --------------------------------------------------------------------- kernel
 // LDS barrier that leaves the wave's outstanding global loads in flight (a plain
 // __syncthreads() may drain vmcnt): LDS writes retired, then s_barrier.
@@ -298,6 +315,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs
   const GemvLds L = gemv_lds_layout(a.M, a.K, ntl);
   f16* xl = (f16*)(smem + L.x);
   uint16_t* sl = (uint16_t*)(smem + L.sc);
+  float* corr = (float*)(smem + L.corr);           // [K/128][16] (int4 only)
   f32x4* slab = (f32x4*)(smem + L.slab);           // [ntl + 1][8][64]
   float* es = (float*)(smem + L.es);
   unsigned long long* best_l = (unsigned long long*)(smem + L.best);
@@ -307,12 +325,21 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs
   const int n_sc = BITS == 16 ? 0 : ntl * KT * 2;  // u32x4 pieces of scales
   const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16);
   u32x4 sc_reg = {0u, 0u, 0u, 0u};
+#if TI_GEMV_EXP & 8   // diagnostic: no dependency on x / scales (constants instead of loads)
+  const int nx16 = a.M * K8;
+  float4 v0 = {1.0f, 1.0f, 1.0f, 1.0f}, v1 = v0, w0 = v0, w1 = v0;
+  u32x4 xr16[XPF];
+  for (int q = 0; q < XPF; ++q) xr16[q] = (u32x4){0x3c003c00u, 0x3c003c00u, 0x3c003c00u, 0x3c003c00u};
+  sc_reg = xr16[0];
+  if (false) {
+#else
   if constexpr (BITS != 16) sc_reg = sg[tid < n_sc ? tid : 0];
 
   const int nx16 = a.M * K8;
   float4 v0, v1, w0, w1;
   u32x4 xr16[XPF];
   if constexpr (XM == XM_NORM1) {
+#endif
     const int k8 = tid < K8 ? tid : K8 - 1;
     const float* xr = (const float*)a.x;
     v0 = *(const float4*)(xr + 8 * k8);
@@ -353,12 +380,17 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs
     if (++rk == KW) { rk = 0; ++rt; }
     return o;
   };
+  // Only the first R0 slots go out before the staging barrier: a CU's memory pipe accepts a
+  // limited number of outstanding loads, so a wave issuing all R slots blocks in issue for
+  // microseconds, and the barrier (hence the first MFMA) would wait for the slowest wave's
+  // whole burst.  The rest of the ring is issued right after the barrier.
+  constexpr int R0 = R >= 8 ? 4 : R;
   u32x4 ring[R][C];
 #pragma unroll
-  for (int s = 0; s < R; ++s) {
+  for (int s = 0; s < R0; ++s) {
     const size_t o = refill_off();
 #pragma unroll
-    for (int c = 0; c < C; ++c) ring[s][c] = tb[o + c * kWave];
+    for (int c = 0; c < C; ++c) ring[s][c] = ld_w(tb + o + c * kWave);
   }
 
   GEMV_TS(1);
@@ -410,6 +442,39 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs
   if (a.epi.kind == TI_EPI_QKV_ROPE_KV && tid < a.M) ((int*)(es + a.M * a.epi.head_dim))[tid] = __builtin_bit_cast(int, pre);
   if (tid < 16) best_l[tid] = 0ull;
   lds_barrier();
+#pragma unroll
+  for (int s = R0; s < R; ++s) {
+    const size_t o = refill_off();
+#pragma unroll
+    for (int c = 0; c < C; ++c) ring[s][c] = ld_w(tb + o + c * kWave);
+  }
+  if constexpr (BITS == 4) {
+    // Offset-folded int4 (deq_int4_raw): scale the high-nibble slots of x by 1/16 (exact in
+    // fp16) and build corr[g][m] = 1032 * sum_lo a + 1152 * sum_hi a per 128-k group.  A
+    // group is 16 consecutive k8 pieces, i.e. 16 consecutive lanes (K8 % 16 == 0).
+    const f16 s16 = (f16)0.0625f;
+    for (int i0 = 0; i0 < a.M * K8; i0 += kGemvThreads) {
+      const int idx = i0 + tid;
+      float part = 0.0f;
+      int m = 0, k8 = 0;
+      if (idx < a.M * K8) {
+        m = idx / K8;
+        k8 = idx - m * K8;
+        f16x8 h = *(const f16x8*)(xl + m * xs + 8 * k8);
+        h[2] *= s16; h[3] *= s16; h[6] *= s16; h[7] *= s16;
+        *(f16x8*)(xl + m * xs + 8 * k8) = h;
+        const float lo = ((float)h[0] + (float)h[1]) + ((float)h[4] + (float)h[5]);
+        const float hi = ((float)h[2] + (float)h[3]) + ((float)h[6] + (float)h[7]);
+        part = 1032.0f * lo + 1152.0f * hi;
+      }
+      part += __shfl_xor(part, 1, kWave);
+      part += __shfl_xor(part, 2, kWave);
+      part += __shfl_xor(part, 4, kWave);
+      part += __shfl_xor(part, 8, kWave);
+      if (idx < a.M * K8 && (lane & 15) == 0) corr[(k8 >> 4) * 16 + m] = part;
+    }
+    lds_barrier();
+  }
 
   // RoPE (cos, sin) of each row's position: issued now, consumed after the stream.
   float cs_reg = 0.0f;
@@ -424,7 +489,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs
   const int r = lane & 15, kq = lane >> 4;
   const f16* xrow = xl + (r < a.M ? r : a.M - 1) * xs + kq * 32;
   f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-  uint32_t magic;   // 0x64006400 in a VGPR (see deq_int4_word)
+  uint32_t magic;   // 0x64006400 in a VGPR (see deq_int4_raw)
   asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
   f32x4* my_slab = slab + wave * kWave + lane;     // + tile * 8 * 64
   constexpr int kSlabStride = kGemvWaves * kWave;
@@ -446,6 +511,10 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs
     if constexpr (BITS == 16) {
       acc = t;
     } else {
+      if constexpr (BITS == 4) {   // remove the folded offsets of this group (deq_int4_raw)
+        const f32x4 cr = *(const f32x4*)(corr + kt * 16 + 4 * kq);
+        t -= cr;
+      }
       const float sc = h2f(sl[(ct * KT + kt) * 16 + r]);
       acc[0] = fmaf(sc, t[0], acc[0]);
       acc[1] = fmaf(sc, t[1], acc[1]);
@@ -466,7 +535,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs
       item(ring[s]);
       const size_t o = refill_off();   // refill this slot R items ahead (clamped past the end)
 #pragma unroll
-      for (int c = 0; c < C; ++c) ring[s][c] = tb[o + c * kWave];
+      for (int c = 0; c < C; ++c) ring[s][c] = ld_w(tb + o + c * kWave);
     }
   }
 #pragma unroll
