@@ -196,3 +196,48 @@ def test_engine_compat_plumbing_matches_reference_generate(ti, oracle, golden):
         lg0 = e.compat_step((len(prompt) - 1) * H)
         np.testing.assert_array_equal(lg0.view(np.uint32), olog.view(np.uint32))
     e.close()
+
+
+def _full_shape_step(ti, oracle, cfg, seed, fill, kv_seed):
+    ref, ref_logits = _oracle_tokens(oracle, cfg, seed, 0.0, [seed % cfg["vocab"]], 1, fill, kv_seed)
+    e = engine_for(ti, cfg)
+    e.synth(seed, 0.0)
+    e.fill_kv(0, fill, kv_seed)
+    got, lg = e.generate([[seed % cfg["vocab"]]], 1, start_pos=[fill], want_logits=True)
+    assert_logits_close(lg[0], ref_logits[0])
+    if margin(ref_logits[0]) > REL * np.max(np.abs(ref_logits[0])):
+        assert int(got[0, 0]) == ref[0]
+    e.close()
+
+
+def test_engine_tinyllama_int8_shape(ti, oracle):
+    """BASELINE config 2 shapes: TinyLlama-1.1B (H 2048, 32 q / 4 kv heads x 64, I 5632,
+    vocab 32000) with INT8 g128 weights, two layers, 2047 cached slots."""
+    cfg = dict(vocab=32000, hidden=2048, layers=2, heads=32, kv_heads=4, head_dim=64, inter=5632,
+               rope_theta=10000.0, eps=1e-5, bits=8, group=128, max_seq=2048)
+    _full_shape_step(ti, oracle, cfg, 1101, 2047, 11)
+
+
+def test_engine_llama3_8b_gqa_long_context_shape(ti, oracle):
+    """BASELINE config 5 shapes: Llama-3-8B (H 4096, 32 q / 8 kv heads x 128, I 14336,
+    vocab 128256, rope theta 5e5) INT4 g128, two layers, 8191 cached slots (8192-token KV)."""
+    cfg = dict(vocab=128256, hidden=4096, layers=2, heads=32, kv_heads=8, head_dim=128, inter=14336,
+               rope_theta=500000.0, eps=1e-5, bits=4, group=128, max_seq=8192)
+    _full_shape_step(ti, oracle, cfg, 808, 8191, 5)
+
+
+def test_engine_batch_beyond_one_gemm_chunk(ti, oracle):
+    """20 streams (more than the 16 rows one GEMV launch takes): chunked M, every stream still
+    an independent request."""
+    seed, jit = 31, 0.1
+    prompts = [[(7 * b + 1) % MID["vocab"], (11 * b + 5) % MID["vocab"]] for b in range(20)]
+    e = engine_for(ti, MID, max_batch=20)
+    e.synth(seed, jit)
+    got = e.generate(prompts, 3)
+    e.close()
+    for b in (0, 7, 16, 19):
+        ref, ref_logits = _oracle_tokens(oracle, MID, seed, jit, prompts[b], 3)
+        for i, (g, r) in enumerate(zip(got[b].tolist(), ref)):
+            if margin(ref_logits[i]) <= REL * np.max(np.abs(ref_logits[i])):
+                break
+            assert g == r, (b, i, got[b], ref)

@@ -94,7 +94,7 @@ int main(int argc, char** argv) {
         CK(hipStreamSynchronize(s));
         static unsigned long long ts[4096 * 8];
         CK(hipMemcpyFromSymbol(ts, HIP_SYMBOL(ti::g_gemv_ts), sizeof(ts)));
-        const int grid = ti::gemv_grid(sh.N, 256);
+        const int grid = ti::gemv_grid(1, sh.N, sh.K, 256);
         unsigned long long t0 = ~0ull, tend = 0;
         double ph[4][3];
         for (int k = 0; k < 4; ++k) ph[k][0] = 1e30, ph[k][1] = 0, ph[k][2] = 0;

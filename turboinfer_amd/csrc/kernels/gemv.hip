@@ -62,14 +62,20 @@ __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
 // weights in flight), never more than there are 16-row tiles.
 static int g_wg_per_cu = 0;   // TI_GEMV_WG_PER_CU (tuning knob), default 1
 
-__host__ inline int gemv_grid(int N, int num_cus) {
+__host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_wg);
+
+// Tiles per workgroup are bounded by the LDS image (partial slabs and scales grow with
+// them): very wide outputs (a 128k vocabulary) get more workgroups than CUs.
+__host__ inline int gemv_grid(int M, int N, int K, int num_cus) {
   if (g_wg_per_cu <= 0) {
     const char* s = getenv("TI_GEMV_WG_PER_CU");
     g_wg_per_cu = s && atoi(s) > 0 ? atoi(s) : 1;
   }
   const int NT = N >> 4;
   const int g = g_wg_per_cu * (num_cus > 0 ? num_cus : 256);
-  return NT < g ? NT : g;
+  int grid = NT < g ? NT : g;
+  while (grid < NT && gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid) > 160 * 1024) grid += grid / 8 + 1;
+  return grid < NT ? grid : NT;
 }
 
 // LDS image of one workgroup (bytes, each region 16-aligned):
@@ -631,7 +637,7 @@ extern "C" int ti_gemm_prepare(void) {
 
 extern "C" int ti_gemm_lds_bytes(int M, int N, int K) {
   if (M < 1 || N < 16 || K < 128) return 0;
-  const int NT = N >> 4, grid = ti::gemv_grid(N, query_cus());
+  const int NT = N >> 4, grid = ti::gemv_grid(M, N, K, query_cus());
   return ti::gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid);
 }
 
@@ -669,7 +675,7 @@ extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bit
     default:
       return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: unknown epilogue %d", epi->kind);
   }
-  const int grid = gemv_grid(N, query_cus());
+  const int grid = gemv_grid(M, N, K, query_cus());
   const int lds = gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid);
   if (lds > 160 * 1024)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: M*K too large for one LDS stage (M=%d K=%d)", M, K);
