@@ -37,7 +37,6 @@ __global__ __launch_bounds__(512, 1) void edge_kernel(u32x2* vec, int N, int rou
                                                       size_t w_items, int* abort_flag, float* out,
                                                       unsigned long long* ts) {
   __shared__ float xs[16384];
-  __shared__ int s_bad;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int per = N / gridDim.x;   // slice of this WG
   u32x4 ring[16];
@@ -56,36 +55,43 @@ __global__ __launch_bounds__(512, 1) void edge_kernel(u32x2* vec, int N, int rou
       const float v = (float)(blockIdx.x * per + i) + acc * 0.0f;
       st_granule(buf + (size_t)blockIdx.x * per + i, (u32x2){__float_as_uint(v), tag});
     }
-    // consume the whole vector
-    int spins = 0;
-    for (;;) {
-      if (tid == 0) s_bad = 0;
-      __syncthreads();
-      // every load of the sweep in flight before any is checked (16 B = 2 granules each)
-      int bad = 0;
+    // consume the whole vector: every lane owns a fixed set of granule pairs, issues all of
+    // its loads, then re-polls only its own stale ones (bounded), staging into LDS.
+    {
+      int spins = 0;
+      const int npairs = N / 2;
       u32x4 g[8];
+      int idx[8];
+      unsigned pending = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const int i2 = tid + k * 512;
-        g[k] = ld_granule2(buf + 2 * (i2 < N / 2 ? i2 : 0));
+        idx[k] = tid + k * 512;
+        if (idx[k] < npairs) pending |= 1u << k;
+        g[k] = ld_granule2(buf + 2 * (idx[k] < npairs ? idx[k] : 0));
       }
+      while (pending) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int i2 = tid + k * 512;
-        if (i2 < N / 2) {
-          if (g[k][1] != tag || g[k][3] != tag) bad = 1;
-          xs[2 * i2] = __uint_as_float(g[k][0]);
-          xs[2 * i2 + 1] = __uint_as_float(g[k][2]);
+        for (int k = 0; k < 8; ++k) {
+          if (pending & (1u << k)) {
+            if (g[k][1] == tag && g[k][3] == tag) {
+              xs[2 * idx[k]] = __uint_as_float(g[k][0]);
+              xs[2 * idx[k] + 1] = __uint_as_float(g[k][2]);
+              pending &= ~(1u << k);
+            }
+          }
         }
+        if (!pending) break;
+        if (++spins > (1 << 22)) {
+          atomicExch(abort_flag, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (pending & (1u << k)) g[k] = ld_granule2(buf + 2 * idx[k]);
       }
-      if (bad) s_bad = 1;
       __syncthreads();
-      if (!s_bad) break;
-      if (++spins > (1 << 20) || *(volatile int*)abort_flag) {
-        if (tid == 0) atomicExch(abort_flag, 1);
-        return;
-      }
-      __builtin_amdgcn_s_sleep(2);
+      if (*(volatile int*)abort_flag) return;
     }
     float s = 0.0f;
     for (int i = tid; i < N; i += 512) s += xs[i];

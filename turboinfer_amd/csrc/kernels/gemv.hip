@@ -32,6 +32,12 @@ namespace ti {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef TI_GEMV_RING_VGPRS
+// VGPRs per lane of packed weights in flight.  Deeper is slower: a CU accepts a bounded
+// number of outstanding loads, and a wave whose refill cannot issue stalls before its next
+// item's math (tools/probe_gemv.hip sweep: 16-24 best, 64 costs ~15 %).
+#define TI_GEMV_RING_VGPRS 24
+#endif
 #ifndef TI_GEMV_EXP
 #define TI_GEMV_EXP 0   // product build; tools/probe_gemv.hip compiles diagnostic variants
 #endif
@@ -306,7 +312,7 @@ __device__ __forceinline__ void lds_barrier() {
 template <int BITS, int XM>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs a) {
   constexpr int C = TileFmt<BITS>::kChunks;
-  constexpr int R = 64 / (4 * C);                  // ring depth: 16 / 8 / 4 items (64 VGPRs of weights)
+  constexpr int R = TI_GEMV_RING_VGPRS / (4 * C) > 2 ? TI_GEMV_RING_VGPRS / (4 * C) : 2;   // ring depth (items)
   constexpr int XPF = 3;                           // fp16 x: 16-byte pieces prefetched per thread
   extern __shared__ __attribute__((aligned(16))) char smem[];
   GEMV_TS(0);
