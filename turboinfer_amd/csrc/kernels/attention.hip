@@ -41,6 +41,9 @@ struct AttnArgs {
   float scale;
 };
 
+#ifndef TI_ATTN_RING
+#define TI_ATTN_RING 2   // K (and V) slots in flight per wave; deeper stalls on issue (tools/probe_attn.hip)
+#endif
 constexpr int kAttnWaves = 8;
 constexpr int kAttnThreads = kAttnWaves * kWave;
 
@@ -73,7 +76,7 @@ template <int HD, int G>
 __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnArgs a) {
   constexpr int LPK = HD / 8;       // lanes per key row
   constexpr int KPW = 64 / LPK;     // keys per slot (wave-load)
-  constexpr int R = 8;              // slots in flight per operand
+  constexpr int R = TI_ATTN_RING;   // slots in flight per operand
   __shared__ float s_m[kAttnWaves][G], s_l[kAttnWaves][G];
   __shared__ __attribute__((aligned(16))) float s_acc[kAttnWaves][G][HD];
   __shared__ __attribute__((aligned(16))) float s_part[48 * 1024 / 4];   // merged rows, then all partials
