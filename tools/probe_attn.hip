@@ -80,6 +80,32 @@ int main(int argc, char** argv) {
              splits, splits * sh.kv, us, 2.0 * kv_bytes * sh.L / max_seq / us / 1e3);
       CK(hipGraphExecDestroy(ge));
       CK(hipGraphDestroy(g));
+#if TI_ATTN_EXP & 4
+      {   // one more launch, then per-workgroup phases: 0 start, 1 stream done, 2 merged, 3 ticket, 4 end (last)
+        const uint16_t* kc = (const uint16_t*)kvbuf;
+        if (ti_attn_decode(q, kc, kc + kv_bytes / 2, (int64_t)sh.kv * max_seq * sh.hd, max_seq, pos, 1, sh.heads,
+                           sh.kv, sh.hd, splits, ws, out, s))
+          return 1;
+        CK(hipStreamSynchronize(s));
+        static unsigned long long ts[4096 * 8];
+        CK(hipMemcpyFromSymbol(ts, HIP_SYMBOL(ti::g_attn_ts), sizeof(ts)));
+        const int nwg = splits * sh.kv;
+        unsigned long long t0 = ~0ull, tend = 0;
+        double ph[3] = {0, 0, 0}, last_tail = 0;
+        int nlast = 0;
+        for (int b = 0; b < nwg; ++b) t0 = ts[b * 8] < t0 ? ts[b * 8] : t0;
+        for (int b = 0; b < nwg; ++b) {
+          for (int k = 0; k < 3; ++k) ph[k] += (double)(ts[b * 8 + k + 1] - ts[b * 8 + k]) * 0.01 / nwg;
+          if (ts[b * 8 + 4] > ts[b * 8 + 3] && ts[b * 8 + 4] - ts[b * 8 + 3] < 100000) {
+            last_tail += (double)(ts[b * 8 + 4] - ts[b * 8 + 3]) * 0.01;
+            ++nlast;
+            tend = ts[b * 8 + 4] > tend ? ts[b * 8 + 4] : tend;
+          }
+        }
+        printf("   span %.2f us | stream %.2f | wave merge %.2f | publish+ticket %.2f | last-arriver merge %.2f (avg)\n",
+               (tend - t0) * 0.01, ph[0], ph[1], ph[2], nlast ? last_tail / nlast : 0.0);
+      }
+#endif
     }
   }
   return 0;

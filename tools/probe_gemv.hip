@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
   printf("TI_GEMV_EXP=%d\n", TI_GEMV_EXP);
   for (auto& sh : shapes) {
     const size_t tb = (size_t)sh.K * sh.N / 2, sb = (size_t)sh.K / 128 * sh.N * 2, per = (tb + sb + 4095) & ~(size_t)4095;
-    const int nbuf = (int)(big / per);
+    const int nbuf = getenv("PROBE_HOT") ? 1 : (int)(big / per);   // PROBE_HOT: same weights every launch (Infinity-Cache hot)
     for (int xk : {TI_X_F16, TI_X_F32_RMSNORM}) {
       ti_epilogue ep{};
       ep.kind = TI_EPI_STORE_F32;
