@@ -44,6 +44,20 @@ struct AttnArgs {
 #ifndef TI_ATTN_RING
 #define TI_ATTN_RING 2   // K (and V) slots in flight per wave; deeper stalls on issue (tools/probe_attn.hip)
 #endif
+#ifndef TI_ATTN_EXP
+#define TI_ATTN_EXP 0   // product build; tools/probe_attn.hip: +4 = per-workgroup phase timestamps
+#endif
+#if TI_ATTN_EXP & 4
+__device__ unsigned long long g_attn_ts[4096 * 8];
+#define ATTN_TS(k)                                                                                        \
+  do {                                                                                                    \
+    if (threadIdx.x == 0)                                                                                 \
+      g_attn_ts[(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x * 8 + blockIdx.x * 8 + (k)] =            \
+          __builtin_amdgcn_s_memrealtime();                                                               \
+  } while (0)
+#else
+#define ATTN_TS(k) do { } while (0)
+#endif
 constexpr int kAttnWaves = 8;
 constexpr int kAttnThreads = kAttnWaves * kWave;
 
@@ -82,6 +96,7 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
   __shared__ __attribute__((aligned(16))) float s_part[48 * 1024 / 4];   // merged rows, then all partials
   __shared__ int s_last;
 
+  ATTN_TS(0);
   const int split = blockIdx.x, kvh = blockIdx.y, m = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -160,6 +175,7 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
   for (int s = 0; s < R; ++s)
     if (j0 + s < total) consume(kr[s], vr[s]);
 
+  ATTN_TS(1);
   // merge the lane groups of the wave (each holds its own max / sum / o)
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -227,6 +243,7 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
   if (a.splits == 1) return;
   __syncthreads();
 
+  ATTN_TS(2);
   // ---- publish: the G rows of this split, write-through 16-byte stores.  Partials of
   // (stream, head) are contiguous: [m][h][split][row].
   constexpr int V4 = (HD + 4) / 4;
@@ -246,6 +263,7 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
     s_last = (t == a.splits - 1);
   }
   __syncthreads();
+  ATTN_TS(3);
   if (!s_last) return;
   // all partials of the group's heads in one round trip: s_part[g][split][row]
   const int nv = G * a.splits * V4;
@@ -272,6 +290,7 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
     a.out[(size_t)m * a.heads * HD + (size_t)h * HD + d] = f2h(num / den);
   }
   if (tid == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  ATTN_TS(4);
 }
 
 template <int HD, int G>
