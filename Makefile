@@ -29,6 +29,11 @@ $(BUILD)/k_ops_exact.o: turboinfer_amd/csrc/kernels/ops_exact.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(DEVFLAGS) -ffp-contract=off -c $< -o $@
 
+# gemv: preload its leading kernel arguments into SGPRs (gfx950 kernarg preload)
+$(BUILD)/k_gemv.o: turboinfer_amd/csrc/kernels/gemv.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(DEVFLAGS) -mllvm -amdgpu-kernarg-preload-count=16 -c $< -o $@
+
 $(BUILD)/k_%.o: turboinfer_amd/csrc/kernels/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(DEVFLAGS) -c $< -o $@

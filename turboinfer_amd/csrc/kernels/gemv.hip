@@ -309,8 +309,26 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// The fields on the prologue's critical path come first as separate arguments: gfx950 can
+// preload leading kernel arguments into SGPRs before the waves start (compiled with
+// -mllvm -amdgpu-kernarg-preload-count, see Makefile), so the first x / weight / epilogue-input
+// loads do not wait for a kernarg s_load round trip (the grid size is passed too: gridDim
+// comes from the hidden kernargs).  The struct carries everything else.
 template <int BITS, int XM>
-__global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs a) {
+__global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
+                                                                   const void* p_x, const float* p_norm_w, int p_M,
+                                                                   int p_N, int p_K, int p_ldx, int p_grid,
+                                                                   const float* p_pre, int p_kind_ldo,
+                                                                   const GemvArgs a_in) {
+  GemvArgs a = a_in;
+  a.tiles = p_tiles;
+  a.scales = p_scales;
+  a.x = p_x;
+  a.norm_w = p_norm_w;
+  a.M = p_M;
+  a.N = p_N;
+  a.K = p_K;
+  a.ldx = p_ldx;
   constexpr int C = TileFmt<BITS>::kChunks;
   constexpr int R = TI_GEMV_RING_VGPRS / (4 * C) > 2 ? TI_GEMV_RING_VGPRS / (4 * C) : 2;   // ring depth (items)
   constexpr int XPF = 3;                           // fp16 x: 16-byte pieces prefetched per thread
@@ -319,8 +337,8 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs
   const int KT = a.K >> 7, xs = a.K + 8, NT = a.N >> 4, K8 = a.K >> 3;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: counters live in SGPRs
-  const int t0 = (int)((int64_t)blockIdx.x * NT / gridDim.x);
-  const int t1 = (int)((int64_t)(blockIdx.x + 1) * NT / gridDim.x);
+  const int t0 = (int)(blockIdx.x * (unsigned)NT / (unsigned)p_grid);   // NT * grid < 2^32
+  const int t1 = (int)((blockIdx.x + 1) * (unsigned)NT / (unsigned)p_grid);
   const int ntl = t1 - t0;
   const int KW = wave < KT ? (KT - wave + kGemvWaves - 1) / kGemvWaves : 0;   // k-tiles per tile, this wave
   const int total = ntl * KW;
@@ -369,14 +387,15 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const GemvArgs
   // Epilogue input, one word per thread, loaded unconditionally (a branch here would make
   // the compiler wait at the join): a residual element of our tiles, this step's position
   // of row tid, or a dummy word of x.
-  const int n_res = a.epi.kind == TI_EPI_RESID_F32 ? ntl * a.M * 16 : 0;
+  // (p_pre / p_kind_ldo are preloaded: epi.out for RESID, epi.pos for QKV, else x)
+  const int kind = p_kind_ldo & 7, ldo = p_kind_ldo >> 3;
+  const int n_res = kind == TI_EPI_RESID_F32 ? ntl * a.M * 16 : 0;
   const float* pre_p;
   {
     const int idx = tid < n_res ? tid : 0;
     const int tl = idx / (a.M * 16), rem = idx - tl * a.M * 16, m = rem >> 4, n = rem & 15;
-    const float* rp = (const float*)a.epi.out + (size_t)m * a.epi.ldo + (t0 + tl) * 16 + n;
-    const float* pp = (const float*)a.epi.pos + (tid < a.M ? tid : 0);
-    pre_p = a.epi.kind == TI_EPI_RESID_F32 ? rp : a.epi.kind == TI_EPI_QKV_ROPE_KV ? pp : (const float*)a.x;
+    pre_p = kind == TI_EPI_RESID_F32 ? p_pre + (size_t)m * ldo + (t0 + tl) * 16 + n
+            : kind == TI_EPI_QKV_ROPE_KV ? p_pre + (tid < a.M ? tid : 0) : p_pre;
   }
   const float pre = *pre_p;
 
@@ -596,11 +615,14 @@ __host__ inline int gemv_xmode(int x_kind, int M, int K) {
 
 template <int BITS>
 static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid) {
+  const float* pre = a.epi.kind == TI_EPI_RESID_F32 ? (const float*)a.epi.out
+                     : a.epi.kind == TI_EPI_QKV_ROPE_KV ? (const float*)a.epi.pos : (const float*)a.x;
+  const int kind_ldo = a.epi.kind | (a.epi.ldo << 3);
   switch (gemv_xmode(a.x_kind, a.M, a.K)) {
-    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16>), dim3(grid), dim3(kGemvThreads), lds, s, a); break;
-    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32>), dim3(grid), dim3(kGemvThreads), lds, s, a); break;
-    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1>), dim3(grid), dim3(kGemvThreads), lds, s, a); break;
-    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM>), dim3(grid), dim3(kGemvThreads), lds, s, a); break;
+    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a); break;
+    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a); break;
+    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a); break;
+    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a); break;
   }
   TI_LAUNCH_CHECK("gemv_wq_kernel");
   return TI_OK;
