@@ -6,12 +6,13 @@
 HIPCC   ?= /opt/rocm/bin/hipcc
 ARCH    ?= gfx950
 JOBS    ?= 8
-BUILD   := build
+BUILD   ?= build
 LIBDIR  := turboinfer_amd/lib
-LIB     := $(LIBDIR)/libturboinfer_amd.so
+LIB     ?= $(LIBDIR)/libturboinfer_amd.so
 
 COMMON  := -std=c++20 -O3 -fPIC -Iinclude -Iturboinfer_amd/csrc/kernels -Wall -Wno-unused-result -Wno-unused-value
-DEVFLAGS:= $(COMMON) --offload-arch=$(ARCH) -fno-gpu-rdc
+EXTRA   ?=
+DEVFLAGS:= $(COMMON) --offload-arch=$(ARCH) -fno-gpu-rdc $(EXTRA)
 
 KERN    := $(wildcard turboinfer_amd/csrc/kernels/*.hip)
 HOST    := $(wildcard turboinfer_amd/csrc/host/*.cpp)
@@ -48,7 +49,7 @@ $(BUILD)/a_%.o: turboinfer_amd/csrc/api/%.cpp $(HDRS)
 	$(HIPCC) $(COMMON) -ffp-contract=off -c $< -o $@
 
 $(LIB): $(KOBJ) $(HOBJ) $(AOBJ)
-	@mkdir -p $(LIBDIR)
+	@mkdir -p $(dir $@)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(KOBJ) $(HOBJ) $(AOBJ) -Wl,-soname,libturboinfer_amd.so
 
 # C++ API test drivers (tests/cpp/*.cpp -> tests/cpp/bin/), linked against the in-tree library

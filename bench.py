@@ -132,6 +132,7 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0x7157)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--attn-splits", type=int, default=0, help="0 = the engine's policy")
     args = ap.parse_args()
 
     import turboinfer_amd as T
@@ -142,7 +143,7 @@ def main() -> int:
     V, H, layers, nh, nkv, hd, I, bits, theta = m
     B, L = args.batch, args.kv
     e = T.Engine(V, H, layers, nh, nkv, hd, I, bits=bits, max_seq=L, max_batch=B, rope_theta=theta,
-                 device=g.local_rank)
+                 device=g.local_rank, attn_splits=args.attn_splits)
     e.synth(args.seed + g.rank, 0.0)
     for s in range(B):
         e.fill_kv(s, L - 1, args.seed + 1000 * g.rank + s)

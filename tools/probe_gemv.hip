@@ -115,6 +115,20 @@ int main(int argc, char** argv) {
             ph[k][2] = d > ph[k][2] ? d : ph[k][2];
           }
         }
+        static unsigned long long wts[4096 * 8];
+        CK(hipMemcpyFromSymbol(wts, HIP_SYMBOL(ti::g_gemv_wts), sizeof(wts)));
+        double skew = 0, w0late = 0, post = 0;
+        for (int b = 0; b < grid; ++b) {
+          unsigned long long lo = ~0ull, hi = 0;
+          for (int w = 0; w < 8; ++w) {
+            lo = wts[b * 8 + w] < lo ? wts[b * 8 + w] : lo;
+            hi = wts[b * 8 + w] > hi ? wts[b * 8 + w] : hi;
+          }
+          skew += (hi - lo) * 0.01 / grid;
+          w0late += (wts[b * 8] - lo) * 0.01 / grid;
+          post += (double)(ts[b * 8 + 4] - ts[b * 8 + 5]) * 0.01 / grid;
+        }
+        printf("   waves: end skew %.2f us, wave0 after first %.2f us | barrier->end %.2f us\n", skew, w0late, post);
         printf("   span %.2f us | start skew avg %.2f max %.2f | issue %.2f/%.2f/%.2f | stage %.2f/%.2f/%.2f | "
                "stream %.2f/%.2f/%.2f | epi %.2f/%.2f/%.2f (min/avg/max)\n",
                (tend - t0) * 0.01, start[1], start[2], ph[0][0], ph[0][1], ph[0][2], ph[1][0], ph[1][1], ph[1][2],

@@ -19,7 +19,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "lib", "libturboinfer_amd.so")
+# TI_LIB: an alternative in-tree build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("TI_LIB") or os.path.join(HERE, "lib", "libturboinfer_amd.so")
 
 TI_OK = 0
 X_F16, X_F32, X_F32_RMSNORM = 0, 1, 2

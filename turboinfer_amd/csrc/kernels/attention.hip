@@ -86,6 +86,18 @@ constexpr int kAuxSc1 = 16;
 // workgroup can stage in its 48 KiB LDS buffer.
 __host__ __device__ constexpr int attn_max_splits(int G, int HD) { return (48 * 1024) / (G * (HD + 4) * 4); }
 
+// K/V rows are read once per step: non-temporal where that pays (TI_ATTN_NT).
+#ifndef TI_ATTN_NT
+#define TI_ATTN_NT 1
+#endif
+__device__ __forceinline__ u32x4 ld_kv(const u32x4* p) {
+#if TI_ATTN_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 template <int HD, int G>
 __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnArgs a) {
   constexpr int LPK = HD / 8;       // lanes per key row
@@ -117,8 +129,8 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
   auto refill = [&](int s) {
     const int key = min(slot_key(rj < total ? rj : max(total - 1, 0)), max(s1 - 1, 0));
     ++rj;
-    kr[s] = *(const u32x4*)(kb + (int64_t)key * HD);
-    vr[s] = *(const u32x4*)(vb + (int64_t)key * HD);
+    kr[s] = ld_kv((const u32x4*)(kb + (int64_t)key * HD));
+    vr[s] = ld_kv((const u32x4*)(vb + (int64_t)key * HD));
   };
 #pragma unroll
   for (int s = 0; s < R; ++s) refill(s);

@@ -36,7 +36,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // VGPRs per lane of packed weights in flight.  Deeper is slower: a CU accepts a bounded
 // number of outstanding loads, and a wave whose refill cannot issue stalls before its next
 // item's math (tools/probe_gemv.hip sweep: 16-24 best, 64 costs ~15 %).
-#define TI_GEMV_RING_VGPRS 24
+#define TI_GEMV_RING_VGPRS 20
+#endif
+#ifndef TI_GEMV_SYNC
+#define TI_GEMV_SYNC 0   // blocks of R items between workgroup barriers in the stream (0 = none)
 #endif
 #ifndef TI_GEMV_EXP
 #define TI_GEMV_EXP 0   // product build; tools/probe_gemv.hip compiles diagnostic variants
@@ -45,7 +48,11 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ unsigned long long g_gemv_ts[4096 * 8];
 #define GEMV_TS(k) \
   do { if (threadIdx.x == 0) g_gemv_ts[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+__device__ unsigned long long g_gemv_wts[4096 * 8];   // per-wave end of stream
+#define GEMV_WTS() \
+  do { if ((threadIdx.x & 63) == 0) g_gemv_wts[blockIdx.x * 8 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
+#define GEMV_WTS() do { } while (0)
 #define GEMV_TS(k) do { } while (0)
 #endif
 
@@ -222,14 +229,15 @@ __device__ __forceinline__ uint32_t float_order_key(float v) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-// Thread (l = lane, i = wave & 3) holds y[m][n] of tile nt with m = 4*(l>>4) + i,
-// n = l & 15 (the v_mfma_f32_16x16x32 C layout, reduced over the 8 waves).  `best` is the
+// Thread (l, i) holds y[m][n] of tile nt with m = 4*(l>>4) + i, n = l & 15 (the
+// v_mfma_f32_16x16x32 C layout, reduced over the 8 waves); l is the lane or, for M <= 4,
+// n alone.  Partners of the shuffles below (n ^ 1, n + 8) sit in the same 16-lane group.  `best` is the
 // thread's running argmax key for LOGITS_ARGMAX.
 __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int l, int i, float v, const float* es,
-                                         unsigned long long& best) {
+                                         unsigned long long& best, bool ok) {
   const ti_epilogue& e = a.epi;
   const int m = 4 * (l >> 4) + i, n = l & 15, ng = nt * 16 + n;
-  const bool live = m < a.M;
+  const bool live = ok && m < a.M;
   switch (e.kind) {
     case TI_EPI_STORE_F32:
       if (live) ((float*)e.out)[(size_t)m * e.ldo + ng] = v;
@@ -290,7 +298,7 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int 
 
 // Weight stream load: read once per launch, so non-temporal where that pays (TI_GEMV_NT).
 #ifndef TI_GEMV_NT
-#define TI_GEMV_NT 0
+#define TI_GEMV_NT 1
 #endif
 __device__ __forceinline__ u32x4 ld_w(const u32x4* p) {
 #if TI_GEMV_NT || (TI_GEMV_EXP & 16)
@@ -363,7 +371,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   sc_reg = xr16[0];
   if (false) {
 #else
-  if constexpr (BITS != 16) sc_reg = sg[tid < n_sc ? tid : 0];
+  if constexpr (BITS != 16) sc_reg = ld_w(sg + (tid < n_sc ? tid : 0));
 
   const int nx16 = a.M * K8;
   float4 v0, v1, w0, w1;
@@ -560,6 +568,26 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
     ct += last ? 1 : 0;
   };
   int j0 = 0;
+#if TI_GEMV_SYNC > 0
+  // Waves of a CU drift apart (the oldest wins issue arbitration); a workgroup barrier every
+  // TI_GEMV_SYNC blocks keeps them together while every wave still has blocks left (the
+  // count of barriers is the same for all waves: blocks below the smallest wave total).
+  const int common = ntl * (KT / kGemvWaves);
+  int blk = 0;
+  for (; j0 + R <= common; j0 += R) {
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      item(ring[s]);
+      const size_t o = refill_off();
+#pragma unroll
+      for (int c = 0; c < C; ++c) ring[s][c] = ld_w(tb + o + c * kWave);
+    }
+    if (++blk == TI_GEMV_SYNC) {
+      blk = 0;
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+#endif
   for (; j0 + R <= total; j0 += R) {   // full blocks: no branches, R items scheduled together
 #pragma unroll
     for (int s = 0; s < R; ++s) {
@@ -576,27 +604,53 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
     for (int tl = 0; tl < ntl; ++tl) my_slab[tl * kSlabStride] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 
   GEMV_TS(3);
+  GEMV_WTS();
   // ---- 5. epilogue inputs into LDS, reduce the 8 partials per tile, epilogue
   if (tid < n_res) es[tid] = pre;
   if (tid < n_cs) es[tid] = cs_reg;
   lds_barrier();
-  unsigned long long best = 0ull;
-  const int i4 = wave & 3;
-  for (int tl = wave >> 2; tl < ntl; tl += 2) {
-    const float* sp = (const float*)(slab + tl * kSlabStride + lane) + i4;
-    float v = 0.0f;
+  GEMV_TS(5);
+  unsigned long long best[4] = {0ull, 0ull, 0ull, 0ull};
+  if (a.M <= 4) {
+    // rows m < 4 live in lanes 0-15 of each partial (C layout m = 4*(l>>4) + i): one thread per
+    // (tile, n), all tiles in one pass over the workgroup, the M components of its f32x4.
+    for (int tb0 = wave * kWave; tb0 < ntl * 16; tb0 += kGemvThreads) {
+      const int t = tb0 + lane, ok = t < ntl * 16, tl = ok ? t >> 4 : 0, n = lane & 15;
+      const f32x4* sp = slab + tl * kSlabStride + n;
+      f32x4 v = sp[0];
 #pragma unroll
-    for (int w = 0; w < kGemvWaves; ++w) v += sp[w * kWave * 4];
-    epilogue(a, t0 + tl, tl, lane, i4, v, es, best);
+      for (int w = 1; w < kGemvWaves; ++w) v += sp[w * kWave];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (i < a.M) epilogue(a, t0 + tl, tl, n, i, v[i], es, best[i], ok);
+    }
+  } else {
+    const int i4 = wave & 3;
+    for (int tl = wave >> 2; tl < ntl; tl += 2) {
+      const float* sp = (const float*)(slab + tl * kSlabStride + lane) + i4;
+      float v = 0.0f;
+#pragma unroll
+      for (int w = 0; w < kGemvWaves; ++w) v += sp[w * kWave * 4];
+      epilogue(a, t0 + tl, tl, lane, i4, v, es, best[0], true);
+    }
   }
   if (a.epi.kind == TI_EPI_LOGITS_ARGMAX) {
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      const unsigned long long other = __shfl_xor(best, o, kWave);
-      best = other > best ? other : best;
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const unsigned long long other = __shfl_xor(best[i], o, kWave);
+        best[i] = other > best[i] ? other : best[i];
+      }
     }
-    const int m = 4 * (lane >> 4) + i4;
-    if ((lane & 15) == 0 && m < a.M && best) atomicMax(best_l + m, best);
+    if (a.M <= 4) {
+      if ((lane & 15) == 0)
+        for (int i = 0; i < a.M; ++i)
+          if (best[i]) atomicMax(best_l + i, best[i]);
+    } else {
+      const int m = 4 * (lane >> 4) + (wave & 3);
+      if ((lane & 15) == 0 && m < a.M && best[0]) atomicMax(best_l + m, best[0]);
+    }
     lds_barrier();
     if (tid < a.M && best_l[tid])
       atomicMax(a.epi.argmax + (size_t)tid * TI_ARGMAX_SLOTS + (blockIdx.x & (TI_ARGMAX_SLOTS - 1)), best_l[tid]);
