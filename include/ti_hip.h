@@ -109,7 +109,7 @@ int ti_fill_kv_uniform(uint64_t seed, uint32_t tensor_id, int n, int kv_heads, i
                        uint16_t* dst, ti_stream_t s);
 
 /* ---------------------------------------------------- fused decode GEMM/GEMV
- * y[m][n] = sum_k xa[m][k] * W[k][n], m < M <= 16, with
+ * y[m][n] = sum_k xa[m][k] * W[k][n], m < M <= TI_GEMM_MAX_ROWS (see ti_gemm_max_rows), with
  *   xa = fp16(x)                               (x_kind TI_X_F16 / TI_X_F32), or
  *   xa = fp16((x / sqrt(mean(x^2)+eps)) * nw)  (x_kind TI_X_F32_RMSNORM; fused rms_norm)
  * fp16 x fp16 products on MFMA v_mfma_f32_16x16x32_f16, fp32 accumulation, group scale
@@ -154,8 +154,21 @@ typedef struct ti_epilogue {
 int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind,
                    int ldx, const float* norm_w, float eps, int M, int N, int K,
                    const ti_epilogue* epi, ti_stream_t s);
-/* LDS bytes one workgroup of ti_gemm_wq_a16 needs for an M x N x K call (<= 160 KiB). */
+/* LDS bytes one workgroup of the fused kernel needs for an M x N x K call (<= 160 KiB). */
 int ti_gemm_lds_bytes(int M, int N, int K);
+/* Rows (M) per ti_gemm_wq_a16 call the library prefers for this shape and activation kind.
+ * Two kernels: the fused one (rms_norm prologue, any bits) takes up to 16 rows while its LDS
+ * image fits; for bits 4 with TI_X_F16 rows the batched-rows kernel takes up to
+ * TI_GEMM_MAX_ROWS rows at any K (batched decode, generate_batch inference_engine.cpp:804-828)
+ * and is used above TI_GEMM_FUSED_ROWS (env, default 2) rows.  An int4 caller with more rows
+ * than this returns for TI_X_F32_RMSNORM should normalise them with ti_rmsnorm_f16 and pass
+ * TI_X_F16 rows.  0 = shape unsupported. */
+#define TI_GEMM_MAX_ROWS 32
+int ti_gemm_max_rows(int bits, int x_kind, int N, int K);
+/* y[m][0:K] = fp16(rms_norm(x[m][0:K]) * w), tensor_engine.cpp:1452-1508 (the batched path's
+ * activation prep; the same arithmetic as the fused TI_X_F32_RMSNORM prologue). */
+int ti_rmsnorm_f16(const float* x, int ldx, const float* w, float eps, uint16_t* y, int ldy, int M, int K,
+                   ti_stream_t s);
 /* One-time kernel attribute setup; call before capturing ti_gemm_wq_a16 into a graph. */
 int ti_gemm_prepare(void);
 

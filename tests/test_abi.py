@@ -28,6 +28,16 @@ def L():
     return T.lib()
 
 
+def test_gemm_max_rows(L):
+    # fused kernel: rows while the LDS image fits; int4 + fp16 rows: the batched-rows kernel
+    assert L.ti_gemm_max_rows(4, T.X_F16, 4096, 4096) == T.GEMM_MAX_ROWS
+    assert L.ti_gemm_max_rows(4, T.X_F16, 4096, 11008) == T.GEMM_MAX_ROWS
+    assert L.ti_gemm_max_rows(4, T.X_F32_RMSNORM, 12288, 4096) == 2
+    assert L.ti_gemm_max_rows(8, T.X_F32_RMSNORM, 12288, 4096) == 16
+    assert 1 <= L.ti_gemm_max_rows(8, T.X_F16, 4096, 11008) < 16
+    assert L.ti_gemm_max_rows(4, T.X_F16, 8, 4096) == 0
+
+
 def test_exports_every_declared_symbol(L):
     declared = header_functions(os.path.join(ROOT, "include", "ti_hip.h")) + \
         header_functions(os.path.join(ROOT, "include", "ti_engine.h"))
@@ -50,6 +60,15 @@ def test_argument_errors_are_reported_without_launch(L):
     assert rc == 1 and b"K %" in L.ti_last_error()
     # bad bits
     rc = L.ti_gemm_wq_a16(1, 1, 3, 1, T.X_F16, 128, None, 1e-5, 1, 16, 128, C.byref(ep), None)
+    assert rc == 1
+    # rows beyond the fused kernel need int4 + fp16 rows (the batched-rows kernel)
+    rc = L.ti_gemm_wq_a16(1, 1, 4, 1, T.X_F32_RMSNORM, 11008, 1, 1e-5, 12, 16, 11008, C.byref(ep), None)
+    assert rc == 3 and b"batched-rows" in L.ti_last_error()
+    rc = L.ti_gemm_wq_a16(1, 1, 8, 1, T.X_F16, 4096, None, 1e-5, 20, 16, 4096, C.byref(ep), None)
+    assert rc == 3
+    rc = L.ti_gemm_wq_a16(1, 1, 4, 1, T.X_F16, 4096, None, 1e-5, T.GEMM_MAX_ROWS + 1, 16, 4096, C.byref(ep), None)
+    assert rc == 1 and b"M must be" in L.ti_last_error()
+    rc = L.ti_rmsnorm_f16(1, 100, 1, 1e-5, 1, 128, 2, 128, None)
     assert rc == 1
     # attention head_dim unsupported
     rc = L.ti_attn_decode(1, 1, 1, 1 << 20, 16, 1, 1, 4, 4, 96, 1, 1, 1, None)

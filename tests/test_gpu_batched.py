@@ -1,0 +1,156 @@
+"""The batched-rows GEMM (gemv_mb_kernel: int4 x fp16 rows beyond the fused kernel's LDS
+image, generate_batch's M = B decode, inference_engine.cpp:804-828) and its rms_norm prep,
+through the ti_hip.h C-ABI, against the oracle's dequantized weights.
+
+Tolerance as in test_gpu_kernels.py: the expected values use the same fp16 activations and
+the oracle's exact int4 x scale weights in float64, so what is left is fp32 summation order
+(|err| <= 2e-5 * sum_k |x_k w_k| + 1e-6); fp16 outputs rtol 2e-3."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from test_gpu_kernels import assert_close_dot, deq, dev
+
+pytestmark = pytest.mark.gpu
+f16, f32 = np.float16, np.float32
+
+
+def run(ti, tiles, scales, x16, M, N, K, ep):
+    L = ti.lib()
+    ti.check(L.ti_gemm_wq_a16(tiles.ptr, scales.ptr, 4, x16.ptr, ti.X_F16, K, None, 1e-5, M, N, K, C.byref(ep), None))
+    ti.sync()
+
+
+# (M, K, N): rows 17-32 (two 16-row blocks), long K at few rows (one block), ragged tiles per
+# workgroup (N/16 not a multiple of the grid), a last k-chunk of fewer than 8 k-tiles,
+# more tiles than 5 per workgroup (grid grows)
+@pytest.mark.parametrize("M,K,N", [(17, 1024, 64), (32, 4096, 4096 + 48), (24, 1152, 4000), (8, 11008, 256),
+                                   (3, 14336, 96), (20, 4096, 25600), (32, 384, 16)])
+def test_batched_store(ti, oracle, M, K, N):
+    rng = np.random.RandomState(M * 7 + K + N)
+    w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
+    x = rng.standard_normal((M, K)).astype(f16)
+    assert ti.lib().ti_gemm_max_rows(4, ti.X_F16, N, K) >= M
+    tiles, scales = ti.wpack_host(w, 4)
+    yd = ti.DeviceBuffer(M * N * 4)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F32, N, yd.ptr
+    run(ti, dev(ti, tiles), dev(ti, scales), dev(ti, x), M, N, K, ep)
+    wf = deq(oracle, w, 4)
+    xa = x.astype(f32)
+    assert_close_dot(yd.download(f32, (M, N)), xa.astype(np.float64) @ wf.astype(np.float64), xa, wf)
+
+
+def test_batched_resid_silu_logits(ti, oracle):
+    M, K = 21, 2048
+    rng = np.random.RandomState(5)
+    x = rng.standard_normal((M, K)).astype(f16)
+    xd, xa = dev(ti, x), x.astype(np.float64)
+    # residual add in place
+    N = 512
+    w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
+    tiles, scales = ti.wpack_host(w, 4)
+    r = rng.standard_normal((M, N)).astype(f32)
+    rd = dev(ti, r)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_RESID_F32, N, rd.ptr
+    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, N, K, ep)
+    wf = deq(oracle, w, 4)
+    assert_close_dot(rd.download(f32, (M, N)) - r, xa @ wf.astype(np.float64), x.astype(f32), wf, rel=5e-5)
+    # SiLU(gate) * up, gate/up interleaved 8 rows each per tile
+    I = 200
+    g = (rng.standard_normal((K, I)) * 0.05).astype(f32)
+    u = (rng.standard_normal((K, I)) * 0.05).astype(f32)
+    tiles, scales = ti.wpack_host(g, 4, n_total=2 * I, row_map=ti.ROWS_INTERLEAVE8, row_offset=0)
+    ti.wpack_host(u, 4, n_total=2 * I, row_map=ti.ROWS_INTERLEAVE8, row_offset=8, tiles=tiles, scales=scales)
+    yd = ti.DeviceBuffer(M * I * 2)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_SILU_MUL_F16, I, yd.ptr
+    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, 2 * I, K, ep)
+    gg, uu = xa @ deq(oracle, g, 4).astype(np.float64), xa @ deq(oracle, u, 4).astype(np.float64)
+    np.testing.assert_allclose(yd.download(f16, (M, I)).astype(np.float64), uu * (gg / (1 + np.exp(-gg))),
+                               rtol=3e-3, atol=2e-3)
+    # logits + argmax (slots per row), step counter
+    V = 3008
+    w = (rng.standard_normal((K, V)) * 0.05).astype(f32)
+    tiles, scales = ti.wpack_host(w, 4)
+    ld, am = ti.DeviceBuffer(M * V * 4), ti.DeviceBuffer(M * ti.ARGMAX_SLOTS * 8)
+    am.zero()
+    ctr = dev(ti, np.array([3], np.int32))
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out, ep.argmax, ep.step_ctr, ep.advance = ti.EPI_LOGITS_ARGMAX, V, ld.ptr, am.ptr, ctr.ptr, 2
+    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, V, K, ep)
+    logits = ld.download(f32, (M, V))
+    keys = am.download(np.uint64, (M, ti.ARGMAX_SLOTS)).max(axis=1)
+    np.testing.assert_array_equal((0xFFFFFFFF - (keys & 0xFFFFFFFF)).astype(np.int64), np.argmax(logits, axis=1))
+    assert ctr.download(np.int32, (1,))[0] == 5
+    np.testing.assert_allclose(logits, xa @ deq(oracle, w, 4).astype(np.float64), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("hd,nh,nkv", [(128, 4, 4), (64, 8, 2)])
+def test_batched_qkv_rope_kv_append(ti, oracle, hd, nh, nkv):
+    M, H, max_seq, theta = 19, 512, 40, 10000.0
+    qd, kvd = nh * hd, nkv * hd
+    N = qd + 2 * kvd
+    rng = np.random.RandomState(hd + nh)
+    ws = [(rng.standard_normal((H, n)) * 0.05).astype(f32) for n in (qd, kvd, kvd)]
+    tiles = scales = None
+    for w, off in zip(ws, (0, qd, qd + kvd)):
+        tiles, scales = ti.wpack_host(w, 4, n_total=N, row_offset=off, tiles=tiles, scales=scales)
+    x = rng.standard_normal((M, H)).astype(f16)
+    pos = rng.randint(0, max_seq, size=M).astype(np.int32)
+    cs = ti.rope_table(np.arange(max_seq, dtype=f32), hd, theta)
+    qbuf = ti.DeviceBuffer(M * qd * 4)
+    stride = nkv * max_seq * hd
+    kc, vc = ti.DeviceBuffer(M * stride * 2), ti.DeviceBuffer(M * stride * 2)
+    kc.zero(), vc.zero()
+    posd, csd = dev(ti, pos), dev(ti, cs)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_QKV_ROPE_KV, qd, qbuf.ptr
+    ep.q_dim, ep.kv_dim, ep.head_dim, ep.max_seq = qd, kvd, hd, max_seq
+    ep.pos, ep.rope_cs, ep.k_cache, ep.v_cache, ep.kv_stream_stride = posd.ptr, csd.ptr, kc.ptr, vc.ptr, stride
+    run(ti, dev(ti, tiles), dev(ti, scales), dev(ti, x), M, N, H, ep)
+    q, k, v = (x.astype(np.float64) @ deq(oracle, w, 4).astype(np.float64) for w in ws)
+    kcache = kc.download(f16, (M, nkv, max_seq, hd)).astype(f32)
+    vcache = vc.download(f16, (M, nkv, max_seq, hd)).astype(f32)
+    qgot = qbuf.download(f32, (M, qd))
+    for m in range(M):
+        p = np.array([pos[m]], f32)
+        qr = oracle.apply_rope(q[m].astype(f32).reshape(1, nh, 1, hd), p, theta).reshape(-1)
+        kr = oracle.apply_rope(k[m].astype(f32).reshape(1, nkv, 1, hd), p, theta).reshape(nkv, hd)
+        np.testing.assert_allclose(qgot[m], qr, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(kcache[m, :, pos[m]], kr, rtol=2e-3, atol=2e-3)
+        np.testing.assert_allclose(vcache[m, :, pos[m]], v[m].reshape(nkv, hd), rtol=2e-3, atol=2e-3)
+
+
+def test_rmsnorm_f16_matches_fused_prologue(ti, oracle):
+    """ti_rmsnorm_f16 rows fed to the fused kernel == its own rms_norm prologue (same arithmetic)."""
+    M, K, N = 2, 4096, 256
+    rng = np.random.RandomState(9)
+    x = (rng.standard_normal((M, K)) * 2).astype(f32)
+    nw = (1 + 0.1 * rng.standard_normal(K)).astype(f32)
+    xd, nwd = dev(ti, x), dev(ti, nw)
+    yd = ti.DeviceBuffer(M * K * 2)
+    ti.check(ti.lib().ti_rmsnorm_f16(xd.ptr, K, nwd.ptr, 1e-5, yd.ptr, K, M, K, None))
+    ti.sync()
+    y = yd.download(f16, (M, K)).astype(f32)
+    ref = oracle.rms_norm(x, nw)
+    np.testing.assert_allclose(y, ref.astype(f16).astype(f32), rtol=1e-3, atol=1e-3)
+    # the fused path's staged rows are the same fp16 values: identical GEMM results
+    w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
+    tiles, scales = ti.wpack_host(w, 4)
+    td, sd = dev(ti, tiles), dev(ti, scales)
+    L = ti.lib()
+    outs = []
+    for xk, src, norm in ((ti.X_F32_RMSNORM, xd, nwd), (ti.X_F16, yd, None)):
+        od = ti.DeviceBuffer(M * N * 4)
+        ep = ti.Epilogue()
+        ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F32, N, od.ptr
+        ti.check(L.ti_gemm_wq_a16(td.ptr, sd.ptr, 4, src.ptr, xk, K, norm.ptr if norm else None, 1e-5, M, N, K,
+                                  C.byref(ep), None))
+        ti.sync()
+        outs.append(od.download(f32, (M, N)))
+    np.testing.assert_array_equal(outs[0], outs[1])

@@ -86,6 +86,7 @@ struct ti_engine {
   float* ws = nullptr;
   uint16_t* attn = nullptr;
   uint16_t* act = nullptr;
+  uint16_t* xn = nullptr;      // fp16 rms_norm rows for the batched-rows GEMM [B][hidden]
   unsigned long long* argmax = nullptr;
   int32_t* pos = nullptr;
   int32_t* base_pos = nullptr;
@@ -143,11 +144,6 @@ struct ti_engine {
     const int cap = std::max(1, c.max_seq / 64);
     return std::max(1, std::min(sp, std::min(cap, 64)));
   }
-  int mchunk(int N, int K) const {
-    int m = 16;
-    while (m > 1 && ti_gemm_lds_bytes(m, N, K) > 160 * 1024) --m;
-    return m;
-  }
 
   ~ti_engine() {
     for (auto& g : graphs) hipGraphExecDestroy(g.second);
@@ -176,6 +172,37 @@ int validate(const ti_engine_config& c) {
   return TI_OK;
 }
 
+// One projection for rows [0, M): the fused kernel in chunks of the rows its LDS image
+// holds, or -- int4, when the rows do not fit -- rms_norm into fp16 rows once (e->xn) and
+// the batched-rows kernel in chunks of TI_GEMM_MAX_ROWS.  Graph-capturable.
+int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind, int ldx, const float* nw,
+              const ti_epilogue& epi, size_t out_elem, bool last_gets_ctr) {
+  const ti_engine_config& c = e->c;
+  int rows = ti_gemm_max_rows(c.bits, x_kind, W.N, W.K);
+  if (x_kind == TI_X_F32_RMSNORM && rows < M && c.bits == 4 && e->xn) {
+    TI_TRY(ti_rmsnorm_f16(static_cast<const float*>(x), ldx, nw, c.eps, e->xn, W.K, M, W.K, e->s));
+    x = e->xn;
+    x_kind = TI_X_F16;
+    ldx = W.K;
+    rows = ti_gemm_max_rows(c.bits, x_kind, W.N, W.K);
+  }
+  if (rows < 1) return ti_set_error(TI_ERR_UNSUPPORTED, "engine: no GEMM kernel for N=%d K=%d", W.N, W.K);
+  const size_t x_elem = x_kind == TI_X_F16 ? 2 : 4;
+  for (int m0 = 0; m0 < M; m0 += rows) {
+    const int mm = std::min(rows, M - m0);
+    ti_epilogue ep = epi;
+    ep.out = static_cast<char*>(epi.out) + (size_t)m0 * epi.ldo * out_elem;
+    if (ep.pos) ep.pos += m0;
+    if (ep.k_cache) ep.k_cache += (size_t)m0 * ep.kv_stream_stride;
+    if (ep.v_cache) ep.v_cache += (size_t)m0 * ep.kv_stream_stride;
+    if (ep.argmax) ep.argmax += (size_t)m0 * TI_ARGMAX_SLOTS;
+    if (!(last_gets_ctr && m0 + mm >= M)) ep.step_ctr = nullptr;
+    const void* xm = static_cast<const char*>(x) + (size_t)m0 * ldx * x_elem;
+    TI_TRY(ti_gemm_wq_a16(W.tiles, W.scales, c.bits, xm, x_kind, ldx, nw, c.eps, mm, W.N, W.K, &ep, e->s));
+  }
+  return TI_OK;
+}
+
 // One decode step for streams [0, M) on e->s.  Graph-capturable (no host sync / alloc).
 int enqueue_step(ti_engine* e, int M, int advance) {
   const ti_engine_config& c = e->c;
@@ -198,22 +225,9 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   TI_TRY(ti_step_begin(&sa, e->s));
 
   const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
-  auto gemm = [&](const DevLinear& W, const void* x, int x_kind, int ldx, size_t x_elem, const float* nw,
+  auto gemm = [&](const DevLinear& W, const void* x, int x_kind, int ldx, size_t /*x_elem*/, const float* nw,
                   ti_epilogue epi, size_t out_elem, bool last_gets_ctr) -> int {
-    const int mc = e->mchunk(W.N, W.K);
-    for (int m0 = 0; m0 < M; m0 += mc) {
-      const int mm = std::min(mc, M - m0);
-      ti_epilogue ep = epi;
-      ep.out = static_cast<char*>(epi.out) + (size_t)m0 * epi.ldo * out_elem;
-      if (ep.pos) ep.pos += m0;
-      if (ep.k_cache) ep.k_cache += (size_t)m0 * ep.kv_stream_stride;
-      if (ep.v_cache) ep.v_cache += (size_t)m0 * ep.kv_stream_stride;
-      if (ep.argmax) ep.argmax += (size_t)m0 * TI_ARGMAX_SLOTS;
-      if (!(last_gets_ctr && m0 + mm >= M)) ep.step_ctr = nullptr;
-      const void* xm = static_cast<const char*>(x) + (size_t)m0 * ldx * x_elem;
-      TI_TRY(ti_gemm_wq_a16(W.tiles, W.scales, c.bits, xm, x_kind, ldx, nw, c.eps, mm, W.N, W.K, &ep, e->s));
-    }
-    return TI_OK;
+    return gemm_rows(e, W, M, x, x_kind, ldx, nw, epi, out_elem, last_gets_ctr);
   };
 
   for (int l = 0; l < c.layers; ++l) {
@@ -368,7 +382,7 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     if ((rc = ti_memcpy_h2d(e->rope_cs, cs.data(), cs.size() * 4, e->s))) return fail(rc);
     e->splits_max = e->splits_for(1);
     if ((rc = e->alloc_t(&e->q, (size_t)B * qd)) || (rc = e->alloc_t(&e->attn, (size_t)B * qd)) ||
-        (rc = e->alloc_t(&e->act, (size_t)B * I)) ||
+        (rc = e->alloc_t(&e->act, (size_t)B * I)) || (rc = e->alloc_t(&e->xn, (size_t)B * H)) ||
         (rc = e->alloc(reinterpret_cast<void**>(&e->ws), ti_attn_workspace_bytes(B, c.heads, hd, e->splits_max))))
       return fail(rc);
   }
@@ -689,12 +703,7 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
     if (which == 5)
       return ti_attn_decode(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, n, c.heads, c.kv_heads, c.head_dim,
                             e->splits_for(n), e->ws, e->attn, e->s);
-    const int mc = e->mchunk(W->N, W->K);
-    for (int m0 = 0; m0 < n; m0 += mc) {
-      const int mm = std::min(mc, n - m0);
-      TI_TRY(ti_gemm_wq_a16(W->tiles, W->scales, c.bits, x, xk, ldx, nw, c.eps, mm, W->N, W->K, &ep, e->s));
-    }
-    return TI_OK;
+    return gemm_rows(e, *W, n, x, xk, ldx, nw, ep, which == 2 ? 2 : 4, false);
   };
   int rc = launch();   // warm
   if (rc == TI_OK) {
@@ -708,13 +717,13 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
   hipEventDestroy(a);
   hipEventDestroy(b);
   TI_TRY(rc);
-  const int launches_per = which == 5 ? 1 : (n + e->mchunk(W->N, W->K) - 1) / e->mchunk(W->N, W->K);
-  *avg_us = (double)ms * 1000.0 / (double)(reps * launches_per);
+  // per projection (all row chunks of it, and the rms_norm prep of the batched path)
+  *avg_us = (double)ms * 1000.0 / (double)reps;
   if (which == 5) {
     *bytes = 2.0 * n * (double)kvd * kv_len * 2.0 + (double)n * qd * (4 + 2);
   } else {
     const double wbytes = (double)ti_wpack_tile_bytes(c.bits, W->K, W->N) + (double)ti_wpack_scale_bytes(c.bits, W->K, W->N);
-    *bytes = wbytes / launches_per + (double)n / launches_per * W->K * (xk == TI_X_F16 ? 2 : 4);
+    *bytes = wbytes + (double)n * W->K * (xk == TI_X_F16 ? 2 : 4);
   }
   return TI_OK;
 }

@@ -659,6 +659,210 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   GEMV_TS(4);
 }
 
+
+// ================================================================= batched rows
+// gemv_mb_kernel<MB, NTL>: int4 weights x fp16 activations for M <= 16*MB rows (MB <= 2):
+// the batched decode of generate_batch (inference_engine.cpp:804-828), and
+// long-K projections whose activation rows no longer fit gemv_wq_kernel's LDS image.
+// Weights are still read once per launch; the activations can no longer be staged whole, so
+// each wave reads the A fragments of ITS k-tile (all rows) straight into registers, once per
+// chunk of 8 k-tiles, and reuses them for every tile of the workgroup:
+//   * item order per wave: chunk c (k-tile 8c + wave) x tile tl; the workgroup's NTL tiles'
+//     weights and the chunk's x fragments are loaded one chunk ahead (two register buffers,
+//     the chunk loop unrolled by two), so no barrier is needed until the end;
+//   * per 32-k step one dequantized weight fragment feeds MB MFMAs (one per 16-row block);
+//     nibble offsets are removed in the dequant (x is used as loaded);
+//   * k-tiles past K (the last chunk) and the dummy tile of workgroups with NTL - 1 tiles use
+//     clamped addresses and a zero scale.
+// After the stream the waves' blocks are summed in a fixed order through LDS and the same
+// epilogue kinds run, their inputs (residual, positions, RoPE table) read from global.
+__host__ __device__ inline int mb_lds_bytes(int MB, int ntl, int K) {
+  return align16(ntl * MB * kGemvWaves * kWave * 16) + align16(ntl * (K >> 7) * 32);
+}
+
+__device__ __forceinline__ f16x8 deq_int4_signed(uint32_t w, uint32_t magic) {
+  const f16x8 r = deq_int4_raw(w, magic);   // lanes (1024 + n) and (1024 + 16 n)
+  const f16x2 lo_off = {(f16)-1032.0f, (f16)-1032.0f}, hi_mul = {(f16)0.0625f, (f16)0.0625f},
+              hi_off = {(f16)-72.0f, (f16)-72.0f};
+  const f16x2 a = (f16x2){r[0], r[1]} + lo_off, b = (f16x2){r[2], r[3]} * hi_mul + hi_off;
+  const f16x2 c = (f16x2){r[4], r[5]} + lo_off, d = (f16x2){r[6], r[7]} * hi_mul + hi_off;
+  return (f16x8){a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
+// Epilogue of one output y[m][nt*16 + n]; the inputs gemv_wq_kernel stages in LDS are read
+// from global.  Shuffle partners (n ^ 1, n + 8) are lanes of the same 16-lane group.
+__device__ __forceinline__ void epilogue_mb(const GemvArgs& a, int nt, int m, int n, float v, bool live) {
+  const ti_epilogue& e = a.epi;
+  const int ng = nt * 16 + n;
+  switch (e.kind) {
+    case TI_EPI_STORE_F32:
+      if (live) ((float*)e.out)[(size_t)m * e.ldo + ng] = v;
+      break;
+    case TI_EPI_STORE_F16:
+      if (live) ((uint16_t*)e.out)[(size_t)m * e.ldo + ng] = f2h(v);
+      break;
+    case TI_EPI_RESID_F32:
+      if (live) {
+        float* o = (float*)e.out + (size_t)m * e.ldo + ng;
+        *o = *o + v;
+      }
+      break;
+    case TI_EPI_SILU_MUL_F16: {
+      const float up = __shfl_down(v, 8, kWave);
+      if (live && n < 8) {
+        const float s = v / (1.0f + expf(-v));
+        ((uint16_t*)e.out)[(size_t)m * e.ldo + nt * 8 + n] = f2h(up * s);
+      }
+      break;
+    }
+    case TI_EPI_QKV_ROPE_KV: {
+      const float partner = __shfl_xor(v, 1, kWave);
+      if (!live) break;
+      const int hd = e.head_dim, p = e.pos[m];
+      if (ng < e.q_dim + e.kv_dim) {
+        const int base = ng < e.q_dim ? 0 : e.q_dim;
+        const int d = (ng - base) % hd;
+        const float2 cs = *(const float2*)(e.rope_cs + (size_t)p * hd + (d & ~1));
+        const float r = (d & 1) == 0 ? fmaf(-partner, cs.y, v * cs.x) : fmaf(v, cs.x, partner * cs.y);
+        if (ng < e.q_dim) {
+          ((float*)e.out)[(size_t)m * e.ldo + ng] = r;
+        } else {
+          const int kvh = (ng - e.q_dim) / hd;
+          e.k_cache[(size_t)m * e.kv_stream_stride + ((size_t)kvh * e.max_seq + p) * hd + d] = f2h(r);
+        }
+      } else {
+        const int c = ng - e.q_dim - e.kv_dim;
+        const int kvh = c / hd, d = c - kvh * hd;
+        e.v_cache[(size_t)m * e.kv_stream_stride + ((size_t)kvh * e.max_seq + p) * hd + d] = f2h(v);
+      }
+      break;
+    }
+    case TI_EPI_LOGITS_ARGMAX: {
+      unsigned long long key = 0ull;
+      if (live) {
+        ((float*)e.out)[(size_t)m * e.ldo + ng] = v;
+        key = ((unsigned long long)float_order_key(v) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)ng);
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const unsigned long long other = __shfl_xor(key, o, kWave);
+        key = other > key ? other : key;
+      }
+      if (n == 0 && key) atomicMax(e.argmax + (size_t)m * TI_ARGMAX_SLOTS + (blockIdx.x & (TI_ARGMAX_SLOTS - 1)), key);
+      break;
+    }
+    default:
+      break;
+  }
+}
+
+template <int MB, int NTL>
+struct MbChunk {       // one chunk's operands of one wave
+  u32x4 w[NTL];        // packed int4 weights of (tile tl, this wave's k-tile)
+  f16x8 x[MB][4];      // A fragments: rows 16 b + (lane & 15), k = kt*128 + 32 (lane >> 4) + 8 s4
+};
+
+template <int MB, int NTL>
+__global__ __launch_bounds__(kGemvThreads, 1) void gemv_mb_kernel(const GemvArgs a, int grid) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int KT = a.K >> 7, NT = a.N >> 4, NC = (KT + kGemvWaves - 1) / kGemvWaves;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, kq = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int t0 = (int)(blockIdx.x * (unsigned)NT / (unsigned)grid);
+  const int t1 = (int)((blockIdx.x + 1) * (unsigned)NT / (unsigned)grid);
+  const int ntl = t1 - t0;                           // NTL or NTL - 1
+  f32x4* slab = (f32x4*)smem;                        // after the stream: [NTL][MB][8][64]
+  uint16_t* sl = (uint16_t*)(smem + align16(NTL * MB * kGemvWaves * kWave * 16));   // [ntl][KT][16]
+
+  // scales of our tiles: loaded first (two pieces per thread cover ntl * KT <= 512 groups)
+  const int n_sc = ntl * KT * 2;
+  const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16);
+  const u32x4 sc0 = ld_w(sg + (tid < n_sc ? tid : 0));
+  const u32x4 sc1 = ld_w(sg + (tid + kGemvThreads < n_sc ? tid + kGemvThreads : 0));
+
+  const f16* xg = (const f16*)a.x;
+  const u32x4* tb = a.tiles + lane;
+  auto load = [&](MbChunk<MB, NTL>& ch, int c) {
+    const int kt = min(c * kGemvWaves + wave, KT - 1);
+#pragma unroll
+    for (int tl = 0; tl < NTL; ++tl) ch.w[tl] = ld_w(tb + ((size_t)(t0 + min(tl, ntl - 1)) * KT + kt) * kWave);
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      const int m = min(b * 16 + r, a.M - 1);
+      const f16* xr = xg + (size_t)m * a.ldx + kt * 128 + kq * 32;   // the tile's k order (B fragments)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) ch.x[b][s4] = *(const f16x8*)(xr + s4 * 8);
+    }
+  };
+  MbChunk<MB, NTL> B0, B1;
+  load(B0, 0);
+  if (tid < n_sc) ((u32x4*)sl)[tid] = sc0;
+  if (tid + kGemvThreads < n_sc) ((u32x4*)sl)[tid + kGemvThreads] = sc1;
+  lds_barrier();
+
+  f32x4 acc[NTL][MB];
+#pragma unroll
+  for (int t = 0; t < NTL; ++t)
+#pragma unroll
+    for (int b = 0; b < MB; ++b) acc[t][b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+  uint32_t magic;
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
+  auto compute = [&](const MbChunk<MB, NTL>& ch, int c) {
+    const int kt = c * kGemvWaves + wave;
+    const bool kvalid = kt < KT;
+#pragma unroll
+    for (int tl = 0; tl < NTL; ++tl) {
+      f32x4 t[MB];
+#pragma unroll
+      for (int b = 0; b < MB; ++b) t[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const f16x8 bf = deq_int4_signed(ch.w[tl][s4], magic);
+#pragma unroll
+        for (int b = 0; b < MB; ++b) t[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ch.x[b][s4], bf, t[b], 0, 0, 0);
+      }
+      const float sc = kvalid ? h2f(sl[(min(tl, ntl - 1) * KT + kt) * 16 + r]) : 0.0f;
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        acc[tl][b][0] = fmaf(sc, t[b][0], acc[tl][b][0]);
+        acc[tl][b][1] = fmaf(sc, t[b][1], acc[tl][b][1]);
+        acc[tl][b][2] = fmaf(sc, t[b][2], acc[tl][b][2]);
+        acc[tl][b][3] = fmaf(sc, t[b][3], acc[tl][b][3]);
+      }
+    }
+  };
+  // chunks two at a time, each loaded one chunk ahead (the reload past the end is harmless)
+  int c = 0;
+  for (; c + 1 < NC; c += 2) {
+    load(B1, c + 1);
+    compute(B0, c);
+    load(B0, c + 2 < NC ? c + 2 : NC - 1);
+    compute(B1, c + 1);
+  }
+  if (c < NC) compute(B0, c);
+
+  // ---- sum the 8 waves' blocks in a fixed order, then the epilogue
+#pragma unroll
+  for (int tl = 0; tl < NTL; ++tl)
+#pragma unroll
+    for (int b = 0; b < MB; ++b) slab[((tl * MB + b) * kGemvWaves + wave) * kWave + lane] = acc[tl][b];
+  lds_barrier();
+  const int n = lane & 15, nblk = ntl * MB * 4;
+  const int nblk_pad = (nblk + kGemvWaves - 1) / kGemvWaves * kGemvWaves;
+  for (int cb = wave; cb < nblk_pad; cb += kGemvWaves) {   // wave-uniform trip count (shuffles inside)
+    const bool ok = cb < nblk;
+    const int cbc = ok ? cb : 0, tl = cbc / (MB * 4), b = (cbc >> 2) % MB, i = cbc & 3;
+    const float* sp = (const float*)(slab + (tl * MB + b) * kGemvWaves * kWave + lane) + i;
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kGemvWaves; ++w) v += sp[w * kWave * 4];
+    const int m = b * 16 + 4 * (lane >> 4) + i;
+    epilogue_mb(a, t0 + tl, m, n, v, ok && m < a.M);
+  }
+  if (a.epi.kind == TI_EPI_LOGITS_ARGMAX && a.epi.step_ctr && blockIdx.x == 0 && tid == 0)
+    *a.epi.step_ctr += a.epi.advance;
+}
+
 static int g_num_cus = 0;
 
 __host__ inline int gemv_xmode(int x_kind, int M, int K) {
@@ -681,6 +885,87 @@ static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid) {
   TI_LAUNCH_CHECK("gemv_wq_kernel");
   return TI_OK;
 }
+
+// rms_norm rows into fp16 (the batched path's activation prep): the same arithmetic as the
+// fused XM_NORM staging above (per-thread k8 pieces, wave sums, 8 waves in order).
+__global__ __launch_bounds__(kGemvThreads) void rmsnorm_f16_kernel(const float* x, int ldx, const float* w, float eps,
+                                                                    uint16_t* y, int ldy, int K) {
+  __shared__ float red[kGemvWaves];
+  const int m = blockIdx.x, tid = threadIdx.x, K8 = K >> 3;
+  const float* xr = x + (size_t)m * ldx;
+  float ss = 0.0f;
+  for (int k8 = tid; k8 < K8; k8 += kGemvThreads) {
+    const float4 v0 = *(const float4*)(xr + 8 * k8), v1 = *(const float4*)(xr + 8 * k8 + 4);
+    ss = fmaf(v0.x, v0.x, ss); ss = fmaf(v0.y, v0.y, ss); ss = fmaf(v0.z, v0.z, ss); ss = fmaf(v0.w, v0.w, ss);
+    ss = fmaf(v1.x, v1.x, ss); ss = fmaf(v1.y, v1.y, ss); ss = fmaf(v1.z, v1.z, ss); ss = fmaf(v1.w, v1.w, ss);
+  }
+  ss = wave_sum_xor<kWave>(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  float tot = 0.0f;
+#pragma unroll
+  for (int i = 0; i < kGemvWaves; ++i) tot += red[i];
+  const float rms = sqrtf(tot / (float)K + eps);
+  for (int k8 = tid; k8 < K8; k8 += kGemvThreads) {
+    const float4 v0 = *(const float4*)(xr + 8 * k8), v1 = *(const float4*)(xr + 8 * k8 + 4);
+    const float4 w0 = *(const float4*)(w + 8 * k8), w1 = *(const float4*)(w + 8 * k8 + 4);
+    f16x8 h;
+    h[0] = (f16)((v0.x / rms) * w0.x); h[1] = (f16)((v0.y / rms) * w0.y);
+    h[2] = (f16)((v0.z / rms) * w0.z); h[3] = (f16)((v0.w / rms) * w0.w);
+    h[4] = (f16)((v1.x / rms) * w1.x); h[5] = (f16)((v1.y / rms) * w1.y);
+    h[6] = (f16)((v1.z / rms) * w1.z); h[7] = (f16)((v1.w / rms) * w1.w);
+    *(f16x8*)(y + (size_t)m * ldy + 8 * k8) = h;
+  }
+}
+
+// Batched-rows geometry: at most 8 tiles per workgroup (register accumulators), and the
+// workgroup's scales in two 16-byte pieces per thread.
+// (MB = 2 keeps 5 tiles of accumulators and two chunk buffers in 256 VGPRs without spilling.)
+__host__ inline int mb_tiles_cap(int MB, int K) {
+  const int lim = MB == 2 ? 5 : 8, cap = 512 / (K >> 7);
+  return cap < 1 ? 1 : (cap > lim ? lim : cap);
+}
+__host__ inline int mb_grid(int MB, int N, int K, int num_cus, int* ntl_out) {
+  const int NT = N >> 4, cap = mb_tiles_cap(MB, K);
+  int grid = NT < num_cus ? NT : num_cus;
+  if ((NT + grid - 1) / grid > cap) grid = (NT + cap - 1) / cap;
+  *ntl_out = (NT + grid - 1) / grid;
+  return grid;
+}
+
+template <int MB, int NTL>
+static int launch_mb_t(const GemvArgs& a, int grid, int lds, hipStream_t s) {
+  hipLaunchKernelGGL((gemv_mb_kernel<MB, NTL>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
+  TI_LAUNCH_CHECK("gemv_mb_kernel");
+  return TI_OK;
+}
+static int launch_mb(const GemvArgs& a, int MB, int grid, int ntl, int lds, hipStream_t s) {
+  if (MB == 2) {
+    switch (ntl) {
+      case 1: return launch_mb_t<2, 1>(a, grid, lds, s);
+      case 2: return launch_mb_t<2, 2>(a, grid, lds, s);
+      case 3: return launch_mb_t<2, 3>(a, grid, lds, s);
+      case 4: return launch_mb_t<2, 4>(a, grid, lds, s);
+      default: return launch_mb_t<2, 5>(a, grid, lds, s);
+    }
+  }
+  switch (ntl) {
+    case 1: return launch_mb_t<1, 1>(a, grid, lds, s);
+    case 2: return launch_mb_t<1, 2>(a, grid, lds, s);
+    case 3: return launch_mb_t<1, 3>(a, grid, lds, s);
+    case 4: return launch_mb_t<1, 4>(a, grid, lds, s);
+    case 5: return launch_mb_t<1, 5>(a, grid, lds, s);
+    case 6: return launch_mb_t<1, 6>(a, grid, lds, s);
+    case 7: return launch_mb_t<1, 7>(a, grid, lds, s);
+    default: return launch_mb_t<1, 8>(a, grid, lds, s);
+  }
+}
+#define TI_MB_FNS                                                                                   \
+  (const void*)gemv_mb_kernel<1, 1>, (const void*)gemv_mb_kernel<1, 2>, (const void*)gemv_mb_kernel<1, 3>,     \
+      (const void*)gemv_mb_kernel<1, 4>, (const void*)gemv_mb_kernel<1, 5>, (const void*)gemv_mb_kernel<1, 6>, \
+      (const void*)gemv_mb_kernel<1, 7>, (const void*)gemv_mb_kernel<1, 8>, (const void*)gemv_mb_kernel<2, 1>, \
+      (const void*)gemv_mb_kernel<2, 2>, (const void*)gemv_mb_kernel<2, 3>, (const void*)gemv_mb_kernel<2, 4>, \
+      (const void*)gemv_mb_kernel<2, 5>
 
 static bool g_prepared = false;
 
@@ -709,7 +994,8 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<8, XM_F16>,  (const void*)gemv_wq_kernel<8, XM_F32>,
       (const void*)gemv_wq_kernel<8, XM_NORM1>, (const void*)gemv_wq_kernel<8, XM_NORM>,
       (const void*)gemv_wq_kernel<16, XM_F16>, (const void*)gemv_wq_kernel<16, XM_F32>,
-      (const void*)gemv_wq_kernel<16, XM_NORM1>, (const void*)gemv_wq_kernel<16, XM_NORM>};
+      (const void*)gemv_wq_kernel<16, XM_NORM1>, (const void*)gemv_wq_kernel<16, XM_NORM>,
+      TI_MB_FNS};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
@@ -723,6 +1009,44 @@ extern "C" int ti_gemm_lds_bytes(int M, int N, int K) {
   return ti::gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid);
 }
 
+// The fused kernel takes the rows while its LDS image fits; int4 with fp16 activations
+// also has the batched-rows kernel (up to TI_GEMM_MAX_ROWS rows, any K).
+// int4 with more than TI_GEMM_FUSED_ROWS rows (default 2; tuning knob) goes to the
+// batched-rows kernel: from 4 rows on it is faster at every 7B projection (bench.py
+// --batch 2..16, rocprof), at 2 rows the two tie.
+static int g_fused_rows = 0;
+static int fused_rows_pref(int bits) {
+  if (g_fused_rows <= 0) {
+    const char* s = getenv("TI_GEMM_FUSED_ROWS");
+    g_fused_rows = s && atoi(s) > 0 ? (atoi(s) < 16 ? atoi(s) : 16) : 2;
+  }
+  return bits == 4 ? g_fused_rows : 16;
+}
+static bool fused_fits(int M, int N, int K) { return M <= 16 && ti_gemm_lds_bytes(M, N, K) <= 160 * 1024; }
+static bool use_batched(int bits, int x_kind, int M, int N, int K) {
+  const bool mb_ok = bits == 4 && x_kind == TI_X_F16;
+  return !fused_fits(M, N, K) || (mb_ok && M > fused_rows_pref(bits));
+}
+
+extern "C" int ti_gemm_max_rows(int bits, int x_kind, int N, int K) {
+  if (N < 16 || K < 128) return 0;
+  if (bits == 4 && x_kind == TI_X_F16) return TI_GEMM_MAX_ROWS;
+  int m = fused_rows_pref(bits);
+  while (m > 1 && !fused_fits(m, N, K)) --m;
+  return fused_fits(m, N, K) ? m : 0;
+}
+
+extern "C" int ti_rmsnorm_f16(const float* x, int ldx, const float* w, float eps, uint16_t* y, int ldy, int M, int K,
+                              ti_stream_t stream) {
+  if (!x || !w || !y) return ti_set_error(TI_ERR_ARG, "ti_rmsnorm_f16: null pointer");
+  if (M < 1 || K < 8 || (K & 7) || ldx < K || ldy < K)
+    return ti_set_error(TI_ERR_ARG, "ti_rmsnorm_f16: bad shape (M=%d K=%d ldx=%d ldy=%d)", M, K, ldx, ldy);
+  hipLaunchKernelGGL(ti::rmsnorm_f16_kernel, dim3(M), dim3(ti::kGemvThreads), 0, (hipStream_t)stream, x, ldx, w, eps,
+                     y, ldy, K);
+  TI_LAUNCH_CHECK("rmsnorm_f16_kernel");
+  return TI_OK;
+}
+
 extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x,
                               int x_kind, int ldx, const float* norm_w, float eps, int M, int N, int K,
                               const ti_epilogue* epi, ti_stream_t stream) {
@@ -731,7 +1055,8 @@ extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bit
   if (bits != 4 && bits != 8 && bits != 16)
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: bits must be 4, 8 or 16 (got %d)", bits);
   if (bits != 16 && !scales) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: scales required for bits %d", bits);
-  if (M < 1 || M > 16) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: M must be in [1,16] (got %d)", M);
+  if (M < 1 || M > TI_GEMM_MAX_ROWS)
+    return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: M must be in [1,%d] (got %d)", TI_GEMM_MAX_ROWS, M);
   if (K <= 0 || (K & 127) || N <= 0 || (N & 15))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: K %% 128 and N %% 16 must be 0 (K=%d N=%d)", K, N);
   if (x_kind < TI_X_F16 || x_kind > TI_X_F32_RMSNORM)
@@ -757,10 +1082,21 @@ extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bit
     default:
       return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: unknown epilogue %d", epi->kind);
   }
-  const int grid = gemv_grid(M, N, K, query_cus());
-  const int lds = gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid);
+  const bool batched = use_batched(bits, x_kind, M, N, K);
+  if (batched && !(bits == 4 && x_kind == TI_X_F16))
+    return ti_set_error(TI_ERR_UNSUPPORTED,
+                        "ti_gemm_wq_a16: M=%d K=%d exceeds the fused kernel (ti_gemm_max_rows); the batched-rows "
+                        "kernel needs bits 4 and fp16 rows (normalise with ti_rmsnorm_f16)", M, K);
+  int grid = 0, lds = 0, ntl = 0;
+  if (batched) {
+    grid = mb_grid(M > 16 ? 2 : 1, N, K, query_cus(), &ntl);
+    lds = mb_lds_bytes(M > 16 ? 2 : 1, ntl, K);
+  } else {
+    grid = gemv_grid(M, N, K, query_cus());
+    lds = gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid);
+  }
   if (lds > 160 * 1024)
-    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: M*K too large for one LDS stage (M=%d K=%d)", M, K);
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: LDS image %d B too large (M=%d N=%d K=%d)", lds, M, N, K);
   if (lds > 64 * 1024 && !g_prepared) {
     const int rc = ti_gemm_prepare();
     if (rc != TI_OK) return rc;
@@ -778,6 +1114,7 @@ extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bit
   a.K = K;
   a.epi = *epi;
   hipStream_t s = (hipStream_t)stream;
+  if (batched) return launch_mb(a, M > 16 ? 2 : 1, grid, ntl, lds, s);
   if (bits == 4) return launch_gemv<4>(a, lds, s, grid);
   if (bits == 8) return launch_gemv<8>(a, lds, s, grid);
   return launch_gemv<16>(a, lds, s, grid);
