@@ -254,6 +254,12 @@ def test_attention_long_context(ti, oracle):
     _attn_case(ti, oracle, 1, 8, 2, 128, [2048], splits=16, max_seq=2048, seed=9)
 
 
+@pytest.mark.parametrize("hd,nh,nkv", [(128, 8, 2), (64, 16, 2), (128, 16, 2)])
+def test_attention_long_range_gqa(ti, oracle, hd, nh, nkv):
+    """GQA groups of >= 4 over >= 1024 keys per split take the deeper K/V ring."""
+    _attn_case(ti, oracle, 2, nh, nkv, hd, [1500, 2048], splits=1, max_seq=2048, seed=hd + nh)
+
+
 # ------------------------------------------------------- fp32 op level (TensorEngine)
 def _same_bits(y, exp):
     np.testing.assert_array_equal(np.ascontiguousarray(y, f32).view(np.uint32).reshape(-1),
