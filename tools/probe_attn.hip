@@ -47,7 +47,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   struct Shape { const char* name; int heads, kv, hd, L; } shapes[] = {
-      {"llama2-7b", 32, 32, 128, 2048}, {"llama3-8b", 32, 8, 128, 2048}, {"llama2-7b@512", 32, 32, 128, 512}};
+      {"llama2-7b", 32, 32, 128, 2048}, {"llama3-8b", 32, 8, 128, 2048}, {"tinyllama", 32, 4, 64, 2048}};
   for (auto& sh : shapes) {
     const int max_seq = sh.L;
     const size_t kv_bytes = (size_t)sh.kv * max_seq * sh.hd * 2;   // one of K or V
@@ -55,7 +55,7 @@ int main(int argc, char** argv) {
     const int nbuf = (int)(big / per);
     const int p = sh.L - 1;
     CK(hipMemcpy(pos, &p, 4, hipMemcpyHostToDevice));
-    for (int splits : {4, 8, 16, 32, 64}) {
+    for (int splits : {4, 8, 16, 22, 32, 64}) {
       hipGraph_t g;
       hipGraphExec_t ge;
       CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));

@@ -104,6 +104,19 @@ __device__ __forceinline__ u32x4 ld_kv(const u32x4* p) {
 #endif
 }
 
+// Merge across the lane groups of a wave (lanes l, l ^ O, ... with O = LPK, 2 LPK, ... 32:
+// the same dims of the other key rows), max and sum.
+template <int O>
+__device__ __forceinline__ float groups_max(float v) {
+  if constexpr (O < 64) return groups_max<2 * O>(fmaxf(v, lane_xor<O>(v)));
+  else return v;
+}
+template <int O>
+__device__ __forceinline__ float groups_sum(float v) {
+  if constexpr (O < 64) return groups_sum<2 * O>(v + lane_xor<O>(v));
+  else return v;
+}
+
 template <int HD, int G, int R>
 __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnArgs a) {
   constexpr int LPK = HD / 8;       // lanes per key row
@@ -169,7 +182,7 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
       float d = 0.0f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) d = fmaf(q[g][e], kf[e], d);
-      d = wave_sum_xor<LPK>(d);
+      d = group_sum<LPK>(d);
       const float sc = valid ? d : -INFINITY;
       const float mn = fmaxf(mrun[g], sc);
       const float alpha = mrun[g] == mn ? 1.0f : __expf(mrun[g] - mn);
@@ -196,20 +209,11 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
   // merge the lane groups of the wave (each holds its own max / sum / o)
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    float mx = mrun[g];
-#pragma unroll
-    for (int o = LPK; o < 64; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, kWave));
+    const float mx = groups_max<LPK>(mrun[g]);
     const float f = mrun[g] == -INFINITY ? 0.0f : __expf(mrun[g] - mx);
-    float l = lrun[g] * f;
+    const float l = groups_sum<LPK>(lrun[g] * f);
 #pragma unroll
-    for (int o = LPK; o < 64; o <<= 1) l += __shfl_xor(l, o, kWave);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float v = acc[g][e] * f;
-#pragma unroll
-      for (int o = LPK; o < 64; o <<= 1) v += __shfl_xor(v, o, kWave);
-      acc[g][e] = v;
-    }
+    for (int e = 0; e < 8; ++e) acc[g][e] = groups_sum<LPK>(acc[g][e] * f);
     mrun[g] = mx;
     lrun[g] = l;
   }

@@ -54,6 +54,47 @@ __device__ __forceinline__ float wave_max_xor(float v) {
   return v;
 }
 
+// Cross-lane exchanges on the VALU (DPP, gfx950 v_permlane16/32_swap) instead of the LDS
+// crossbar (__shfl_xor -> ds_bpermute_b32, a round trip through the LDS pipe per step).
+__device__ __forceinline__ unsigned lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0u, __builtin_bit_cast(unsigned, v), CTRL, 0xf, 0xf, false));
+}
+// v of lane l ^ O, exactly (O in {1, 2, 8, 16, 32}).
+template <int O>
+__device__ __forceinline__ float lane_xor(float v) {
+  if constexpr (O == 1) {
+    return dpp_f<0xB1>(v);            // quad_perm [1,0,3,2]
+  } else if constexpr (O == 2) {
+    return dpp_f<0x4E>(v);            // quad_perm [2,3,0,1]
+  } else if constexpr (O == 8) {
+    return dpp_f<0x128>(v);           // row_ror:8 within 16-lane rows == xor 8
+  } else if constexpr (O == 16) {
+    const unsigned u = __builtin_bit_cast(unsigned, v);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __builtin_bit_cast(float, (lane_id() & 16) ? r[0] : r[1]);
+  } else {
+    static_assert(O == 32, "lane_xor: O in {1, 2, 8, 16, 32}");
+    const unsigned u = __builtin_bit_cast(unsigned, v);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __builtin_bit_cast(float, lane_id() < 32 ? r[1] : r[0]);
+  }
+}
+// All-reduce sum over aligned groups of WIDTH lanes (butterfly; the width-4 and width-8
+// stages pair quads / half-rows by mirroring, which is valid once the smaller stages have
+// made each quad / half-row uniform).
+template <int WIDTH>
+__device__ __forceinline__ float group_sum(float v) {
+  if constexpr (WIDTH >= 2) v += lane_xor<1>(v);
+  if constexpr (WIDTH >= 4) v += lane_xor<2>(v);
+  if constexpr (WIDTH >= 8) v += dpp_f<0x141>(v);   // row_half_mirror: quad <-> other quad of the 8
+  if constexpr (WIDTH >= 16) v += dpp_f<0x140>(v);  // row_mirror: half-row <-> other half of the 16
+  if constexpr (WIDTH >= 32) v += lane_xor<16>(v);
+  if constexpr (WIDTH >= 64) v += lane_xor<32>(v);
+  return v;
+}
+
 // ----------------------------------------------------- synthetic model stream
 // Bit-identical to or_splitmix64 / or_synth_unit in oracle/ti_oracle.c.
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
