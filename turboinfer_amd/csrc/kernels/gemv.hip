@@ -664,20 +664,26 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
 // gemv_mb_kernel<MB, NTL>: int4 weights x fp16 activations for M <= 16*MB rows (MB <= 2):
 // the batched decode of generate_batch (inference_engine.cpp:804-828), and
 // long-K projections whose activation rows no longer fit gemv_wq_kernel's LDS image.
-// Weights are still read once per launch; the activations can no longer be staged whole, so
-// each wave reads the A fragments of ITS k-tile (all rows) straight into registers, once per
-// chunk of 8 k-tiles, and reuses them for every tile of the workgroup:
-//   * item order per wave: chunk c (k-tile 8c + wave) x tile tl; the workgroup's NTL tiles'
-//     weights and the chunk's x fragments are loaded one chunk ahead (two register buffers,
-//     the chunk loop unrolled by two), so no barrier is needed until the end;
+// Weights are still read once per launch, straight into registers; the activations are
+// staged in k-chunks of 1024 (8 k-tiles, one per wave):
+//   * a chunk of all rows is copied by LDS-DMA (global_load_lds_dwordx4: every wave
+//     instruction one contiguous KiB of a row) into one of two LDS buffers, one chunk ahead;
+//   * item order per wave: chunk c (k-tile 8c + wave) x tile tl; the NTL tiles' weights of
+//     chunk c + 1 are loaded into the other register buffer while chunk c computes (the chunk
+//     loop unrolled by two), and one barrier per chunk hands the x buffers over;
 //   * per 32-k step one dequantized weight fragment feeds MB MFMAs (one per 16-row block);
-//     nibble offsets are removed in the dequant (x is used as loaded);
+//     nibble offsets are removed in the dequant (x is used as staged);
 //   * k-tiles past K (the last chunk) and the dummy tile of workgroups with NTL - 1 tiles use
 //     clamped addresses and a zero scale.
-// After the stream the waves' blocks are summed in a fixed order through LDS and the same
-// epilogue kinds run, their inputs (residual, positions, RoPE table) read from global.
+// After the stream the waves' blocks are summed in a fixed order through LDS (the x buffers
+// are reused) and the same epilogue kinds run, their inputs read from global.
+constexpr int kMbChunkK = 1024;
+constexpr int kMbXs = kMbChunkK + 8;   // LDS row (halfs): 516 dwords = 4 mod 64 banks, conflict-free A reads
+
+__host__ __device__ inline int mb_xbuf_bytes(int MB) { return align16(2 * 16 * MB * kMbXs * 2); }
 __host__ __device__ inline int mb_lds_bytes(int MB, int ntl, int K) {
-  return align16(ntl * MB * kGemvWaves * kWave * 16) + align16(ntl * (K >> 7) * 32);
+  const int x = mb_xbuf_bytes(MB), slab = align16(ntl * MB * kGemvWaves * kWave * 16);
+  return (x > slab ? x : slab) + align16(ntl * (K >> 7) * 32);
 }
 
 __device__ __forceinline__ f16x8 deq_int4_signed(uint32_t w, uint32_t magic) {
@@ -756,14 +762,152 @@ __device__ __forceinline__ void epilogue_mb(const GemvArgs& a, int nt, int m, in
   }
 }
 
+__device__ __forceinline__ void dma_1k(const void* src_lane, void* lds_wave) {   // 64 lanes x 16 B -> LDS
+  __builtin_amdgcn_global_load_lds(src_lane, lds_wave, 16, 0, 0);
+}
+
 template <int MB, int NTL>
-struct MbChunk {       // one chunk's operands of one wave
+__global__ __launch_bounds__(kGemvThreads, 1) void gemv_mb_kernel(const GemvArgs a, int grid) {
+  constexpr int XDMA = 2 * 16 * MB / kGemvWaves;   // x-chunk DMA instructions per wave (2 per row)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int KT = a.K >> 7, NT = a.N >> 4, NC = (KT + kGemvWaves - 1) / kGemvWaves;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, kq = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int t0 = (int)(blockIdx.x * (unsigned)NT / (unsigned)grid);
+  const int t1 = (int)((blockIdx.x + 1) * (unsigned)NT / (unsigned)grid);
+  const int ntl = t1 - t0;                           // NTL or NTL - 1
+  f16* xb = (f16*)smem;                              // [2][16 MB][kMbXs]
+  const int xslab = mb_xbuf_bytes(MB) > align16(NTL * MB * kGemvWaves * kWave * 16)
+                        ? mb_xbuf_bytes(MB) : align16(NTL * MB * kGemvWaves * kWave * 16);
+  f32x4* slab = (f32x4*)smem;                        // after the stream: [NTL][MB][8][64]
+  uint16_t* sl = (uint16_t*)(smem + xslab);          // [ntl][KT][16]
+
+  // scales of our tiles first (two pieces per thread cover ntl * KT <= 512 groups)
+  const int n_sc = ntl * KT * 2;
+  const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16);
+  const u32x4 sc0 = ld_w(sg + (tid < n_sc ? tid : 0));
+  const u32x4 sc1 = ld_w(sg + (tid + kGemvThreads < n_sc ? tid + kGemvThreads : 0));
+
+  const f16* xg = (const f16*)a.x;
+  auto issue_x = [&](int c) {   // chunk c of every row into buffer c & 1 (rows >= M repeat row M-1)
+#pragma unroll
+    for (int q = 0; q < XDMA; ++q) {
+      const int piece = wave * XDMA + q, row = piece >> 1, half = piece & 1;
+      const int m = row < a.M ? row : a.M - 1;
+      int k = c * kMbChunkK + half * 512 + lane * 8;
+      k = k < a.K ? k : a.K - 8;
+      dma_1k(xg + (size_t)m * a.ldx + k, xb + ((c & 1) * 16 * MB + row) * kMbXs + half * 512);
+    }
+  };
+  const u32x4* tb = a.tiles + lane;
+  auto load = [&](u32x4 (&w)[NTL], int c) {
+    const int kt = min(c * kGemvWaves + wave, KT - 1);
+#pragma unroll
+    for (int tl = 0; tl < NTL; ++tl) w[tl] = ld_w(tb + ((size_t)(t0 + min(tl, ntl - 1)) * KT + kt) * kWave);
+  };
+  u32x4 B0[NTL], B1[NTL];
+  issue_x(0);
+  load(B0, 0);
+  if (tid < n_sc) ((u32x4*)sl)[tid] = sc0;
+  if (tid + kGemvThreads < n_sc) ((u32x4*)sl)[tid + kGemvThreads] = sc1;
+  asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NTL) : "memory");   // x chunk 0 landed (B0 may fly)
+  lds_barrier();
+
+  f32x4 acc[NTL][MB];
+#pragma unroll
+  for (int t = 0; t < NTL; ++t)
+#pragma unroll
+    for (int b = 0; b < MB; ++b) acc[t][b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+  uint32_t magic;
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
+  auto compute = [&](const u32x4 (&w)[NTL], int c) {
+    const int kt = c * kGemvWaves + wave;
+    const bool kvalid = kt < KT;
+    const f16* xr = xb + ((c & 1) * 16 * MB + r) * kMbXs + wave * 128 + kq * 32;   // the tile's k order
+    f16x8 xf[MB][4];
+#pragma unroll
+    for (int b = 0; b < MB; ++b)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) xf[b][s4] = *(const f16x8*)(xr + b * 16 * kMbXs + s4 * 8);
+#pragma unroll
+    for (int tl = 0; tl < NTL; ++tl) {
+      f32x4 t[MB];
+#pragma unroll
+      for (int b = 0; b < MB; ++b) t[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const f16x8 bf = deq_int4_signed(w[tl][s4], magic);
+#pragma unroll
+        for (int b = 0; b < MB; ++b) t[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[b][s4], bf, t[b], 0, 0, 0);
+      }
+      const float sc = kvalid ? h2f(sl[(min(tl, ntl - 1) * KT + kt) * 16 + r]) : 0.0f;
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        acc[tl][b][0] = fmaf(sc, t[b][0], acc[tl][b][0]);
+        acc[tl][b][1] = fmaf(sc, t[b][1], acc[tl][b][1]);
+        acc[tl][b][2] = fmaf(sc, t[b][2], acc[tl][b][2]);
+        acc[tl][b][3] = fmaf(sc, t[b][3], acc[tl][b][3]);
+      }
+    }
+  };
+  // Per chunk: DMA the next x chunk into the other buffer, load the next weights, compute,
+  // wait for our DMA (the NTL weight loads after it may still fly), barrier.  Reloads past the
+  // end are clamped and harmless; the tail computes load nothing.
+  int c = 0;
+  for (; c + 1 < NC; c += 2) {
+    issue_x(c + 1);
+    load(B1, c + 1);
+    compute(B0, c);
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NTL) : "memory");
+    lds_barrier();
+    issue_x(c + 2 < NC ? c + 2 : NC - 1);
+    load(B0, c + 2 < NC ? c + 2 : NC - 1);
+    compute(B1, c + 1);
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NTL) : "memory");
+    lds_barrier();
+  }
+  if (c < NC) compute(B0, c);
+
+  // ---- sum the 8 waves' blocks in a fixed order, then the epilogue
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // clamped reloads / DMA done before the slab reuses LDS
+  lds_barrier();
+#pragma unroll
+  for (int tl = 0; tl < NTL; ++tl)
+#pragma unroll
+    for (int b = 0; b < MB; ++b) slab[((tl * MB + b) * kGemvWaves + wave) * kWave + lane] = acc[tl][b];
+  lds_barrier();
+  const int n = lane & 15, nblk = ntl * MB * 4;
+  const int nblk_pad = (nblk + kGemvWaves - 1) / kGemvWaves * kGemvWaves;
+  for (int cb = wave; cb < nblk_pad; cb += kGemvWaves) {   // wave-uniform trip count (shuffles inside)
+    const bool ok = cb < nblk;
+    const int cbc = ok ? cb : 0, tl = cbc / (MB * 4), b = (cbc >> 2) % MB, i = cbc & 3;
+    const float* sp = (const float*)(slab + (tl * MB + b) * kGemvWaves * kWave + lane) + i;
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kGemvWaves; ++w) v += sp[w * kWave * 4];
+    const int m = b * 16 + 4 * (lane >> 4) + i;
+    epilogue_mb(a, t0 + tl, m, n, v, ok && m < a.M);
+  }
+  if (a.epi.kind == TI_EPI_LOGITS_ARGMAX && a.epi.step_ctr && blockIdx.x == 0 && tid == 0)
+    *a.epi.step_ctr += a.epi.advance;
+}
+
+__host__ __device__ inline int mbr_slab_bytes(int MB, int ntl) { return align16(ntl * MB * kGemvWaves * kWave * 16); }
+__host__ __device__ inline int mbr_lds_bytes(int MB, int ntl, int K) {
+  return mbr_slab_bytes(MB, ntl) + align16(ntl * (K >> 7) * 32);
+}
+
+template <int MB, int NTL>
+struct MbrChunk {       // one chunk's operands of one wave
   u32x4 w[NTL];        // packed int4 weights of (tile tl, this wave's k-tile)
   f16x8 x[MB][4];      // A fragments: rows 16 b + (lane & 15), k = kt*128 + 32 (lane >> 4) + 8 s4
 };
 
+// Register-fragment variant (one 16-row block): each wave loads the A fragments of its own
+// k-tile straight into registers, one chunk ahead, so no barrier is needed until the end;
+// at <= 16 rows this beats the LDS-staged kernel (bench.py --batch 8/16).
 template <int MB, int NTL>
-__global__ __launch_bounds__(kGemvThreads, 1) void gemv_mb_kernel(const GemvArgs a, int grid) {
+__global__ __launch_bounds__(kGemvThreads, 1) void gemv_mbr_kernel(const GemvArgs a, int grid) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KT = a.K >> 7, NT = a.N >> 4, NC = (KT + kGemvWaves - 1) / kGemvWaves;
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, kq = lane >> 4;
@@ -772,7 +916,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_mb_kernel(const GemvArgs
   const int t1 = (int)((blockIdx.x + 1) * (unsigned)NT / (unsigned)grid);
   const int ntl = t1 - t0;                           // NTL or NTL - 1
   f32x4* slab = (f32x4*)smem;                        // after the stream: [NTL][MB][8][64]
-  uint16_t* sl = (uint16_t*)(smem + align16(NTL * MB * kGemvWaves * kWave * 16));   // [ntl][KT][16]
+  uint16_t* sl = (uint16_t*)(smem + mbr_slab_bytes(MB, NTL));   // [ntl][KT][16]
 
   // scales of our tiles: loaded first (two pieces per thread cover ntl * KT <= 512 groups)
   const int n_sc = ntl * KT * 2;
@@ -782,7 +926,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_mb_kernel(const GemvArgs
 
   const f16* xg = (const f16*)a.x;
   const u32x4* tb = a.tiles + lane;
-  auto load = [&](MbChunk<MB, NTL>& ch, int c) {
+  auto load = [&](MbrChunk<MB, NTL>& ch, int c) {
     const int kt = min(c * kGemvWaves + wave, KT - 1);
 #pragma unroll
     for (int tl = 0; tl < NTL; ++tl) ch.w[tl] = ld_w(tb + ((size_t)(t0 + min(tl, ntl - 1)) * KT + kt) * kWave);
@@ -794,7 +938,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_mb_kernel(const GemvArgs
       for (int s4 = 0; s4 < 4; ++s4) ch.x[b][s4] = *(const f16x8*)(xr + s4 * 8);
     }
   };
-  MbChunk<MB, NTL> B0, B1;
+  MbrChunk<MB, NTL> B0, B1;
   load(B0, 0);
   if (tid < n_sc) ((u32x4*)sl)[tid] = sc0;
   if (tid + kGemvThreads < n_sc) ((u32x4*)sl)[tid + kGemvThreads] = sc1;
@@ -807,7 +951,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_mb_kernel(const GemvArgs
     for (int b = 0; b < MB; ++b) acc[t][b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
   uint32_t magic;
   asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
-  auto compute = [&](const MbChunk<MB, NTL>& ch, int c) {
+  auto compute = [&](const MbrChunk<MB, NTL>& ch, int c) {
     const int kt = c * kGemvWaves + wave;
     const bool kvalid = kt < KT;
 #pragma unroll
@@ -933,10 +1077,24 @@ __host__ inline int mb_grid(int MB, int N, int K, int num_cus, int* ntl_out) {
   return grid;
 }
 
+// One 16-row block: the register-fragment kernel unless TI_GEMM_MB_LDS=1 (A/B knob).
+static int g_mb_lds = -1;
+static bool mb_use_lds(int MB) {
+  if (g_mb_lds < 0) {
+    const char* s = getenv("TI_GEMM_MB_LDS");
+    g_mb_lds = s && atoi(s) > 0 ? 1 : 0;
+  }
+  return MB == 2 || g_mb_lds == 1;
+}
 template <int MB, int NTL>
 static int launch_mb_t(const GemvArgs& a, int grid, int lds, hipStream_t s) {
-  hipLaunchKernelGGL((gemv_mb_kernel<MB, NTL>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
-  TI_LAUNCH_CHECK("gemv_mb_kernel");
+  if (mb_use_lds(MB)) {
+    hipLaunchKernelGGL((gemv_mb_kernel<MB, NTL>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
+    TI_LAUNCH_CHECK("gemv_mb_kernel");
+  } else {
+    hipLaunchKernelGGL((gemv_mbr_kernel<MB, NTL>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
+    TI_LAUNCH_CHECK("gemv_mbr_kernel");
+  }
   return TI_OK;
 }
 static int launch_mb(const GemvArgs& a, int MB, int grid, int ntl, int lds, hipStream_t s) {
@@ -960,10 +1118,11 @@ static int launch_mb(const GemvArgs& a, int MB, int grid, int ntl, int lds, hipS
     default: return launch_mb_t<1, 8>(a, grid, lds, s);
   }
 }
-#define TI_MB_FNS                                                                                   \
-  (const void*)gemv_mb_kernel<1, 1>, (const void*)gemv_mb_kernel<1, 2>, (const void*)gemv_mb_kernel<1, 3>,     \
-      (const void*)gemv_mb_kernel<1, 4>, (const void*)gemv_mb_kernel<1, 5>, (const void*)gemv_mb_kernel<1, 6>, \
-      (const void*)gemv_mb_kernel<1, 7>, (const void*)gemv_mb_kernel<1, 8>, (const void*)gemv_mb_kernel<2, 1>, \
+#define TI_MB_FNS1(K)                                                                                \
+  (const void*)K<1, 1>, (const void*)K<1, 2>, (const void*)K<1, 3>, (const void*)K<1, 4>, (const void*)K<1, 5>, \
+      (const void*)K<1, 6>, (const void*)K<1, 7>, (const void*)K<1, 8>
+#define TI_MB_FNS                                                                                      \
+  TI_MB_FNS1(gemv_mb_kernel), TI_MB_FNS1(gemv_mbr_kernel), (const void*)gemv_mb_kernel<2, 1>,           \
       (const void*)gemv_mb_kernel<2, 2>, (const void*)gemv_mb_kernel<2, 3>, (const void*)gemv_mb_kernel<2, 4>, \
       (const void*)gemv_mb_kernel<2, 5>
 
@@ -1089,8 +1248,9 @@ extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bit
                         "kernel needs bits 4 and fp16 rows (normalise with ti_rmsnorm_f16)", M, K);
   int grid = 0, lds = 0, ntl = 0;
   if (batched) {
-    grid = mb_grid(M > 16 ? 2 : 1, N, K, query_cus(), &ntl);
-    lds = mb_lds_bytes(M > 16 ? 2 : 1, ntl, K);
+    const int MB = M > 16 ? 2 : 1;
+    grid = mb_grid(MB, N, K, query_cus(), &ntl);
+    lds = mb_use_lds(MB) ? mb_lds_bytes(MB, ntl, K) : mbr_lds_bytes(MB, ntl, K);
   } else {
     grid = gemv_grid(M, N, K, query_cus());
     lds = gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid);
