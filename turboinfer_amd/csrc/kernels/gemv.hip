@@ -796,11 +796,17 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_mb_kernel(const GemvArgs
       const int m = row < a.M ? row : a.M - 1;
       int k = c * kMbChunkK + half * 512 + lane * 8;
       k = k < a.K ? k : a.K - 8;
+#if TI_GEMV_EXP & 8   // diagnostic: no activation traffic (the first chunk only)
+      if (c > 0) continue;
+#endif
       dma_1k(xg + (size_t)m * a.ldx + k, xb + ((c & 1) * 16 * MB + row) * kMbXs + half * 512);
     }
   };
   const u32x4* tb = a.tiles + lane;
   auto load = [&](u32x4 (&w)[NTL], int c) {
+#if TI_GEMV_EXP & 32  // diagnostic: no weight traffic (the first chunk's weights re-used)
+    c = 0;
+#endif
     const int kt = min(c * kGemvWaves + wave, KT - 1);
 #pragma unroll
     for (int tl = 0; tl < NTL; ++tl) w[tl] = ld_w(tb + ((size_t)(t0 + min(tl, ntl - 1)) * KT + kt) * kWave);
@@ -1064,9 +1070,8 @@ __global__ __launch_bounds__(kGemvThreads) void rmsnorm_f16_kernel(const float* 
 
 // Batched-rows geometry: at most 8 tiles per workgroup (register accumulators), and the
 // workgroup's scales in two 16-byte pieces per thread.
-// (MB = 2 keeps 5 tiles of accumulators and two chunk buffers in 256 VGPRs without spilling.)
 __host__ inline int mb_tiles_cap(int MB, int K) {
-  const int lim = MB == 2 ? 5 : 8, cap = 512 / (K >> 7);
+  const int lim = MB == 2 ? 6 : 8, cap = 512 / (K >> 7);   // (register budget: no spills)
   return cap < 1 ? 1 : (cap > lim ? lim : cap);
 }
 __host__ inline int mb_grid(int MB, int N, int K, int num_cus, int* ntl_out) {
@@ -1088,13 +1093,15 @@ static bool mb_use_lds(int MB) {
 }
 template <int MB, int NTL>
 static int launch_mb_t(const GemvArgs& a, int grid, int lds, hipStream_t s) {
-  if (mb_use_lds(MB)) {
-    hipLaunchKernelGGL((gemv_mb_kernel<MB, NTL>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
-    TI_LAUNCH_CHECK("gemv_mb_kernel");
-  } else {
-    hipLaunchKernelGGL((gemv_mbr_kernel<MB, NTL>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
-    TI_LAUNCH_CHECK("gemv_mbr_kernel");
+  if constexpr (MB == 1) {
+    if (!mb_use_lds(MB)) {
+      hipLaunchKernelGGL((gemv_mbr_kernel<MB, NTL>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
+      TI_LAUNCH_CHECK("gemv_mbr_kernel");
+      return TI_OK;
+    }
   }
+  hipLaunchKernelGGL((gemv_mb_kernel<MB, NTL>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
+  TI_LAUNCH_CHECK("gemv_mb_kernel");
   return TI_OK;
 }
 static int launch_mb(const GemvArgs& a, int MB, int grid, int ntl, int lds, hipStream_t s) {
@@ -1104,7 +1111,8 @@ static int launch_mb(const GemvArgs& a, int MB, int grid, int ntl, int lds, hipS
       case 2: return launch_mb_t<2, 2>(a, grid, lds, s);
       case 3: return launch_mb_t<2, 3>(a, grid, lds, s);
       case 4: return launch_mb_t<2, 4>(a, grid, lds, s);
-      default: return launch_mb_t<2, 5>(a, grid, lds, s);
+      case 5: return launch_mb_t<2, 5>(a, grid, lds, s);
+      default: return launch_mb_t<2, 6>(a, grid, lds, s);
     }
   }
   switch (ntl) {
@@ -1124,7 +1132,7 @@ static int launch_mb(const GemvArgs& a, int MB, int grid, int ntl, int lds, hipS
 #define TI_MB_FNS                                                                                      \
   TI_MB_FNS1(gemv_mb_kernel), TI_MB_FNS1(gemv_mbr_kernel), (const void*)gemv_mb_kernel<2, 1>,           \
       (const void*)gemv_mb_kernel<2, 2>, (const void*)gemv_mb_kernel<2, 3>, (const void*)gemv_mb_kernel<2, 4>, \
-      (const void*)gemv_mb_kernel<2, 5>
+      (const void*)gemv_mb_kernel<2, 5>, (const void*)gemv_mb_kernel<2, 6>
 
 static bool g_prepared = false;
 
