@@ -69,6 +69,12 @@ int ti_engine_generate(ti_engine* e, int n_streams, const int32_t* prompts, cons
                        int prompt_stride, const int32_t* start_pos, int max_new, int32_t* out_tokens,
                        float* last_logits);
 
+/* Prefill of ti_engine_generate's prompts (reference forward_pass, inference_engine.cpp:
+ * 1429-1491): all but the last token of the shortest prompt are processed `rows` tokens at a
+ * time as rows of the batched GEMMs and causal attention over the stream's own KV cache,
+ * instead of one token per decode step.  Default: TI_GEMM_MAX_ROWS (int4) or 16; 0 = off. */
+int ti_engine_set_prefill(ti_engine* e, int rows);
+
 /* One decode step: token[s] at position pos[s] for each stream; logits [n][vocab] to host
  * (used for non-greedy sampling and per-step parity). */
 int ti_engine_step(ti_engine* e, int n_streams, const int32_t* tokens, const int32_t* pos, float* logits);

@@ -143,7 +143,7 @@ typedef struct ti_epilogue {
   const float* rope_cs;              /* device [max_seq][head_dim/2] (cos, sin) pairs */
   uint16_t* k_cache;                 /* device fp16, this layer: [stream][kv_head][max_seq][head_dim] */
   uint16_t* v_cache;
-  int64_t kv_stream_stride;          /* elements between streams */
+  int64_t kv_stream_stride;          /* elements between streams; 0 = rows of one stream (prefill) */
   /* TI_EPI_LOGITS_ARGMAX */
   unsigned long long* argmax;        /* device [M][TI_ARGMAX_SLOTS] keys, zeroed before the call */
   int32_t* step_ctr;                 /* device counter += advance by one thread (nullable) */
@@ -175,7 +175,8 @@ int ti_gemm_prepare(void);
 /* ------------------------------------------------------------- decode attention
  * Single-query attention of M streams against their fp16 KV caches, GQA aware:
  * q fp32 [M][heads*head_dim]; stream m attends to cache slots [0, pos[m]] of layer cache
- * k_cache/v_cache ([stream][kv_head][max_seq][head_dim], stream stride kv_stream_stride).
+ * k_cache/v_cache ([stream][kv_head][max_seq][head_dim], stream stride kv_stream_stride; 0 = the
+ * M rows are tokens of one stream at their own positions: causal prefill attention).
  * Split-K over the sequence (flash-decoding): `splits` partial (max, sum, o) per
  * (stream, head) in workspace, merged in the same launch by the last-arriving split, which
  * writes fp16 out [M][heads*head_dim].

@@ -72,27 +72,29 @@ def test_gemm_store(ti, oracle, bits, M, K, N):
     assert_close_dot(y, xa.astype(np.float64) @ wf.astype(np.float64), xa, wf)
 
 
-def test_gemm_f16_input_and_store_f16_resid(ti, oracle):
-    M, K, N = 2, 512, 48
+@pytest.mark.parametrize("M,N,bits", [(2, 48, 4), (16, 12288, 8)])
+def test_gemm_f16_input_and_store_f16_resid(ti, oracle, M, N, bits):
+    """(16 rows x 4 tiles per workgroup: residual inputs beyond the one-per-thread prefetch.)"""
+    K = 512
     rng = np.random.RandomState(11)
     w = (rng.standard_normal((K, N)) * 0.05).astype(f32)
     x = rng.standard_normal((M, K)).astype(f16)
-    tiles, scales = ti.wpack_host(w, 4)
+    tiles, scales = ti.wpack_host(w, bits)
     td, sd, xd = dev(ti, tiles), dev(ti, scales), dev(ti, x)
-    wf = deq(oracle, w, 4)
+    wf = deq(oracle, w, bits)
     ref = x.astype(np.float64) @ wf.astype(np.float64)
     # fp16 store
     yd = ti.DeviceBuffer(M * N * 2)
     ep = ti.Epilogue()
     ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F16, N, yd.ptr
-    gemm(ti, td, sd, 4, xd, ti.X_F16, K, M, N, K, ep)
+    gemm(ti, td, sd, bits, xd, ti.X_F16, K, M, N, K, ep)
     y = yd.download(f16, (M, N)).astype(np.float64)
     np.testing.assert_allclose(y, ref, rtol=2e-3, atol=2e-3)
     # residual add in place
     r = rng.standard_normal((M, N)).astype(f32)
     rd = dev(ti, r)
     ep.kind, ep.out = ti.EPI_RESID_F32, rd.ptr
-    gemm(ti, td, sd, 4, xd, ti.X_F16, K, M, N, K, ep)
+    gemm(ti, td, sd, bits, xd, ti.X_F16, K, M, N, K, ep)
     assert_close_dot(rd.download(f32, (M, N)) - r, ref, x.astype(f32), wf, rel=5e-5)
 
 
@@ -138,18 +140,20 @@ def test_gemm_silu_mul_interleaved(ti, oracle):
     np.testing.assert_allclose(yd.download(f16, (M, I)).astype(np.float64), ref, rtol=3e-3, atol=2e-3)
 
 
-@pytest.mark.parametrize("hd,nh,nkv", [(64, 4, 2), (128, 4, 4), (128, 8, 1)])
-def test_gemm_qkv_rope_kv_append(ti, oracle, hd, nh, nkv):
-    M, H, max_seq, theta = 2, 256, 32, 10000.0
+@pytest.mark.parametrize("hd,nh,nkv,M,bits", [(64, 4, 2, 2, 4), (128, 4, 4, 2, 4), (128, 8, 1, 2, 4),
+                                             (128, 4, 4, 12, 8), (64, 8, 2, 16, 8)])
+def test_gemm_qkv_rope_kv_append(ti, oracle, hd, nh, nkv, M, bits):
+    """(M * head_dim > 512: RoPE inputs beyond the one-per-thread prefetch of the fused kernel.)"""
+    H, max_seq, theta = 256, 32, 10000.0
     qd, kvd = nh * hd, nkv * hd
     N = qd + 2 * kvd
     rng = np.random.RandomState(41 + hd + nh)
     ws = [(rng.standard_normal((H, n)) * 0.05).astype(f32) for n in (qd, kvd, kvd)]
     tiles = scales = None
     for w, off in zip(ws, (0, qd, qd + kvd)):
-        tiles, scales = ti.wpack_host(w, 4, n_total=N, row_offset=off, tiles=tiles, scales=scales)
+        tiles, scales = ti.wpack_host(w, bits, n_total=N, row_offset=off, tiles=tiles, scales=scales)
     x = rng.standard_normal((M, H)).astype(f32)
-    pos = np.array([5, 17], np.int32)
+    pos = np.array([5, 17] if M == 2 else list(rng.permutation(max_seq)[:M]), np.int32)
     cs = ti.rope_table(np.arange(max_seq, dtype=f32), hd, theta)
     qd_buf = ti.DeviceBuffer(M * qd * 4)
     stride = nkv * max_seq * hd
@@ -161,9 +165,9 @@ def test_gemm_qkv_rope_kv_append(ti, oracle, hd, nh, nkv):
     ep.kind, ep.ldo, ep.out = ti.EPI_QKV_ROPE_KV, qd, qd_buf.ptr
     ep.q_dim, ep.kv_dim, ep.head_dim, ep.max_seq = qd, kvd, hd, max_seq
     ep.pos, ep.rope_cs, ep.k_cache, ep.v_cache, ep.kv_stream_stride = posd.ptr, csd.ptr, kc.ptr, vc.ptr, stride
-    gemm(ti, dev(ti, tiles), dev(ti, scales), 4, dev(ti, x), ti.X_F32, H, M, N, H, ep)
+    gemm(ti, dev(ti, tiles), dev(ti, scales), bits, dev(ti, x), ti.X_F32, H, M, N, H, ep)
     xa = x.astype(f16).astype(f32)
-    q, k, v = (xa.astype(np.float64) @ deq(oracle, w, 4).astype(np.float64) for w in ws)
+    q, k, v = (xa.astype(np.float64) @ deq(oracle, w, bits).astype(np.float64) for w in ws)
     kcache = kc.download(f16, (M, nkv, max_seq, hd)).astype(f32)
     vcache = vc.download(f16, (M, nkv, max_seq, hd)).astype(f32)
     qgot = qd_buf.download(f32, (M, qd))

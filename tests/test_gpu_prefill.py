@@ -1,0 +1,77 @@
+"""Prefill (reference forward_pass, inference_engine.cpp:1429-1491, keeping the KV): a prompt's
+tokens run as rows of the batched GEMMs with causal attention over the stream's own cache
+(ti_engine_set_prefill), instead of one token per decode step.
+
+Bars as in test_gpu_engine.py: greedy tokens equal wherever the reference's top-2 margin
+exceeds the logits tolerance, logits within 1e-2 x max|logit| of the oracle's
+reference-composed decode; prefill and token-by-token feeding of the same prompt agree to the
+same bar (they differ only in fp32 summation order and fp16 rounding of the KV)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from test_gpu_engine import MID, REL, _oracle_tokens, assert_logits_close, engine_for, margin
+
+pytestmark = pytest.mark.gpu
+
+MID8 = dict(MID, kv_heads=4, head_dim=128, heads=4, bits=8)
+
+
+def _first_tokens_equal(got, ref, ref_logits):
+    for i, (g, r) in enumerate(zip(got, ref)):
+        if margin(ref_logits[i]) <= REL * np.max(np.abs(ref_logits[i])):
+            return
+        assert g == r, (i, got, ref)
+
+
+@pytest.mark.parametrize("cfg", [MID, MID8], ids=["gqa8_w4", "mha_hd128_w8"])
+def test_prefill_long_prompt_vs_oracle(ti, oracle, cfg):
+    """70-token prompt: 3 prefill chunks (32, 32, 5 rows) + the decode loop."""
+    seed, jit = 13, 0.1
+    rng = np.random.RandomState(3)
+    prompt = rng.randint(0, cfg["vocab"], size=70).tolist()
+    ref, ref_logits = _oracle_tokens(oracle, cfg, seed, jit, prompt, 4)
+    e = engine_for(ti, cfg)
+    e.synth(seed, jit)
+    got, lg = e.generate([prompt], 4, want_logits=True)
+    _first_tokens_equal(got[0].tolist(), ref, ref_logits)
+    if got[0].tolist() == ref:
+        assert_logits_close(lg[0], ref_logits[-1])
+    e.close()
+
+
+def test_prefill_matches_token_by_token(ti):
+    """Same engine, same prompt: prefill on vs off (and several streams, ragged prompts)."""
+    seed, jit = 17, 0.1
+    rng = np.random.RandomState(5)
+    prompts = [rng.randint(0, MID["vocab"], size=n).tolist() for n in (41, 45, 64)]
+    outs = []
+    for rows in (ti.GEMM_MAX_ROWS, 0):
+        e = engine_for(ti, MID, max_batch=3)
+        e.synth(seed, jit)
+        e.set_prefill(rows)
+        outs.append(e.generate(prompts, 5, want_logits=True))
+        e.close()
+    (tp, lp), (tt, lt) = outs
+    for b in range(3):
+        if tp[b].tolist() == tt[b].tolist():
+            assert_logits_close(lp[b], lt[b])
+        else:   # only a near-tie may flip a greedy token between the two summation orders
+            assert margin(lt[b]) <= REL * float(np.max(np.abs(lt[b]))) or margin(lp[b]) <= REL * float(np.max(np.abs(lp[b])))
+
+
+def test_prefill_start_pos_and_cache_contents(ti, oracle):
+    """Prefill from a non-zero start position over a synthetic cache prefix."""
+    seed, jit, kv_seed, fill = 5, 0.1, 77, 100
+    rng = np.random.RandomState(7)
+    prompt = rng.randint(0, MID["vocab"], size=37).tolist()
+    ref, ref_logits = _oracle_tokens(oracle, MID, seed, jit, prompt, 3, fill, kv_seed)
+    e = engine_for(ti, MID)
+    e.synth(seed, jit)
+    e.fill_kv(0, fill, kv_seed)
+    got, lg = e.generate([prompt], 3, start_pos=[fill], want_logits=True)
+    _first_tokens_equal(got[0].tolist(), ref, ref_logits)
+    if got[0].tolist() == ref:
+        assert_logits_close(lg[0], ref_logits[-1])
+    e.close()

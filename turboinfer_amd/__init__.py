@@ -72,7 +72,7 @@ EXPORTED = [
     "ti_rope_f32", "ti_silu_f32", "ti_relu_f32", "ti_add_f32", "ti_mul_f32", "ti_softmax_f32", "ti_attention_f32",
     "ti_argmax_f32", "ti_engine_create", "ti_engine_destroy", "ti_engine_get_stream", "ti_engine_memory", "ti_engine_set_tensor",
     "ti_engine_synth", "ti_engine_fill_kv", "ti_engine_generate", "ti_engine_step", "ti_engine_compat_step",
-    "ti_engine_replay_prepare", "ti_engine_replay_run", "ti_engine_sync", "ti_engine_last_tokens",
+    "ti_engine_replay_prepare", "ti_engine_set_prefill", "ti_engine_replay_run", "ti_engine_sync", "ti_engine_last_tokens",
     "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token",
 ]
 
@@ -137,6 +137,7 @@ def lib() -> C.CDLL:
         L.ti_engine_fill_kv.argtypes = [vp, i32, i32, u64]
         L.ti_engine_generate.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp]
         L.ti_engine_step.argtypes = [vp, i32, vp, vp, vp]
+        L.ti_engine_set_prefill.argtypes = [vp, i32]
         L.ti_engine_compat_step.argtypes = [vp, i32, vp]
         L.ti_engine_replay_prepare.argtypes = [vp, i32, i32, i32]
         L.ti_engine_replay_run.argtypes = [vp, i32]
@@ -293,6 +294,10 @@ class Engine:
         check(lib().ti_engine_generate(self.h, n, _ptr(P), _ptr(lens), stride, None if sp is None else _ptr(sp),
                                        max_new, _ptr(out), None if logits is None else _ptr(logits)))
         return (out, logits) if want_logits else out
+
+    def set_prefill(self, rows):
+        """Prompt tokens per prefill chunk (0 = consume prompts one token per decode step)."""
+        check(lib().ti_engine_set_prefill(self.h, rows))
 
     def step(self, tokens, pos):
         t = np.ascontiguousarray(tokens, np.int32)

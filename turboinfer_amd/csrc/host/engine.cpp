@@ -86,7 +86,14 @@ struct ti_engine {
   float* ws = nullptr;
   uint16_t* attn = nullptr;
   uint16_t* act = nullptr;
-  uint16_t* xn = nullptr;      // fp16 rms_norm rows for the batched-rows GEMM [B][hidden]
+  uint16_t* xn = nullptr;      // fp16 rms_norm rows for the batched-rows GEMM [R][hidden]
+  // prefill (forward_pass over prompt tokens): up to pf_rows prompt tokens of one stream run
+  // as rows of the batched path, sharing that stream's KV cache (stride 0)
+  int pf_rows = 0;             // 0 = off (prompts consumed one token per decode step)
+  int rows_cap = 0;            // R = max(max_batch, pf_rows): rows the step buffers hold
+  int32_t* pf_ones = nullptr;  // [pf_rows] 1
+  int32_t* pf_zero = nullptr;  // [1] 0
+  int32_t* pf_base = nullptr;  // [pf_rows] positions of the chunk's rows
   unsigned long long* argmax = nullptr;
   int32_t* pos = nullptr;
   int32_t* base_pos = nullptr;
@@ -278,6 +285,73 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   return gemm(e->lm, e->h, TI_X_F32_RMSNORM, H, 4, e->out_norm, el, 4, true);
 }
 
+// Prefill (reference forward_pass, inference_engine.cpp:1429-1491, with the KV kept): prompt
+// tokens [t0, t0 + rows) of stream m at positions base + t0 + j, as `rows` rows of the
+// batched path that share stream m's KV cache (epilogue / attention stream stride 0: row j
+// appends at its own position and attends to [0, base + t0 + j], causal).  No lm_head: the
+// decode loop takes over at the last prompt token.  Not graph-captured (host position upload).
+int enqueue_prefill(ti_engine* e, int m, int t0, int rows, int base) {
+  const ti_engine_config& c = e->c;
+  std::vector<int32_t> bp(rows);
+  for (int j = 0; j < rows; ++j) bp[j] = base + t0 + j;
+  TI_TRY(ti_memcpy_h2d(e->pf_base, bp.data(), (size_t)rows * 4, e->s));
+  ti_step_args sa{};
+  sa.emb = e->emb;
+  sa.h = e->h;
+  sa.hidden = c.hidden;
+  sa.M = rows;
+  sa.vocab = c.vocab;
+  sa.in_stride = 1;                       // row j reads in_tokens[j + step_ctr] = token t0 + j
+  sa.out_stride = 0;
+  sa.placeholder_first = -1;
+  sa.in_tokens = e->in_tokens + (size_t)m * e->in_cap + t0;
+  sa.n_in = e->pf_ones;
+  sa.argmax = e->argmax;
+  sa.out_tokens = nullptr;
+  sa.pos = e->pos;
+  sa.base_pos = e->pf_base;
+  sa.step_ctr = e->pf_zero;
+  TI_TRY(ti_step_begin(&sa, e->s));
+  const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter;
+  for (int l = 0; l < c.layers; ++l) {
+    DevLayer& L = e->layer[l];
+    uint16_t* kc = L.kc + (size_t)m * e->kv_stride;
+    uint16_t* vc = L.vc + (size_t)m * e->kv_stride;
+    ti_epilogue ep{};
+    ep.kind = TI_EPI_QKV_ROPE_KV;
+    ep.ldo = qd;
+    ep.out = e->q;
+    ep.q_dim = qd;
+    ep.kv_dim = kvd;
+    ep.head_dim = c.head_dim;
+    ep.max_seq = c.max_seq;
+    ep.pos = e->pos;
+    ep.rope_cs = e->rope_cs;
+    ep.k_cache = kc;
+    ep.v_cache = vc;
+    ep.kv_stream_stride = 0;
+    TI_TRY(gemm_rows(e, L.qkv, rows, e->h, TI_X_F32_RMSNORM, H, L.attn_norm, ep, 4, false));
+    TI_TRY(ti_attn_decode(e->q, kc, vc, 0, c.max_seq, e->pos, rows, c.heads, c.kv_heads, c.head_dim,
+                          e->splits_for(rows), e->ws, e->attn, e->s));
+    ti_epilogue eo{};
+    eo.kind = TI_EPI_RESID_F32;
+    eo.ldo = H;
+    eo.out = e->h;
+    TI_TRY(gemm_rows(e, L.o, rows, e->attn, TI_X_F16, qd, nullptr, eo, 4, false));
+    ti_epilogue eg{};
+    eg.kind = TI_EPI_SILU_MUL_F16;
+    eg.ldo = I;
+    eg.out = e->act;
+    TI_TRY(gemm_rows(e, L.gu, rows, e->h, TI_X_F32_RMSNORM, H, L.ffn_norm, eg, 2, false));
+    ti_epilogue ed{};
+    ed.kind = TI_EPI_RESID_F32;
+    ed.ldo = H;
+    ed.out = e->h;
+    TI_TRY(gemm_rows(e, L.down, rows, e->act, TI_X_F16, I, nullptr, ed, 4, false));
+  }
+  return TI_OK;
+}
+
 int get_graph(ti_engine* e, int M, int advance, hipGraphExec_t* out) {
   auto key = std::make_pair(M, advance);
   auto it = e->graphs.find(key);
@@ -381,13 +455,22 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     if ((rc = ti_rope_table(pv.data(), c.max_seq, hd, c.rope_theta, cs.data()))) return fail(rc);
     if ((rc = ti_memcpy_h2d(e->rope_cs, cs.data(), cs.size() * 4, e->s))) return fail(rc);
     e->splits_max = e->splits_for(1);
-    if ((rc = e->alloc_t(&e->q, (size_t)B * qd)) || (rc = e->alloc_t(&e->attn, (size_t)B * qd)) ||
-        (rc = e->alloc_t(&e->act, (size_t)B * I)) || (rc = e->alloc_t(&e->xn, (size_t)B * H)) ||
-        (rc = e->alloc(reinterpret_cast<void**>(&e->ws), ti_attn_workspace_bytes(B, c.heads, hd, e->splits_max))))
+    e->pf_rows = c.bits == 4 ? TI_GEMM_MAX_ROWS : 16;
+    e->rows_cap = std::max(B, e->pf_rows);
+    const int R = e->rows_cap;
+    if ((rc = e->alloc_t(&e->q, (size_t)R * qd)) || (rc = e->alloc_t(&e->attn, (size_t)R * qd)) ||
+        (rc = e->alloc_t(&e->act, (size_t)R * I)) || (rc = e->alloc_t(&e->xn, (size_t)R * H)) ||
+        (rc = e->alloc(reinterpret_cast<void**>(&e->ws), ti_attn_workspace_bytes(R, c.heads, hd, e->splits_max))) ||
+        (rc = e->alloc_t(&e->pf_ones, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->pf_zero, (size_t)1)) ||
+        (rc = e->alloc_t(&e->pf_base, (size_t)e->pf_rows)))
+      return fail(rc);
+    std::vector<int32_t> ones(e->pf_rows, 1);
+    if ((rc = ti_memcpy_h2d(e->pf_ones, ones.data(), ones.size() * 4, e->s)) || (rc = ti_memset(e->pf_zero, 0, 4, e->s)))
       return fail(rc);
   }
-  if ((rc = e->alloc_t(&e->h, (size_t)B * H)) || (rc = e->alloc_t(&e->logits, (size_t)B * V)) ||
-      (rc = e->alloc_t(&e->argmax, (size_t)B * TI_ARGMAX_SLOTS)) || (rc = e->alloc_t(&e->pos, (size_t)B)) ||
+  const int R = std::max(B, e->rows_cap);
+  if ((rc = e->alloc_t(&e->h, (size_t)R * H)) || (rc = e->alloc_t(&e->logits, (size_t)B * V)) ||
+      (rc = e->alloc_t(&e->argmax, (size_t)R * TI_ARGMAX_SLOTS)) || (rc = e->alloc_t(&e->pos, (size_t)R)) ||
       (rc = e->alloc_t(&e->base_pos, (size_t)B)) || (rc = e->alloc_t(&e->step_ctr, (size_t)1)) ||
       (rc = e->alloc_t(&e->n_in, (size_t)B)) || (rc = ensure_io(e, 8, 8)))
     return fail(rc);
@@ -537,10 +620,18 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
   TI_TRY(ti_memcpy_h2d(e->in_tokens, in.data(), in.size() * 4, e->s));
   TI_TRY(ti_memcpy_h2d(e->n_in, nin.data(), (size_t)n * 4, e->s));
   TI_TRY(ti_memcpy_h2d(e->base_pos, base.data(), (size_t)n * 4, e->s));
-  TI_TRY(ti_memset(e->step_ctr, 0, 4, e->s));
+  // all but the last prompt token of the shortest prompt go through prefill; the decode loop
+  // then starts at that step (same positions, same token feed, same outputs)
+  int s0 = 0;
+  if (e->pf_rows > 0) {
+    s0 = *std::min_element(nin.begin(), nin.end()) - 1;
+    for (int m = 0; m < n; ++m)
+      for (int t0 = 0; t0 < s0; t0 += e->pf_rows) TI_TRY(enqueue_prefill(e, m, t0, std::min(e->pf_rows, s0 - t0), base[m]));
+  }
+  TI_TRY(ti_memcpy_h2d(e->step_ctr, &s0, 4, e->s));
   hipGraphExec_t g = nullptr;
   TI_TRY(get_graph(e, n, 1, &g));
-  for (int s = 0; s < steps; ++s) E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
+  for (int s = s0; s < steps; ++s) E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
   TI_TRY(ti_stream_sync(e->s));
   std::vector<int32_t> outd((size_t)n * e->out_cap);
   std::vector<unsigned long long> am;
@@ -557,6 +648,13 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
     }
   }
   if (last_logits) TI_TRY(ti_memcpy_d2h(last_logits, e->logits, (size_t)n * c.vocab * 4, e->s));
+  return TI_OK;
+}
+
+int ti_engine_set_prefill(ti_engine* e, int rows) {
+  if (!e || e->c.compat || rows < 0 || rows > e->rows_cap || (rows > 0 && rows > (e->c.bits == 4 ? TI_GEMM_MAX_ROWS : 16)))
+    return ti_set_error(TI_ERR_ARG, "ti_engine_set_prefill: rows %d", rows);
+  e->pf_rows = rows;
   return TI_OK;
 }
 

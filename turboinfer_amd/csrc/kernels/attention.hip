@@ -362,7 +362,9 @@ extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uin
                         kv_heads, splits);
   if (head_dim != 64 && head_dim != 128)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_attn_decode: head_dim %d not in {64,128}", head_dim);
-  if (kv_stream_stride < (int64_t)kv_heads * max_seq * head_dim)
+  // stride 0: the M rows are tokens of ONE stream (prefill), each attending to its own
+  // prefix [0, pos[m]] of the shared cache
+  if (kv_stream_stride != 0 && kv_stream_stride < (int64_t)kv_heads * max_seq * head_dim)
     return ti_set_error(TI_ERR_ARG, "ti_attn_decode: kv_stream_stride too small");
   const int G = heads / kv_heads;
   // splits only shape the work (results agree to rounding); the merge stages all partials

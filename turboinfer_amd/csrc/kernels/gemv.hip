@@ -608,6 +608,15 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   // ---- 5. epilogue inputs into LDS, reduce the 8 partials per tile, epilogue
   if (tid < n_res) es[tid] = pre;
   if (tid < n_cs) es[tid] = cs_reg;
+  // inputs past the one-per-thread prefetch (ntl * M * 16 or M * head_dim > 512): loaded now
+  for (int i = tid + kGemvThreads; i < n_res; i += kGemvThreads) {
+    const int tl = i / (a.M * 16), rem = i - tl * a.M * 16, m = rem >> 4, n = rem & 15;
+    es[i] = p_pre[(size_t)m * ldo + (t0 + tl) * 16 + n];
+  }
+  for (int i = tid + kGemvThreads; i < n_cs; i += kGemvThreads) {
+    const int hd = a.epi.head_dim, m = i / hd, j = i - m * hd;
+    es[i] = a.epi.rope_cs[(size_t)((const int*)(es + a.M * hd))[m] * hd + j];
+  }
   lds_barrier();
   GEMV_TS(5);
   unsigned long long best[4] = {0ull, 0ull, 0ull, 0ull};
