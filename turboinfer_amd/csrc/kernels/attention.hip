@@ -47,6 +47,9 @@ struct AttnArgs {
 // range for a GQA group (Llama-3-8B, 32 streams x 8192 keys: 236 -> 197 us per layer).
 #define TI_ATTN_RING 2
 #endif
+#ifndef TI_ATTN_RING_HP
+#define TI_ATTN_RING_HP 8   // keys in flight per wave in the head-parallel layout
+#endif
 #ifndef TI_ATTN_RING_LONG
 #define TI_ATTN_RING_LONG 4
 #endif
@@ -117,8 +120,9 @@ __device__ __forceinline__ float groups_sum(float v) {
   else return v;
 }
 
-template <int HD, int G, int R>
+template <int HD, int G, int R, bool HP>   // HP: head-parallel lanes (G >= 4, HD / (64 / G) == 8; see below)
 __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnArgs a) {
+  static_assert(!HP || (G >= 4 && HD / (64 / G) == 8), "head-parallel layout: 8 dims per lane");
   constexpr int LPK = HD / 8;       // lanes per key row
   constexpr int KPW = 64 / LPK;     // keys per slot (wave-load)
   __shared__ float s_m[kAttnWaves][G], s_l[kAttnWaves][G];
@@ -140,97 +144,167 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
   const uint16_t* kb = a.kc + base;
   const uint16_t* vb = a.vc + base;
 
-  // the K/V ring first (nothing else to wait for), then q
-  int rj = 0;
-  auto slot_key = [&](int i) { return s0 + (wave + kAttnWaves * i) * KPW + kg; };
-  u32x4 kr[R], vr[R];
-  auto refill = [&](int s) {
-    const int key = min(slot_key(rj < total ? rj : max(total - 1, 0)), max(s1 - 1, 0));
-    ++rj;
-    kr[s] = ld_kv((const u32x4*)(kb + (int64_t)key * HD));
-    vr[s] = ld_kv((const u32x4*)(vb + (int64_t)key * HD));
-  };
+  if constexpr (HP) {
+    // head-parallel layout (G >= 4 q-heads per kv-head): lane l serves q-head l / LPH of the
+    // group, dims 8 (l % LPH) .. +8, one key per wave step; every head's (max, sum, o) stays
+    // in its own LPH lanes, so no lane-group merge is needed after the stream.
+    constexpr int LPH = 64 / G;
+    const int hg = lane / LPH, dh = lane % LPH;
+    const int64_t hb = (int64_t)m * a.stride + (int64_t)kvh * a.max_seq * HD + dh * 8;
+    const int nkey = s1 > s0 ? s1 - s0 : 0;
+    const int total = wave < nkey ? (nkey - wave + kAttnWaves - 1) / kAttnWaves : 0;   // this wave's keys
+    int rj = 0;
+    u32x4 kr[R], vr[R];
+    auto refill = [&](int s) {
+      const int key = min(s0 + wave + kAttnWaves * (rj < total ? rj : max(total - 1, 0)), max(s1 - 1, 0));
+      ++rj;
+      kr[s] = ld_kv((const u32x4*)(a.kc + hb + (int64_t)key * HD));
+      vr[s] = ld_kv((const u32x4*)(a.vc + hb + (int64_t)key * HD));
+    };
 #pragma unroll
-  for (int s = 0; s < R; ++s) refill(s);
-
-  float q[G][8];
+    for (int s = 0; s < R; ++s) refill(s);
+    float qh[8];
+    {
+      const float* qp = a.q + (size_t)m * a.heads * HD + (size_t)(kvh * G + hg) * HD + dh * 8;
+      const float4 q0 = *(const float4*)qp, q1 = *(const float4*)(qp + 4);
+      qh[0] = q0.x * a.scale; qh[1] = q0.y * a.scale; qh[2] = q0.z * a.scale; qh[3] = q0.w * a.scale;
+      qh[4] = q1.x * a.scale; qh[5] = q1.y * a.scale; qh[6] = q1.z * a.scale; qh[7] = q1.w * a.scale;
+    }
+    float m1 = -INFINITY, l1 = 0.0f, acc1[8];
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const float* qp = a.q + (size_t)m * a.heads * HD + (size_t)(kvh * G + g) * HD + dl * 8;
-    const float4 q0 = *(const float4*)qp, q1 = *(const float4*)(qp + 4);
-    q[g][0] = q0.x * a.scale; q[g][1] = q0.y * a.scale; q[g][2] = q0.z * a.scale; q[g][3] = q0.w * a.scale;
-    q[g][4] = q1.x * a.scale; q[g][5] = q1.y * a.scale; q[g][6] = q1.z * a.scale; q[g][7] = q1.w * a.scale;
-  }
-  float mrun[G], lrun[G], acc[G][8];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    mrun[g] = -INFINITY;
-    lrun[g] = 0.0f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[g][e] = 0.0f;
-  }
-
-  int ci = 0;   // compute cursor (slot index of this wave)
-  auto consume = [&](const u32x4& kv, const u32x4& vv) {
-    const bool valid = slot_key(ci) < s1;
-    ++ci;
-    float kf[8], vf[8];
-    unpack8(kv, kf);
-    unpack8(vv, vf);
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
+    for (int e = 0; e < 8; ++e) acc1[e] = 0.0f;
+    int ci = 0;
+    auto consume = [&](const u32x4& kv, const u32x4& vv) {
+      const bool valid = ci < total;
+      ++ci;
+      float kf[8], vf[8];
+      unpack8(kv, kf);
+      unpack8(vv, vf);
       float d = 0.0f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d = fmaf(q[g][e], kf[e], d);
-      d = group_sum<LPK>(d);
+      for (int e = 0; e < 8; ++e) d = fmaf(qh[e], kf[e], d);
+      d = group_sum<LPH>(d);
       const float sc = valid ? d : -INFINITY;
-      const float mn = fmaxf(mrun[g], sc);
-      const float alpha = mrun[g] == mn ? 1.0f : __expf(mrun[g] - mn);
-      const float p = valid ? __expf(sc - mn) : 0.0f;
-      lrun[g] = fmaf(lrun[g], alpha, p);
-      mrun[g] = mn;
+      const float mn = fmaxf(m1, sc);
+      const float alpha = m1 == mn ? 1.0f : __expf(m1 - mn);
+      const float pr = valid ? __expf(sc - mn) : 0.0f;
+      l1 = fmaf(l1, alpha, pr);
+      m1 = mn;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(p, vf[e], acc[g][e] * alpha);
+      for (int e = 0; e < 8; ++e) acc1[e] = fmaf(pr, vf[e], acc1[e] * alpha);
+    };
+    int j0 = 0;
+    for (; j0 + R <= total; j0 += R) {
+#pragma unroll
+      for (int s = 0; s < R; ++s) {
+        consume(kr[s], vr[s]);
+        refill(s);
+      }
     }
-  };
-  int j0 = 0;
-  for (; j0 + R <= total; j0 += R) {
 #pragma unroll
-    for (int s = 0; s < R; ++s) {
-      consume(kr[s], vr[s]);
-      refill(s);
+    for (int s = 0; s < R; ++s)
+      if (j0 + s < total) consume(kr[s], vr[s]);
+    ATTN_TS(1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s_acc[wave][hg][dh * 8 + e] = acc1[e];
+    if (dh == 0) {
+      s_m[wave][hg] = m1;
+      s_l[wave][hg] = l1;
     }
-  }
-#pragma unroll
-  for (int s = 0; s < R; ++s)
-    if (j0 + s < total) consume(kr[s], vr[s]);
+    __syncthreads();
+  } else {
+    // the K/V ring first (nothing else to wait for), then q
+    int rj = 0;
+    auto slot_key = [&](int i) { return s0 + (wave + kAttnWaves * i) * KPW + kg; };
+    u32x4 kr[R], vr[R];
+    auto refill = [&](int s) {
+      const int key = min(slot_key(rj < total ? rj : max(total - 1, 0)), max(s1 - 1, 0));
+      ++rj;
+      kr[s] = ld_kv((const u32x4*)(kb + (int64_t)key * HD));
+      vr[s] = ld_kv((const u32x4*)(vb + (int64_t)key * HD));
+    };
+  #pragma unroll
+    for (int s = 0; s < R; ++s) refill(s);
 
-  ATTN_TS(1);
-  // merge the lane groups of the wave (each holds its own max / sum / o)
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const float mx = groups_max<LPK>(mrun[g]);
-    const float f = mrun[g] == -INFINITY ? 0.0f : __expf(mrun[g] - mx);
-    const float l = groups_sum<LPK>(lrun[g] * f);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[g][e] = groups_sum<LPK>(acc[g][e] * f);
-    mrun[g] = mx;
-    lrun[g] = l;
-  }
-  if (lane < LPK) {
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s_acc[wave][g][dl * 8 + e] = acc[g][e];
-  }
-  if (lane == 0) {
-#pragma unroll
+    float q[G][8];
+  #pragma unroll
     for (int g = 0; g < G; ++g) {
-      s_m[wave][g] = mrun[g];
-      s_l[wave][g] = lrun[g];
+      const float* qp = a.q + (size_t)m * a.heads * HD + (size_t)(kvh * G + g) * HD + dl * 8;
+      const float4 q0 = *(const float4*)qp, q1 = *(const float4*)(qp + 4);
+      q[g][0] = q0.x * a.scale; q[g][1] = q0.y * a.scale; q[g][2] = q0.z * a.scale; q[g][3] = q0.w * a.scale;
+      q[g][4] = q1.x * a.scale; q[g][5] = q1.y * a.scale; q[g][6] = q1.z * a.scale; q[g][7] = q1.w * a.scale;
     }
+    float mrun[G], lrun[G], acc[G][8];
+  #pragma unroll
+    for (int g = 0; g < G; ++g) {
+      mrun[g] = -INFINITY;
+      lrun[g] = 0.0f;
+  #pragma unroll
+      for (int e = 0; e < 8; ++e) acc[g][e] = 0.0f;
+    }
+
+    int ci = 0;   // compute cursor (slot index of this wave)
+    auto consume = [&](const u32x4& kv, const u32x4& vv) {
+      const bool valid = slot_key(ci) < s1;
+      ++ci;
+      float kf[8], vf[8];
+      unpack8(kv, kf);
+      unpack8(vv, vf);
+  #pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float d = 0.0f;
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) d = fmaf(q[g][e], kf[e], d);
+        d = group_sum<LPK>(d);
+        const float sc = valid ? d : -INFINITY;
+        const float mn = fmaxf(mrun[g], sc);
+        const float alpha = mrun[g] == mn ? 1.0f : __expf(mrun[g] - mn);
+        const float p = valid ? __expf(sc - mn) : 0.0f;
+        lrun[g] = fmaf(lrun[g], alpha, p);
+        mrun[g] = mn;
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(p, vf[e], acc[g][e] * alpha);
+      }
+    };
+    int j0 = 0;
+    for (; j0 + R <= total; j0 += R) {
+  #pragma unroll
+      for (int s = 0; s < R; ++s) {
+        consume(kr[s], vr[s]);
+        refill(s);
+      }
+    }
+  #pragma unroll
+    for (int s = 0; s < R; ++s)
+      if (j0 + s < total) consume(kr[s], vr[s]);
+
+    ATTN_TS(1);
+    // merge the lane groups of the wave (each holds its own max / sum / o)
+  #pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float mx = groups_max<LPK>(mrun[g]);
+      const float f = mrun[g] == -INFINITY ? 0.0f : __expf(mrun[g] - mx);
+      const float l = groups_sum<LPK>(lrun[g] * f);
+  #pragma unroll
+      for (int e = 0; e < 8; ++e) acc[g][e] = groups_sum<LPK>(acc[g][e] * f);
+      mrun[g] = mx;
+      lrun[g] = l;
+    }
+    if (lane < LPK) {
+  #pragma unroll
+      for (int g = 0; g < G; ++g)
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) s_acc[wave][g][dl * 8 + e] = acc[g][e];
+    }
+    if (lane == 0) {
+  #pragma unroll
+      for (int g = 0; g < G; ++g) {
+        s_m[wave][g] = mrun[g];
+        s_l[wave][g] = lrun[g];
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   // merge the waves; one thread per (q-head of the group, dim)
   const int row = ws_row(HD);
@@ -317,11 +391,19 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
 template <int HD, int G>
 static int launch_attn(const AttnArgs& a, hipStream_t s) {
   const bool long_range = G >= 4 && a.max_seq / a.splits >= 1024;   // keys per split (upper bound)
+  if constexpr (G >= 4 && HD / (64 / G) == 8) {
+    if (!long_range) {   // head-parallel lanes: one key per wave step, 8 in flight
+      hipLaunchKernelGGL((attn_split_kernel<HD, G, TI_ATTN_RING_HP, true>), dim3(a.splits, a.kv_heads, a.M),
+                         dim3(kAttnThreads), 0, s, a);
+      TI_LAUNCH_CHECK("attn_split_kernel");
+      return TI_OK;
+    }
+  }
   if (long_range)
-    hipLaunchKernelGGL((attn_split_kernel<HD, G, TI_ATTN_RING_LONG>), dim3(a.splits, a.kv_heads, a.M), dim3(kAttnThreads),
+    hipLaunchKernelGGL((attn_split_kernel<HD, G, TI_ATTN_RING_LONG, false>), dim3(a.splits, a.kv_heads, a.M), dim3(kAttnThreads),
                        0, s, a);
   else
-    hipLaunchKernelGGL((attn_split_kernel<HD, G, TI_ATTN_RING>), dim3(a.splits, a.kv_heads, a.M), dim3(kAttnThreads), 0,
+    hipLaunchKernelGGL((attn_split_kernel<HD, G, TI_ATTN_RING, false>), dim3(a.splits, a.kv_heads, a.M), dim3(kAttnThreads), 0,
                        s, a);
   TI_LAUNCH_CHECK("attn_split_kernel");
   return TI_OK;
