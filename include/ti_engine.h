@@ -75,6 +75,15 @@ int ti_engine_generate(ti_engine* e, int n_streams, const int32_t* prompts, cons
  * instead of one token per decode step.  Default: TI_GEMM_MAX_ROWS (int4) or 16; 0 = off. */
 int ti_engine_set_prefill(ti_engine* e, int rows);
 
+/* Chained decode steps (ti_hip.h ti_chain): single-stream steps are issued as launches that
+ * order themselves in-kernel (hipExtAnyOrderLaunch) instead of a replayed hipGraph, so a
+ * launch's weight stream starts while its predecessor finishes.  on = 1 (or env TI_CHAIN=1)
+ * applies it wherever every launch of the step is chainable (one stream, fused GEMV kernel);
+ * 0 (the default: measured 12 % slower than the replayed graph on MI355X)
+ * always uses the graph; -1 leaves the setting.  *active (nullable) receives whether steps
+ * of 1 stream will be chained. */
+int ti_engine_set_chain(ti_engine* e, int on, int* active);
+
 /* One decode step: token[s] at position pos[s] for each stream; logits [n][vocab] to host
  * (used for non-greedy sampling and per-step parity). */
 int ti_engine_step(ti_engine* e, int n_streams, const int32_t* tokens, const int32_t* pos, float* logits);

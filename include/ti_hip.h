@@ -108,6 +108,28 @@ int ti_fill_uniform_f32(uint64_t seed, uint32_t tensor_id, uint64_t n, float mul
 int ti_fill_kv_uniform(uint64_t seed, uint32_t tensor_id, int n, int kv_heads, int head_dim, int max_seq,
                        uint16_t* dst, ti_stream_t s);
 
+/* ------------------------------------------------------------ chained launches
+ * A decode step is a fixed sequence of dependent launches.  Chained, each launch is issued
+ * with hipExtAnyOrderLaunch (the queue does not wait for the previous launch to retire) and
+ * orders itself in-kernel instead: a workgroup first issues the loads that do not depend on
+ * the previous launch (its packed weights), then waits until the predecessor's counter
+ * reaches `wait_target`, and only then reads the predecessor's outputs.  Outputs are stored
+ * write-through (sc1) and drained; one lane per workgroup then adds 1 to its shard
+ * (blockIdx & 7) of `signal_ctr` (agent-scope atomic); dependent inputs are read with sc1
+ * loads (MI355X_MICROARCH.md, "Hand-offs measured with sc1 loads").  A wait longer than
+ * ~20 ms gives up, sets *abort_flag and proceeds (the caller must treat the step as failed).
+ * `signaled` is an output: the workgroups of the launch, i.e. what it adds to signal_ctr. */
+#define TI_CHAIN_SHARDS 8
+typedef struct ti_chain {
+  const uint32_t* wait_ctr;          /* [TI_CHAIN_SHARDS] predecessor counter, NULL = no wait */
+  uint32_t wait_target;              /* proceed once the shards sum to >= wait_target */
+  uint32_t signaled;                 /* out: workgroups of this launch */
+  uint32_t* signal_ctr;              /* [TI_CHAIN_SHARDS] this launch's counter */
+  uint32_t* abort_flag;              /* device word, set when a wait times out */
+  int32_t any_order;                 /* 1: hipExtAnyOrderLaunch */
+  int32_t _pad;
+} ti_chain;
+
 /* ---------------------------------------------------- fused decode GEMM/GEMV
  * y[m][n] = sum_k xa[m][k] * W[k][n], m < M <= TI_GEMM_MAX_ROWS (see ti_gemm_max_rows), with
  *   xa = fp16(x)                               (x_kind TI_X_F16 / TI_X_F32), or
@@ -169,6 +191,13 @@ int ti_gemm_max_rows(int bits, int x_kind, int N, int K);
  * activation prep; the same arithmetic as the fused TI_X_F32_RMSNORM prologue). */
 int ti_rmsnorm_f16(const float* x, int ldx, const float* w, float eps, uint16_t* y, int ldy, int M, int K,
                    ti_stream_t s);
+/* The same GEMM as one launch of a chain (see ti_chain): M == 1, fused kernel only
+ * (TI_ERR_UNSUPPORTED otherwise, nothing launched). */
+int ti_gemm_wq_a16_chained(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind,
+                           int ldx, const float* norm_w, float eps, int M, int N, int K,
+                           const ti_epilogue* epi, ti_chain* chain, ti_stream_t s);
+/* 1 if ti_gemm_wq_a16_chained accepts this shape (M == 1, fused kernel, x staged in registers). */
+int ti_gemm_chainable(int bits, int x_kind, int M, int N, int K);
 /* One-time kernel attribute setup; call before capturing ti_gemm_wq_a16 into a graph. */
 int ti_gemm_prepare(void);
 
@@ -191,6 +220,12 @@ int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_ca
                    int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
                    int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
                    ti_stream_t s);
+/* One launch of a chain (ti_chain): the same attention; K/V, q and pos read with sc1 loads
+ * after the wait, out stored write-through. */
+int ti_attn_decode_chained(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                           int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
+                           int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
+                           ti_chain* chain, ti_stream_t s);
 
 /* ------------------------------------------------------- step begin (device loop)
  * One block per stream: picks the token of this step (prompt token while step < n_in[m],
@@ -212,6 +247,9 @@ typedef struct ti_step_args {
   const int32_t* step_ctr;
 } ti_step_args;
 int ti_step_begin(const ti_step_args* a, ti_stream_t s);
+/* One launch of a chain (ti_chain): waits for the previous step's last launch (argmax keys,
+ * step counter), stores h / pos / tokens write-through. */
+int ti_step_begin_chained(const ti_step_args* a, ti_chain* chain, ti_stream_t s);
 
 /* -------------------------------------------------------------- fp32 op level */
 /* y[r][n] (+)= sum_k a[r][k]*b[k][n], b the reference [K][N] fp32 layout, one fmaf per k

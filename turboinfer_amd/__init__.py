@@ -73,7 +73,8 @@ EXPORTED = [
     "ti_argmax_f32", "ti_engine_create", "ti_engine_destroy", "ti_engine_get_stream", "ti_engine_memory", "ti_engine_set_tensor",
     "ti_engine_synth", "ti_engine_fill_kv", "ti_engine_generate", "ti_engine_step", "ti_engine_compat_step",
     "ti_engine_replay_prepare", "ti_engine_set_prefill", "ti_engine_replay_run", "ti_engine_sync", "ti_engine_last_tokens",
-    "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token",
+    "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token", "ti_gemm_wq_a16_chained", "ti_gemm_chainable",
+    "ti_attn_decode_chained", "ti_step_begin_chained", "ti_engine_set_chain",
 ]
 
 _lib = None
@@ -138,6 +139,8 @@ def lib() -> C.CDLL:
         L.ti_engine_generate.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp]
         L.ti_engine_step.argtypes = [vp, i32, vp, vp, vp]
         L.ti_engine_set_prefill.argtypes = [vp, i32]
+        L.ti_engine_set_chain.argtypes = [vp, i32, C.POINTER(C.c_int)]
+        L.ti_gemm_chainable.argtypes = [i32, i32, i32, i32, i32]
         L.ti_engine_compat_step.argtypes = [vp, i32, vp]
         L.ti_engine_replay_prepare.argtypes = [vp, i32, i32, i32]
         L.ti_engine_replay_run.argtypes = [vp, i32]
@@ -298,6 +301,12 @@ class Engine:
     def set_prefill(self, rows):
         """Prompt tokens per prefill chunk (0 = consume prompts one token per decode step)."""
         check(lib().ti_engine_set_prefill(self.h, rows))
+
+    def set_chain(self, on=None) -> bool:
+        """Chained single-stream steps on/off (None: query); returns whether they are active."""
+        act = C.c_int(0)
+        check(lib().ti_engine_set_chain(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
+        return bool(act.value)
 
     def step(self, tokens, pos):
         t = np.ascontiguousarray(tokens, np.int32)

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <utility>
@@ -107,6 +108,14 @@ struct ti_engine {
   size_t weight_bytes = 0, kv_bytes = 0;
   std::map<std::pair<int, int>, hipGraphExec_t> graphs;  // (M, advance)
   int replay_M = 0;
+  // chained single-stream steps (ti_hip.h ti_chain): launch slot k of a step signals
+  // chain_ctr[k][0..7]; chain_cum[k] = its cumulative workgroup count (the next wait target)
+  bool chain_on = false;       // TI_CHAIN=1 / ti_engine_set_chain (measured slower than the graph)
+  int chain_ok = -1;           // -1 unknown, 0/1: every launch of a 1-stream step chainable
+  int chain_slots = 0;
+  uint32_t* chain_ctr = nullptr;
+  uint32_t* chain_abort = nullptr;
+  std::vector<uint32_t> chain_cum;
 
   int qd() const { return c.heads * c.head_dim; }
   int kvd() const { return c.kv_heads * c.head_dim; }
@@ -207,6 +216,152 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
     const void* xm = static_cast<const char*>(x) + (size_t)m0 * ldx * x_elem;
     TI_TRY(ti_gemm_wq_a16(W.tiles, W.scales, c.bits, xm, x_kind, ldx, nw, c.eps, mm, W.N, W.K, &ep, e->s));
   }
+  return TI_OK;
+}
+
+// ------------------------------------------------------------- chained steps
+bool chain_usable(ti_engine* e, int M) {
+  const ti_engine_config& c = e->c;
+  if (!e->chain_on || M != 1 || c.compat || !e->chain_ctr) return false;
+  if (e->chain_ok < 0) {
+    const int H = c.hidden, I = c.inter, qd = e->qd(), kvd = e->kvd();
+    const int b = c.bits;
+    e->chain_ok = ti_gemm_chainable(b, TI_X_F32_RMSNORM, 1, qd + 2 * kvd, H) && ti_gemm_chainable(b, TI_X_F16, 1, H, qd) &&
+                  ti_gemm_chainable(b, TI_X_F32_RMSNORM, 1, 2 * I, H) && ti_gemm_chainable(b, TI_X_F16, 1, H, I) &&
+                  ti_gemm_chainable(b, TI_X_F32_RMSNORM, 1, c.vocab, H);
+  }
+  return e->chain_ok == 1;
+}
+
+// One single-stream decode step as chained launches: step_begin, 5 per layer, lm_head.  The
+// first step of a run is an ordinary (barrier) launch with no wait, so it follows whatever
+// the stream did before; every later launch waits in-kernel for the launch before it.
+int enqueue_step_chained(ti_engine* e, int advance, bool first) {
+  const ti_engine_config& c = e->c;
+  if (first) {
+    uint32_t mx = 0;
+    for (uint32_t v : e->chain_cum) mx = std::max(mx, v);
+    if (mx > (1u << 30)) {   // counters are monotonic u32: rewind while the stream drains
+      E_CHECK(hipMemsetAsync(e->chain_ctr, 0, (size_t)e->chain_slots * TI_CHAIN_SHARDS * 4, e->s), "hipMemsetAsync(chain)");
+      std::fill(e->chain_cum.begin(), e->chain_cum.end(), 0u);
+    }
+  }
+  int slot = 0, prev = first ? -1 : e->chain_slots - 1;
+  ti_chain ch{};
+  auto link = [&]() -> ti_chain* {
+    if (slot >= e->chain_slots) return nullptr;
+    ch = ti_chain{};
+    if (prev >= 0) {
+      ch.wait_ctr = e->chain_ctr + (size_t)prev * TI_CHAIN_SHARDS;
+      ch.wait_target = e->chain_cum[prev];
+      ch.any_order = 1;
+    }
+    ch.signal_ctr = e->chain_ctr + (size_t)slot * TI_CHAIN_SHARDS;
+    ch.abort_flag = e->chain_abort;
+    return &ch;
+  };
+  auto done = [&]() {
+    e->chain_cum[slot] += ch.signaled;
+    prev = slot++;
+  };
+  ti_step_args sa{};
+  sa.emb = e->emb;
+  sa.h = e->h;
+  sa.hidden = c.hidden;
+  sa.M = 1;
+  sa.vocab = c.vocab;
+  sa.in_stride = e->in_cap;
+  sa.out_stride = e->out_cap;
+  sa.placeholder_first = -1;
+  sa.in_tokens = e->in_tokens;
+  sa.n_in = e->n_in;
+  sa.argmax = e->argmax;
+  sa.out_tokens = e->out_tokens;
+  sa.pos = e->pos;
+  sa.base_pos = e->base_pos;
+  sa.step_ctr = e->step_ctr;
+  if (!link()) return ti_set_error(TI_ERR_ARG, "engine: chain slots");
+  TI_TRY(ti_step_begin_chained(&sa, &ch, e->s));
+  done();
+  const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
+  auto gemm = [&](const DevLinear& W, const void* x, int x_kind, int ldx, const float* nw, const ti_epilogue& ep) -> int {
+    if (!link()) return ti_set_error(TI_ERR_ARG, "engine: chain slots");
+    TI_TRY(ti_gemm_wq_a16_chained(W.tiles, W.scales, c.bits, x, x_kind, ldx, nw, c.eps, 1, W.N, W.K, &ep, &ch, e->s));
+    done();
+    return TI_OK;
+  };
+  for (int l = 0; l < c.layers; ++l) {
+    DevLayer& L = e->layer[l];
+    ti_epilogue ep{};
+    ep.kind = TI_EPI_QKV_ROPE_KV;
+    ep.ldo = qd;
+    ep.out = e->q;
+    ep.q_dim = qd;
+    ep.kv_dim = kvd;
+    ep.head_dim = c.head_dim;
+    ep.max_seq = c.max_seq;
+    ep.pos = e->pos;
+    ep.rope_cs = e->rope_cs;
+    ep.k_cache = L.kc;
+    ep.v_cache = L.vc;
+    ep.kv_stream_stride = e->kv_stride;
+    TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, L.attn_norm, ep));
+    if (!link()) return ti_set_error(TI_ERR_ARG, "engine: chain slots");
+    TI_TRY(ti_attn_decode_chained(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, 1, c.heads, c.kv_heads, c.head_dim,
+                                  e->splits_for(1), e->ws, e->attn, &ch, e->s));
+    done();
+    ti_epilogue eo{};
+    eo.kind = TI_EPI_RESID_F32;
+    eo.ldo = H;
+    eo.out = e->h;
+    TI_TRY(gemm(L.o, e->attn, TI_X_F16, qd, nullptr, eo));
+    ti_epilogue eg{};
+    eg.kind = TI_EPI_SILU_MUL_F16;
+    eg.ldo = I;
+    eg.out = e->act;
+    TI_TRY(gemm(L.gu, e->h, TI_X_F32_RMSNORM, H, L.ffn_norm, eg));
+    ti_epilogue ed{};
+    ed.kind = TI_EPI_RESID_F32;
+    ed.ldo = H;
+    ed.out = e->h;
+    TI_TRY(gemm(L.down, e->act, TI_X_F16, I, nullptr, ed));
+  }
+  ti_epilogue el{};
+  el.kind = TI_EPI_LOGITS_ARGMAX;
+  el.ldo = V;
+  el.out = e->logits;
+  el.argmax = e->argmax;
+  el.step_ctr = e->step_ctr;
+  el.advance = advance;
+  TI_TRY(gemm(e->lm, e->h, TI_X_F32_RMSNORM, H, e->out_norm, el));
+  return slot == e->chain_slots ? TI_OK : ti_set_error(TI_ERR_ARG, "engine: chain slot count %d != %d", slot, e->chain_slots);
+}
+
+// After a synchronisation: fail (and re-arm) if any chained wait timed out.
+int chain_check(ti_engine* e) {
+  if (!e->chain_abort) return TI_OK;
+  uint32_t ab = 0;
+  TI_TRY(ti_memcpy_d2h(&ab, e->chain_abort, 4, e->s));
+  if (ab) {
+    TI_TRY(ti_memset(e->chain_abort, 0, 4, e->s));
+    TI_TRY(ti_stream_sync(e->s));
+    return ti_set_error(TI_ERR_HIP, "engine: a chained launch's in-kernel wait timed out (results invalid)");
+  }
+  return TI_OK;
+}
+
+int get_graph(ti_engine* e, int M, int advance, hipGraphExec_t* out);
+
+// n steps of M streams from the current device state: chained when possible, else the graph.
+int run_steps(ti_engine* e, int M, int advance, int n) {
+  if (n <= 0) return TI_OK;
+  if (chain_usable(e, M)) {
+    for (int s = 0; s < n; ++s) TI_TRY(enqueue_step_chained(e, advance, s == 0));
+    return TI_OK;
+  }
+  hipGraphExec_t g = nullptr;
+  TI_TRY(get_graph(e, M, advance, &g));
+  for (int s = 0; s < n; ++s) E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
   return TI_OK;
 }
 
@@ -464,6 +619,11 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
         (rc = e->alloc_t(&e->pf_ones, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->pf_zero, (size_t)1)) ||
         (rc = e->alloc_t(&e->pf_base, (size_t)e->pf_rows)))
       return fail(rc);
+    e->chain_slots = 2 + 5 * c.layers;
+    e->chain_cum.assign((size_t)e->chain_slots, 0u);
+    if ((rc = e->alloc_t(&e->chain_ctr, (size_t)e->chain_slots * TI_CHAIN_SHARDS)) || (rc = e->alloc_t(&e->chain_abort, (size_t)1)))
+      return fail(rc);
+    if (const char* env = getenv("TI_CHAIN")) e->chain_on = atoi(env) != 0;
     std::vector<int32_t> ones(e->pf_rows, 1);
     if ((rc = ti_memcpy_h2d(e->pf_ones, ones.data(), ones.size() * 4, e->s)) || (rc = ti_memset(e->pf_zero, 0, 4, e->s)))
       return fail(rc);
@@ -629,10 +789,9 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
       for (int t0 = 0; t0 < s0; t0 += e->pf_rows) TI_TRY(enqueue_prefill(e, m, t0, std::min(e->pf_rows, s0 - t0), base[m]));
   }
   TI_TRY(ti_memcpy_h2d(e->step_ctr, &s0, 4, e->s));
-  hipGraphExec_t g = nullptr;
-  TI_TRY(get_graph(e, n, 1, &g));
-  for (int s = s0; s < steps; ++s) E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
+  TI_TRY(run_steps(e, n, 1, steps - s0));
   TI_TRY(ti_stream_sync(e->s));
+  TI_TRY(chain_check(e));
   std::vector<int32_t> outd((size_t)n * e->out_cap);
   std::vector<unsigned long long> am;
   TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
@@ -672,10 +831,9 @@ int ti_engine_step(ti_engine* e, int n, const int32_t* tokens, const int32_t* po
   TI_TRY(ti_memcpy_h2d(e->n_in, one.data(), (size_t)n * 4, e->s));
   TI_TRY(ti_memcpy_h2d(e->base_pos, pos, (size_t)n * 4, e->s));
   TI_TRY(ti_memset(e->step_ctr, 0, 4, e->s));
-  hipGraphExec_t g = nullptr;
-  TI_TRY(get_graph(e, n, 1, &g));
-  E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
+  TI_TRY(run_steps(e, n, 1, 1));
   TI_TRY(ti_stream_sync(e->s));
+  TI_TRY(chain_check(e));
   if (logits) TI_TRY(ti_memcpy_d2h(logits, e->logits, (size_t)n * c.vocab * 4, e->s));
   return TI_OK;
 }
@@ -732,14 +890,20 @@ int ti_engine_replay_prepare(ti_engine* e, int n, int kv_len, int start_token) {
 
 int ti_engine_replay_run(ti_engine* e, int steps) {
   if (!e || e->replay_M < 1) return ti_set_error(TI_ERR_ARG, "ti_engine_replay_run: call ti_engine_replay_prepare first");
-  hipGraphExec_t g = e->graphs.at(std::make_pair(e->replay_M, 0));
-  for (int s = 0; s < steps; ++s) E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
-  return TI_OK;
+  return run_steps(e, e->replay_M, 0, steps);
 }
 
 int ti_engine_sync(ti_engine* e) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_sync: null");
-  return ti_stream_sync(e->s);
+  TI_TRY(ti_stream_sync(e->s));
+  return chain_check(e);
+}
+
+int ti_engine_set_chain(ti_engine* e, int on, int* active) {
+  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_chain: null");
+  if (on >= 0) e->chain_on = on != 0;
+  if (active) *active = chain_usable(e, 1) ? 1 : 0;
+  return TI_OK;
 }
 
 int ti_engine_last_tokens(ti_engine* e, int n, int32_t* tokens) {

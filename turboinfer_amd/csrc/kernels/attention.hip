@@ -39,6 +39,7 @@ struct AttnArgs {
   int64_t stride;
   int32_t max_seq, M, heads, kv_heads, splits;
   float scale;
+  ChainDev chain;   // chained launches only (CH)
 };
 
 #ifndef TI_ATTN_RING
@@ -52,6 +53,9 @@ struct AttnArgs {
 #endif
 #ifndef TI_ATTN_RING_LONG
 #define TI_ATTN_RING_LONG 4
+#endif
+#ifndef TI_ATTN_CH_ALL_SC1
+#define TI_ATTN_CH_ALL_SC1 0   // chained: sc1 loads for every K/V row (else only the fresh one)
 #endif
 #ifndef TI_ATTN_EXP
 #define TI_ATTN_EXP 0   // product build; tools/probe_attn.hip: +4 = per-workgroup phase timestamps
@@ -120,7 +124,9 @@ __device__ __forceinline__ float groups_sum(float v) {
   else return v;
 }
 
-template <int HD, int G, int R, bool HP>   // HP: head-parallel lanes (G >= 4, HD / (64 / G) == 8; see below)
+// CH: one launch of a chain (ti_chain): wait first, then pos, q and K/V with sc1 loads, the
+// output stored write-through in fp16 pairs, and every workgroup signals once.
+template <int HD, int G, int R, bool HP, bool CH = false>   // HP: head-parallel lanes (G >= 4, HD / (64 / G) == 8; see below)
 __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnArgs a) {
   static_assert(!HP || (G >= 4 && HD / (64 / G) == 8), "head-parallel layout: 8 dims per lane");
   constexpr int LPK = HD / 8;       // lanes per key row
@@ -135,14 +141,58 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int dl = lane % LPK, kg = lane / LPK;
-  const int L = a.pos[m] + 1;
+  const unsigned flat_block = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  if constexpr (CH) chain_wait(a.chain);
+  const int L = (CH ? (int)__builtin_amdgcn_readfirstlane(ld_sc1_u32(a.pos + m)) : a.pos[m]) + 1;
+  // K/V of this workgroup's (stream, kv-head): [max_seq][HD] fp16 from wg_off
+  const int64_t wg_off = (int64_t)m * a.stride + (int64_t)kvh * a.max_seq * HD;
+  const __amdgpu_buffer_rsrc_t rk = sc1_rsrc(a.kc + wg_off), rv = sc1_rsrc(a.vc + wg_off), rq = sc1_rsrc(a.q);
+  // Chained: only the row at L - 1 was written by the previous launch (the QKV epilogue of
+  // this step); rows before it were written by earlier steps and never change afterwards, so
+  // they keep the non-temporal loads and the fresh row is read with an sc1 load.
+  const int64_t fresh_lo = (int64_t)(L - 1) * HD, fresh_hi = fresh_lo + HD;
+  auto ld_k = [&](int64_t elem) -> u32x4 {   // elem: offset within the workgroup's K
+    if constexpr (CH) {
+#if TI_ATTN_CH_ALL_SC1
+      return __builtin_amdgcn_raw_buffer_load_b128(rk, (uint32_t)(elem * 2), 0, kAuxSc1Load);
+#else
+      if (elem >= fresh_lo && elem < fresh_hi) return __builtin_amdgcn_raw_buffer_load_b128(rk, (uint32_t)(elem * 2), 0, kAuxSc1Load);
+      return ld_kv((const u32x4*)(a.kc + wg_off + elem));
+#endif
+    } else {
+      return ld_kv((const u32x4*)(a.kc + wg_off + elem));
+    }
+  };
+  auto ld_v = [&](int64_t elem) -> u32x4 {
+    if constexpr (CH) {
+#if TI_ATTN_CH_ALL_SC1
+      return __builtin_amdgcn_raw_buffer_load_b128(rv, (uint32_t)(elem * 2), 0, kAuxSc1Load);
+#else
+      if (elem >= fresh_lo && elem < fresh_hi) return __builtin_amdgcn_raw_buffer_load_b128(rv, (uint32_t)(elem * 2), 0, kAuxSc1Load);
+      return ld_kv((const u32x4*)(a.vc + wg_off + elem));
+#endif
+    } else {
+      return ld_kv((const u32x4*)(a.vc + wg_off + elem));
+    }
+  };
+  auto ld_q4 = [&](size_t elem) -> float4 {
+    if constexpr (CH) return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(elem * 4), 0, kAuxSc1Load));
+    else return *(const float4*)(a.q + elem);
+  };
+  // fp16 output element idx (thread parity == idx parity): chained, lane pairs store 4 bytes
+  auto store_out = [&](size_t idx, float val) {
+    const uint32_t hv = f2h(val);
+    if constexpr (CH) {
+      const uint32_t hp = (uint32_t)__shfl_xor((int)hv, 1, kWave);
+      if (!(idx & 1)) st_sc1_u32(a.out + idx, hv | (hp << 16));
+    } else {
+      a.out[idx] = (uint16_t)hv;
+    }
+  };
   const int chunk = (L + a.splits - 1) / a.splits;
   const int s0 = split * chunk, s1 = min(L, s0 + chunk);
   const int nslot = s1 > s0 ? (s1 - s0 + KPW - 1) / KPW : 0;               // slots of the chunk
   const int total = wave < nslot ? (nslot - wave + kAttnWaves - 1) / kAttnWaves : 0;   // this wave's
-  const int64_t base = (int64_t)m * a.stride + (int64_t)kvh * a.max_seq * HD + dl * 8;
-  const uint16_t* kb = a.kc + base;
-  const uint16_t* vb = a.vc + base;
 
   if constexpr (HP) {
     // head-parallel layout (G >= 4 q-heads per kv-head): lane l serves q-head l / LPH of the
@@ -150,7 +200,6 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
     // in its own LPH lanes, so no lane-group merge is needed after the stream.
     constexpr int LPH = 64 / G;
     const int hg = lane / LPH, dh = lane % LPH;
-    const int64_t hb = (int64_t)m * a.stride + (int64_t)kvh * a.max_seq * HD + dh * 8;
     const int nkey = s1 > s0 ? s1 - s0 : 0;
     const int total = wave < nkey ? (nkey - wave + kAttnWaves - 1) / kAttnWaves : 0;   // this wave's keys
     int rj = 0;
@@ -158,15 +207,15 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
     auto refill = [&](int s) {
       const int key = min(s0 + wave + kAttnWaves * (rj < total ? rj : max(total - 1, 0)), max(s1 - 1, 0));
       ++rj;
-      kr[s] = ld_kv((const u32x4*)(a.kc + hb + (int64_t)key * HD));
-      vr[s] = ld_kv((const u32x4*)(a.vc + hb + (int64_t)key * HD));
+      kr[s] = ld_k((int64_t)key * HD + dh * 8);
+      vr[s] = ld_v((int64_t)key * HD + dh * 8);
     };
 #pragma unroll
     for (int s = 0; s < R; ++s) refill(s);
     float qh[8];
     {
-      const float* qp = a.q + (size_t)m * a.heads * HD + (size_t)(kvh * G + hg) * HD + dh * 8;
-      const float4 q0 = *(const float4*)qp, q1 = *(const float4*)(qp + 4);
+      const size_t qe = (size_t)m * a.heads * HD + (size_t)(kvh * G + hg) * HD + dh * 8;
+      const float4 q0 = ld_q4(qe), q1 = ld_q4(qe + 4);
       qh[0] = q0.x * a.scale; qh[1] = q0.y * a.scale; qh[2] = q0.z * a.scale; qh[3] = q0.w * a.scale;
       qh[4] = q1.x * a.scale; qh[5] = q1.y * a.scale; qh[6] = q1.z * a.scale; qh[7] = q1.w * a.scale;
     }
@@ -220,8 +269,8 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
     auto refill = [&](int s) {
       const int key = min(slot_key(rj < total ? rj : max(total - 1, 0)), max(s1 - 1, 0));
       ++rj;
-      kr[s] = ld_kv((const u32x4*)(kb + (int64_t)key * HD));
-      vr[s] = ld_kv((const u32x4*)(vb + (int64_t)key * HD));
+      kr[s] = ld_k((int64_t)key * HD + dl * 8);
+      vr[s] = ld_v((int64_t)key * HD + dl * 8);
     };
   #pragma unroll
     for (int s = 0; s < R; ++s) refill(s);
@@ -229,8 +278,8 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
     float q[G][8];
   #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const float* qp = a.q + (size_t)m * a.heads * HD + (size_t)(kvh * G + g) * HD + dl * 8;
-      const float4 q0 = *(const float4*)qp, q1 = *(const float4*)(qp + 4);
+      const size_t qe = (size_t)m * a.heads * HD + (size_t)(kvh * G + g) * HD + dl * 8;
+      const float4 q0 = ld_q4(qe), q1 = ld_q4(qe + 4);
       q[g][0] = q0.x * a.scale; q[g][1] = q0.y * a.scale; q[g][2] = q0.z * a.scale; q[g][3] = q0.w * a.scale;
       q[g][4] = q1.x * a.scale; q[g][5] = q1.y * a.scale; q[g][6] = q1.z * a.scale; q[g][7] = q1.w * a.scale;
     }
@@ -324,7 +373,7 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
     }
     const int h = kvh * G + g;
     if (a.splits == 1) {     // the whole sequence is ours: normalise and write out directly
-      a.out[(size_t)m * a.heads * HD + (size_t)h * HD + d] = f2h(l > 0.0f ? o / l : 0.0f);
+      store_out((size_t)m * a.heads * HD + (size_t)h * HD + d, l > 0.0f ? o / l : 0.0f);
       continue;
     }
     s_part[g * row + d] = o;   // this split's row [o | max, sum, 0, 0]
@@ -335,7 +384,10 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
       s_part[g * row + HD + 3] = 0.0f;
     }
   }
-  if (a.splits == 1) return;
+  if (a.splits == 1) {
+    if constexpr (CH) chain_signal(a.chain, flat_block);
+    return;
+  }
   __syncthreads();
 
   ATTN_TS(2);
@@ -359,7 +411,10 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
   }
   __syncthreads();
   ATTN_TS(3);
-  if (!s_last) return;
+  if (!s_last) {
+    if constexpr (CH) chain_signal(a.chain, flat_block);
+    return;
+  }
   // all partials of the group's heads in one round trip: s_part[g][split][row]
   const int nv = G * a.splits * V4;
   for (int i = tid; i < nv; i += kAttnThreads) {
@@ -382,40 +437,43 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
       den = fmaf(f, pb[sp * row + HD + 1], den);
       num = fmaf(f, pb[sp * row + d], num);
     }
-    a.out[(size_t)m * a.heads * HD + (size_t)h * HD + d] = f2h(num / den);
+    store_out((size_t)m * a.heads * HD + (size_t)h * HD + d, num / den);
   }
   if (tid == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  if constexpr (CH) chain_signal(a.chain, flat_block);
   ATTN_TS(4);
 }
 
-template <int HD, int G>
-static int launch_attn(const AttnArgs& a, hipStream_t s) {
-  const bool long_range = G >= 4 && a.max_seq / a.splits >= 1024;   // keys per split (upper bound)
-  if constexpr (G >= 4 && HD / (64 / G) == 8) {
-    if (!long_range) {   // head-parallel lanes: one key per wave step, 8 in flight
-      hipLaunchKernelGGL((attn_split_kernel<HD, G, TI_ATTN_RING_HP, true>), dim3(a.splits, a.kv_heads, a.M),
-                         dim3(kAttnThreads), 0, s, a);
-      TI_LAUNCH_CHECK("attn_split_kernel");
-      return TI_OK;
-    }
+template <int HD, int G, int R, bool HP>
+static int launch_one(const AttnArgs& a, hipStream_t s, const ti_chain* chain) {
+  const dim3 grid(a.splits, a.kv_heads, a.M);
+  if (chain) {
+    TI_HIP_CHECK(ti_launch_ext(attn_split_kernel<HD, G, R, HP, true>, grid, dim3(kAttnThreads), 0, s, chain->any_order != 0, a),
+                 "hipExtLaunchKernel(attn_split_kernel chained)");
+    return TI_OK;
   }
-  if (long_range)
-    hipLaunchKernelGGL((attn_split_kernel<HD, G, TI_ATTN_RING_LONG, false>), dim3(a.splits, a.kv_heads, a.M), dim3(kAttnThreads),
-                       0, s, a);
-  else
-    hipLaunchKernelGGL((attn_split_kernel<HD, G, TI_ATTN_RING, false>), dim3(a.splits, a.kv_heads, a.M), dim3(kAttnThreads), 0,
-                       s, a);
+  hipLaunchKernelGGL((attn_split_kernel<HD, G, R, HP>), grid, dim3(kAttnThreads), 0, s, a);
   TI_LAUNCH_CHECK("attn_split_kernel");
   return TI_OK;
 }
 
+template <int HD, int G>
+static int launch_attn(const AttnArgs& a, hipStream_t s, const ti_chain* chain) {
+  const bool long_range = G >= 4 && a.max_seq / a.splits >= 1024;   // keys per split (upper bound)
+  if constexpr (G >= 4 && HD / (64 / G) == 8) {
+    if (!long_range) return launch_one<HD, G, TI_ATTN_RING_HP, true>(a, s, chain);   // head-parallel lanes
+  }
+  if (long_range) return launch_one<HD, G, TI_ATTN_RING_LONG, false>(a, s, chain);
+  return launch_one<HD, G, TI_ATTN_RING, false>(a, s, chain);
+}
+
 template <int HD>
-static int dispatch_group(const AttnArgs& a, int G, hipStream_t s) {
+static int dispatch_group(const AttnArgs& a, int G, hipStream_t s, const ti_chain* chain) {
   switch (G) {
-    case 1: return launch_attn<HD, 1>(a, s);
-    case 2: return launch_attn<HD, 2>(a, s);
-    case 4: return launch_attn<HD, 4>(a, s);
-    case 8: return launch_attn<HD, 8>(a, s);
+    case 1: return launch_attn<HD, 1>(a, s, chain);
+    case 2: return launch_attn<HD, 2>(a, s, chain);
+    case 4: return launch_attn<HD, 4>(a, s, chain);
+    case 8: return launch_attn<HD, 8>(a, s, chain);
     default: return ti_set_error(TI_ERR_UNSUPPORTED, "ti_attn_decode: heads/kv_heads = %d not in {1,2,4,8}", G);
   }
 }
@@ -432,10 +490,9 @@ extern "C" size_t ti_attn_workspace_bytes(int M, int heads, int head_dim, int sp
   return ticket_bytes(heads) + (size_t)M * heads * splits * ti::ws_row(head_dim) * sizeof(float);
 }
 
-extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
-                              int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
-                              int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
-                              ti_stream_t stream) {
+static int attn_impl(const float* q, const uint16_t* k_cache, const uint16_t* v_cache, int64_t kv_stream_stride,
+                     int max_seq, const int32_t* pos, int M, int heads, int kv_heads, int head_dim, int splits,
+                     float* workspace, uint16_t* out, ti_chain* chain, ti_stream_t stream) {
   using namespace ti;
   if (!q || !k_cache || !v_cache || !pos || !workspace || !out)
     return ti_set_error(TI_ERR_ARG, "ti_attn_decode: null pointer");
@@ -467,6 +524,31 @@ extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uin
   a.kv_heads = kv_heads;
   a.splits = splits;
   a.scale = 1.0f / sqrtf((float)head_dim);   // tensor_engine.cpp:1288 (hidden = head_dim per head)
+  a.chain = chain_dev(chain);
+  if (chain) {
+    if (!chain->abort_flag || ((uintptr_t)out & 3))
+      return ti_set_error(TI_ERR_ARG, "ti_attn_decode_chained: abort_flag required, out 4-byte aligned");
+    if ((int64_t)max_seq * head_dim * 2 >= 0x7fffffffLL)
+      return ti_set_error(TI_ERR_UNSUPPORTED, "ti_attn_decode_chained: a (stream, kv-head) cache exceeds 2 GiB");
+    chain->signaled = (uint32_t)(splits * kv_heads * M);
+  }
   hipStream_t s = (hipStream_t)stream;
-  return head_dim == 128 ? dispatch_group<128>(a, G, s) : dispatch_group<64>(a, G, s);
+  return head_dim == 128 ? dispatch_group<128>(a, G, s, chain) : dispatch_group<64>(a, G, s, chain);
+}
+
+extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                              int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
+                              int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
+                              ti_stream_t stream) {
+  return attn_impl(q, k_cache, v_cache, kv_stream_stride, max_seq, pos, M, heads, kv_heads, head_dim, splits, workspace,
+                   out, nullptr, stream);
+}
+
+extern "C" int ti_attn_decode_chained(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                                      int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
+                                      int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
+                                      ti_chain* chain, ti_stream_t stream) {
+  if (!chain) return ti_set_error(TI_ERR_ARG, "ti_attn_decode_chained: null chain");
+  return attn_impl(q, k_cache, v_cache, kv_stream_stride, max_seq, pos, M, heads, kv_heads, head_dim, splits, workspace,
+                   out, chain, stream);
 }

@@ -67,6 +67,7 @@ struct GemvArgs {
   float eps;
   int32_t x_kind, ldx, M, N, K;
   ti_epilogue epi;
+  ChainDev chain;   // chained launches only (gemv_wq_kernel<..., CH = true>)
 };
 
 __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
@@ -173,7 +174,7 @@ enum { XM_F16 = 0, XM_F32 = 1, XM_NORM1 = 2, XM_NORM = 3 };
 
 // Generic staging (M > 1 with rms_norm, f32 rows, or rows longer than the register
 // prefetch covers).  Runs after the ring is issued, so its loads wait behind the ring.
-template <int XM>
+template <int XM, bool CH = false>
 __device__ __forceinline__ void stage_x_generic(const GemvArgs& a, f16* xl, float* red, int k8_from) {
   const int tid = threadIdx.x, K = a.K, xs = K + 8, K8 = K >> 3;
   if constexpr (XM == XM_NORM || XM == XM_NORM1) {
@@ -218,7 +219,11 @@ __device__ __forceinline__ void stage_x_generic(const GemvArgs& a, f16* xl, floa
   } else {
     for (int i = tid + k8_from; i < a.M * K8; i += kGemvThreads) {
       const int m = i / K8, k8 = i - m * K8;
-      *(u32x4*)(xl + m * xs + 8 * k8) = *(const u32x4*)((const f16*)a.x + (size_t)m * a.ldx + 8 * k8);
+      if constexpr (CH)
+        *(u32x4*)(xl + m * xs + 8 * k8) =
+            __builtin_amdgcn_raw_buffer_load_b128(sc1_rsrc(a.x), ((size_t)m * a.ldx + 8 * k8) * 2, 0, kAuxSc1Load);
+      else
+        *(u32x4*)(xl + m * xs + 8 * k8) = *(const u32x4*)((const f16*)a.x + (size_t)m * a.ldx + 8 * k8);
     }
   }
 }
@@ -233,6 +238,9 @@ __device__ __forceinline__ uint32_t float_order_key(float v) {
 // v_mfma_f32_16x16x32 C layout, reduced over the 8 waves); l is the lane or, for M <= 4,
 // n alone.  Partners of the shuffles below (n ^ 1, n + 8) sit in the same 16-lane group.  `best` is the
 // thread's running argmax key for LOGITS_ARGMAX.
+// Chained launches (CH) store write-through: 4-byte sc1 stores, fp16 outputs packed in pairs
+// (lane n even stores n and n + 1; its partner n ^ 1 sits in the same 16-lane group).
+template <bool CH>
 __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int l, int i, float v, const float* es,
                                          unsigned long long& best, bool ok) {
   const ti_epilogue& e = a.epi;
@@ -240,45 +248,75 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int 
   const bool live = ok && m < a.M;
   switch (e.kind) {
     case TI_EPI_STORE_F32:
-      if (live) ((float*)e.out)[(size_t)m * e.ldo + ng] = v;
+      if (live) {
+        if constexpr (CH) st_sc1_f32((float*)e.out + (size_t)m * e.ldo + ng, v);
+        else ((float*)e.out)[(size_t)m * e.ldo + ng] = v;
+      }
       break;
     case TI_EPI_STORE_F16:
-      if (live) ((uint16_t*)e.out)[(size_t)m * e.ldo + ng] = f2h(v);
+      if constexpr (CH) {
+        const uint32_t hv = f2h(v), hp = (uint32_t)__shfl_xor((int)hv, 1, kWave);
+        if (live && !(n & 1)) st_sc1_u32((uint16_t*)e.out + (size_t)m * e.ldo + ng, hv | (hp << 16));
+      } else if (live) {
+        ((uint16_t*)e.out)[(size_t)m * e.ldo + ng] = f2h(v);
+      }
       break;
     case TI_EPI_RESID_F32:   // add(residual, y), tensor_engine.cpp:1626-1678; residual pre-staged in LDS
-      if (live) ((float*)e.out)[(size_t)m * e.ldo + ng] = es[(tl * a.M + m) * 16 + n] + v;
+      if (live) {
+        const float r = es[(tl * a.M + m) * 16 + n] + v;
+        if constexpr (CH) st_sc1_f32((float*)e.out + (size_t)m * e.ldo + ng, r);
+        else ((float*)e.out)[(size_t)m * e.ldo + ng] = r;
+      }
       break;
     case TI_EPI_SILU_MUL_F16: {
       // compute_ffn (inference_engine.cpp:386-391): multiply(up, silu(gate)).
       const float up = __shfl_down(v, 8, kWave);
-      if (live && n < 8) {
-        const float s = v / (1.0f + expf(-v));
+      const float s = v / (1.0f + expf(-v));
+      if constexpr (CH) {
+        const uint32_t hv = f2h(up * s), hp = (uint32_t)__shfl_xor((int)hv, 1, kWave);
+        if (live && n < 8 && !(n & 1)) st_sc1_u32((uint16_t*)e.out + (size_t)m * e.ldo + nt * 8 + n, hv | (hp << 16));
+      } else if (live && n < 8) {
         ((uint16_t*)e.out)[(size_t)m * e.ldo + nt * 8 + n] = f2h(up * s);
       }
       break;
     }
     case TI_EPI_QKV_ROPE_KV: {
       const float partner = __shfl_xor(v, 1, kWave);
-      if (!live) break;
       const int hd = e.head_dim;
-      const int p = ((const int*)(es + a.M * hd))[m];
-      if (ng < e.q_dim + e.kv_dim) {
-        const int base = ng < e.q_dim ? 0 : e.q_dim;
-        const int d = (ng - base) % hd;
-        const float2 cs = *(const float2*)(es + m * hd + (d & ~1));   // (cos, sin) of pos[m], staged
-        // apply_rope (tensor_engine.cpp:1602-1612): even = x*c - y*s, odd = x*s + y*c,
-        // evaluated with the reference build's contraction pattern.
-        const float r = (d & 1) == 0 ? fmaf(-partner, cs.y, v * cs.x) : fmaf(v, cs.x, partner * cs.y);
-        if (ng < e.q_dim) {
-          ((float*)e.out)[(size_t)m * e.ldo + ng] = r;
-        } else {
-          const int kvh = (ng - e.q_dim) / hd;
-          e.k_cache[(size_t)m * e.kv_stream_stride + ((size_t)kvh * e.max_seq + p) * hd + d] = f2h(r);
+      const bool qk = ng < e.q_dim + e.kv_dim;
+      float r = v;
+      int p = 0;
+      if (live) {
+        p = ((const int*)(es + a.M * hd))[m];
+        if (qk) {
+          const int base = ng < e.q_dim ? 0 : e.q_dim;
+          const int d = (ng - base) % hd;
+          const float2 cs = *(const float2*)(es + m * hd + (d & ~1));   // (cos, sin) of pos[m], staged
+          // apply_rope (tensor_engine.cpp:1602-1612): even = x*c - y*s, odd = x*s + y*c,
+          // evaluated with the reference build's contraction pattern.
+          r = (d & 1) == 0 ? fmaf(-partner, cs.y, v * cs.x) : fmaf(v, cs.x, partner * cs.y);
         }
+      }
+      uint32_t pair = 0;
+      if constexpr (CH) {
+        const uint32_t hv = f2h(r), hp = (uint32_t)__shfl_xor((int)hv, 1, kWave);
+        pair = hv | (hp << 16);
+      }
+      if (!live) break;
+      if (ng < e.q_dim) {
+        if constexpr (CH) st_sc1_f32((float*)e.out + (size_t)m * e.ldo + ng, r);
+        else ((float*)e.out)[(size_t)m * e.ldo + ng] = r;
       } else {
-        const int c = ng - e.q_dim - e.kv_dim;
+        const bool is_k = qk;
+        const int c = ng - e.q_dim - (is_k ? 0 : e.kv_dim);
         const int kvh = c / hd, d = c - kvh * hd;
-        e.v_cache[(size_t)m * e.kv_stream_stride + ((size_t)kvh * e.max_seq + p) * hd + d] = f2h(v);
+        uint16_t* cache = is_k ? e.k_cache : e.v_cache;
+        uint16_t* dst = cache + (size_t)m * e.kv_stream_stride + ((size_t)kvh * e.max_seq + p) * hd + d;
+        if constexpr (CH) {
+          if (!(d & 1)) st_sc1_u32(dst, pair);
+        } else {
+          *dst = f2h(r);
+        }
       }
       break;
     }
@@ -322,7 +360,7 @@ __device__ __forceinline__ void lds_barrier() {
 // -mllvm -amdgpu-kernarg-preload-count, see Makefile), so the first x / weight / epilogue-input
 // loads do not wait for a kernarg s_load round trip (the grid size is passed too: gridDim
 // comes from the hidden kernargs).  The struct carries everything else.
-template <int BITS, int XM>
+template <int BITS, int XM, bool CH = false>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
                                                                    const void* p_x, const float* p_norm_w, int p_M,
                                                                    int p_N, int p_K, int p_ldx, int p_grid,
@@ -369,6 +407,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   u32x4 xr16[XPF];
   for (int q = 0; q < XPF; ++q) xr16[q] = (u32x4){0x3c003c00u, 0x3c003c00u, 0x3c003c00u, 0x3c003c00u};
   sc_reg = xr16[0];
+  auto load_x = [&]() {};
   if (false) {
 #else
   if constexpr (BITS != 16) sc_reg = ld_w(sg + (tid < n_sc ? tid : 0));
@@ -376,22 +415,39 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   const int nx16 = a.M * K8;
   float4 v0, v1, w0, w1;
   u32x4 xr16[XPF];
+  // x rows and the epilogue input depend on the previous launch: loaded here, or -- chained
+  // (CH) -- after the in-kernel wait, with sc1 loads (load_x below).
+  auto load_x = [&]() {
+    if constexpr (XM == XM_NORM1) {
+      const int k8 = tid < K8 ? tid : K8 - 1;
+      if constexpr (CH) {
+        const __amdgpu_buffer_rsrc_t rx = sc1_rsrc(a.x);
+        v0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, 32 * k8, 0, kAuxSc1Load));
+        v1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, 32 * k8 + 16, 0, kAuxSc1Load));
+      } else {
+        const float* xr = (const float*)a.x;
+        v0 = *(const float4*)(xr + 8 * k8);
+        v1 = *(const float4*)(xr + 8 * k8 + 4);
+      }
+    } else if constexpr (XM == XM_F16) {
+#pragma unroll
+      for (int q = 0; q < XPF; ++q) {
+        const int i = tid + q * kGemvThreads < nx16 ? tid + q * kGemvThreads : nx16 - 1;
+        const int m = i / K8, k8 = i - m * K8;
+        if constexpr (CH)
+          xr16[q] = __builtin_amdgcn_raw_buffer_load_b128(sc1_rsrc(a.x), ((size_t)m * a.ldx + 8 * k8) * 2, 0, kAuxSc1Load);
+        else
+          xr16[q] = *(const u32x4*)((const f16*)a.x + (size_t)m * a.ldx + 8 * k8);
+      }
+    }
+  };
   if constexpr (XM == XM_NORM1) {
 #endif
     const int k8 = tid < K8 ? tid : K8 - 1;
-    const float* xr = (const float*)a.x;
-    v0 = *(const float4*)(xr + 8 * k8);
-    v1 = *(const float4*)(xr + 8 * k8 + 4);
     w0 = *(const float4*)(a.norm_w + 8 * k8);
     w1 = *(const float4*)(a.norm_w + 8 * k8 + 4);
-  } else if constexpr (XM == XM_F16) {
-#pragma unroll
-    for (int q = 0; q < XPF; ++q) {
-      const int i = tid + q * kGemvThreads < nx16 ? tid + q * kGemvThreads : nx16 - 1;
-      const int m = i / K8, k8 = i - m * K8;
-      xr16[q] = *(const u32x4*)((const f16*)a.x + (size_t)m * a.ldx + 8 * k8);
-    }
   }
+  if constexpr (!CH) load_x();
   // Epilogue input, one word per thread, loaded unconditionally (a branch here would make
   // the compiler wait at the join): a residual element of our tiles, this step's position
   // of row tid, or a dummy word of x.
@@ -405,7 +461,8 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
     pre_p = kind == TI_EPI_RESID_F32 ? p_pre + (size_t)m * ldo + (t0 + tl) * 16 + n
             : kind == TI_EPI_QKV_ROPE_KV ? p_pre + (tid < a.M ? tid : 0) : p_pre;
   }
-  const float pre = *pre_p;
+  float pre = 0.0f;
+  if constexpr (!CH) pre = *pre_p;
 
   // ---- 2. the weight ring.  Item j of this wave = (tile j / KW, k-tile wave + 8 * (j % KW));
   // items past the end re-load the last item (no branch around loads); coordinates advance
@@ -423,13 +480,21 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   // limited number of outstanding loads, so a wave issuing all R slots blocks in issue for
   // microseconds, and the barrier (hence the first MFMA) would wait for the slowest wave's
   // whole burst.  The rest of the ring is issued right after the barrier.
-  constexpr int R0 = R >= 8 ? 4 : R;
+#ifndef TI_CHAIN_R0
+#define TI_CHAIN_R0 2   // chained: ring slots issued before the wait (x loads queue behind them)
+#endif
+  constexpr int R0 = CH ? (TI_CHAIN_R0 < R ? TI_CHAIN_R0 : R) : (R >= 8 ? 4 : R);
   u32x4 ring[R][C];
 #pragma unroll
   for (int s = 0; s < R0; ++s) {
     const size_t o = refill_off();
 #pragma unroll
     for (int c = 0; c < C; ++c) ring[s][c] = ld_w(tb + o + c * kWave);
+  }
+  if constexpr (CH) {
+    chain_wait(a.chain);
+    load_x();
+    pre = ld_sc1_f32(pre_p);
   }
 
   GEMV_TS(1);
@@ -474,8 +539,9 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
     for (int i = tid + kGemvThreads; i < n_sc; i += kGemvThreads) ((u32x4*)sl)[i] = sg[i];
   }
   if constexpr (XM == XM_F16) {
-    if (nx16 > XPF * kGemvThreads) stage_x_generic<XM>(a, xl, red, XPF * kGemvThreads);
+    if (nx16 > XPF * kGemvThreads) stage_x_generic<XM, CH>(a, xl, red, XPF * kGemvThreads);
   } else if constexpr (XM != XM_NORM1) {
+    static_assert(!CH, "chained launches stage x in registers (XM_F16 / XM_NORM1)");
     stage_x_generic<XM>(a, xl, red, 0);
   }
   if (a.epi.kind == TI_EPI_QKV_ROPE_KV && tid < a.M) ((int*)(es + a.M * a.epi.head_dim))[tid] = __builtin_bit_cast(int, pre);
@@ -611,7 +677,9 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   // inputs past the one-per-thread prefetch (ntl * M * 16 or M * head_dim > 512): loaded now
   for (int i = tid + kGemvThreads; i < n_res; i += kGemvThreads) {
     const int tl = i / (a.M * 16), rem = i - tl * a.M * 16, m = rem >> 4, n = rem & 15;
-    es[i] = p_pre[(size_t)m * ldo + (t0 + tl) * 16 + n];
+    const float* pp = p_pre + (size_t)m * ldo + (t0 + tl) * 16 + n;
+    if constexpr (CH) es[i] = ld_sc1_f32(pp);
+    else es[i] = *pp;
   }
   for (int i = tid + kGemvThreads; i < n_cs; i += kGemvThreads) {
     const int hd = a.epi.head_dim, m = i / hd, j = i - m * hd;
@@ -631,7 +699,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       for (int w = 1; w < kGemvWaves; ++w) v += sp[w * kWave];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (i < a.M) epilogue(a, t0 + tl, tl, n, i, v[i], es, best[i], ok);
+        if (i < a.M) epilogue<CH>(a, t0 + tl, tl, n, i, v[i], es, best[i], ok);
     }
   } else {
     const int i4 = wave & 3;
@@ -640,7 +708,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       float v = 0.0f;
 #pragma unroll
       for (int w = 0; w < kGemvWaves; ++w) v += sp[w * kWave * 4];
-      epilogue(a, t0 + tl, tl, lane, i4, v, es, best[0], true);
+      epilogue<CH>(a, t0 + tl, tl, lane, i4, v, es, best[0], true);
     }
   }
   if (a.epi.kind == TI_EPI_LOGITS_ARGMAX) {
@@ -663,8 +731,12 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
     lds_barrier();
     if (tid < a.M && best_l[tid])
       atomicMax(a.epi.argmax + (size_t)tid * TI_ARGMAX_SLOTS + (blockIdx.x & (TI_ARGMAX_SLOTS - 1)), best_l[tid]);
-    if (a.epi.step_ctr && blockIdx.x == 0 && tid == 0) *a.epi.step_ctr += a.epi.advance;
+    if (a.epi.step_ctr && blockIdx.x == 0 && tid == 0) {
+      if constexpr (CH) __hip_atomic_fetch_add(a.epi.step_ctr, a.epi.advance, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else *a.epi.step_ctr += a.epi.advance;
+    }
   }
+  if constexpr (CH) chain_signal(a.chain, blockIdx.x);
   GEMV_TS(4);
 }
 
@@ -1031,11 +1103,24 @@ __host__ inline int gemv_xmode(int x_kind, int M, int K) {
 }
 
 template <int BITS>
-static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid) {
+static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid, const ti_chain* chain) {
   const float* pre = a.epi.kind == TI_EPI_RESID_F32 ? (const float*)a.epi.out
                      : a.epi.kind == TI_EPI_QKV_ROPE_KV ? (const float*)a.epi.pos : (const float*)a.x;
   const int kind_ldo = a.epi.kind | (a.epi.ldo << 3);
-  switch (gemv_xmode(a.x_kind, a.M, a.K)) {
+  const int xm = gemv_xmode(a.x_kind, a.M, a.K);
+  if (chain) {   // chained: x staged in registers only (checked by the caller)
+    const bool ao = chain->any_order != 0;
+    hipError_t err;
+    if (xm == XM_F16)
+      err = ti_launch_ext(gemv_wq_kernel<BITS, XM_F16, true>, dim3(grid), dim3(kGemvThreads), lds, s, ao, a.tiles, a.scales,
+                          a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a);
+    else
+      err = ti_launch_ext(gemv_wq_kernel<BITS, XM_NORM1, true>, dim3(grid), dim3(kGemvThreads), lds, s, ao, a.tiles,
+                          a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a);
+    TI_HIP_CHECK(err, "hipExtLaunchKernel(gemv_wq_kernel chained)");
+    return TI_OK;
+  }
+  switch (xm) {
     case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a); break;
     case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a); break;
     case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a); break;
@@ -1171,6 +1256,9 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<8, XM_NORM1>, (const void*)gemv_wq_kernel<8, XM_NORM>,
       (const void*)gemv_wq_kernel<16, XM_F16>, (const void*)gemv_wq_kernel<16, XM_F32>,
       (const void*)gemv_wq_kernel<16, XM_NORM1>, (const void*)gemv_wq_kernel<16, XM_NORM>,
+      (const void*)gemv_wq_kernel<4, XM_F16, true>, (const void*)gemv_wq_kernel<4, XM_NORM1, true>,
+      (const void*)gemv_wq_kernel<8, XM_F16, true>, (const void*)gemv_wq_kernel<8, XM_NORM1, true>,
+      (const void*)gemv_wq_kernel<16, XM_F16, true>, (const void*)gemv_wq_kernel<16, XM_NORM1, true>,
       TI_MB_FNS};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
@@ -1223,9 +1311,9 @@ extern "C" int ti_rmsnorm_f16(const float* x, int ldx, const float* w, float eps
   return TI_OK;
 }
 
-extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x,
-                              int x_kind, int ldx, const float* norm_w, float eps, int M, int N, int K,
-                              const ti_epilogue* epi, ti_stream_t stream) {
+static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind, int ldx,
+                     const float* norm_w, float eps, int M, int N, int K, const ti_epilogue* epi, ti_chain* chain,
+                     ti_stream_t stream) {
   using namespace ti;
   if (!tiles || !x || !epi || !epi->out) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: null pointer");
   if (bits != 4 && bits != 8 && bits != 16)
@@ -1274,7 +1362,14 @@ extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bit
   }
   if (lds > 160 * 1024)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: LDS image %d B too large (M=%d N=%d K=%d)", lds, M, N, K);
-  if (lds > 64 * 1024 && !g_prepared) {
+  if (chain) {
+    const int xm = gemv_xmode(x_kind, M, K);
+    if (M != 1 || batched || (xm != XM_F16 && xm != XM_NORM1))
+      return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16_chained: M=%d K=%d x_kind=%d is not chainable", M, K, x_kind);
+    if (!chain->abort_flag || ((uintptr_t)epi->out & 3) || ((uintptr_t)epi->k_cache & 3) || ((uintptr_t)epi->v_cache & 3))
+      return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16_chained: abort_flag required, outputs 4-byte aligned");
+  }
+  if ((lds > 64 * 1024 || chain) && !g_prepared) {
     const int rc = ti_gemm_prepare();
     if (rc != TI_OK) return rc;
   }
@@ -1290,9 +1385,34 @@ extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bit
   a.N = N;
   a.K = K;
   a.epi = *epi;
+  a.chain = chain_dev(chain);
+  if (chain) chain->signaled = (uint32_t)grid;
   hipStream_t s = (hipStream_t)stream;
   if (batched) return launch_mb(a, M > 16 ? 2 : 1, grid, ntl, lds, s);
-  if (bits == 4) return launch_gemv<4>(a, lds, s, grid);
-  if (bits == 8) return launch_gemv<8>(a, lds, s, grid);
-  return launch_gemv<16>(a, lds, s, grid);
+  if (bits == 4) return launch_gemv<4>(a, lds, s, grid, chain);
+  if (bits == 8) return launch_gemv<8>(a, lds, s, grid, chain);
+  return launch_gemv<16>(a, lds, s, grid, chain);
+}
+
+extern "C" int ti_gemm_chainable(int bits, int x_kind, int M, int N, int K) {
+  using namespace ti;
+  if ((bits != 4 && bits != 8 && bits != 16) || M != 1 || N < 16 || K < 128 || (K & 127) || (N & 15)) return 0;
+  if (x_kind < TI_X_F16 || x_kind > TI_X_F32_RMSNORM || use_batched(bits, x_kind, M, N, K)) return 0;
+  const int xm = gemv_xmode(x_kind, M, K);
+  if (xm != XM_F16 && xm != XM_NORM1) return 0;
+  const int grid = gemv_grid(M, N, K, query_cus());
+  return gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid) <= 160 * 1024 ? 1 : 0;
+}
+
+extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x,
+                              int x_kind, int ldx, const float* norm_w, float eps, int M, int N, int K,
+                              const ti_epilogue* epi, ti_stream_t stream) {
+  return gemm_impl(tiles, scales, bits, x, x_kind, ldx, norm_w, eps, M, N, K, epi, nullptr, stream);
+}
+
+extern "C" int ti_gemm_wq_a16_chained(const void* tiles, const uint16_t* scales, int bits, const void* x,
+                                      int x_kind, int ldx, const float* norm_w, float eps, int M, int N, int K,
+                                      const ti_epilogue* epi, ti_chain* chain, ti_stream_t stream) {
+  if (!chain) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16_chained: null chain");
+  return gemm_impl(tiles, scales, bits, x, x_kind, ldx, norm_w, eps, M, N, K, epi, chain, stream);
 }

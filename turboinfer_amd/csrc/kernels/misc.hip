@@ -9,15 +9,19 @@ namespace ti {
 // One block per stream m.  The decode loop runs entirely on the device: the token of
 // step s is the prompt token while s < n_in[m], else the previous step's greedy argmax
 // (the key packs (value, 0xFFFFFFFF - index), so the max is the lowest-index maximum).
-__global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a) {
+// CH: one launch of a chain (ti_chain): waits for the previous step's last launch, reads
+// the step counter and argmax keys with sc1 loads and stores h / pos / tokens write-through.
+template <bool CH>
+__global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a, const ChainDev chain) {
   __shared__ int s_tok;
   const int m = blockIdx.x, tid = threadIdx.x;
-  const int s = *a.step_ctr;
+  if constexpr (CH) chain_wait(chain);
+  const int s = CH ? (int)ld_sc1_u32(a.step_ctr) : *a.step_ctr;
   const int nin = a.n_in ? a.n_in[m] : 0;
   unsigned long long* am = a.argmax + (size_t)m * TI_ARGMAX_SLOTS;
   unsigned long long key = 0ull;
   if (tid < 64) {   // row m's key = max over its slots (wave 0)
-    key = tid < TI_ARGMAX_SLOTS ? am[tid] : 0ull;
+    key = tid < TI_ARGMAX_SLOTS ? (CH ? ld_sc1_u64(am + tid) : am[tid]) : 0ull;
 #pragma unroll
     for (int o = 1; o < TI_ARGMAX_SLOTS; o <<= 1) {
       const unsigned long long other = __shfl_xor(key, o, 64);
@@ -30,24 +34,40 @@ __global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a) {
       tok = a.in_tokens[(size_t)m * a.in_stride + s];
     } else {
       tok = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
-      if (a.out_tokens && s - nin < a.out_stride) a.out_tokens[(size_t)m * a.out_stride + (s - nin)] = tok;
+      if (a.out_tokens && s - nin < a.out_stride) {
+        int32_t* o = a.out_tokens + (size_t)m * a.out_stride + (s - nin);
+        if constexpr (CH) st_sc1_u32(o, (uint32_t)tok);
+        else *o = tok;
+      }
     }
     if (tok < 0 || tok >= a.vocab) tok = 0;     // never index outside the table
     s_tok = tok;
-    a.pos[m] = a.base_pos[m] + s;
+    if constexpr (CH) st_sc1_u32(a.pos + m, (uint32_t)(a.base_pos[m] + s));
+    else a.pos[m] = a.base_pos[m] + s;
   }
   __syncthreads();   // every slot read before any is cleared
-  if (tid < TI_ARGMAX_SLOTS) am[tid] = 0ull;
+  if (tid < TI_ARGMAX_SLOTS) {
+    if constexpr (CH) st_sc1_u64(am + tid, 0ull);
+    else am[tid] = 0ull;
+  }
   float* h = a.h + (size_t)m * a.hidden;
   if (a.placeholder_first >= 0) {
     // forward_pass / forward_pass_incremental placeholder rows (inference_engine.cpp:1444-1448,
     // 1509-1512): 0.1f * (flat_index % 100).
     const size_t off = s == 0 ? (size_t)a.placeholder_first : 0;
-    for (int i = tid; i < a.hidden; i += 256) h[i] = 0.1f * (float)((off + (size_t)i) % 100);
+    for (int i = tid; i < a.hidden; i += 256) {
+      const float v = 0.1f * (float)((off + (size_t)i) % 100);
+      if constexpr (CH) st_sc1_f32(h + i, v);
+      else h[i] = v;
+    }
   } else {
     const uint16_t* e = a.emb + (size_t)s_tok * a.hidden;
-    for (int i = tid; i < a.hidden; i += 256) h[i] = h2f(e[i]);
+    for (int i = tid; i < a.hidden; i += 256) {
+      if constexpr (CH) st_sc1_f32(h + i, h2f(e[i]));
+      else h[i] = h2f(e[i]);
+    }
   }
+  if constexpr (CH) chain_signal(chain, blockIdx.x);
 }
 
 // ---------------------------------------------------------- synthetic weights
@@ -160,8 +180,22 @@ extern "C" int ti_step_begin(const ti_step_args* a, ti_stream_t stream) {
     return ti_set_error(TI_ERR_ARG, "ti_step_begin: bad arguments");
   if (a->placeholder_first < 0 && !a->emb) return ti_set_error(TI_ERR_ARG, "ti_step_begin: emb required");
   if (a->n_in && !a->in_tokens) return ti_set_error(TI_ERR_ARG, "ti_step_begin: in_tokens required");
-  hipLaunchKernelGGL(step_begin_kernel, dim3(a->M), dim3(256), 0, (hipStream_t)stream, *a);
+  hipLaunchKernelGGL(step_begin_kernel<false>, dim3(a->M), dim3(256), 0, (hipStream_t)stream, *a, ChainDev{});
   TI_LAUNCH_CHECK("step_begin_kernel");
+  return TI_OK;
+}
+
+extern "C" int ti_step_begin_chained(const ti_step_args* a, ti_chain* chain, ti_stream_t stream) {
+  using namespace ti;
+  if (!a || !chain || !chain->abort_flag || !a->h || !a->argmax || !a->pos || !a->base_pos || !a->step_ctr || a->M < 1 ||
+      a->hidden < 1)
+    return ti_set_error(TI_ERR_ARG, "ti_step_begin_chained: bad arguments");
+  if (a->placeholder_first < 0 && !a->emb) return ti_set_error(TI_ERR_ARG, "ti_step_begin_chained: emb required");
+  if (a->n_in && !a->in_tokens) return ti_set_error(TI_ERR_ARG, "ti_step_begin_chained: in_tokens required");
+  chain->signaled = (uint32_t)a->M;
+  TI_HIP_CHECK(ti_launch_ext(step_begin_kernel<true>, dim3(a->M), dim3(256), 0, (hipStream_t)stream,
+                             chain->any_order != 0, *a, chain_dev(chain)),
+               "hipExtLaunchKernel(step_begin_kernel chained)");
   return TI_OK;
 }
 
