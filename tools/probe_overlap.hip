@@ -33,6 +33,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     }                                                                                   \
   } while (0)
 
+#ifndef POLL_SLEEP
+#define POLL_SLEEP 1   // s_sleep immediate between polls (x 64 clocks)
+#endif
 constexpr int kWG = 256, kThreads = 512, kR = 5, kVec = 4096;
 
 __device__ __forceinline__ int ld_sc1_i32(const unsigned* p) {
@@ -71,7 +74,7 @@ void link_kernel(const u32x4* w, int ipw, const float* xin, float* xout, unsigne
     if (tid == 0) {
       int n = 0;
       while (ld_sc1_i32(ctr + idx - 1) < kWG) {
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(POLL_SLEEP);
         if (++n > (1 << 22)) { atomicOr(abort_flag, 1u); break; }
       }
     }
@@ -170,7 +173,7 @@ int main(int argc, char** argv) {
                             mode == 2 || mode >= 4 ? hipExtAnyOrderLaunch : 0));
     }
   };
-  for (int mode : {0, 2}) {
+  for (int mode : {0, 1, 2, 3}) {
     double best = 1e30;
     for (int round = 0; round < 6; ++round) {
       CK(hipMemset(ctr, 0, 64 * n * 4));

@@ -81,6 +81,10 @@ __device__ __forceinline__ float lane_xor(float v) {
     return __builtin_bit_cast(float, lane_id() < 32 ? r[1] : r[0]);
   }
 }
+template <int O>
+__device__ __forceinline__ uint32_t lane_xor_u32(uint32_t v) {
+  return __builtin_bit_cast(uint32_t, lane_xor<O>(__builtin_bit_cast(float, v)));
+}
 // All-reduce sum over aligned groups of WIDTH lanes (butterfly; the width-4 and width-8
 // stages pair quads / half-rows by mirroring, which is valid once the smaller stages have
 // made each quad / half-row uniform).

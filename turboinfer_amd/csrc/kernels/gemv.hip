@@ -187,7 +187,7 @@ __device__ __forceinline__ void stage_x_generic(const GemvArgs& a, f16* xl, floa
         ss = fmaf(v0.x, v0.x, ss); ss = fmaf(v0.y, v0.y, ss); ss = fmaf(v0.z, v0.z, ss); ss = fmaf(v0.w, v0.w, ss);
         ss = fmaf(v1.x, v1.x, ss); ss = fmaf(v1.y, v1.y, ss); ss = fmaf(v1.z, v1.z, ss); ss = fmaf(v1.w, v1.w, ss);
       }
-      ss = wave_sum_xor<kWave>(ss);
+      ss = group_sum<kWave>(ss);
       if ((tid & 63) == 0) red[tid >> 6] = ss;
       __syncthreads();
       float tot = 0.0f;
@@ -255,7 +255,7 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int 
       break;
     case TI_EPI_STORE_F16:
       if constexpr (CH) {
-        const uint32_t hv = f2h(v), hp = (uint32_t)__shfl_xor((int)hv, 1, kWave);
+        const uint32_t hv = f2h(v), hp = lane_xor_u32<1>(hv);
         if (live && !(n & 1)) st_sc1_u32((uint16_t*)e.out + (size_t)m * e.ldo + ng, hv | (hp << 16));
       } else if (live) {
         ((uint16_t*)e.out)[(size_t)m * e.ldo + ng] = f2h(v);
@@ -270,10 +270,10 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int 
       break;
     case TI_EPI_SILU_MUL_F16: {
       // compute_ffn (inference_engine.cpp:386-391): multiply(up, silu(gate)).
-      const float up = __shfl_down(v, 8, kWave);
+      const float up = lane_xor<8>(v);   // lanes n < 8: the up row n + 8 of the same tile
       const float s = v / (1.0f + expf(-v));
       if constexpr (CH) {
-        const uint32_t hv = f2h(up * s), hp = (uint32_t)__shfl_xor((int)hv, 1, kWave);
+        const uint32_t hv = f2h(up * s), hp = lane_xor_u32<1>(hv);
         if (live && n < 8 && !(n & 1)) st_sc1_u32((uint16_t*)e.out + (size_t)m * e.ldo + nt * 8 + n, hv | (hp << 16));
       } else if (live && n < 8) {
         ((uint16_t*)e.out)[(size_t)m * e.ldo + nt * 8 + n] = f2h(up * s);
@@ -281,7 +281,7 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int 
       break;
     }
     case TI_EPI_QKV_ROPE_KV: {
-      const float partner = __shfl_xor(v, 1, kWave);
+      const float partner = lane_xor<1>(v);
       const int hd = e.head_dim;
       const bool qk = ng < e.q_dim + e.kv_dim;
       float r = v;
@@ -299,7 +299,7 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int 
       }
       uint32_t pair = 0;
       if constexpr (CH) {
-        const uint32_t hv = f2h(r), hp = (uint32_t)__shfl_xor((int)hv, 1, kWave);
+        const uint32_t hv = f2h(r), hp = lane_xor_u32<1>(hv);
         pair = hv | (hp << 16);
       }
       if (!live) break;
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       ss = fmaf(v0.x, v0.x, ss); ss = fmaf(v0.y, v0.y, ss); ss = fmaf(v0.z, v0.z, ss); ss = fmaf(v0.w, v0.w, ss);
       ss = fmaf(v1.x, v1.x, ss); ss = fmaf(v1.y, v1.y, ss); ss = fmaf(v1.z, v1.z, ss); ss = fmaf(v1.w, v1.w, ss);
     }
-    ss = wave_sum_xor<kWave>(ss);
+    ss = group_sum<kWave>(ss);
     if (lane == 0) red[wave] = ss;
     lds_barrier();
     float tot = 0.0f;
@@ -572,10 +572,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
         const float hi = ((float)h[2] + (float)h[3]) + ((float)h[6] + (float)h[7]);
         part = 1032.0f * lo + 1152.0f * hi;
       }
-      part += __shfl_xor(part, 1, kWave);
-      part += __shfl_xor(part, 2, kWave);
-      part += __shfl_xor(part, 4, kWave);
-      part += __shfl_xor(part, 8, kWave);
+      part = group_sum<16>(part);
       if (idx < a.M * K8 && (lane & 15) == 0) corr[(k8 >> 4) * 16 + m] = part;
     }
     lds_barrier();
@@ -1143,7 +1140,7 @@ __global__ __launch_bounds__(kGemvThreads) void rmsnorm_f16_kernel(const float* 
     ss = fmaf(v0.x, v0.x, ss); ss = fmaf(v0.y, v0.y, ss); ss = fmaf(v0.z, v0.z, ss); ss = fmaf(v0.w, v0.w, ss);
     ss = fmaf(v1.x, v1.x, ss); ss = fmaf(v1.y, v1.y, ss); ss = fmaf(v1.z, v1.z, ss); ss = fmaf(v1.w, v1.w, ss);
   }
-  ss = wave_sum_xor<kWave>(ss);
+  ss = group_sum<kWave>(ss);
   if ((tid & 63) == 0) red[tid >> 6] = ss;
   __syncthreads();
   float tot = 0.0f;
