@@ -80,9 +80,16 @@ int ti_engine_set_prefill(ti_engine* e, int rows);
  * launch's weight stream starts while its predecessor finishes.  on = 1 (or env TI_CHAIN=1)
  * applies it wherever every launch of the step is chainable (one stream, fused GEMV kernel);
  * 0 (the default: measured 12 % slower than the replayed graph on MI355X)
- * always uses the graph; -1 leaves the setting.  *active (nullable) receives whether steps
+ * always uses the graph; chaining also needs the fold off (ti_engine_set_fold); -1 leaves the setting.  *active (nullable) receives whether steps
  * of 1 stream will be chained. */
 int ti_engine_set_chain(ti_engine* e, int on, int* active);
+
+/* Folded rms_norm hand-off for single-stream steps (ti_hip.h TI_X_F16_FOLDED): the epilogue
+ * that updates the residual also writes fp16(h * next norm weight) and per-workgroup sums of
+ * h^2, and the next projection divides its outputs by the rms instead of normalising its
+ * input first.  Default on (env TI_FOLD=0 turns it off); chained steps need it off.  on = 0/1
+ * sets it, -1 leaves it; *active (nullable) receives whether 1-stream steps use it. */
+int ti_engine_set_fold(ti_engine* e, int on, int* active);
 
 /* One decode step: token[s] at position pos[s] for each stream; logits [n][vocab] to host
  * (used for non-greedy sampling and per-step parity). */

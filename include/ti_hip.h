@@ -135,8 +135,14 @@ typedef struct ti_chain {
  *   xa = fp16(x)                               (x_kind TI_X_F16 / TI_X_F32), or
  *   xa = fp16((x / sqrt(mean(x^2)+eps)) * nw)  (x_kind TI_X_F32_RMSNORM; fused rms_norm)
  * fp16 x fp16 products on MFMA v_mfma_f32_16x16x32_f16, fp32 accumulation, group scale
- * applied in fp32 per 128-k group.  Epilogue (all outputs of one call): */
-enum ti_x_kind { TI_X_F16 = 0, TI_X_F32 = 1, TI_X_F32_RMSNORM = 2 };
+ * applied in fp32 per 128-k group.
+ * TI_X_F16_FOLDED (M == 1, norm_w NULL) is the same rms_norm with the normalisation moved
+ * behind the GEMM, y = (W . x) / sqrt(sum(epi->ss_in[0 .. n_ss)) / K + eps): x holds
+ * fp16(h * nw), written together with the partial sums of h^2 by the epilogue that produced h
+ * (TI_EPI_RESID_F32 with fold_x, or ti_step_begin with fold_x), so the launch stages 2-byte
+ * rows with no block-wide reduction in front of its first MFMA.  Epilogue (all outputs of one
+ * call): */
+enum ti_x_kind { TI_X_F16 = 0, TI_X_F32 = 1, TI_X_F32_RMSNORM = 2, TI_X_F16_FOLDED = 3 };
 enum ti_epilogue_kind {
   TI_EPI_STORE_F32 = 0,      /* out_f32[m*ldo + n] = y                                  */
   TI_EPI_STORE_F16 = 1,      /* out_f16[m*ldo + n] = fp16(y)                             */
@@ -170,7 +176,15 @@ typedef struct ti_epilogue {
   unsigned long long* argmax;        /* device [M][TI_ARGMAX_SLOTS] keys, zeroed before the call */
   int32_t* step_ctr;                 /* device counter += advance by one thread (nullable) */
   int32_t advance;
-  int32_t _pad;
+  /* TI_X_F16_FOLDED input: n_ss partial sums of squares of the row at ss_in */
+  int32_t n_ss;
+  const float* ss_in;
+  /* TI_EPI_RESID_F32, M == 1, fold_x non-NULL: besides h, write fold_x[n] = fp16(h[n] * fold_w[n])
+   * and fold_ss[b] = sum of h[n]^2 over the outputs of workgroup b (b < ti_gemm_grid(...)): the
+   * next launch's TI_X_F16_FOLDED input */
+  const float* fold_w;
+  uint16_t* fold_x;
+  float* fold_ss;
 } ti_epilogue;
 
 int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind,
@@ -198,6 +212,9 @@ int ti_gemm_wq_a16_chained(const void* tiles, const uint16_t* scales, int bits, 
                            const ti_epilogue* epi, ti_chain* chain, ti_stream_t s);
 /* 1 if ti_gemm_wq_a16_chained accepts this shape (M == 1, fused kernel, x staged in registers). */
 int ti_gemm_chainable(int bits, int x_kind, int M, int N, int K);
+/* Workgroups of the fused kernel for an M x N x K call: the fold_ss partials a
+ * TI_EPI_RESID_F32 fold epilogue writes (0 = shape not taken by the fused kernel). */
+int ti_gemm_grid(int M, int N, int K);
 /* One-time kernel attribute setup; call before capturing ti_gemm_wq_a16 into a graph. */
 int ti_gemm_prepare(void);
 
@@ -233,7 +250,9 @@ int ti_attn_decode_chained(const float* q, const uint16_t* k_cache, const uint16
  * into h (fp32), sets pos[m] = base_pos[m] + *step_ctr, clears argmax row m (all slots).
  * placeholder_first >= 0 selects the reference_compat placeholder embedding
  * 0.1f*((offset + i) % 100) (inference_engine.cpp:1444-1448, 1509-1512) with offset
- * placeholder_first on step 0 and 0 afterwards. */
+ * placeholder_first on step 0 and 0 afterwards.
+ * fold_x non-NULL: also fold_x[m][i] = fp16(h[m][i] * fold_w[i]) and fold_ss[m] = sum_i
+ * h[m][i]^2, the TI_X_F16_FOLDED input (n_ss = 1) of the first layer's projection. */
 typedef struct ti_step_args {
   const uint16_t* emb;               /* [vocab][hidden] fp16 */
   float* h;                          /* [M][hidden] */
@@ -245,6 +264,9 @@ typedef struct ti_step_args {
   int32_t* pos;                      /* [M] */
   const int32_t* base_pos;           /* [M] */
   const int32_t* step_ctr;
+  const float* fold_w;               /* [hidden] (with fold_x) */
+  uint16_t* fold_x;                  /* [M][hidden] fp16, nullable */
+  float* fold_ss;                    /* [M] */
 } ti_step_args;
 int ti_step_begin(const ti_step_args* a, ti_stream_t s);
 /* One launch of a chain (ti_chain): waits for the previous step's last launch (argmax keys,

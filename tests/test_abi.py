@@ -70,6 +70,17 @@ def test_argument_errors_are_reported_without_launch(L):
     assert rc == 1 and b"M must be" in L.ti_last_error()
     rc = L.ti_rmsnorm_f16(1, 100, 1, 1e-5, 1, 128, 2, 128, None)
     assert rc == 1
+    # folded rms_norm input: one row, ss partials required; fold producer: one row
+    rc = L.ti_gemm_wq_a16(1, 1, 4, 1, T.X_F16_FOLDED, 4096, None, 1e-5, 2, 16, 4096, C.byref(ep), None)
+    assert rc == 1 and b"TI_X_F16_FOLDED" in L.ti_last_error()
+    rc = L.ti_gemm_wq_a16(1, 1, 4, 1, T.X_F16_FOLDED, 4096, None, 1e-5, 1, 16, 4096, C.byref(ep), None)
+    assert rc == 1 and b"TI_X_F16_FOLDED" in L.ti_last_error()
+    fe = T.Epilogue()
+    fe.kind, fe.ldo, fe.out, fe.fold_x = T.EPI_RESID_F32, 16, 1234, 1234
+    rc = L.ti_gemm_wq_a16(1, 1, 4, 1, T.X_F16, 4096, None, 1e-5, 1, 16, 4096, C.byref(fe), None)
+    assert rc == 1 and b"fold_x" in L.ti_last_error()
+    assert L.ti_gemm_grid(1, 4096, 4096) >= 1 and L.ti_gemm_grid(1, 4096, 4096) <= 256
+    assert L.ti_gemm_grid(0, 4096, 4096) == 0
     # attention head_dim unsupported
     rc = L.ti_attn_decode(1, 1, 1, 1 << 20, 16, 1, 1, 4, 4, 96, 1, 1, 1, None)
     assert rc == 3

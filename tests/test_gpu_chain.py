@@ -27,6 +27,7 @@ def make(ti, name, max_seq=640):
     v, h, l, nh, nkv, hd, inter, bits = CFGS[name]
     e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=bits, max_seq=max_seq, max_batch=1)
     e.synth(0x7157, 0.1)
+    e.set_fold(False)   # chained launches run the unfolded kernels (ti_engine_set_fold)
     return e
 
 

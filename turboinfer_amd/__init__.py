@@ -23,7 +23,7 @@ ROOT = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("TI_LIB") or os.path.join(HERE, "lib", "libturboinfer_amd.so")
 
 TI_OK = 0
-X_F16, X_F32, X_F32_RMSNORM = 0, 1, 2
+X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED = 0, 1, 2, 3
 EPI_STORE_F32, EPI_STORE_F16, EPI_RESID_F32, EPI_SILU_MUL_F16, EPI_QKV_ROPE_KV, EPI_LOGITS_ARGMAX = range(6)
 ARGMAX_SLOTS = 32
 GEMM_MAX_ROWS = 32                 # TI_GEMM_MAX_ROWS (include/ti_hip.h)   # TI_ARGMAX_SLOTS (include/ti_hip.h)
@@ -41,7 +41,8 @@ class Epilogue(C.Structure):
                 ("q_dim", C.c_int32), ("kv_dim", C.c_int32), ("head_dim", C.c_int32), ("max_seq", C.c_int32),
                 ("pos", C.c_void_p), ("rope_cs", C.c_void_p), ("k_cache", C.c_void_p), ("v_cache", C.c_void_p),
                 ("kv_stream_stride", C.c_int64), ("argmax", C.c_void_p), ("step_ctr", C.c_void_p),
-                ("advance", C.c_int32), ("_pad", C.c_int32)]
+                ("advance", C.c_int32), ("n_ss", C.c_int32), ("ss_in", C.c_void_p),
+                ("fold_w", C.c_void_p), ("fold_x", C.c_void_p), ("fold_ss", C.c_void_p)]
 
 
 class StepArgs(C.Structure):
@@ -49,7 +50,8 @@ class StepArgs(C.Structure):
                 ("vocab", C.c_int32), ("in_stride", C.c_int32), ("out_stride", C.c_int32),
                 ("placeholder_first", C.c_int32), ("in_tokens", C.c_void_p), ("n_in", C.c_void_p),
                 ("argmax", C.c_void_p), ("out_tokens", C.c_void_p), ("pos", C.c_void_p),
-                ("base_pos", C.c_void_p), ("step_ctr", C.c_void_p)]
+                ("base_pos", C.c_void_p), ("step_ctr", C.c_void_p), ("fold_w", C.c_void_p),
+                ("fold_x", C.c_void_p), ("fold_ss", C.c_void_p)]
 
 
 class EngineConfig(C.Structure):
@@ -74,7 +76,7 @@ EXPORTED = [
     "ti_engine_synth", "ti_engine_fill_kv", "ti_engine_generate", "ti_engine_step", "ti_engine_compat_step",
     "ti_engine_replay_prepare", "ti_engine_set_prefill", "ti_engine_replay_run", "ti_engine_sync", "ti_engine_last_tokens",
     "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token", "ti_gemm_wq_a16_chained", "ti_gemm_chainable",
-    "ti_attn_decode_chained", "ti_step_begin_chained", "ti_engine_set_chain",
+    "ti_attn_decode_chained", "ti_step_begin_chained", "ti_engine_set_chain", "ti_gemm_grid", "ti_engine_set_fold",
 ]
 
 _lib = None
@@ -141,6 +143,9 @@ def lib() -> C.CDLL:
         L.ti_engine_set_prefill.argtypes = [vp, i32]
         L.ti_engine_set_chain.argtypes = [vp, i32, C.POINTER(C.c_int)]
         L.ti_gemm_chainable.argtypes = [i32, i32, i32, i32, i32]
+        if hasattr(L, "ti_engine_set_fold"):   # (older TI_LIB builds in A/B runs lack it)
+            L.ti_gemm_grid.argtypes = [i32, i32, i32]
+            L.ti_engine_set_fold.argtypes = [vp, i32, C.POINTER(C.c_int)]
         L.ti_engine_compat_step.argtypes = [vp, i32, vp]
         L.ti_engine_replay_prepare.argtypes = [vp, i32, i32, i32]
         L.ti_engine_replay_run.argtypes = [vp, i32]
@@ -306,6 +311,12 @@ class Engine:
         """Chained single-stream steps on/off (None: query); returns whether they are active."""
         act = C.c_int(0)
         check(lib().ti_engine_set_chain(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
+        return bool(act.value)
+
+    def set_fold(self, on=None) -> bool:
+        """Folded rms_norm hand-off on/off (None: query); returns whether 1-stream steps use it."""
+        act = C.c_int(0)
+        check(lib().ti_engine_set_fold(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
         return bool(act.value)
 
     def step(self, tokens, pos):

@@ -88,6 +88,12 @@ struct ti_engine {
   uint16_t* attn = nullptr;
   uint16_t* act = nullptr;
   uint16_t* xn = nullptr;      // fp16 rms_norm rows for the batched-rows GEMM [R][hidden]
+  // single-stream steps with the rms_norm folded behind the GEMM (ti_hip.h TI_X_F16_FOLDED):
+  // the epilogue that writes h also writes fx = fp16(h * next norm weight) and its workgroups'
+  // sums of h^2 (ss); the next projection stages fx and divides its outputs by the rms
+  bool fold_on = true;         // TI_FOLD=0 / ti_engine_set_fold
+  uint16_t* fx = nullptr;      // [hidden]
+  float* ss = nullptr;         // [256]
   // prefill (forward_pass over prompt tokens): up to pf_rows prompt tokens of one stream run
   // as rows of the batched path, sharing that stream's KV cache (stride 0)
   int pf_rows = 0;             // 0 = off (prompts consumed one token per decode step)
@@ -203,7 +209,7 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
     rows = ti_gemm_max_rows(c.bits, x_kind, W.N, W.K);
   }
   if (rows < 1) return ti_set_error(TI_ERR_UNSUPPORTED, "engine: no GEMM kernel for N=%d K=%d", W.N, W.K);
-  const size_t x_elem = x_kind == TI_X_F16 ? 2 : 4;
+  const size_t x_elem = x_kind == TI_X_F16 || x_kind == TI_X_F16_FOLDED ? 2 : 4;
   for (int m0 = 0; m0 < M; m0 += rows) {
     const int mm = std::min(rows, M - m0);
     ti_epilogue ep = epi;
@@ -222,7 +228,7 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
 // ------------------------------------------------------------- chained steps
 bool chain_usable(ti_engine* e, int M) {
   const ti_engine_config& c = e->c;
-  if (!e->chain_on || M != 1 || c.compat || !e->chain_ctr) return false;
+  if (!e->chain_on || M != 1 || c.compat || !e->chain_ctr || e->fold_on) return false;   // chained kernels: no fold
   if (e->chain_ok < 0) {
     const int H = c.hidden, I = c.inter, qd = e->qd(), kvd = e->kvd();
     const int b = c.bits;
@@ -365,6 +371,16 @@ int run_steps(ti_engine* e, int M, int advance, int n) {
   return TI_OK;
 }
 
+// The folded rms_norm hand-off applies to single-stream steps whose producers (O, down) run on
+// the fused kernel with at most 256 workgroups.
+bool fold_usable(ti_engine* e, int M) {
+  const ti_engine_config& c = e->c;
+  if (!e->fold_on || M != 1 || c.compat || !e->fx) return false;
+  const int H = c.hidden, I = c.inter, qd = e->qd();
+  const int g_o = ti_gemm_grid(1, H, qd), g_d = ti_gemm_grid(1, H, I);
+  return g_o > 0 && g_o <= 256 && g_d > 0 && g_d <= 256 && ti_gemm_max_rows(c.bits, TI_X_F16, H, qd) >= 1;
+}
+
 // One decode step for streams [0, M) on e->s.  Graph-capturable (no host sync / alloc).
 int enqueue_step(ti_engine* e, int M, int advance) {
   const ti_engine_config& c = e->c;
@@ -384,12 +400,39 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   sa.pos = e->pos;
   sa.base_pos = e->base_pos;
   sa.step_ctr = e->step_ctr;
-  TI_TRY(ti_step_begin(&sa, e->s));
-
   const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
+  // fold (M == 1): every rms_norm input is handed over as fx + ss partials by its producer
+  const bool fold = fold_usable(e, M);
+  auto next_norm = [&](int l) -> const float* { return l < c.layers ? e->layer[l].attn_norm : e->out_norm; };
+  if (fold) {
+    sa.fold_w = next_norm(0);
+    sa.fold_x = e->fx;
+    sa.fold_ss = e->ss;
+  }
+  TI_TRY(ti_step_begin(&sa, e->s));
+  int n_ss = 1;   // partials the last producer wrote (step_begin: one)
+  auto fold_into = [&](ti_epilogue& ep, const float* w) {   // producer side (RESID epilogue)
+    if (!fold) return;
+    ep.fold_w = w;
+    ep.fold_x = e->fx;
+    ep.fold_ss = e->ss;
+  };
+  auto norm_in = [&](const void*& x, int& xk, int& ldx, const float*& nw, ti_epilogue& ep) {   // consumer side
+    if (!fold) return;
+    x = e->fx;
+    xk = TI_X_F16_FOLDED;
+    ldx = H;
+    nw = nullptr;
+    ep.ss_in = e->ss;
+    ep.n_ss = n_ss;
+  };
+
   auto gemm = [&](const DevLinear& W, const void* x, int x_kind, int ldx, size_t /*x_elem*/, const float* nw,
                   ti_epilogue epi, size_t out_elem, bool last_gets_ctr) -> int {
-    return gemm_rows(e, W, M, x, x_kind, ldx, nw, epi, out_elem, last_gets_ctr);
+    if (x_kind == TI_X_F32_RMSNORM) norm_in(x, x_kind, ldx, nw, epi);
+    TI_TRY(gemm_rows(e, W, M, x, x_kind, ldx, nw, epi, out_elem, last_gets_ctr));
+    if (epi.fold_x) n_ss = ti_gemm_grid(M, W.N, W.K);
+    return TI_OK;
   };
 
   for (int l = 0; l < c.layers; ++l) {
@@ -416,6 +459,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     eo.kind = TI_EPI_RESID_F32;
     eo.ldo = H;
     eo.out = e->h;
+    fold_into(eo, L.ffn_norm);
     TI_TRY(gemm(L.o, e->attn, TI_X_F16, qd, 2, nullptr, eo, 4, false));
 
     ti_epilogue eg{};
@@ -428,6 +472,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     ed.kind = TI_EPI_RESID_F32;
     ed.ldo = H;
     ed.out = e->h;
+    fold_into(ed, next_norm(l + 1));
     TI_TRY(gemm(L.down, e->act, TI_X_F16, I, 2, nullptr, ed, 4, false));
   }
   ti_epilogue el{};
@@ -617,8 +662,10 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
         (rc = e->alloc_t(&e->act, (size_t)R * I)) || (rc = e->alloc_t(&e->xn, (size_t)R * H)) ||
         (rc = e->alloc(reinterpret_cast<void**>(&e->ws), ti_attn_workspace_bytes(R, c.heads, hd, e->splits_max))) ||
         (rc = e->alloc_t(&e->pf_ones, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->pf_zero, (size_t)1)) ||
-        (rc = e->alloc_t(&e->pf_base, (size_t)e->pf_rows)))
+        (rc = e->alloc_t(&e->pf_base, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->fx, (size_t)H)) ||
+        (rc = e->alloc_t(&e->ss, (size_t)256)))
       return fail(rc);
+    if (const char* env = getenv("TI_FOLD")) e->fold_on = atoi(env) != 0;
     e->chain_slots = 2 + 5 * c.layers;
     e->chain_cum.assign((size_t)e->chain_slots, 0u);
     if ((rc = e->alloc_t(&e->chain_ctr, (size_t)e->chain_slots * TI_CHAIN_SHARDS)) || (rc = e->alloc_t(&e->chain_abort, (size_t)1)))
@@ -906,6 +953,18 @@ int ti_engine_set_chain(ti_engine* e, int on, int* active) {
   return TI_OK;
 }
 
+int ti_engine_set_fold(ti_engine* e, int on, int* active) {
+  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_fold: null");
+  if (on >= 0 && (on != 0) != e->fold_on) {
+    TI_TRY(ti_stream_sync(e->s));   // captured step graphs bake the setting in
+    for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
+    e->graphs.clear();
+    e->fold_on = on != 0;
+  }
+  if (active) *active = fold_usable(e, 1) ? 1 : 0;
+  return TI_OK;
+}
+
 int ti_engine_last_tokens(ti_engine* e, int n, int32_t* tokens) {
   if (!e || !tokens || n < 1 || n > e->c.max_batch) return ti_set_error(TI_ERR_ARG, "ti_engine_last_tokens");
   std::vector<unsigned long long> am;
@@ -919,6 +978,7 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
     return ti_set_error(TI_ERR_ARG, "ti_engine_time_kernel: bad arguments");
   const ti_engine_config& c = e->c;
   const int H = c.hidden, I = c.inter, qd = e->qd(), kvd = e->kvd();
+  const bool fold = fold_usable(e, n);
   // Launch r uses layer r % layers, so (as in a real step) its weights are not still in
   // the 256 MB Infinity Cache from the previous launch.
   int cur = 0;
@@ -943,6 +1003,19 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
       // STORE_F32 into a scratch of n*H floats: q holds n*qd >= n*H only if qd >= H
       if ((size_t)qd < (size_t)H) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_time_kernel: scratch too small");
       ep.out = e->q;
+      if (fold) {   // the step's producer form: residual add into the scratch + fold outputs
+        ep.kind = TI_EPI_RESID_F32;
+        ep.fold_w = L.ffn_norm;
+        ep.fold_x = e->fx;
+        ep.fold_ss = e->ss;
+      }
+    }
+    if (fold && xk == TI_X_F32_RMSNORM) {   // the step's consumer form (enqueue_step)
+      x = e->fx;
+      xk = TI_X_F16_FOLDED;
+      nw = nullptr;
+      ep.ss_in = e->ss;
+      ep.n_ss = ti_gemm_grid(1, H, which == 2 ? qd : I);
     }
     return TI_OK;
   };
@@ -985,7 +1058,7 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
     *bytes = 2.0 * n * (double)kvd * kv_len * 2.0 + (double)n * qd * (4 + 2);
   } else {
     const double wbytes = (double)ti_wpack_tile_bytes(c.bits, W->K, W->N) + (double)ti_wpack_scale_bytes(c.bits, W->K, W->N);
-    *bytes = wbytes + (double)n * W->K * (xk == TI_X_F16 ? 2 : 4);
+    *bytes = wbytes + (double)n * W->K * (xk == TI_X_F16 || xk == TI_X_F16_FOLDED ? 2 : 4);
   }
   return TI_OK;
 }

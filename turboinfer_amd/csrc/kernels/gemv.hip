@@ -41,6 +41,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef TI_GEMV_SYNC
 #define TI_GEMV_SYNC 0   // blocks of R items between workgroup barriers in the stream (0 = none)
 #endif
+#ifndef TI_GEMV_RING_DELAY
+#define TI_GEMV_RING_DELAY 0
+#endif
 #ifndef TI_GEMV_EXP
 #define TI_GEMV_EXP 0   // product build; tools/probe_gemv.hip compiles diagnostic variants
 #endif
@@ -97,7 +100,8 @@ __host__ inline int gemv_grid(int M, int N, int K, int num_cus) {
 //   scales [ntl][K/128][16] fp16      group scales of the workgroup's tiles
 //   corr   [K/128][16] f32            int4: per (group, row) offset correction (see deq_int4_raw)
 //   slab   [ntl + 1][8][64] f32x4     per-wave partial tiles (+ one dummy slab)
-//   es     epilogue inputs: residual [ntl][M][16] f32, or RoPE (cos, sin) [M][hd] + pos [M]
+//   es     epilogue inputs: residual [ntl][M][16] f32 (+ the fold weights of the same
+//          outputs, TI_EPI_RESID_F32 with fold_x), or RoPE (cos, sin) [M][hd] + pos [M]
 //   best   [16] u64                   argmax keys of the workgroup
 struct GemvLds {
   int x, sc, corr, slab, es, best, total;
@@ -109,7 +113,7 @@ __host__ __device__ inline GemvLds gemv_lds_layout(int M, int K, int ntl) {
   l.corr = l.sc + align16(ntl * (K >> 7) * 32);
   l.slab = l.corr + (K >> 7) * 16 * 4;         // int4 offset correction [K/128][16 rows] f32
   l.es = l.slab + (ntl + 1) * kGemvWaves * kWave * 16;
-  const int es_bytes = ntl * M * 16 * 4 > M * 128 * 4 + 64 ? ntl * M * 16 * 4 : M * 128 * 4 + 64;
+  const int es_bytes = 2 * ntl * M * 16 * 4 > M * 128 * 4 + 64 ? 2 * ntl * M * 16 * 4 : M * 128 * 4 + 64;
   l.best = l.es + align16(es_bytes);
   l.total = l.best + 16 * 8;
   return l;
@@ -170,7 +174,9 @@ __device__ __forceinline__ f16x8 dequant_step(const u32x4 (&w)[BITS / 4], int s4
 // ------------------------------------------------------------- x staging (LDS)
 // x staging modes (chosen on the host): fp16 rows prefetched into registers; fp32 rows;
 // rms_norm of ONE row of K <= 4096 held in registers; rms_norm of several / longer rows.
-enum { XM_F16 = 0, XM_F32 = 1, XM_NORM1 = 2, XM_NORM = 3 };
+// XM_F16F: fp16 rows of h * nw (TI_X_F16_FOLDED, one row) staged like XM_F16; the rms comes
+// from the producer's partial sums of squares and divides the outputs before the epilogue.
+enum { XM_F16 = 0, XM_F32 = 1, XM_NORM1 = 2, XM_NORM = 3, XM_F16F = 4 };
 
 // Generic staging (M > 1 with rms_norm, f32 rows, or rows longer than the register
 // prefetch covers).  Runs after the ring is issued, so its loads wait behind the ring.
@@ -240,9 +246,11 @@ __device__ __forceinline__ uint32_t float_order_key(float v) {
 // thread's running argmax key for LOGITS_ARGMAX.
 // Chained launches (CH) store write-through: 4-byte sc1 stores, fp16 outputs packed in pairs
 // (lane n even stores n and n + 1; its partner n ^ 1 sits in the same 16-lane group).
+// RESID with fold_x (M == 1): also the fp16 h * nw of the next projection's TI_X_F16_FOLDED input
+// (fold weights pre-staged at fw) and this thread's running sum of h^2 (ssacc).
 template <bool CH>
 __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int l, int i, float v, const float* es,
-                                         unsigned long long& best, bool ok) {
+                                         unsigned long long& best, bool ok, const float* fw, float& ssacc) {
   const ti_epilogue& e = a.epi;
   const int m = 4 * (l >> 4) + i, n = l & 15, ng = nt * 16 + n;
   const bool live = ok && m < a.M;
@@ -266,6 +274,10 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int 
         const float r = es[(tl * a.M + m) * 16 + n] + v;
         if constexpr (CH) st_sc1_f32((float*)e.out + (size_t)m * e.ldo + ng, r);
         else ((float*)e.out)[(size_t)m * e.ldo + ng] = r;
+        if (!CH && e.fold_x) {
+          e.fold_x[ng] = f2h(r * fw[tl * 16 + n]);
+          ssacc = fmaf(r, r, ssacc);
+        }
       }
       break;
     case TI_EPI_SILU_MUL_F16: {
@@ -359,22 +371,26 @@ __device__ __forceinline__ void lds_barrier() {
 // preload leading kernel arguments into SGPRs before the waves start (compiled with
 // -mllvm -amdgpu-kernarg-preload-count, see Makefile), so the first x / weight / epilogue-input
 // loads do not wait for a kernarg s_load round trip (the grid size is passed too: gridDim
-// comes from the hidden kernargs).  The struct carries everything else.
+// comes from the hidden kernargs).  Everything read before the weight ring is issued sits in
+// the 14 dwords the hardware preloads (s[2:15]; packed below); the struct carries the rest.
+//   p_aux: the rms_norm weight (XM_NORM*), the producer's ss partials (XM_F16F) or, for a
+//          TI_EPI_RESID_F32 fold producer with fp16 x, the fold weight (else NULL)
+//   p_mgk: M | grid << 6 | epilogue kind << 18       p_kx: K | (ldx, or n_ss for XM_F16F) << 16
 template <int BITS, int XM, bool CH = false>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
-                                                                   const void* p_x, const float* p_norm_w, int p_M,
-                                                                   int p_N, int p_K, int p_ldx, int p_grid,
-                                                                   const float* p_pre, int p_kind_ldo,
+                                                                   const void* p_x, const float* p_aux, int p_mgk,
+                                                                   int p_N, int p_kx, int p_ldo, const float* p_pre,
                                                                    const GemvArgs a_in) {
   GemvArgs a = a_in;
   a.tiles = p_tiles;
   a.scales = p_scales;
   a.x = p_x;
-  a.norm_w = p_norm_w;
-  a.M = p_M;
+  a.norm_w = p_aux;
+  a.M = p_mgk & 63;
   a.N = p_N;
-  a.K = p_K;
-  a.ldx = p_ldx;
+  a.K = p_kx & 0xffff;
+  a.ldx = XM == XM_F16F ? a.K : (int)((unsigned)p_kx >> 16);
+  const int p_grid = (p_mgk >> 6) & 0xfff;
   constexpr int C = TileFmt<BITS>::kChunks;
   constexpr int R = TI_GEMV_RING_VGPRS / (4 * C) > 2 ? TI_GEMV_RING_VGPRS / (4 * C) : 2;   // ring depth (items)
   constexpr int XPF = 3;                           // fp16 x: 16-byte pieces prefetched per thread
@@ -429,7 +445,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
         v0 = *(const float4*)(xr + 8 * k8);
         v1 = *(const float4*)(xr + 8 * k8 + 4);
       }
-    } else if constexpr (XM == XM_F16) {
+    } else if constexpr (XM == XM_F16 || XM == XM_F16F) {
 #pragma unroll
       for (int q = 0; q < XPF; ++q) {
         const int i = tid + q * kGemvThreads < nx16 ? tid + q * kGemvThreads : nx16 - 1;
@@ -451,8 +467,8 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   // Epilogue input, one word per thread, loaded unconditionally (a branch here would make
   // the compiler wait at the join): a residual element of our tiles, this step's position
   // of row tid, or a dummy word of x.
-  // (p_pre / p_kind_ldo are preloaded: epi.out for RESID, epi.pos for QKV, else x)
-  const int kind = p_kind_ldo & 7, ldo = p_kind_ldo >> 3;
+  // (p_pre / kind / ldo are preloaded: epi.out for RESID, epi.pos for QKV, else x)
+  const int kind = (p_mgk >> 18) & 7, ldo = p_ldo;
   const int n_res = kind == TI_EPI_RESID_F32 ? ntl * a.M * 16 : 0;
   const float* pre_p;
   {
@@ -463,6 +479,18 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   }
   float pre = 0.0f;
   if constexpr (!CH) pre = *pre_p;
+  // RESID with fold_x: the fold weight of the same output (one row), consumed by the epilogue
+  const bool fold = !CH && XM == XM_F16 && kind == TI_EPI_RESID_F32 && p_aux != nullptr;
+  const float* fw_p = fold ? p_aux + (size_t)t0 * 16 + (tid < n_res ? tid : 0) : pre_p;
+  const float fw_pre = *fw_p;   // unconditional (no branch join in front of the ring)
+  // XM_F16F: this lane's share of the producer's partial sums of squares (up to 256 of them),
+  // clamped loads; masked and summed after the stream
+  float ss4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  const int n_ss = (int)((unsigned)p_kx >> 16);
+  if constexpr (XM == XM_F16F) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ss4[j] = p_aux[lane + 64 * j < n_ss ? lane + 64 * j : 0];
+  }
 
   // ---- 2. the weight ring.  Item j of this wave = (tile j / KW, k-tile wave + 8 * (j % KW));
   // items past the end re-load the last item (no branch around loads); coordinates advance
@@ -485,6 +513,9 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
 #endif
   constexpr int R0 = CH ? (TI_CHAIN_R0 < R ? TI_CHAIN_R0 : R) : (R >= 8 ? 4 : R);
   u32x4 ring[R][C];
+#if TI_GEMV_RING_DELAY > 0   // A/B knob: hold the ring back (x 64 clocks) behind the small loads
+  __builtin_amdgcn_s_sleep(TI_GEMV_RING_DELAY);
+#endif
 #pragma unroll
   for (int s = 0; s < R0; ++s) {
     const size_t o = refill_off();
@@ -524,7 +555,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       h[6] = (f16)((v1.z / rms) * w1.z); h[7] = (f16)((v1.w / rms) * w1.w);
       *(f16x8*)(xl + 8 * tid) = h;
     }
-  } else if constexpr (XM == XM_F16) {
+  } else if constexpr (XM == XM_F16 || XM == XM_F16F) {
 #pragma unroll
     for (int q = 0; q < XPF; ++q) {
       const int i = tid + q * kGemvThreads;
@@ -538,7 +569,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   if constexpr (BITS != 16) {
     for (int i = tid + kGemvThreads; i < n_sc; i += kGemvThreads) ((u32x4*)sl)[i] = sg[i];
   }
-  if constexpr (XM == XM_F16) {
+  if constexpr (XM == XM_F16 || XM == XM_F16F) {
     if (nx16 > XPF * kGemvThreads) stage_x_generic<XM, CH>(a, xl, red, XPF * kGemvThreads);
   } else if constexpr (XM != XM_NORM1) {
     static_assert(!CH, "chained launches stage x in registers (XM_F16 / XM_NORM1)");
@@ -670,6 +701,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   GEMV_WTS();
   // ---- 5. epilogue inputs into LDS, reduce the 8 partials per tile, epilogue
   if (tid < n_res) es[tid] = pre;
+  if (fold && tid < n_res) es[n_res + tid] = fw_pre;
   if (tid < n_cs) es[tid] = cs_reg;
   // inputs past the one-per-thread prefetch (ntl * M * 16 or M * head_dim > 512): loaded now
   for (int i = tid + kGemvThreads; i < n_res; i += kGemvThreads) {
@@ -677,7 +709,20 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
     const float* pp = p_pre + (size_t)m * ldo + (t0 + tl) * 16 + n;
     if constexpr (CH) es[i] = ld_sc1_f32(pp);
     else es[i] = *pp;
+    if (fold) es[n_res + i] = p_aux[(size_t)t0 * 16 + i];
   }
+  // XM_F16F: rms of the row from the producer's partials, the same fixed-order sum in every
+  // wave (rms_norm, tensor_engine.cpp:1488-1505, with the division moved behind the GEMM)
+  float rms = 1.0f;
+  if constexpr (XM == XM_F16F) {
+    float t = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t += lane + 64 * j < n_ss ? ss4[j] : 0.0f;
+    t = group_sum<kWave>(t);
+    rms = sqrtf(t / (float)a.K + a.eps);
+  }
+  float ssacc = 0.0f;
+  const float* fw_l = es + n_res;
   for (int i = tid + kGemvThreads; i < n_cs; i += kGemvThreads) {
     const int hd = a.epi.head_dim, m = i / hd, j = i - m * hd;
     es[i] = a.epi.rope_cs[(size_t)((const int*)(es + a.M * hd))[m] * hd + j];
@@ -696,7 +741,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       for (int w = 1; w < kGemvWaves; ++w) v += sp[w * kWave];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (i < a.M) epilogue<CH>(a, t0 + tl, tl, n, i, v[i], es, best[i], ok);
+        if (i < a.M) epilogue<CH>(a, t0 + tl, tl, n, i, XM == XM_F16F ? v[i] / rms : v[i], es, best[i], ok, fw_l, ssacc);
     }
   } else {
     const int i4 = wave & 3;
@@ -705,7 +750,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       float v = 0.0f;
 #pragma unroll
       for (int w = 0; w < kGemvWaves; ++w) v += sp[w * kWave * 4];
-      epilogue<CH>(a, t0 + tl, tl, lane, i4, v, es, best[0], true);
+      epilogue<CH>(a, t0 + tl, tl, lane, i4, v, es, best[0], true, fw_l, ssacc);
     }
   }
   if (a.epi.kind == TI_EPI_LOGITS_ARGMAX) {
@@ -731,6 +776,18 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
     if (a.epi.step_ctr && blockIdx.x == 0 && tid == 0) {
       if constexpr (CH) __hip_atomic_fetch_add(a.epi.step_ctr, a.epi.advance, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else *a.epi.step_ctr += a.epi.advance;
+    }
+  }
+  if (fold) {   // this workgroup's sum of h^2, waves in a fixed order (best_l: unused by RESID)
+    float* red2 = (float*)best_l;
+    const float sw = group_sum<kWave>(ssacc);
+    if (lane == 0) red2[wave] = sw;
+    lds_barrier();
+    if (tid == 0) {
+      float t = 0.0f;
+#pragma unroll
+      for (int w = 0; w < kGemvWaves; ++w) t += red2[w];
+      a.epi.fold_ss[blockIdx.x] = t;
     }
   }
   if constexpr (CH) chain_signal(a.chain, blockIdx.x);
@@ -1095,6 +1152,7 @@ static int g_num_cus = 0;
 
 __host__ inline int gemv_xmode(int x_kind, int M, int K) {
   if (x_kind == TI_X_F16) return XM_F16;
+  if (x_kind == TI_X_F16_FOLDED) return XM_F16F;
   if (x_kind == TI_X_F32) return XM_F32;
   return M == 1 && (K >> 3) <= kGemvThreads ? XM_NORM1 : XM_NORM;
 }
@@ -1103,25 +1161,31 @@ template <int BITS>
 static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid, const ti_chain* chain) {
   const float* pre = a.epi.kind == TI_EPI_RESID_F32 ? (const float*)a.epi.out
                      : a.epi.kind == TI_EPI_QKV_ROPE_KV ? (const float*)a.epi.pos : (const float*)a.x;
-  const int kind_ldo = a.epi.kind | (a.epi.ldo << 3);
   const int xm = gemv_xmode(a.x_kind, a.M, a.K);
+  // packed preloaded arguments (see gemv_wq_kernel)
+  const float* aux = xm == XM_F16F ? a.epi.ss_in : xm == XM_F16 ? (a.epi.kind == TI_EPI_RESID_F32 && a.epi.fold_x ? a.epi.fold_w : nullptr)
+                     : a.norm_w;
+  const int mgk = a.M | (grid << 6) | (a.epi.kind << 18);
+  const int kx = a.K | ((xm == XM_F16F ? a.epi.n_ss : a.ldx) << 16);
+  const int ldo = a.epi.ldo;
   if (chain) {   // chained: x staged in registers only (checked by the caller)
     const bool ao = chain->any_order != 0;
     hipError_t err;
     if (xm == XM_F16)
       err = ti_launch_ext(gemv_wq_kernel<BITS, XM_F16, true>, dim3(grid), dim3(kGemvThreads), lds, s, ao, a.tiles, a.scales,
-                          a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a);
+                          a.x, aux, mgk, a.N, kx, ldo, pre, a);
     else
       err = ti_launch_ext(gemv_wq_kernel<BITS, XM_NORM1, true>, dim3(grid), dim3(kGemvThreads), lds, s, ao, a.tiles,
-                          a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a);
+                          a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a);
     TI_HIP_CHECK(err, "hipExtLaunchKernel(gemv_wq_kernel chained)");
     return TI_OK;
   }
   switch (xm) {
-    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a); break;
-    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a); break;
-    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a); break;
-    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, a.norm_w, a.M, a.N, a.K, a.ldx, grid, pre, kind_ldo, a); break;
+    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F16F: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16F>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
   }
   TI_LAUNCH_CHECK("gemv_wq_kernel");
   return TI_OK;
@@ -1256,7 +1320,8 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<4, XM_F16, true>, (const void*)gemv_wq_kernel<4, XM_NORM1, true>,
       (const void*)gemv_wq_kernel<8, XM_F16, true>, (const void*)gemv_wq_kernel<8, XM_NORM1, true>,
       (const void*)gemv_wq_kernel<16, XM_F16, true>, (const void*)gemv_wq_kernel<16, XM_NORM1, true>,
-      TI_MB_FNS};
+      (const void*)gemv_wq_kernel<4, XM_F16F>, (const void*)gemv_wq_kernel<8, XM_F16F>,
+      (const void*)gemv_wq_kernel<16, XM_F16F>, TI_MB_FNS};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
@@ -1320,8 +1385,15 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: M must be in [1,%d] (got %d)", TI_GEMM_MAX_ROWS, M);
   if (K <= 0 || (K & 127) || N <= 0 || (N & 15))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: K %% 128 and N %% 16 must be 0 (K=%d N=%d)", K, N);
-  if (x_kind < TI_X_F16 || x_kind > TI_X_F32_RMSNORM)
+  if (x_kind < TI_X_F16 || x_kind > TI_X_F16_FOLDED)
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: bad x_kind %d", x_kind);
+  if (x_kind == TI_X_F16_FOLDED && (M != 1 || chain || !epi->ss_in || epi->n_ss < 1 || epi->n_ss > 256))
+    return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: TI_X_F16_FOLDED needs M == 1, ss_in and 1 <= n_ss <= 256");
+  if (epi->kind == TI_EPI_RESID_F32 && epi->fold_x &&
+      (M != 1 || chain || !epi->fold_w || !epi->fold_ss || x_kind != TI_X_F16))
+    return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: fold_x needs M == 1, fp16 x, fold_w and fold_ss");
+  if (K > 0xffff || ldx > 0xffff)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: K %d / ldx %d above 65535", K, ldx);
   if (x_kind == TI_X_F32_RMSNORM && !norm_w) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: norm_w required");
   if (ldx < K) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: ldx %d < K %d", ldx, K);
   switch (epi->kind) {
@@ -1344,6 +1416,8 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
       return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: unknown epilogue %d", epi->kind);
   }
   const bool batched = use_batched(bits, x_kind, M, N, K);
+  if (batched && epi->kind == TI_EPI_RESID_F32 && epi->fold_x)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: fold_x needs the fused kernel");
   if (batched && !(bits == 4 && x_kind == TI_X_F16))
     return ti_set_error(TI_ERR_UNSUPPORTED,
                         "ti_gemm_wq_a16: M=%d K=%d exceeds the fused kernel (ti_gemm_max_rows); the batched-rows "
@@ -1359,6 +1433,8 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   }
   if (lds > 160 * 1024)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: LDS image %d B too large (M=%d N=%d K=%d)", lds, M, N, K);
+  if (!batched && grid > 0xfff)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: %d workgroups (N=%d) above 4095", grid, N);
   if (chain) {
     const int xm = gemv_xmode(x_kind, M, K);
     if (M != 1 || batched || (xm != XM_F16 && xm != XM_NORM1))
@@ -1389,6 +1465,11 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   if (bits == 4) return launch_gemv<4>(a, lds, s, grid, chain);
   if (bits == 8) return launch_gemv<8>(a, lds, s, grid, chain);
   return launch_gemv<16>(a, lds, s, grid, chain);
+}
+
+extern "C" int ti_gemm_grid(int M, int N, int K) {
+  if (M < 1 || M > 16 || N < 16 || K < 128 || (N & 15) || (K & 127) || !fused_fits(M, N, K)) return 0;
+  return ti::gemv_grid(M, N, K, query_cus());
 }
 
 extern "C" int ti_gemm_chainable(int bits, int x_kind, int M, int N, int K) {

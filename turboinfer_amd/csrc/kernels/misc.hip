@@ -62,9 +62,25 @@ __global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a, c
     }
   } else {
     const uint16_t* e = a.emb + (size_t)s_tok * a.hidden;
+    float ss = 0.0f;
     for (int i = tid; i < a.hidden; i += 256) {
-      if constexpr (CH) st_sc1_f32(h + i, h2f(e[i]));
-      else h[i] = h2f(e[i]);
+      const float v = h2f(e[i]);
+      if constexpr (CH) {
+        st_sc1_f32(h + i, v);
+      } else {
+        h[i] = v;
+        if (a.fold_x) {   // the first projection's TI_X_F16_FOLDED input (ti_hip.h)
+          a.fold_x[(size_t)m * a.hidden + i] = f2h(v * a.fold_w[i]);
+          ss = fmaf(v, v, ss);
+        }
+      }
+    }
+    if (!CH && a.fold_x) {
+      __shared__ float s_red[4];
+      ss = group_sum<64>(ss);
+      if ((tid & 63) == 0) s_red[tid >> 6] = ss;
+      __syncthreads();
+      if (tid == 0) a.fold_ss[m] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
     }
   }
   if constexpr (CH) chain_signal(chain, blockIdx.x);
@@ -180,6 +196,8 @@ extern "C" int ti_step_begin(const ti_step_args* a, ti_stream_t stream) {
     return ti_set_error(TI_ERR_ARG, "ti_step_begin: bad arguments");
   if (a->placeholder_first < 0 && !a->emb) return ti_set_error(TI_ERR_ARG, "ti_step_begin: emb required");
   if (a->n_in && !a->in_tokens) return ti_set_error(TI_ERR_ARG, "ti_step_begin: in_tokens required");
+  if (a->fold_x && (!a->fold_w || !a->fold_ss || a->placeholder_first >= 0))
+    return ti_set_error(TI_ERR_ARG, "ti_step_begin: fold_x needs fold_w, fold_ss and the embedding gather");
   hipLaunchKernelGGL(step_begin_kernel<false>, dim3(a->M), dim3(256), 0, (hipStream_t)stream, *a, ChainDev{});
   TI_LAUNCH_CHECK("step_begin_kernel");
   return TI_OK;
@@ -192,6 +210,7 @@ extern "C" int ti_step_begin_chained(const ti_step_args* a, ti_chain* chain, ti_
     return ti_set_error(TI_ERR_ARG, "ti_step_begin_chained: bad arguments");
   if (a->placeholder_first < 0 && !a->emb) return ti_set_error(TI_ERR_ARG, "ti_step_begin_chained: emb required");
   if (a->n_in && !a->in_tokens) return ti_set_error(TI_ERR_ARG, "ti_step_begin_chained: in_tokens required");
+  if (a->fold_x) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_step_begin_chained: fold_x");
   chain->signaled = (uint32_t)a->M;
   TI_HIP_CHECK(ti_launch_ext(step_begin_kernel<true>, dim3(a->M), dim3(256), 0, (hipStream_t)stream,
                              chain->any_order != 0, *a, chain_dev(chain)),
