@@ -84,11 +84,13 @@ int ti_engine_set_prefill(ti_engine* e, int rows);
  * of 1 stream will be chained. */
 int ti_engine_set_chain(ti_engine* e, int on, int* active);
 
-/* Folded rms_norm hand-off for single-stream steps (ti_hip.h TI_X_F16_FOLDED): the epilogue
- * that updates the residual also writes fp16(h * next norm weight) and per-workgroup sums of
- * h^2, and the next projection divides its outputs by the rms instead of normalising its
- * input first.  Default on (env TI_FOLD=0 turns it off); chained steps need it off.  on = 0/1
- * sets it, -1 leaves it; *active (nullable) receives whether 1-stream steps use it. */
+/* Fused hand-offs of single-stream steps: (1) the folded rms_norm (ti_hip.h TI_X_F16_FOLDED):
+ * the epilogue that updates the residual also writes fp16(h * next norm weight) and
+ * per-workgroup sums of h^2, and the next projection divides its outputs by the rms instead of
+ * normalising its input first; (2) the attention's split partials (ti_attn_decode_partials)
+ * merged by the O projection (TI_X_ATTN_SPLITS) when the step uses 2..8 splits.  Default on
+ * (env TI_FOLD=0 / TI_ATTN_PART=0 turn them off one by one); chained steps need both off.
+ * on = 0/1 sets both, -1 leaves them; *active (nullable) receives whether 1-stream steps fold. */
 int ti_engine_set_fold(ti_engine* e, int on, int* active);
 
 /* One decode step: token[s] at position pos[s] for each stream; logits [n][vocab] to host

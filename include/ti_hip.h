@@ -140,9 +140,13 @@ typedef struct ti_chain {
  * behind the GEMM, y = (W . x) / sqrt(sum(epi->ss_in[0 .. n_ss)) / K + eps): x holds
  * fp16(h * nw), written together with the partial sums of h^2 by the epilogue that produced h
  * (TI_EPI_RESID_F32 with fold_x, or ti_step_begin with fold_x), so the launch stages 2-byte
- * rows with no block-wide reduction in front of its first MFMA.  Epilogue (all outputs of one
- * call): */
-enum ti_x_kind { TI_X_F16 = 0, TI_X_F32 = 1, TI_X_F32_RMSNORM = 2, TI_X_F16_FOLDED = 3 };
+ * rows with no block-wide reduction in front of its first MFMA.
+ * TI_X_ATTN_SPLITS (M == 1, K = heads * head_dim <= 4096, norm_w NULL): x is the attention
+ * output still split, x = part_o of ti_attn_decode_partials with epi->ss_in = part_ml,
+ * epi->n_ss = splits (<= TI_ATTN_MAX_PART_SPLITS) and epi->head_dim; the launch merges the
+ * splits (max-rescaled, sum-weighted, as the attention's own merge) while staging x.
+ * Epilogue (all outputs of one call): */
+enum ti_x_kind { TI_X_F16 = 0, TI_X_F32 = 1, TI_X_F32_RMSNORM = 2, TI_X_F16_FOLDED = 3, TI_X_ATTN_SPLITS = 4 };
 enum ti_epilogue_kind {
   TI_EPI_STORE_F32 = 0,      /* out_f32[m*ldo + n] = y                                  */
   TI_EPI_STORE_F16 = 1,      /* out_f16[m*ldo + n] = fp16(y)                             */
@@ -237,6 +241,17 @@ int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_ca
                    int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
                    int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
                    ti_stream_t s);
+/* The same attention with the split merge left to the consumer: split s of (stream m, head h)
+ * writes its normalised row part_o[((m*heads + h)*splits + s)*head_dim + d] (fp16) and
+ * (max, sum) at part_ml[2*((m*heads + h)*splits + s)]; an empty split writes (-inf, 0) and a
+ * zero row.  The O projection merges them while staging its input (TI_X_ATTN_SPLITS), so the
+ * attention launch ends without the arrival-ticket hand-off.  2 <= splits <=
+ * TI_ATTN_MAX_PART_SPLITS; no workspace. */
+#define TI_ATTN_MAX_PART_SPLITS 8
+int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                            int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
+                            int kv_heads, int head_dim, int splits, uint16_t* part_o, float* part_ml,
+                            ti_stream_t s);
 /* One launch of a chain (ti_chain): the same attention; K/V, q and pos read with sc1 loads
  * after the wait, out stored write-through. */
 int ti_attn_decode_chained(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,

@@ -114,3 +114,53 @@ def test_engine_fold_matches_unfolded_steps(ti, name):
             toks.append(int(np.argmax(lu)))
     for e in eng.values():
         e.close()
+
+
+@pytest.mark.parametrize("heads,kv_heads,hd,L,splits", [(32, 32, 128, 2048, 8), (32, 32, 128, 5, 8),
+                                                         (16, 4, 64, 300, 4), (32, 8, 128, 777, 3)])
+def test_attention_partials_merged_by_o_projection(ti, oracle, heads, kv_heads, hd, L, splits):
+    """ti_attn_decode_partials + the O projection with TI_X_ATTN_SPLITS against ti_attn_decode
+    (merged in its own launch, fp16 out) + the O projection with TI_X_F16 on the same cache.
+    The staged activation differs by the fp16 rounding of each split's normalised row (one
+    fp16 ulp of the merged value) -- the rms_norm-prologue bound; L = 5 leaves splits empty."""
+    rng = np.random.RandomState(heads + L + splits)
+    max_seq, H = max(L, 64), 512
+    q = rng.standard_normal((1, heads * hd)).astype(f32)
+    kc = (rng.standard_normal((kv_heads, max_seq, hd)) * 0.5).astype(f16)
+    vc = rng.standard_normal((kv_heads, max_seq, hd)).astype(f16)
+    pos = np.array([L - 1], np.int32)
+    qd, kd, vd, pd = dev(ti, q), dev(ti, kc), dev(ti, vc), dev(ti, pos)
+    L_ = ti.lib()
+    po = ti.DeviceBuffer(heads * splits * hd * 2)
+    pml = ti.DeviceBuffer(heads * splits * 8)
+    ti.check(L_.ti_attn_decode_partials(qd.ptr, kd.ptr, vd.ptr, 0, max_seq, pd.ptr, 1, heads, kv_heads, hd, splits,
+                                        po.ptr, pml.ptr, None))
+    ws = ti.DeviceBuffer(L_.ti_attn_workspace_bytes(1, heads, hd, splits))
+    ws.zero()
+    out = ti.DeviceBuffer(heads * hd * 2)
+    ti.check(L_.ti_attn_decode(qd.ptr, kd.ptr, vd.ptr, 0, max_seq, pd.ptr, 1, heads, kv_heads, hd, splits, ws.ptr,
+                               out.ptr, None))
+    ti.sync()
+    ml = pml.download(f32, (heads, splits, 2))
+    chunk = -(-L // splits)
+    for s in range(splits):
+        if s * chunk >= L:   # empty split: (-inf, 0) and a zero row
+            assert np.all(np.isneginf(ml[:, s, 0])) and np.all(ml[:, s, 1] == 0)
+    K = heads * hd
+    w = (rng.standard_normal((K, H)) * 0.03).astype(f32)
+    t, sc = ti.wpack_host(w, 4)
+    td, sd = dev(ti, t), dev(ti, sc)
+    ya, yb = ti.DeviceBuffer(H * 4), ti.DeviceBuffer(H * 4)
+    ea = ti.Epilogue()
+    ea.kind, ea.ldo, ea.out, ea.ss_in, ea.n_ss, ea.head_dim = ti.EPI_STORE_F32, H, ya.ptr, pml.ptr, splits, hd
+    gemm(ti, td, sd, 4, po.ptr, ti.X_ATTN_SPLITS, K, 1, H, K, ea)
+    eb = ti.Epilogue()
+    eb.kind, eb.ldo, eb.out = ti.EPI_STORE_F32, H, yb.ptr
+    gemm(ti, td, sd, 4, out.ptr, ti.X_F16, K, 1, H, K, eb)
+    xa = out.download(f16, K).astype(np.float64)
+    q4, s4 = oracle.quantize_groups(w, 4)
+    wf = np.abs(oracle.dequantize_groups(q4, s4).astype(np.float64))
+    got, ref = ya.download(f32, H).astype(np.float64), yb.download(f32, H).astype(np.float64)
+    bound = 2.5e-3 * (np.abs(xa) @ wf) + 1e-6
+    err = np.abs(got - ref)
+    assert np.all(err <= bound), f"max err {err.max()} (bound {bound.min()})"

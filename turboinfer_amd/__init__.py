@@ -23,7 +23,8 @@ ROOT = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("TI_LIB") or os.path.join(HERE, "lib", "libturboinfer_amd.so")
 
 TI_OK = 0
-X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED = 0, 1, 2, 3
+X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED, X_ATTN_SPLITS = 0, 1, 2, 3, 4
+ATTN_MAX_PART_SPLITS = 8           # TI_ATTN_MAX_PART_SPLITS (include/ti_hip.h)
 EPI_STORE_F32, EPI_STORE_F16, EPI_RESID_F32, EPI_SILU_MUL_F16, EPI_QKV_ROPE_KV, EPI_LOGITS_ARGMAX = range(6)
 ARGMAX_SLOTS = 32
 GEMM_MAX_ROWS = 32                 # TI_GEMM_MAX_ROWS (include/ti_hip.h)   # TI_ARGMAX_SLOTS (include/ti_hip.h)
@@ -77,6 +78,7 @@ EXPORTED = [
     "ti_engine_replay_prepare", "ti_engine_set_prefill", "ti_engine_replay_run", "ti_engine_sync", "ti_engine_last_tokens",
     "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token", "ti_gemm_wq_a16_chained", "ti_gemm_chainable",
     "ti_attn_decode_chained", "ti_step_begin_chained", "ti_engine_set_chain", "ti_gemm_grid", "ti_engine_set_fold",
+    "ti_attn_decode_partials",
 ]
 
 _lib = None
@@ -120,6 +122,8 @@ def lib() -> C.CDLL:
         L.ti_attn_workspace_bytes.argtypes = [i32, i32, i32, i32]
         L.ti_attn_workspace_bytes.restype = sz
         L.ti_attn_decode.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
+        if hasattr(L, "ti_attn_decode_partials"):
+            L.ti_attn_decode_partials.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
         L.ti_step_begin.argtypes = [C.POINTER(StepArgs), vp]
         L.ti_matmul_f32.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, vp]
         L.ti_rms_norm_f32.argtypes = [vp, vp, vp, i32, i32, f32, vp]

@@ -94,6 +94,11 @@ struct ti_engine {
   bool fold_on = true;         // TI_FOLD=0 / ti_engine_set_fold
   uint16_t* fx = nullptr;      // [hidden]
   float* ss = nullptr;         // [256]
+  // single-stream attention leaves its split merge to the O projection (ti_attn_decode_partials
+  // + TI_X_ATTN_SPLITS): no arrival-ticket hand-off at the end of the attention launch
+  bool part_on = true;         // TI_ATTN_PART=0 turns it off
+  uint16_t* part_o = nullptr;  // [heads][TI_ATTN_MAX_PART_SPLITS][head_dim]
+  float* part_ml = nullptr;    // [heads][TI_ATTN_MAX_PART_SPLITS][2]
   // prefill (forward_pass over prompt tokens): up to pf_rows prompt tokens of one stream run
   // as rows of the batched path, sharing that stream's KV cache (stride 0)
   int pf_rows = 0;             // 0 = off (prompts consumed one token per decode step)
@@ -228,7 +233,8 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
 // ------------------------------------------------------------- chained steps
 bool chain_usable(ti_engine* e, int M) {
   const ti_engine_config& c = e->c;
-  if (!e->chain_on || M != 1 || c.compat || !e->chain_ctr || e->fold_on) return false;   // chained kernels: no fold
+  // chained kernels have neither the folded rms_norm nor the split partials hand-off
+  if (!e->chain_on || M != 1 || c.compat || !e->chain_ctr || e->fold_on || e->part_on) return false;
   if (e->chain_ok < 0) {
     const int H = c.hidden, I = c.inter, qd = e->qd(), kvd = e->kvd();
     const int b = c.bits;
@@ -381,6 +387,14 @@ bool fold_usable(ti_engine* e, int M) {
   return g_o > 0 && g_o <= 256 && g_d > 0 && g_d <= 256 && ti_gemm_max_rows(c.bits, TI_X_F16, H, qd) >= 1;
 }
 
+// Split partials merged by the O projection: one stream, 2..8 splits, heads*head_dim <= 4096.
+bool part_usable(ti_engine* e, int M) {
+  const ti_engine_config& c = e->c;
+  const int sp = e->splits_for(M);
+  return e->part_on && e->part_o && M == 1 && !c.compat && sp >= 2 && sp <= TI_ATTN_MAX_PART_SPLITS &&
+         e->qd() <= 4096;
+}
+
 // One decode step for streams [0, M) on e->s.  Graph-capturable (no host sync / alloc).
 int enqueue_step(ti_engine* e, int M, int advance) {
   const ti_engine_config& c = e->c;
@@ -402,7 +416,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   sa.step_ctr = e->step_ctr;
   const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
   // fold (M == 1): every rms_norm input is handed over as fx + ss partials by its producer
-  const bool fold = fold_usable(e, M);
+  const bool fold = fold_usable(e, M), part = part_usable(e, M);
   auto next_norm = [&](int l) -> const float* { return l < c.layers ? e->layer[l].attn_norm : e->out_norm; };
   if (fold) {
     sa.fold_w = next_norm(0);
@@ -452,15 +466,23 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     ep.kv_stream_stride = e->kv_stride;
     TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));
 
-    TI_TRY(ti_attn_decode(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M, c.heads, c.kv_heads, c.head_dim,
-                          e->splits_for(M), e->ws, e->attn, e->s));
-
     ti_epilogue eo{};
     eo.kind = TI_EPI_RESID_F32;
     eo.ldo = H;
     eo.out = e->h;
     fold_into(eo, L.ffn_norm);
-    TI_TRY(gemm(L.o, e->attn, TI_X_F16, qd, 2, nullptr, eo, 4, false));
+    if (part) {   // the O projection merges the attention's splits while staging its input
+      TI_TRY(ti_attn_decode_partials(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M, c.heads, c.kv_heads,
+                                     c.head_dim, e->splits_for(M), e->part_o, e->part_ml, e->s));
+      eo.ss_in = e->part_ml;
+      eo.n_ss = e->splits_for(M);
+      eo.head_dim = c.head_dim;
+      TI_TRY(gemm(L.o, e->part_o, TI_X_ATTN_SPLITS, qd, 2, nullptr, eo, 4, false));
+    } else {
+      TI_TRY(ti_attn_decode(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M, c.heads, c.kv_heads, c.head_dim,
+                            e->splits_for(M), e->ws, e->attn, e->s));
+      TI_TRY(gemm(L.o, e->attn, TI_X_F16, qd, 2, nullptr, eo, 4, false));
+    }
 
     ti_epilogue eg{};
     eg.kind = TI_EPI_SILU_MUL_F16;
@@ -663,8 +685,11 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
         (rc = e->alloc(reinterpret_cast<void**>(&e->ws), ti_attn_workspace_bytes(R, c.heads, hd, e->splits_max))) ||
         (rc = e->alloc_t(&e->pf_ones, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->pf_zero, (size_t)1)) ||
         (rc = e->alloc_t(&e->pf_base, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->fx, (size_t)H)) ||
-        (rc = e->alloc_t(&e->ss, (size_t)256)))
+        (rc = e->alloc_t(&e->ss, (size_t)256)) ||
+        (rc = e->alloc_t(&e->part_o, (size_t)c.heads * TI_ATTN_MAX_PART_SPLITS * hd)) ||
+        (rc = e->alloc_t(&e->part_ml, (size_t)c.heads * TI_ATTN_MAX_PART_SPLITS * 2)))
       return fail(rc);
+    if (const char* env = getenv("TI_ATTN_PART")) e->part_on = atoi(env) != 0;
     if (const char* env = getenv("TI_FOLD")) e->fold_on = atoi(env) != 0;
     e->chain_slots = 2 + 5 * c.layers;
     e->chain_cum.assign((size_t)e->chain_slots, 0u);
@@ -955,11 +980,11 @@ int ti_engine_set_chain(ti_engine* e, int on, int* active) {
 
 int ti_engine_set_fold(ti_engine* e, int on, int* active) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_fold: null");
-  if (on >= 0 && (on != 0) != e->fold_on) {
+  if (on >= 0 && ((on != 0) != e->fold_on || (on != 0) != e->part_on)) {
     TI_TRY(ti_stream_sync(e->s));   // captured step graphs bake the setting in
     for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
     e->graphs.clear();
-    e->fold_on = on != 0;
+    e->fold_on = e->part_on = on != 0;
   }
   if (active) *active = fold_usable(e, 1) ? 1 : 0;
   return TI_OK;
@@ -978,7 +1003,7 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
     return ti_set_error(TI_ERR_ARG, "ti_engine_time_kernel: bad arguments");
   const ti_engine_config& c = e->c;
   const int H = c.hidden, I = c.inter, qd = e->qd(), kvd = e->kvd();
-  const bool fold = fold_usable(e, n);
+  const bool fold = fold_usable(e, n), part = part_usable(e, n);
   // Launch r uses layer r % layers, so (as in a real step) its weights are not still in
   // the 256 MB Infinity Cache from the previous launch.
   int cur = 0;
@@ -1009,6 +1034,13 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
         ep.fold_x = e->fx;
         ep.fold_ss = e->ss;
       }
+      if (which == 1 && part) {   // O merges the attention's split partials
+        x = e->part_o;
+        xk = TI_X_ATTN_SPLITS;
+        ep.ss_in = e->part_ml;
+        ep.n_ss = e->splits_for(n);
+        ep.head_dim = c.head_dim;
+      }
     }
     if (fold && xk == TI_X_F32_RMSNORM) {   // the step's consumer form (enqueue_step)
       x = e->fx;
@@ -1035,6 +1067,9 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
     cur = (cur + 1) % c.layers;
     TI_TRY(setup(L, W, x, xk, ldx, nw, ep));
     // (the one lm_head, 68 MB at 7B, fits the Infinity Cache: back-to-back it runs warm)
+    if (which == 5 && part)
+      return ti_attn_decode_partials(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, n, c.heads, c.kv_heads,
+                                     c.head_dim, e->splits_for(n), e->part_o, e->part_ml, e->s);
     if (which == 5)
       return ti_attn_decode(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, n, c.heads, c.kv_heads, c.head_dim,
                             e->splits_for(n), e->ws, e->attn, e->s);
@@ -1059,6 +1094,7 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
   } else {
     const double wbytes = (double)ti_wpack_tile_bytes(c.bits, W->K, W->N) + (double)ti_wpack_scale_bytes(c.bits, W->K, W->N);
     *bytes = wbytes + (double)n * W->K * (xk == TI_X_F16 || xk == TI_X_F16_FOLDED ? 2 : 4);
+    if (xk == TI_X_ATTN_SPLITS) *bytes = wbytes + (double)n * W->K * 2;   // the merged row, as the unsplit input
   }
   return TI_OK;
 }

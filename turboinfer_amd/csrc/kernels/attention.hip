@@ -40,6 +40,10 @@ struct AttnArgs {
   int32_t max_seq, M, heads, kv_heads, splits;
   float scale;
   ChainDev chain;   // chained launches only (CH)
+  // partials mode (ti_attn_decode_partials): every split writes its normalised row and
+  // (max, sum) and the merge is left to the consumer (the O projection's x staging)
+  uint16_t* part_o;   // [M][heads][splits][HD] fp16, nullptr = merge in this launch
+  float* part_ml;     // [M][heads][splits][2]
 };
 
 #ifndef TI_ATTN_RING
@@ -376,6 +380,12 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
       store_out((size_t)m * a.heads * HD + (size_t)h * HD + d, l > 0.0f ? o / l : 0.0f);
       continue;
     }
+    if (!CH && a.part_o) {   // partials mode: this split's normalised row and (max, sum)
+      const size_t r = ((size_t)m * a.heads + h) * a.splits + split;
+      a.part_o[r * HD + d] = f2h(l > 0.0f ? o / l : 0.0f);
+      if (d == 0) *(float2*)(a.part_ml + 2 * r) = make_float2(mx, l);
+      continue;
+    }
     s_part[g * row + d] = o;   // this split's row [o | max, sum, 0, 0]
     if (d == 0) {
       s_part[g * row + HD] = mx;
@@ -384,7 +394,7 @@ __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnA
       s_part[g * row + HD + 3] = 0.0f;
     }
   }
-  if (a.splits == 1) {
+  if (a.splits == 1 || (!CH && a.part_o)) {
     if constexpr (CH) chain_signal(a.chain, flat_block);
     return;
   }
@@ -492,9 +502,10 @@ extern "C" size_t ti_attn_workspace_bytes(int M, int heads, int head_dim, int sp
 
 static int attn_impl(const float* q, const uint16_t* k_cache, const uint16_t* v_cache, int64_t kv_stream_stride,
                      int max_seq, const int32_t* pos, int M, int heads, int kv_heads, int head_dim, int splits,
-                     float* workspace, uint16_t* out, ti_chain* chain, ti_stream_t stream) {
+                     float* workspace, uint16_t* out, ti_chain* chain, ti_stream_t stream,
+                     uint16_t* part_o = nullptr, float* part_ml = nullptr) {
   using namespace ti;
-  if (!q || !k_cache || !v_cache || !pos || !workspace || !out)
+  if (!q || !k_cache || !v_cache || !pos || ((!workspace || !out) && !part_o))
     return ti_set_error(TI_ERR_ARG, "ti_attn_decode: null pointer");
   if (M < 1 || M > TI_ATTN_MAX_M || heads < 1 || kv_heads < 1 || heads % kv_heads || splits < 1 || max_seq < 1)
     return ti_set_error(TI_ERR_ARG, "ti_attn_decode: bad sizes M=%d heads=%d kv_heads=%d splits=%d", M, heads,
@@ -508,14 +519,16 @@ static int attn_impl(const float* q, const uint16_t* k_cache, const uint16_t* v_
   const int G = heads / kv_heads;
   // splits only shape the work (results agree to rounding); the merge stages all partials
   // of a kv-head group in LDS, which bounds them.
-  splits = std::min(splits, std::max(1, ti::attn_max_splits(G, head_dim)));
+  if (!part_o) splits = std::min(splits, std::max(1, ti::attn_max_splits(G, head_dim)));
   AttnArgs a;
+  a.part_o = part_o;
+  a.part_ml = part_ml;
   a.q = q;
   a.kc = k_cache;
   a.vc = v_cache;
   a.pos = pos;
   a.counters = (int32_t*)workspace;
-  a.ws = (float*)((char*)workspace + ticket_bytes(heads));
+  a.ws = workspace ? (float*)((char*)workspace + ticket_bytes(heads)) : nullptr;
   a.out = out;
   a.stride = kv_stream_stride;
   a.max_seq = max_seq;
@@ -551,4 +564,15 @@ extern "C" int ti_attn_decode_chained(const float* q, const uint16_t* k_cache, c
   if (!chain) return ti_set_error(TI_ERR_ARG, "ti_attn_decode_chained: null chain");
   return attn_impl(q, k_cache, v_cache, kv_stream_stride, max_seq, pos, M, heads, kv_heads, head_dim, splits, workspace,
                    out, chain, stream);
+}
+
+extern "C" int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                                       int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
+                                       int kv_heads, int head_dim, int splits, uint16_t* part_o, float* part_ml,
+                                       ti_stream_t stream) {
+  if (!part_o || !part_ml) return ti_set_error(TI_ERR_ARG, "ti_attn_decode_partials: null partials");
+  if (splits < 2 || splits > TI_ATTN_MAX_PART_SPLITS)
+    return ti_set_error(TI_ERR_ARG, "ti_attn_decode_partials: splits %d not in [2, %d]", splits, TI_ATTN_MAX_PART_SPLITS);
+  return attn_impl(q, k_cache, v_cache, kv_stream_stride, max_seq, pos, M, heads, kv_heads, head_dim, splits, nullptr,
+                   nullptr, nullptr, stream, part_o, part_ml);
 }

@@ -176,7 +176,8 @@ __device__ __forceinline__ f16x8 dequant_step(const u32x4 (&w)[BITS / 4], int s4
 // rms_norm of ONE row of K <= 4096 held in registers; rms_norm of several / longer rows.
 // XM_F16F: fp16 rows of h * nw (TI_X_F16_FOLDED, one row) staged like XM_F16; the rms comes
 // from the producer's partial sums of squares and divides the outputs before the epilogue.
-enum { XM_F16 = 0, XM_F32 = 1, XM_NORM1 = 2, XM_NORM = 3, XM_F16F = 4 };
+// XM_ATTN: the attention's split partials (TI_X_ATTN_SPLITS, one row), merged while staging.
+enum { XM_F16 = 0, XM_F32 = 1, XM_NORM1 = 2, XM_NORM = 3, XM_F16F = 4, XM_ATTN = 5 };
 
 // Generic staging (M > 1 with rms_norm, f32 rows, or rows longer than the register
 // prefetch covers).  Runs after the ring is issued, so its loads wait behind the ring.
@@ -373,9 +374,10 @@ __device__ __forceinline__ void lds_barrier() {
 // loads do not wait for a kernarg s_load round trip (the grid size is passed too: gridDim
 // comes from the hidden kernargs).  Everything read before the weight ring is issued sits in
 // the 14 dwords the hardware preloads (s[2:15]; packed below); the struct carries the rest.
-//   p_aux: the rms_norm weight (XM_NORM*), the producer's ss partials (XM_F16F) or, for a
-//          TI_EPI_RESID_F32 fold producer with fp16 x, the fold weight (else NULL)
-//   p_mgk: M | grid << 6 | epilogue kind << 18       p_kx: K | (ldx, or n_ss for XM_F16F) << 16
+//   p_aux: the rms_norm weight (XM_NORM*), the producer's ss partials (XM_F16F), the splits'
+//          (max, sum) pairs (XM_ATTN), else NULL
+//   p_mgk: M | grid << 6 | epilogue kind << 18 | head_dim / 64 << 21 (XM_ATTN)
+//   p_kx:  K | (ldx, or n_ss for XM_F16F, or splits for XM_ATTN) << 16
 template <int BITS, int XM, bool CH = false>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
                                                                    const void* p_x, const float* p_aux, int p_mgk,
@@ -389,7 +391,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   a.M = p_mgk & 63;
   a.N = p_N;
   a.K = p_kx & 0xffff;
-  a.ldx = XM == XM_F16F ? a.K : (int)((unsigned)p_kx >> 16);
+  a.ldx = XM == XM_F16F || XM == XM_ATTN ? a.K : (int)((unsigned)p_kx >> 16);
   const int p_grid = (p_mgk >> 6) & 0xfff;
   constexpr int C = TileFmt<BITS>::kChunks;
   constexpr int R = TI_GEMV_RING_VGPRS / (4 * C) > 2 ? TI_GEMV_RING_VGPRS / (4 * C) : 2;   // ring depth (items)
@@ -433,8 +435,21 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   u32x4 xr16[XPF];
   // x rows and the epilogue input depend on the previous launch: loaded here, or -- chained
   // (CH) -- after the in-kernel wait, with sc1 loads (load_x below).
+  // XM_ATTN: this thread's 8 dims (one head) of every split, and the splits' (max, sum)
+  constexpr int kPS = TI_ATTN_MAX_PART_SPLITS;
+  u32x4 po[XM == XM_ATTN ? kPS : 1];
+  float2 pml[XM == XM_ATTN ? kPS : 1];
   auto load_x = [&]() {
-    if constexpr (XM == XM_NORM1) {
+    if constexpr (XM == XM_ATTN) {
+      const int S = (int)((unsigned)p_kx >> 16), hsh = ((p_mgk >> 21) & 3) == 2 ? 7 : 6;
+      const int i = tid < K8 ? tid : K8 - 1, h = (8 * i) >> hsh, d = (8 * i) & ((1 << hsh) - 1);
+#pragma unroll
+      for (int sp = 0; sp < kPS; ++sp) {
+        const int r = h * S + (sp < S ? sp : S - 1);
+        po[sp] = *(const u32x4*)((const f16*)a.x + ((size_t)r << hsh) + d);
+        pml[sp] = *(const float2*)(p_aux + 2 * r);
+      }
+    } else if constexpr (XM == XM_NORM1) {
       const int k8 = tid < K8 ? tid : K8 - 1;
       if constexpr (CH) {
         const __amdgpu_buffer_rsrc_t rx = sc1_rsrc(a.x);
@@ -480,9 +495,9 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   float pre = 0.0f;
   if constexpr (!CH) pre = *pre_p;
   // RESID with fold_x: the fold weight of the same output (one row), consumed by the epilogue
-  const bool fold = !CH && XM == XM_F16 && kind == TI_EPI_RESID_F32 && p_aux != nullptr;
-  const float* fw_p = fold ? p_aux + (size_t)t0 * 16 + (tid < n_res ? tid : 0) : pre_p;
-  const float fw_pre = *fw_p;   // unconditional (no branch join in front of the ring)
+  // (its pointer comes from the kernarg struct: loaded after the ring is issued, below)
+  const bool fold = !CH && (XM == XM_F16 || XM == XM_ATTN) && kind == TI_EPI_RESID_F32 && a.epi.fold_x != nullptr;
+  float fw_pre = 0.0f;
   // XM_F16F: this lane's share of the producer's partial sums of squares (up to 256 of them),
   // clamped loads; masked and summed after the stream
   float ss4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -522,6 +537,10 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
 #pragma unroll
     for (int c = 0; c < C; ++c) ring[s][c] = ld_w(tb + o + c * kWave);
   }
+  if constexpr (!CH && (XM == XM_F16 || XM == XM_ATTN)) {   // fold weight (consumed by the epilogue)
+    const float* fw_p = fold ? a.epi.fold_w + (size_t)t0 * 16 + (tid < n_res ? tid : 0) : pre_p;
+    fw_pre = *fw_p;
+  }
   if constexpr (CH) {
     chain_wait(a.chain);
     load_x();
@@ -555,6 +574,28 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       h[6] = (f16)((v1.z / rms) * w1.z); h[7] = (f16)((v1.w / rms) * w1.w);
       *(f16x8*)(xl + 8 * tid) = h;
     }
+  } else if constexpr (XM == XM_ATTN) {
+    // the attention's split merge (attention.hip last-arriver merge): weights
+    // l_s * exp(m_s - max), normalised rows o_s, empty splits (m = -inf) weigh 0
+    const int S = (int)((unsigned)p_kx >> 16);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int sp = 0; sp < kPS; ++sp) mx = sp < S ? fmaxf(mx, pml[sp].x) : mx;
+    float num[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, den = 0.0f;
+#pragma unroll
+    for (int sp = 0; sp < kPS; ++sp) {
+      const float f = sp < S && pml[sp].x != -INFINITY ? pml[sp].y * __expf(pml[sp].x - mx) : 0.0f;
+      den += f;
+      const f16x8 o = __builtin_bit_cast(f16x8, po[sp]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) num[e] = fmaf(f, (float)o[e], num[e]);
+    }
+    if (tid < K8) {
+      f16x8 hx;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) hx[e] = (f16)(den > 0.0f ? num[e] / den : 0.0f);
+      *(f16x8*)(xl + 8 * tid) = hx;
+    }
   } else if constexpr (XM == XM_F16 || XM == XM_F16F) {
 #pragma unroll
     for (int q = 0; q < XPF; ++q) {
@@ -571,7 +612,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   }
   if constexpr (XM == XM_F16 || XM == XM_F16F) {
     if (nx16 > XPF * kGemvThreads) stage_x_generic<XM, CH>(a, xl, red, XPF * kGemvThreads);
-  } else if constexpr (XM != XM_NORM1) {
+  } else if constexpr (XM != XM_NORM1 && XM != XM_ATTN) {
     static_assert(!CH, "chained launches stage x in registers (XM_F16 / XM_NORM1)");
     stage_x_generic<XM>(a, xl, red, 0);
   }
@@ -709,7 +750,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
     const float* pp = p_pre + (size_t)m * ldo + (t0 + tl) * 16 + n;
     if constexpr (CH) es[i] = ld_sc1_f32(pp);
     else es[i] = *pp;
-    if (fold) es[n_res + i] = p_aux[(size_t)t0 * 16 + i];
+    if (fold) es[n_res + i] = a.epi.fold_w[(size_t)t0 * 16 + i];
   }
   // XM_F16F: rms of the row from the producer's partials, the same fixed-order sum in every
   // wave (rms_norm, tensor_engine.cpp:1488-1505, with the division moved behind the GEMM)
@@ -1153,6 +1194,7 @@ static int g_num_cus = 0;
 __host__ inline int gemv_xmode(int x_kind, int M, int K) {
   if (x_kind == TI_X_F16) return XM_F16;
   if (x_kind == TI_X_F16_FOLDED) return XM_F16F;
+  if (x_kind == TI_X_ATTN_SPLITS) return XM_ATTN;
   if (x_kind == TI_X_F32) return XM_F32;
   return M == 1 && (K >> 3) <= kGemvThreads ? XM_NORM1 : XM_NORM;
 }
@@ -1163,10 +1205,9 @@ static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid, cons
                      : a.epi.kind == TI_EPI_QKV_ROPE_KV ? (const float*)a.epi.pos : (const float*)a.x;
   const int xm = gemv_xmode(a.x_kind, a.M, a.K);
   // packed preloaded arguments (see gemv_wq_kernel)
-  const float* aux = xm == XM_F16F ? a.epi.ss_in : xm == XM_F16 ? (a.epi.kind == TI_EPI_RESID_F32 && a.epi.fold_x ? a.epi.fold_w : nullptr)
-                     : a.norm_w;
-  const int mgk = a.M | (grid << 6) | (a.epi.kind << 18);
-  const int kx = a.K | ((xm == XM_F16F ? a.epi.n_ss : a.ldx) << 16);
+  const float* aux = xm == XM_F16F || xm == XM_ATTN ? a.epi.ss_in : xm == XM_F16 ? nullptr : a.norm_w;
+  const int mgk = a.M | (grid << 6) | (a.epi.kind << 18) | (xm == XM_ATTN ? (a.epi.head_dim / 64) << 21 : 0);
+  const int kx = a.K | ((xm == XM_F16F || xm == XM_ATTN ? a.epi.n_ss : a.ldx) << 16);
   const int ldo = a.epi.ldo;
   if (chain) {   // chained: x staged in registers only (checked by the caller)
     const bool ao = chain->any_order != 0;
@@ -1183,6 +1224,7 @@ static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid, cons
   switch (xm) {
     case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
     case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_ATTN: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_ATTN>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
     case XM_F16F: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16F>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
     case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
     default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
@@ -1321,7 +1363,8 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<8, XM_F16, true>, (const void*)gemv_wq_kernel<8, XM_NORM1, true>,
       (const void*)gemv_wq_kernel<16, XM_F16, true>, (const void*)gemv_wq_kernel<16, XM_NORM1, true>,
       (const void*)gemv_wq_kernel<4, XM_F16F>, (const void*)gemv_wq_kernel<8, XM_F16F>,
-      (const void*)gemv_wq_kernel<16, XM_F16F>, TI_MB_FNS};
+      (const void*)gemv_wq_kernel<16, XM_F16F>, (const void*)gemv_wq_kernel<4, XM_ATTN>,
+      (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
@@ -1385,12 +1428,17 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: M must be in [1,%d] (got %d)", TI_GEMM_MAX_ROWS, M);
   if (K <= 0 || (K & 127) || N <= 0 || (N & 15))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: K %% 128 and N %% 16 must be 0 (K=%d N=%d)", K, N);
-  if (x_kind < TI_X_F16 || x_kind > TI_X_F16_FOLDED)
+  if (x_kind < TI_X_F16 || x_kind > TI_X_ATTN_SPLITS)
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: bad x_kind %d", x_kind);
+  if (x_kind == TI_X_ATTN_SPLITS &&
+      (M != 1 || chain || !epi->ss_in || epi->n_ss < 1 || epi->n_ss > TI_ATTN_MAX_PART_SPLITS ||
+       (epi->head_dim != 64 && epi->head_dim != 128) || K % epi->head_dim || K > 4096))
+    return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: TI_X_ATTN_SPLITS needs M == 1, ss_in, 1 <= n_ss <= %d, head_dim "
+                        "64/128 and K <= 4096", TI_ATTN_MAX_PART_SPLITS);
   if (x_kind == TI_X_F16_FOLDED && (M != 1 || chain || !epi->ss_in || epi->n_ss < 1 || epi->n_ss > 256))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: TI_X_F16_FOLDED needs M == 1, ss_in and 1 <= n_ss <= 256");
   if (epi->kind == TI_EPI_RESID_F32 && epi->fold_x &&
-      (M != 1 || chain || !epi->fold_w || !epi->fold_ss || x_kind != TI_X_F16))
+      (M != 1 || chain || !epi->fold_w || !epi->fold_ss || (x_kind != TI_X_F16 && x_kind != TI_X_ATTN_SPLITS)))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: fold_x needs M == 1, fp16 x, fold_w and fold_ss");
   if (K > 0xffff || ldx > 0xffff)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: K %d / ldx %d above 65535", K, ldx);
