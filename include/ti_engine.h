@@ -69,6 +69,17 @@ int ti_engine_generate(ti_engine* e, int n_streams, const int32_t* prompts, cons
                        int prompt_stride, const int32_t* start_pos, int max_new, int32_t* out_tokens,
                        float* last_logits);
 
+/* ti_engine_generate with the reference sampler on the device: after each
+ * step's lm_head, ti_sample_step applies sample_next_token (inference_engine.cpp:1554-1673:
+ * temperature, top-k, softmax, top-p, the draw) and feeds the token back, so the loop never
+ * returns to the host.  draws [n][max_new]: the uniform draw of each stream's t-th new token
+ * (the reference takes them from its engine's mt19937, uniform_real_distribution<float>);
+ * 1 <= top_k <= min(vocab, TI_SAMPLE_MAX_K).  out_logprobs (nullable) [n][max_new] = log p of
+ * each sampled token. */
+int ti_engine_generate_sampled(ti_engine* e, int n_streams, const int32_t* prompts, const int32_t* prompt_lens,
+                               int prompt_stride, const int32_t* start_pos, int max_new, float temperature,
+                               int top_k, float top_p, const float* draws, int32_t* out_tokens, float* out_logprobs);
+
 /* Prefill of ti_engine_generate's prompts (reference forward_pass, inference_engine.cpp:
  * 1429-1491): all but the last token of the shortest prompt are processed `rows` tokens at a
  * time as rows of the batched GEMMs and causal attention over the stream's own KV cache,

@@ -288,6 +288,26 @@ int ti_step_begin(const ti_step_args* a, ti_stream_t s);
  * step counter), stores h / pos / tokens write-through. */
 int ti_step_begin_chained(const ti_step_args* a, ti_chain* chain, ti_stream_t s);
 
+/* ------------------------------------------------------- on-device sampling
+ * InferenceEngine::sample_next_token (inference_engine.cpp:1554-1673) per stream, the uniform
+ * draw supplied (the reference draws it from the engine's mt19937): temperature, top-k
+ * (1 <= top_k <= min(V, TI_SAMPLE_MAX_K)), softmax, top-p, the draw.  Sums run over the
+ * survivors in index order (the reference's loops over V add exact zeros elsewhere); exp/log
+ * are the device's, equal logits at the k-th place and equal probabilities at the top-p cut
+ * go lowest index first.  One 1024-thread workgroup per stream. */
+#define TI_SAMPLE_MAX_K 1024
+/* logits [M][ldl] fp32, draws [M] -> tokens [M], logprobs [M] (nullable) = log p(token). */
+int ti_sample_device(const float* logits, int ldl, int M, int V, float temperature, int top_k, float top_p,
+                     const float* draws, int32_t* tokens, float* logprobs, ti_stream_t s);
+/* The decode loop's form (graph-capturable, after the lm_head): stream m's token of step
+ * s = *step_ctr - advance is its t-th new token, t = s - (n_in[m] - 1); prompt steps (t < 0)
+ * and t >= draw_stride do nothing.  The draw is draws[m*draw_stride + t], log p goes to
+ * logprobs[m*draw_stride + t] (nullable), and argmax[m*TI_ARGMAX_SLOTS] receives a key above
+ * every logit key, so ti_step_begin feeds the sampled token back. */
+int ti_sample_step(const float* logits, int ldl, int M, int V, float temperature, int top_k, float top_p,
+                   const float* draws, int draw_stride, const int32_t* step_ctr, int advance, const int32_t* n_in,
+                   unsigned long long* argmax, float* logprobs, ti_stream_t s);
+
 /* -------------------------------------------------------------- fp32 op level */
 /* y[r][n] (+)= sum_k a[r][k]*b[k][n], b the reference [K][N] fp32 layout, one fmaf per k
  * in ascending order (bit-identical to matmul_3d_2d).  mode: 0 store, 1 relu(store),

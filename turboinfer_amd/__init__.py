@@ -78,7 +78,7 @@ EXPORTED = [
     "ti_engine_replay_prepare", "ti_engine_set_prefill", "ti_engine_replay_run", "ti_engine_sync", "ti_engine_last_tokens",
     "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token", "ti_gemm_wq_a16_chained", "ti_gemm_chainable",
     "ti_attn_decode_chained", "ti_step_begin_chained", "ti_engine_set_chain", "ti_gemm_grid", "ti_engine_set_fold",
-    "ti_attn_decode_partials",
+    "ti_attn_decode_partials", "ti_sample_device", "ti_sample_step", "ti_engine_generate_sampled",
 ]
 
 _lib = None
@@ -122,6 +122,9 @@ def lib() -> C.CDLL:
         L.ti_attn_workspace_bytes.argtypes = [i32, i32, i32, i32]
         L.ti_attn_workspace_bytes.restype = sz
         L.ti_attn_decode.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
+        if hasattr(L, "ti_sample_device"):
+            L.ti_sample_device.argtypes = [vp, i32, i32, i32, f32, i32, f32, vp, vp, vp, vp]
+            L.ti_engine_generate_sampled.argtypes = [vp, i32, vp, vp, i32, vp, i32, f32, i32, f32, vp, vp, vp]
         if hasattr(L, "ti_attn_decode_partials"):
             L.ti_attn_decode_partials.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
         L.ti_step_begin.argtypes = [C.POINTER(StepArgs), vp]
@@ -306,6 +309,22 @@ class Engine:
         check(lib().ti_engine_generate(self.h, n, _ptr(P), _ptr(lens), stride, None if sp is None else _ptr(sp),
                                        max_new, _ptr(out), None if logits is None else _ptr(logits)))
         return (out, logits) if want_logits else out
+
+    def generate_sampled(self, prompts, max_new, temperature, top_k, top_p, draws, start_pos=None):
+        """ti_engine_generate_sampled: tokens [n][max_new] and log-probs [n][max_new]."""
+        n = len(prompts)
+        stride = max(len(p) for p in prompts)
+        P = np.zeros((n, stride), np.int32)
+        for i, p in enumerate(prompts):
+            P[i, : len(p)] = p
+        lens = np.array([len(p) for p in prompts], np.int32)
+        d = np.ascontiguousarray(draws, np.float32).reshape(n, max_new)
+        out = np.zeros((n, max_new), np.int32)
+        lp = np.zeros((n, max_new), np.float32)
+        sp = None if start_pos is None else np.ascontiguousarray(start_pos, np.int32)
+        check(lib().ti_engine_generate_sampled(self.h, n, _ptr(P), _ptr(lens), stride, None if sp is None else _ptr(sp),
+                                               max_new, temperature, top_k, top_p, _ptr(d), _ptr(out), _ptr(lp)))
+        return out, lp
 
     def set_prefill(self, rows):
         """Prompt tokens per prefill chunk (0 = consume prompts one token per decode step)."""

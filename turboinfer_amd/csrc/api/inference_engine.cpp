@@ -352,6 +352,31 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
         const size_t b = budget(batches[c0 + m].size());
         for (size_t t = 0; t < std::min(b, steps_new); ++t) fresh[m].push_back(out[(size_t)m * steps_new + t]);
       }
+    } else if (n == 1 && config_.top_k >= 1 && config_.top_k <= (size_t)std::min(V, TI_SAMPLE_MAX_K)) {
+      // one request, top-k in the device sampler's range: the whole loop on the device
+      // (ti_engine_generate_sampled), fed the engine's mt19937 draws in the reference's order;
+      // the generator then advances by the draws the request actually used (one per token)
+      const auto& p = batches[c0];
+      const size_t steps_new = std::min(want, (size_t)im.cfg.max_seq + 1 - p.size());
+      std::mt19937 saved = im.rng;
+      std::uniform_real_distribution<float> dist(0.0f, 1.0f);
+      std::vector<float> draws(steps_new), lp(steps_new);
+      for (float& d : draws) d = dist(im.rng);
+      std::vector<int32_t> prompt(p.begin(), p.end()), out(steps_new);
+      const int32_t len = (int32_t)p.size();
+      check(ti_engine_generate_sampled(im.eng, 1, prompt.data(), &len, (int)p.size(), nullptr, (int)steps_new,
+                                       config_.temperature, (int)config_.top_k, config_.top_p, draws.data(), out.data(),
+                                       lp.data()),
+            "ti_engine_generate_sampled");
+      im.total_forward_passes += p.size() + steps_new - 1;
+      const size_t b = budget(p.size());
+      for (size_t t = 0; t < std::min(b, steps_new); ++t) {
+        fresh[0].push_back(out[t]);
+        if (include_logprobs) lps[0].push_back(lp[t]);
+        if (out[t] == config_.eos_token_id || p.size() + fresh[0].size() >= maxlen) break;
+      }
+      im.rng = saved;
+      im.rng.discard(fresh[0].size());
     } else {
       // logits to the host every step: the reference sampler (temperature / top-k / top-p / draw)
       std::vector<float> logits((size_t)n * V);

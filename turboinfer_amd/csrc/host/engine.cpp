@@ -99,6 +99,13 @@ struct ti_engine {
   bool part_on = true;         // TI_ATTN_PART=0 turns it off
   uint16_t* part_o = nullptr;  // [heads][TI_ATTN_MAX_PART_SPLITS][head_dim]
   float* part_ml = nullptr;    // [heads][TI_ATTN_MAX_PART_SPLITS][2]
+  // on-device sampling (ti_engine_generate_sampled): the step graph ends with ti_sample_step
+  bool samp_on = false;
+  float samp_t = 1.0f, samp_p = 1.0f;
+  int samp_k = 1;
+  float* draws = nullptr;      // [max_batch][draw_cap] uniform draws, per new token
+  float* lps = nullptr;        // [max_batch][draw_cap] log p of the sampled tokens
+  int draw_cap = 0;
   // prefill (forward_pass over prompt tokens): up to pf_rows prompt tokens of one stream run
   // as rows of the batched path, sharing that stream's KV cache (stride 0)
   int pf_rows = 0;             // 0 = off (prompts consumed one token per decode step)
@@ -117,7 +124,7 @@ struct ti_engine {
   int splits_max = 1;
   int64_t kv_stride = 0;
   size_t weight_bytes = 0, kv_bytes = 0;
-  std::map<std::pair<int, int>, hipGraphExec_t> graphs;  // (M, advance)
+  std::map<std::pair<int, int>, hipGraphExec_t> graphs;  // (M, advance | sampled << 1)
   int replay_M = 0;
   // chained single-stream steps (ti_hip.h ti_chain): launch slot k of a step signals
   // chain_ctr[k][0..7]; chain_cum[k] = its cumulative workgroup count (the next wait target)
@@ -234,7 +241,7 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
 bool chain_usable(ti_engine* e, int M) {
   const ti_engine_config& c = e->c;
   // chained kernels have neither the folded rms_norm nor the split partials hand-off
-  if (!e->chain_on || M != 1 || c.compat || !e->chain_ctr || e->fold_on || e->part_on) return false;
+  if (!e->chain_on || M != 1 || c.compat || !e->chain_ctr || e->fold_on || e->part_on || e->samp_on) return false;
   if (e->chain_ok < 0) {
     const int H = c.hidden, I = c.inter, qd = e->qd(), kvd = e->kvd();
     const int b = c.bits;
@@ -504,7 +511,11 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   el.argmax = e->argmax;
   el.step_ctr = e->step_ctr;
   el.advance = advance;
-  return gemm(e->lm, e->h, TI_X_F32_RMSNORM, H, 4, e->out_norm, el, 4, true);
+  TI_TRY(gemm(e->lm, e->h, TI_X_F32_RMSNORM, H, 4, e->out_norm, el, 4, true));
+  if (e->samp_on)   // sample_next_token on the device; its key feeds the token back (ti_hip.h)
+    TI_TRY(ti_sample_step(e->logits, V, M, V, e->samp_t, e->samp_k, e->samp_p, e->draws, e->draw_cap, e->step_ctr,
+                          advance, e->n_in, e->argmax, e->lps, e->s));
+  return TI_OK;
 }
 
 // Prefill (reference forward_pass, inference_engine.cpp:1429-1491, with the KV kept): prompt
@@ -575,7 +586,7 @@ int enqueue_prefill(ti_engine* e, int m, int t0, int rows, int base) {
 }
 
 int get_graph(ti_engine* e, int M, int advance, hipGraphExec_t* out) {
-  auto key = std::make_pair(M, advance);
+  auto key = std::make_pair(M, advance | (e->samp_on ? 2 : 0));
   auto it = e->graphs.find(key);
   if (it != e->graphs.end()) {
     *out = it->second;
@@ -879,6 +890,52 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
     }
   }
   if (last_logits) TI_TRY(ti_memcpy_d2h(last_logits, e->logits, (size_t)n * c.vocab * 4, e->s));
+  return TI_OK;
+}
+
+int ti_engine_generate_sampled(ti_engine* e, int n, const int32_t* prompts, const int32_t* lens, int stride,
+                               const int32_t* start_pos, int max_new, float temperature, int top_k, float top_p,
+                               const float* draws, int32_t* out_tokens, float* out_logprobs) {
+  if (!e || !draws) return ti_set_error(TI_ERR_ARG, "ti_engine_generate_sampled: null");
+  const ti_engine_config& c = e->c;
+  if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_generate_sampled: compat engine");
+  if (n < 1 || n > c.max_batch || max_new < 1) return ti_set_error(TI_ERR_ARG, "ti_engine_generate_sampled: n=%d max_new=%d", n, max_new);
+  if (top_k < 1 || top_k > TI_SAMPLE_MAX_K || top_k > c.vocab)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_generate_sampled: top_k %d not in [1, %d]", top_k,
+                        std::min(c.vocab, TI_SAMPLE_MAX_K));
+  auto drop_graphs = [&]() -> int {
+    TI_TRY(ti_stream_sync(e->s));
+    for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
+    e->graphs.clear();
+    return TI_OK;
+  };
+  if (max_new > e->draw_cap) {   // graphs bake the buffers in
+    TI_TRY(drop_graphs());
+    const int cap = std::max(max_new, 64);
+    TI_TRY(e->alloc_t(&e->draws, (size_t)c.max_batch * cap));
+    TI_TRY(e->alloc_t(&e->lps, (size_t)c.max_batch * cap));
+    e->draw_cap = cap;
+  }
+  if (e->samp_t != temperature || e->samp_k != top_k || e->samp_p != top_p) {   // kernel arguments of the graph
+    TI_TRY(drop_graphs());
+    e->samp_t = temperature;
+    e->samp_k = top_k;
+    e->samp_p = top_p;
+  }
+  std::vector<float> d((size_t)n * e->draw_cap, 0.5f);
+  for (int m = 0; m < n; ++m) std::memcpy(&d[(size_t)m * e->draw_cap], draws + (size_t)m * max_new, (size_t)max_new * 4);
+  TI_TRY(ti_memcpy_h2d(e->draws, d.data(), d.size() * 4, e->s));
+  e->samp_on = true;
+  const int rc = ti_engine_generate(e, n, prompts, lens, stride, start_pos, max_new, out_tokens, nullptr);
+  e->samp_on = false;
+  TI_TRY(rc);
+  if (out_logprobs) {
+    std::vector<float> lp((size_t)n * e->draw_cap);
+    TI_TRY(ti_memcpy_d2h(lp.data(), e->lps, lp.size() * 4, e->s));
+    for (int m = 0; m < n; ++m)
+      for (int t = 0; t < max_new; ++t)
+        out_logprobs[(size_t)m * max_new + t] = out_tokens[(size_t)m * max_new + t] < 0 ? 0.0f : lp[(size_t)m * e->draw_cap + t];
+  }
   return TI_OK;
 }
 
