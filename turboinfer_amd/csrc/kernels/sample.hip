@@ -85,6 +85,18 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
   const float* row = a.logits + (size_t)m * a.ldl;
   const bool temp = a.temperature != 1.0f && a.temperature > 0.0f;
   auto lg = [&](int i) { return temp ? row[i] / a.temperature : row[i]; };
+  // f(i, key) over the row, 16 loads in flight per thread (the passes are latency-bound)
+  auto sweep = [&](auto&& f) {
+    constexpr int U = 16;
+    for (int b = tid; b < V; b += U * kSampThreads) {
+      float v[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) v[j] = b + j * kSampThreads < V ? row[b + j * kSampThreads] : 0.0f;
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (b + j * kSampThreads < V) f(samp_key(temp ? v[j] / a.temperature : v[j]));
+    }
+  };
 
   int t = 0;   // which draw (and logprob slot) this step's token is
   if (a.step_ctr) t = (*a.step_ctr - a.advance) - (a.n_in ? a.n_in[m] - 1 : 0);
@@ -101,22 +113,18 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
     if (tid < 256) hist[tid] = 0u;
     __syncthreads();
     const uint32_t pre = s_prefix;
-    for (int i = tid; i < V; i += kSampThreads) {
-      const uint32_t key = samp_key(lg(i));
+    sweep([&](uint32_t key) {
       if ((key & mask) == pre) atomicAdd(&hist[(key >> shift) & 255u], 1u);
-    }
+    });
     __syncthreads();
-    if (tid == 0) {
-      int cum = 0;
-      for (int b = 255; b >= 0; --b) {
-        const int h = (int)hist[b];
-        if (cum + h >= s_left) {
-          s_prefix = pre | ((uint32_t)b << shift);
-          s_left -= cum;
-          break;
-        }
-        cum += h;
-      }
+    // the bin holding the s_left-th largest key: counts above each bin by one block scan over
+    // the bins in descending order (thread j <-> bin 255 - j)
+    const int h = tid < 256 ? (int)hist[255 - tid] : 0, left = s_left;
+    int tot_h;
+    const int above = block_excl_scan(h, &tot_h, s_w);
+    if (tid < 256 && h > 0 && above < left && left <= above + h) {
+      s_prefix = pre | ((uint32_t)(255 - tid) << shift);
+      s_left = left - above;
     }
     mask |= 255u << shift;
     __syncthreads();
@@ -127,10 +135,17 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
   // ---- survivors in index order: thread tid owns indices [c0, c1)
   const int C = (V + kSampThreads - 1) / kSampThreads, c0 = min(V, tid * C), c1 = min(V, c0 + C);
   int ng = 0, ne = 0;
-  for (int i = c0; i < c1; ++i) {
-    const uint32_t key = samp_key(lg(i));
-    ng += key > kth;
-    ne += key == kth;
+  for (int i0 = c0; i0 < c1; i0 += 16) {   // the thread's own contiguous run, 16 loads in flight
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = i0 + j < c1 ? row[i0 + j] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (i0 + j < c1) {
+        const uint32_t key = samp_key(temp ? v[j] / a.temperature : v[j]);
+        ng += key > kth;
+        ne += key == kth;
+      }
   }
   int tot;
   const int eq_before = block_excl_scan(ne, &tot, s_w);
