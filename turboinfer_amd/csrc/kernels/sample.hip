@@ -12,9 +12,12 @@
 // Only the k <= TI_SAMPLE_MAX_K survivors carry probability, so after the selection every
 // step runs on a list of them kept in index order: the sums see the same fp32 values in the
 // same order as the reference's loops over all V entries (the others add exact zeros).
-// Selection: a 4-pass 8-bit radix select of the k-th largest order key over the row (LDS
-// histograms), then the survivors (keys above it, and the lowest-index ties at it) compacted
-// with block scans.  Differences to the reference: exp / log are the device's (<= 1 ulp from
+// Selection: the k-th largest of the 1024 threads' run maxima bounds the k-th largest logit
+// from below; the few keys above that bound are ranked exactly in LDS (a 4-pass 8-bit radix
+// select over the whole row, LDS histograms, when there are more than 2048 of them); the
+// survivors (ties lowest index first) are compacted in index order with block scans.  (A
+// radix pass over the row costs ~14 us: one bin takes most keys, so the LDS atomics
+// serialise.)  Differences to the reference: exp / log are the device's (<= 1 ulp from
 // glibc), and equal logits at the k-th place / equal probabilities at the top-p cut are taken
 // lowest index first (libstdc++'s std::sort leaves their order unspecified).
 #include <math.h>
@@ -57,14 +60,16 @@ __device__ int block_excl_scan(int v, int* total, int* s_w) {
   }
   if (lane == 63) s_w[w] = x;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int run = 0;
-    for (int i = 0; i < kSampWaves; ++i) {
-      const int t = s_w[i];
-      s_w[i] = run;
-      run += t;
+  if (threadIdx.x < 64) {   // the wave totals, scanned by wave 0
+    const int t = lane < kSampWaves ? s_w[lane] : 0;
+    int y = t;
+#pragma unroll
+    for (int o = 1; o < kSampWaves; o <<= 1) {
+      const int z = __shfl_up(y, o, 64);
+      if (lane >= o) y += z;
     }
-    s_w[kSampWaves] = run;
+    if (lane < kSampWaves) s_w[lane] = y - t;
+    if (lane == kSampWaves - 1) s_w[kSampWaves] = y;
   }
   __syncthreads();
   const int r = s_w[w] + x - v;
@@ -79,130 +84,263 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
   __shared__ uint32_t s_prefix;
   __shared__ int s_left, s_tok;
   __shared__ float s_lp;
-  __shared__ float s_val[TI_SAMPLE_MAX_K], s_p[TI_SAMPLE_MAX_K];
-  __shared__ int s_idx[TI_SAMPLE_MAX_K], s_order[TI_SAMPLE_MAX_K];
+  __shared__ float s_val[TI_SAMPLE_MAX_K];
+  __shared__ __attribute__((aligned(16))) float s_p[TI_SAMPLE_MAX_K], s_sorted[TI_SAMPLE_MAX_K];
+  __shared__ int s_cut;
+  __shared__ int s_idx[TI_SAMPLE_MAX_K];
+  constexpr int kCand = 2048;
+  __shared__ uint32_t s_ck[kCand];
+  __shared__ int s_ci[kCand];
+  __shared__ uint8_t s_cf[kCand];
   const int m = blockIdx.x, tid = threadIdx.x, V = a.V, k = a.top_k;
   const float* row = a.logits + (size_t)m * a.ldl;
   const bool temp = a.temperature != 1.0f && a.temperature > 0.0f;
   auto lg = [&](int i) { return temp ? row[i] / a.temperature : row[i]; };
-  // f(i, key) over the row, 16 loads in flight per thread (the passes are latency-bound)
-  auto sweep = [&](auto&& f) {
-    constexpr int U = 16;
-    for (int b = tid; b < V; b += U * kSampThreads) {
-      float v[U];
-#pragma unroll
-      for (int j = 0; j < U; ++j) v[j] = b + j * kSampThreads < V ? row[b + j * kSampThreads] : 0.0f;
-#pragma unroll
-      for (int j = 0; j < U; ++j)
-        if (b + j * kSampThreads < V) f(samp_key(temp ? v[j] / a.temperature : v[j]));
-    }
-  };
 
   int t = 0;   // which draw (and logprob slot) this step's token is
   if (a.step_ctr) t = (*a.step_ctr - a.advance) - (a.n_in ? a.n_in[m] - 1 : 0);
   if (t < 0 || t >= a.draw_stride) return;   // a prompt step (its token is the prompt's) or past the budget
   const float u = a.draws[(size_t)m * a.draw_stride + t];
 
-  // ---- k-th largest order key: 8 bits per pass, most significant first
-  if (tid == 0) {
-    s_prefix = 0u;
-    s_left = k;
-  }
-  uint32_t mask = 0u;
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    if (tid < 256) hist[tid] = 0u;
-    __syncthreads();
-    const uint32_t pre = s_prefix;
-    sweep([&](uint32_t key) {
-      if ((key & mask) == pre) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+  // ---- k-th largest of per-thread keys: 8 bits per pass, most significant first; each pass
+  // histograms the keys of `sweep_fn` that match the prefix so far (LDS atomics)
+  auto select_kth = [&](auto&& sweep_fn, int kk, uint32_t* kth_out, int* need_eq_out) {
+    if (tid == 0) {
+      s_prefix = 0u;
+      s_left = kk;
+    }
+    uint32_t mask = 0u;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      if (tid < 256) hist[tid] = 0u;
+      __syncthreads();
+      const uint32_t pre = s_prefix;
+      sweep_fn([&](uint32_t key) {
+        if ((key & mask) == pre) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+      });
+      __syncthreads();
+      // the bin holding the s_left-th largest key: counts above each bin by one block scan
+      // over the bins in descending order (thread j <-> bin 255 - j)
+      const int h = tid < 256 ? (int)hist[255 - tid] : 0, left = s_left;
+      int tot_h;
+      const int above = block_excl_scan(h, &tot_h, s_w);
+      if (tid < 256 && h > 0 && above < left && left <= above + h) {
+        s_prefix = pre | ((uint32_t)(255 - tid) << shift);
+        s_left = left - above;
+      }
+      mask |= 255u << shift;
+      __syncthreads();
+    }
+    *kth_out = s_prefix;
+    *need_eq_out = s_left;
+  };
+  // wave wv owns the index segment [g0, g1), read 64 consecutive indices per wave load
+  // (coalesced), 8 loads in flight per lane; f(i, key, ok) sees every wave-load slot in index
+  // order with a wave-uniform trip count (ok = i inside the segment), so ballots can order it
+  const int wv = tid >> 6, lane = tid & 63;
+  const int SEG = (((V + kSampWaves - 1) / kSampWaves) + 63) & ~63;
+  const int g0 = min(V, wv * SEG), g1 = min(V, g0 + SEG);
+  // Rows up to kCacheV keep the lane's 32 keys in registers after the first sweep (one CU
+  // streams the row at ~25 GB/s: each sweep from memory costs ~5 us at V = 32000).
+  constexpr int kCacheV = kSampWaves * 64 * 32;
+  const bool cached = V <= kCacheV;
+  uint32_t rk[32];
+  bool loaded = false;
+  auto own = [&](auto&& f) {
+    if (cached) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int b = g0 + c * 64 * 8;
+        if (!loaded) {
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int i = b + 64 * j + lane;
+            v[j] = i < g1 ? row[i] : 0.0f;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rk[c * 8 + j] = samp_key(temp ? v[j] / a.temperature : v[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = b + 64 * j + lane;
+          f(i, rk[c * 8 + j], i < g1);
+        }
+      }
+      loaded = true;
+      return;
+    }
+    for (int b = g0; b < g1; b += 64 * 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = b + 64 * j + lane;
+        v[j] = i < g1 ? row[i] : 0.0f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = b + 64 * j + lane;
+        f(i, samp_key(temp ? v[j] / a.temperature : v[j]), i < g1);
+      }
+    }
+  };
+  auto below = [&](unsigned long long mask) {   // set bits of mask in lanes below this one
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+  };
+  // the wave's starting offset in a block-ordered compaction of per-thread counts
+  auto wave_base = [&](int cnt, int* total) { return __shfl(block_excl_scan(cnt, total, s_w), 0, 64); };
+
+  // ---- candidates: every key at or above tau0, the k-th largest of the threads' maxima
+  // (k elements reach it; for smooth logits a few dozen more).  The k largest candidates,
+  // ties lowest index first, are the survivors; with more than kCand candidates the full
+  // row goes through the radix select instead.
+  uint32_t tmax = 0u;   // below every finite key
+  own([&](int, uint32_t key, bool ok) { tmax = ok && key > tmax ? key : tmax; });
+  uint32_t tau0;
+  int unused;
+  select_kth([&](auto&& f) { f(tmax); }, k, &tau0, &unused);
+  int ncand = 0;
+  own([&](int, uint32_t key, bool ok) { ncand += ok && key >= tau0; });
+  int tot;
+  const int cbase = wave_base(ncand, &tot);
+  const int C_tot = tot;
+  int n;
+  if (C_tot <= kCand) {
+    int run = cbase;
+    own([&](int i, uint32_t key, bool ok) {
+      const bool c = ok && key >= tau0;
+      const unsigned long long m = __ballot(c);
+      if (c) {
+        s_ck[run + below(m)] = key;
+        s_ci[run + below(m)] = i;
+      }
+      run += __popcll(m);
     });
     __syncthreads();
-    // the bin holding the s_left-th largest key: counts above each bin by one block scan over
-    // the bins in descending order (thread j <-> bin 255 - j)
-    const int h = tid < 256 ? (int)hist[255 - tid] : 0, left = s_left;
-    int tot_h;
-    const int above = block_excl_scan(h, &tot_h, s_w);
-    if (tid < 256 && h > 0 && above < left && left <= above + h) {
-      s_prefix = pre | ((uint32_t)(255 - tid) << shift);
-      s_left = left - above;
+    // rank among the candidates (they are in index order): survivors have rank < k
+    for (int i = tid; i < C_tot; i += kSampThreads) {
+      const uint32_t ki = s_ck[i];
+      int r = 0;
+      for (int j = 0; j < C_tot; ++j) r += s_ck[j] > ki || (s_ck[j] == ki && j < i);
+      s_cf[i] = r < k;
     }
-    mask |= 255u << shift;
     __syncthreads();
-  }
-  const uint32_t kth = s_prefix;
-  const int need_eq = s_left;   // keys equal to the k-th that survive (lowest indices first)
-
-  // ---- survivors in index order: thread tid owns indices [c0, c1)
-  const int C = (V + kSampThreads - 1) / kSampThreads, c0 = min(V, tid * C), c1 = min(V, c0 + C);
-  int ng = 0, ne = 0;
-  for (int i0 = c0; i0 < c1; i0 += 16) {   // the thread's own contiguous run, 16 loads in flight
-    float v[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = i0 + j < c1 ? row[i0 + j] : 0.0f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (i0 + j < c1) {
-        const uint32_t key = samp_key(temp ? v[j] / a.temperature : v[j]);
-        ng += key > kth;
-        ne += key == kth;
+    // survivors in index order: thread tid compacts candidates [q0, q1)
+    const int Q = (C_tot + kSampThreads - 1) / kSampThreads, q0 = min(C_tot, tid * Q), q1 = min(C_tot, q0 + Q);
+    int nk = 0;
+    for (int i = q0; i < q1; ++i) nk += s_cf[i];
+    int at = block_excl_scan(nk, &tot, s_w);
+    for (int i = q0; i < q1; ++i)
+      if (s_cf[i] && at < TI_SAMPLE_MAX_K) {
+        const int idx = s_ci[i];
+        s_val[at] = lg(idx);
+        s_idx[at] = idx;
+        ++at;
       }
+    __syncthreads();
+    n = min(tot, TI_SAMPLE_MAX_K);
+  } else {
+    uint32_t kth;
+    int need_eq;
+    select_kth(
+        [&](auto&& f) {
+          constexpr int U = 16;   // the whole row, strided, 16 loads in flight per thread
+          for (int b = tid; b < V; b += U * kSampThreads) {
+            float v[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) v[j] = b + j * kSampThreads < V ? row[b + j * kSampThreads] : 0.0f;
+#pragma unroll
+            for (int j = 0; j < U; ++j)
+              if (b + j * kSampThreads < V) f(samp_key(temp ? v[j] / a.temperature : v[j]));
+          }
+        },
+        k, &kth, &need_eq);
+    // survivors in index order: keys above the k-th, and the lowest-index ties at it
+    int ng = 0, ne = 0;
+    own([&](int, uint32_t key, bool ok) {
+      ng += ok && key > kth;
+      ne += ok && key == kth;
+    });
+    int tot_e;
+    const int eq_base = wave_base(ne, &tot_e);                 // equal keys before this wave
+    const int ne_w = __reduce_add_sync(~0ull, ne);             // this wave's equal keys
+    const int keep_eq_w = max(0, min(ne_w, need_eq - eq_base));
+    const int ng_w = __reduce_add_sync(~0ull, ng);
+    const int kbase = wave_base(lane == 0 ? ng_w + keep_eq_w : 0, &tot);
+    int run = kbase, eq_run = eq_base;
+    own([&](int i, uint32_t key, bool ok) {
+      const bool eq = ok && key == kth;
+      const unsigned long long me = __ballot(eq);
+      const bool keep = (ok && key > kth) || (eq && eq_run + below(me) < need_eq);
+      const unsigned long long mk = __ballot(keep);
+      if (keep && run + below(mk) < TI_SAMPLE_MAX_K) {
+        s_val[run + below(mk)] = temp ? row[i] / a.temperature : row[i];
+        s_idx[run + below(mk)] = i;
+      }
+      run += __popcll(mk);
+      eq_run += __popcll(me);
+    });
+    __syncthreads();
+    n = min(tot, TI_SAMPLE_MAX_K);   // == k
   }
-  int tot;
-  const int eq_before = block_excl_scan(ne, &tot, s_w);
-  const int keep_eq = max(0, min(ne, need_eq - eq_before));
-  const int at = block_excl_scan(ng + keep_eq, &tot, s_w);
-  int w = at, eq_seen = 0;
-  for (int i = c0; i < c1; ++i) {
-    const float v = lg(i);
-    const uint32_t key = samp_key(v);
-    const bool keep = key > kth || (key == kth && eq_seen++ < keep_eq);
-    if (keep && w < TI_SAMPLE_MAX_K) {
-      s_val[w] = v;
-      s_idx[w] = i;
-      ++w;
-    }
-  }
-  __syncthreads();
-  const int n = min(tot, TI_SAMPLE_MAX_K);   // == k
 
   // ---- softmax over the survivors (the others are exp(-inf) = 0 in the reference's loops)
   float mx = -INFINITY;
   for (int i = 0; i < n; ++i) mx = fmaxf(mx, s_val[i]);   // every thread, exact in any order
   if (tid < n) s_p[tid] = expf(s_val[tid] - mx);
   __syncthreads();
-  if (tid == 0) {
+  // The sequential sums run in one thread (the reference's order), 8 values fetched per step.
+  auto seq_sum = [&](const float* p) {
     float sum = 0.0f;
-    for (int i = 0; i < n; ++i) sum += s_p[i];
-    s_lp = sum;
-  }
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {
+      const float4 x = *(const float4*)(p + i), y = *(const float4*)(p + i + 4);
+      sum += x.x; sum += x.y; sum += x.z; sum += x.w;
+      sum += y.x; sum += y.y; sum += y.z; sum += y.w;
+    }
+    for (; i < n; ++i) sum += p[i];
+    return sum;
+  };
+  // first r (in order) whose running sum reaches `target` (cmp: sum >= target / target <= sum), or -1
+  auto seq_find = [&](const float* p, float target) {
+    float cum = 0.0f;
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {
+      const float4 x = *(const float4*)(p + i), y = *(const float4*)(p + i + 4);
+      const float v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        cum += v[j];
+        if (target <= cum) return i + j;
+      }
+    }
+    for (; i < n; ++i) {
+      cum += p[i];
+      if (target <= cum) return i;
+    }
+    return -1;
+  };
+  if (tid == 0) s_lp = seq_sum(s_p);
   __syncthreads();
   if (tid < n) s_p[tid] = s_p[tid] / s_lp;
   __syncthreads();
 
   // ---- top-p: rank by probability (descending, lower index first on ties), cut, renormalise
   if (a.top_p < 1.0f) {
+    int rank = 0;
     if (tid < n) {
       const float p = s_p[tid];
-      int r = 0;
-      for (int j = 0; j < n; ++j) r += s_p[j] > p || (s_p[j] == p && j < tid);
-      s_order[r] = tid;
+      for (int j = 0; j < n; ++j) rank += s_p[j] > p || (s_p[j] == p && j < tid);
+      s_sorted[rank] = p;
     }
     __syncthreads();
     if (tid == 0) {
-      float cum = 0.0f;
-      int cut = n;
-      for (int r = 0; r < n; ++r) {
-        cum += s_p[s_order[r]];
-        if (cum >= a.top_p) {
-          cut = r + 1;
-          break;
-        }
-      }
-      for (int r = cut; r < n; ++r) s_p[s_order[r]] = 0.0f;
-      float ns = 0.0f;
-      for (int i = 0; i < n; ++i) ns += s_p[i];
-      s_lp = ns;
+      const int r = seq_find(s_sorted, a.top_p);
+      s_cut = r < 0 ? n : r + 1;
     }
+    __syncthreads();
+    if (tid < n && rank >= s_cut) s_p[tid] = 0.0f;
+    __syncthreads();
+    if (tid == 0) s_lp = seq_sum(s_p);
     __syncthreads();
     if (tid < n && s_lp > 0.0f) s_p[tid] = s_p[tid] / s_lp;
     __syncthreads();
@@ -216,14 +354,10 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
       tok = 0;
       pt = s_idx[0] == 0 ? s_p[0] : 0.0f;
     } else {
-      float cum = 0.0f;
-      for (int i = 0; i < n; ++i) {
-        cum += s_p[i];
-        if (u <= cum) {
-          tok = s_idx[i];
-          pt = s_p[i];
-          break;
-        }
+      const int i = seq_find(s_p, u);
+      if (i >= 0) {
+        tok = s_idx[i];
+        pt = s_p[i];
       }
     }
     s_tok = tok;
