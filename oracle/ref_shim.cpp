@@ -286,4 +286,36 @@ int ref_time_decode(uint64_t H, uint64_t heads, uint64_t I, uint64_t V, uint64_t
   });
 }
 
+// Quantizer::quantize_model + save_quantized_model (quantization.cpp:79-211) on a ModelData of
+// fp32 tensors added in the given order: the TINQ fixtures of tests/golden/gen_tinq.py.
+int ref_tinq_save(const char* path, int qtype, int symmetric, int n, const char* const* names,
+                  const float* const* data, const int* ndims, const uint64_t* dims, const char* name,
+                  const char* arch, const char* version, const uint64_t* sizes /* vocab hidden layers heads inter */,
+                  float rope_theta) {
+  return guard([&] {
+    turboinfer::model::ModelData md;
+    auto& m = md.metadata();
+    m.name = name;
+    m.architecture = arch;
+    m.version = version;
+    m.vocab_size = sizes[0];
+    m.hidden_size = sizes[1];
+    m.num_layers = sizes[2];
+    m.num_heads = sizes[3];
+    m.intermediate_size = sizes[4];
+    m.rope_theta = rope_theta;
+    const uint64_t* d = dims;
+    for (int i = 0; i < n; ++i) {
+      md.add_tensor(names[i], make(data[i], ndims[i], d));
+      d += ndims[i];
+    }
+    turboinfer::optimize::QuantizationConfig qc;
+    qc.type = qtype == 0 ? turboinfer::optimize::QuantizationType::kInt8 : turboinfer::optimize::QuantizationType::kInt4;
+    qc.symmetric = symmetric != 0;
+    turboinfer::optimize::Quantizer qz(qc);
+    qz.save_quantized_model(qz.quantize_model(md), path);
+    return 0;
+  });
+}
+
 }  // extern "C"

@@ -8,6 +8,10 @@
 //   api_check op <name> <out> <in...> [param]         TensorEngine op on the GPU
 //   api_check generate <model_dir> <prompts> <n_new> <top_k> <weight_bits> <out>
 //                                                     InferenceEngine::generate_batch on the GPU
+//   api_check tinq_save <model_dir> <bits> <sym> <out.tinq>
+//                                                     Quantizer::quantize_model + save_quantized_model
+//   api_check tinq_load <in.tinq> <out_dir>           Quantizer::load_quantized_model -> meta.txt,
+//                                                     names.txt and <i>.bin in the file's order
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -198,6 +202,40 @@ static int generate(const std::string& dir, const std::string& prompts_file, int
   return 0;
 }
 
+// model_dir/tinq_manifest.txt: "meta <name> <arch> <version> <vocab> <hidden> <layers> <heads> <inter>
+// <rope_theta>" then "<tensor name> <file>" lines, added in that order
+static int tinq_save(const std::string& dir, int bits, int sym, const std::string& out) {
+  model::ModelData md;
+  std::ifstream man(dir + "/tinq_manifest.txt");
+  std::string tag;
+  auto& m = md.metadata();
+  man >> tag >> m.name >> m.architecture >> m.version >> m.vocab_size >> m.hidden_size >> m.num_layers >> m.num_heads >>
+      m.intermediate_size >> m.rope_theta;
+  if (tag != "meta") throw std::runtime_error("tinq_manifest: expected meta line");
+  std::string name, file;
+  while (man >> name >> file) md.add_tensor(name, read_array(dir + "/" + file));
+  optimize::QuantizationConfig qc;
+  qc.type = bits == 8 ? optimize::QuantizationType::kInt8 : optimize::QuantizationType::kInt4;
+  qc.symmetric = sym != 0;
+  optimize::Quantizer qz(qc);
+  qz.save_quantized_model(qz.quantize_model(md), out);
+  return 0;
+}
+
+static int tinq_load(const std::string& in, const std::string& dir) {
+  const model::ModelData md = optimize::Quantizer::load_quantized_model(in);
+  const auto& m = md.metadata();
+  std::ofstream meta(dir + "/meta.txt"), names(dir + "/names.txt");
+  meta << m.name << " " << m.architecture << " " << m.version << " " << m.vocab_size << " " << m.hidden_size << " "
+       << m.num_layers << " " << m.num_heads << " " << m.intermediate_size << " " << m.rope_theta << "\n";
+  int i = 0;
+  for (const auto& n : md.tensor_names()) {
+    names << n << "\n";
+    write_array(dir + "/" + std::to_string(i++) + ".bin", *md.get_tensor(n));
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   try {
     if (argc < 2) throw std::runtime_error("usage: api_check tensor|quant|op|generate ...");
@@ -205,6 +243,8 @@ int main(int argc, char** argv) {
     if (mode == "tensor") return tensor_checks();
     if (mode == "quant" && argc == 6) return quant(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argv[5]);
     if (mode == "op" && argc >= 5) return op(argc, argv);
+    if (mode == "tinq_save" && argc == 6) return tinq_save(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argv[5]);
+    if (mode == "tinq_load" && argc == 4) return tinq_load(argv[2], argv[3]);
     if (mode == "generate" && argc == 8)
       return generate(argv[2], argv[3], std::atoi(argv[4]), std::atoi(argv[5]), std::atoi(argv[6]), argv[7]);
     throw std::runtime_error("bad arguments for mode " + mode);

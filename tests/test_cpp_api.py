@@ -16,7 +16,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import ROOT, inp
+from conftest import GOLDEN, ROOT, inp
 
 f32 = np.float32
 BIN = os.path.join(ROOT, "tests", "cpp", "bin", "api_check")
@@ -223,3 +223,91 @@ def test_inference_engine_llama_greedy_matches_reference(api_check, golden, orac
             if s[-1] - s[-2] <= 1e-2 * float(np.max(np.abs(lg))):
                 break                      # near-tie: later tokens may legitimately diverge
             assert g == r, f"token {i}: C++ API {g} reference {r}"
+
+
+# ---------------------------------------------------------------- TINQ
+def _tinq_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_tinq", os.path.join(ROOT, "tests", "golden", "gen_tinq.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)        # definitions only (main() needs the reference build)
+    return mod
+
+
+def _parse_tinq(raw: bytes):
+    """An independent reader of the reference's TINQ layout (quantization.cpp:120-211)."""
+    o = 0
+
+    def take(fmt_dtype, n=1):
+        nonlocal o
+        a = np.frombuffer(raw, fmt_dtype, n, o)
+        o += a.nbytes
+        return a
+
+    def string():
+        n = int(take(np.uint32)[0])
+        nonlocal o
+        s = raw[o:o + n].decode()
+        o += n
+        return s
+
+    assert int(take(np.uint32)[0]) == 0x54494E51 and int(take(np.uint32)[0]) == 1
+    qtype, sym, per_ch = int(take(np.int32)[0]), int(take(np.uint8)[0]), int(take(np.uint8)[0])
+    meta = [string(), string(), string()] + [int(v) for v in take(np.uint64, 5)] + [float(take(np.float32)[0])]
+    tensors = []
+    for _ in range(int(take(np.uint32)[0])):
+        name, code, nd = string(), int(take(np.uint32)[0]), int(take(np.uint32)[0])
+        shape = tuple(int(v) for v in take(np.uint64, nd))
+        nbytes = int(take(np.uint64)[0])
+        dt = {0: np.float32, 2: np.int32, 4: np.int8}[code]
+        data = take(dt, nbytes // np.dtype(dt).itemsize).reshape(shape)
+        extra = None
+        if code in (2, 4):
+            scales = take(np.float32, int(take(np.uint32)[0]))
+            zps = take(np.float32, int(take(np.uint32)[0]))
+            extra = (scales.tolist(), zps.tolist(), int(take(np.uint64)[0]), int(take(np.uint64)[0]),
+                     float(take(np.float32)[0]))
+        tensors.append((name, data, extra))
+    assert o == len(raw)
+    return (qtype, sym, per_ch), meta, tensors
+
+
+@pytest.mark.parametrize("case", ["tinq_int8_sym", "tinq_int4_sym", "tinq_int8_asym"])
+def test_tinq_save_is_byte_identical_to_reference(api_check, tmp_path, case):
+    """Quantizer::quantize_model + save_quantized_model on the fixture's fp32 model writes the
+    same bytes as the compiled reference did (tests/golden/gen_tinq.py)."""
+    g = _tinq_module()
+    x = np.load(os.path.join(GOLDEN, "tinq_inputs.npz"))
+    m = g.META
+    lines = [f"meta {m['name']} {m['arch']} {m['version']} " + " ".join(str(v) for v in m["sizes"]) +
+             f" {m['rope_theta']!r}"]
+    for j, (name, _) in enumerate(g.TENSORS):
+        write(tmp_path / f"t{j}.bin", x[name.replace(".", "__")])
+        lines.append(f"{name} t{j}.bin")
+    (tmp_path / "tinq_manifest.txt").write_text("\n".join(lines) + "\n")
+    qtype, sym = g.CASES[case]
+    api_check("tinq_save", tmp_path, 8 if qtype == 0 else 4, sym, tmp_path / "out.tinq")
+    want = open(os.path.join(GOLDEN, case + ".tinq"), "rb").read()
+    got = open(tmp_path / "out.tinq", "rb").read()
+    assert got == want
+
+
+@pytest.mark.parametrize("case", ["tinq_int8_sym", "tinq_int4_sym"])
+def test_tinq_load_reads_reference_file(api_check, tmp_path, case):
+    """Quantizer::load_quantized_model on the reference's file: metadata, tensor names, dtypes,
+    shapes and values as an independent parse of the file (the loaded ModelData iterates in its
+    unordered_map's order, as the reference's does)."""
+    raw = open(os.path.join(GOLDEN, case + ".tinq"), "rb").read()
+    _, meta, tensors = _parse_tinq(raw)
+    out = tmp_path / "loaded"
+    out.mkdir()
+    api_check("tinq_load", os.path.join(GOLDEN, case + ".tinq"), out)
+    got_meta = (out / "meta.txt").read_text().split()
+    assert got_meta[:3] == meta[:3] and [int(v) for v in got_meta[3:8]] == meta[3:8]
+    assert float(got_meta[8]) == meta[8]
+    names = (out / "names.txt").read_text().split()   # the container's iteration order
+    assert sorted(names) == sorted(t[0] for t in tensors)
+    for name, data, _ in tensors:
+        got = read(out / f"{names.index(name)}.bin")
+        assert got.dtype == data.dtype and got.shape == data.shape, name
+        np.testing.assert_array_equal(got, data)
