@@ -80,6 +80,18 @@ int ti_engine_generate_sampled(ti_engine* e, int n_streams, const int32_t* promp
                                int prompt_stride, const int32_t* start_pos, int max_new, float temperature,
                                int top_k, float top_p, const float* draws, int32_t* out_tokens, float* out_logprobs);
 
+/* InferenceEngine::generate_beam_search (inference_engine.cpp:830-871, 1912-2069): the
+ * reference's beam loop (max-heap on log-probability, expansion by the beam_size most probable
+ * tokens after temperature / softmax / top-k / top-p renormalisation (:1798-1910), length-
+ * normalised ranking log_prob / len^length_penalty, early stop at beam_size finished beams),
+ * with each candidate's next-token distribution from a device forward pass over its tokens.
+ * Results best first: out_tokens [beam_size][max_new] (new tokens, -1 padded), out_log_prob,
+ * out_score (normalised), out_finished [beam_size] (nullable), *out_count beams returned. */
+int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int prompt_len, int max_new, int beam_size,
+                          float temperature, int top_k, float top_p, float length_penalty, int eos_token,
+                          int32_t* out_tokens, float* out_log_prob, float* out_score, int32_t* out_finished,
+                          int* out_count);
+
 /* Prefill of ti_engine_generate's prompts (reference forward_pass, inference_engine.cpp:
  * 1429-1491): all but the last token of the shortest prompt are processed `rows` tokens at a
  * time as rows of the batched GEMMs and causal attention over the stream's own KV cache,

@@ -79,6 +79,7 @@ EXPORTED = [
     "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token", "ti_gemm_wq_a16_chained", "ti_gemm_chainable",
     "ti_attn_decode_chained", "ti_step_begin_chained", "ti_engine_set_chain", "ti_gemm_grid", "ti_engine_set_fold",
     "ti_attn_decode_partials", "ti_sample_device", "ti_sample_step", "ti_engine_generate_sampled",
+    "ti_engine_beam_search",
 ]
 
 _lib = None
@@ -125,6 +126,9 @@ def lib() -> C.CDLL:
         if hasattr(L, "ti_sample_device"):
             L.ti_sample_device.argtypes = [vp, i32, i32, i32, f32, i32, f32, vp, vp, vp, vp]
             L.ti_engine_generate_sampled.argtypes = [vp, i32, vp, vp, i32, vp, i32, f32, i32, f32, vp, vp, vp]
+        if hasattr(L, "ti_engine_beam_search"):
+            L.ti_engine_beam_search.argtypes = [vp, vp, i32, i32, i32, f32, i32, f32, f32, i32, vp, vp, vp, vp,
+                                                C.POINTER(C.c_int)]
         if hasattr(L, "ti_attn_decode_partials"):
             L.ti_attn_decode_partials.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
         L.ti_step_begin.argtypes = [C.POINTER(StepArgs), vp]
@@ -325,6 +329,19 @@ class Engine:
         check(lib().ti_engine_generate_sampled(self.h, n, _ptr(P), _ptr(lens), stride, None if sp is None else _ptr(sp),
                                                max_new, temperature, top_k, top_p, _ptr(d), _ptr(out), _ptr(lp)))
         return out, lp
+
+    def beam_search(self, prompt, max_new, beam_size, temperature=1.0, top_k=0, top_p=1.0, length_penalty=1.0,
+                    eos=2):
+        """ti_engine_beam_search -> [(new tokens, log_prob, normalised score, finished)], best first."""
+        p = np.ascontiguousarray(prompt, np.int32)
+        out = np.zeros((beam_size, max_new), np.int32)
+        lp, sc = np.zeros(beam_size, np.float32), np.zeros(beam_size, np.float32)
+        fin, cnt = np.zeros(beam_size, np.int32), C.c_int(0)
+        check(lib().ti_engine_beam_search(self.h, _ptr(p), p.size, max_new, beam_size, temperature, top_k, top_p,
+                                          length_penalty, eos, _ptr(out), _ptr(lp), _ptr(sc), _ptr(fin),
+                                          C.byref(cnt)))
+        return [([int(t) for t in out[r] if t >= 0], float(lp[r]), float(sc[r]), bool(fin[r]))
+                for r in range(cnt.value)]
 
     def set_prefill(self, rows):
         """Prompt tokens per prefill chunk (0 = consume prompts one token per decode step)."""

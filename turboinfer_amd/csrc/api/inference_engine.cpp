@@ -414,8 +414,39 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
   return results;
 }
 
-std::vector<GenerationResult> InferenceEngine::generate_beam_search(const std::vector<int>&, size_t, size_t, bool) {
-  off_path("generate_beam_search", "rank 4");
+// generate_beam_search (inference_engine.cpp:830-871): the beam loop runs in ti_engine_beam_search
+// (device forward passes, the reference's host ranking); results keep only the new tokens and,
+// with include_logprobs, the beam's average log-probability per token.
+std::vector<GenerationResult> InferenceEngine::generate_beam_search(const std::vector<int>& input_tokens,
+                                                                   size_t max_new_tokens, size_t beam_size,
+                                                                   bool include_logprobs) {
+  if (beam_size == 0) throw std::runtime_error("Beam size must be greater than 0");
+  validate_input_tokens(input_tokens);
+  InferenceEngineImpl& im = *impl_;
+  if (im.compat) off_path("generate_beam_search on the reference_compat plumbing model", "rank 4");
+  std::vector<GenerationResult> results;
+  if (max_new_tokens == 0) return results;
+  const int nb = (int)beam_size, mn = (int)max_new_tokens;
+  std::vector<int32_t> prompt(input_tokens.begin(), input_tokens.end()), out((size_t)nb * mn);
+  std::vector<float> lp(nb);
+  std::vector<int32_t> fin(nb);
+  int count = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  check(ti_engine_beam_search(im.eng, prompt.data(), (int)prompt.size(), mn, nb, config_.temperature,
+                              (int)std::min<size_t>(config_.top_k, (size_t)im.cfg.vocab), config_.top_p,
+                              config_.length_penalty, config_.eos_token_id, out.data(), lp.data(), nullptr, fin.data(),
+                              &count),
+        "ti_engine_beam_search");
+  const float ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  for (int r = 0; r < count; ++r) {
+    GenerationResult g;
+    for (int t = 0; t < mn && out[(size_t)r * mn + t] >= 0; ++t) g.tokens.push_back(out[(size_t)r * mn + t]);
+    g.finished = fin[r] != 0;
+    if (include_logprobs && !g.tokens.empty()) g.logprobs.assign(g.tokens.size(), lp[r] / (float)g.tokens.size());
+    g.total_time_ms = ms;
+    results.push_back(std::move(g));
+  }
+  return results;
 }
 std::vector<float> InferenceEngine::compute_logprobs(const std::vector<int>&) { off_path("compute_logprobs", "rank 1"); }
 std::vector<int> InferenceEngine::encode(const std::string&) { off_path("encode", "-- the tokenizer"); }

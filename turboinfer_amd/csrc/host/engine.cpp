@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <queue>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -935,6 +936,161 @@ int ti_engine_generate_sampled(ti_engine* e, int n, const int32_t* prompts, cons
     for (int m = 0; m < n; ++m)
       for (int t = 0; t < max_new; ++t)
         out_logprobs[(size_t)m * max_new + t] = out_tokens[(size_t)m * max_new + t] < 0 ? 0.0f : lp[(size_t)m * e->draw_cap + t];
+  }
+  return TI_OK;
+}
+
+// ------------------------------------------------------------------------- beam search
+// InferenceEngine::generate_beam_search / beam_search_decode (inference_engine.cpp:830-871,
+// 1912-2069) with the reference's control flow, scoring and container orders (max-heap on
+// log_prob, std::sort on probabilities and normalised scores) and its helpers softmax /
+// apply_top_k_filtering / apply_top_p_filtering (:1798-1910).  One deviation: the reference
+// reads seq_len x vocab "logits" of its full-sequence forward pass as one distribution; here
+// a candidate's next-token distribution is its last position's logits, computed on the device
+// by a full forward pass over the candidate's tokens (prefill + one step), as the reference
+// recomputes each candidate from scratch.
+namespace {
+struct Beam {
+  std::vector<int32_t> tokens;
+  float log_prob = 0.0f;
+  float normalized_score = 0.0f;
+  bool finished = false;
+};
+
+std::vector<float> beam_softmax(const std::vector<float>& lg) {
+  std::vector<float> p(lg.size());
+  const float mx = *std::max_element(lg.begin(), lg.end());
+  float sum = 0.0f;
+  for (size_t i = 0; i < lg.size(); ++i) {
+    p[i] = std::exp(lg[i] - mx);
+    sum += p[i];
+  }
+  if (sum > 0.0f)
+    for (auto& x : p) x /= sum;
+  return p;
+}
+
+std::vector<float> beam_top_k(const std::vector<float>& probs, size_t k) {
+  std::vector<float> f = probs;
+  if (k >= probs.size()) return f;
+  std::vector<std::pair<float, size_t>> pi;
+  for (size_t i = 0; i < probs.size(); ++i) pi.emplace_back(probs[i], i);
+  std::sort(pi.begin(), pi.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  for (size_t i = k; i < pi.size(); ++i) f[pi[i].second] = 0.0f;
+  float sum = 0.0f;
+  for (float x : f) sum += x;
+  if (sum > 0.0f)
+    for (auto& x : f) x /= sum;
+  return f;
+}
+
+std::vector<float> beam_top_p(const std::vector<float>& probs, float p) {
+  std::vector<float> f = probs;
+  if (p >= 1.0f) return f;
+  std::vector<std::pair<float, size_t>> pi;
+  for (size_t i = 0; i < probs.size(); ++i) pi.emplace_back(probs[i], i);
+  std::sort(pi.begin(), pi.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  float cum = 0.0f;
+  std::vector<bool> in(probs.size(), false);
+  for (const auto& pr : pi) {
+    cum += pr.first;
+    in[pr.second] = true;
+    if (cum >= p) break;
+  }
+  for (size_t i = 0; i < probs.size(); ++i)
+    if (!in[i]) f[i] = 0.0f;
+  float sum = 0.0f;
+  for (float x : f) sum += x;
+  if (sum > 0.0f)
+    for (auto& x : f) x /= sum;
+  return f;
+}
+}  // namespace
+
+int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int len, int max_new, int beam_size, float temperature,
+                          int top_k, float top_p, float length_penalty, int eos, int32_t* out_tokens,
+                          float* out_log_prob, float* out_score, int32_t* out_finished, int* out_count) {
+  if (!e || !prompt || !out_tokens || !out_count || len < 1 || max_new < 1)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_beam_search: bad arguments");
+  if (beam_size < 1) return ti_set_error(TI_ERR_ARG, "ti_engine_beam_search: Beam size must be greater than 0");
+  const ti_engine_config& c = e->c;
+  if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_beam_search: compat engine");
+  if (len + max_new - 1 > c.max_seq)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_beam_search: %d + %d tokens exceed max_seq %d", len, max_new, c.max_seq);
+  const size_t V = (size_t)c.vocab;
+  std::vector<float> logits(V);
+  auto forward = [&](const std::vector<int32_t>& toks) -> int {   // last position's logits
+    int32_t n = (int32_t)toks.size(), tok = 0;
+    return ti_engine_generate(e, 1, toks.data(), &n, n, nullptr, 1, &tok, logits.data());
+  };
+  auto cmp = [](const Beam& a, const Beam& b) { return a.log_prob < b.log_prob; };
+  std::priority_queue<Beam, std::vector<Beam>, decltype(cmp)> beam(cmp);
+  Beam init;
+  init.tokens.assign(prompt, prompt + len);
+  beam.push(init);
+  std::vector<Beam> done;
+  const size_t bs = (size_t)beam_size, target = (size_t)len + (size_t)max_new;
+  for (int step = 0; step < max_new; ++step) {
+    std::vector<Beam> cur;
+    while (!beam.empty()) {
+      cur.push_back(beam.top());
+      beam.pop();
+    }
+    if (cur.empty()) break;
+    std::vector<Beam> next;
+    for (const auto& cand : cur) {
+      if (cand.finished) {
+        done.push_back(cand);
+        continue;
+      }
+      TI_TRY(forward(cand.tokens));
+      std::vector<float> lg = logits;
+      if (temperature != 1.0f)
+        for (auto& x : lg) x /= temperature;
+      std::vector<float> probs = beam_softmax(lg);
+      if (top_k > 0 && (size_t)top_k < probs.size()) probs = beam_top_k(probs, (size_t)top_k);
+      if (top_p < 1.0f) probs = beam_top_p(probs, top_p);
+      std::vector<std::pair<float, int>> pt;
+      for (size_t i = 0; i < probs.size(); ++i)
+        if (probs[i] > 0.0f) pt.emplace_back(probs[i], (int)i);
+      std::sort(pt.begin(), pt.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+      const size_t ex = std::min(bs, pt.size());
+      for (size_t i = 0; i < ex; ++i) {
+        if (pt[i].first <= 0.0f) continue;
+        Beam nb = cand;
+        nb.tokens.push_back(pt[i].second);
+        nb.log_prob += std::log(pt[i].first);
+        nb.finished = pt[i].second == eos || nb.tokens.size() >= target;
+        next.push_back(std::move(nb));
+      }
+    }
+    for (auto& b : next) b.normalized_score = b.log_prob / std::pow((float)b.tokens.size(), length_penalty);
+    std::sort(next.begin(), next.end(), [](const Beam& a, const Beam& b) { return a.normalized_score > b.normalized_score; });
+    const size_t keep = std::min(bs, next.size());
+    for (size_t i = 0; i < keep; ++i) {
+      if (next[i].finished) done.push_back(next[i]);
+      else beam.push(next[i]);
+    }
+    if (done.size() >= bs) break;
+  }
+  while (!beam.empty()) {
+    Beam b = beam.top();
+    beam.pop();
+    b.finished = true;
+    done.push_back(b);
+  }
+  std::sort(done.begin(), done.end(), [](const Beam& a, const Beam& b) { return a.normalized_score > b.normalized_score; });
+  const size_t nres = std::min(bs, done.size());
+  *out_count = (int)nres;
+  for (size_t r = 0; r < nres; ++r) {
+    const Beam& b = done[r];
+    for (int t = 0; t < max_new; ++t) {
+      const size_t j = (size_t)len + (size_t)t;
+      out_tokens[r * max_new + t] = j < b.tokens.size() ? b.tokens[j] : -1;
+    }
+    if (out_log_prob) out_log_prob[r] = b.log_prob;
+    if (out_score) out_score[r] = b.normalized_score;
+    if (out_finished) out_finished[r] = b.finished ? 1 : 0;
   }
   return TI_OK;
 }
