@@ -92,6 +92,17 @@ int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int prompt_len, i
                           int32_t* out_tokens, float* out_log_prob, float* out_score, int32_t* out_finished,
                           int* out_count);
 
+/* Continuous batching (generate_batch, inference_engine.cpp:804-828, at
+ * serving scale): n_req greedy requests through the engine's max_batch stream slots.  The
+ * device loop runs in chunks of up to `chunk` steps; between chunks, requests that ended
+ * (eos_token, max_new) leave their slot and queued requests take it: the prompt is prefilled
+ * into that slot's KV and the request joins the next chunk at its last prompt token, while the
+ * other slots continue at their own positions.  prompts: concatenated token ids, request r
+ * = prompts[offsets[r] .. offsets[r+1]); out_tokens [n_req][max_new] (-1 padded), out_len
+ * [n_req] = tokens produced (the eos token included). */
+int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32_t* offsets, int max_new, int eos_token,
+                    int chunk, int32_t* out_tokens, int32_t* out_len);
+
 /* Prefill of ti_engine_generate's prompts (reference forward_pass, inference_engine.cpp:
  * 1429-1491): all but the last token of the shortest prompt are processed `rows` tokens at a
  * time as rows of the batched GEMMs and causal attention over the stream's own KV cache,

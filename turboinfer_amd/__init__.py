@@ -79,7 +79,7 @@ EXPORTED = [
     "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token", "ti_gemm_wq_a16_chained", "ti_gemm_chainable",
     "ti_attn_decode_chained", "ti_step_begin_chained", "ti_engine_set_chain", "ti_gemm_grid", "ti_engine_set_fold",
     "ti_attn_decode_partials", "ti_sample_device", "ti_sample_step", "ti_engine_generate_sampled",
-    "ti_engine_beam_search",
+    "ti_engine_beam_search", "ti_engine_serve",
 ]
 
 _lib = None
@@ -126,6 +126,8 @@ def lib() -> C.CDLL:
         if hasattr(L, "ti_sample_device"):
             L.ti_sample_device.argtypes = [vp, i32, i32, i32, f32, i32, f32, vp, vp, vp, vp]
             L.ti_engine_generate_sampled.argtypes = [vp, i32, vp, vp, i32, vp, i32, f32, i32, f32, vp, vp, vp]
+        if hasattr(L, "ti_engine_serve"):
+            L.ti_engine_serve.argtypes = [vp, i32, vp, vp, i32, i32, i32, vp, vp]
         if hasattr(L, "ti_engine_beam_search"):
             L.ti_engine_beam_search.argtypes = [vp, vp, i32, i32, i32, f32, i32, f32, f32, i32, vp, vp, vp, vp,
                                                 C.POINTER(C.c_int)]
@@ -342,6 +344,16 @@ class Engine:
                                           C.byref(cnt)))
         return [([int(t) for t in out[r] if t >= 0], float(lp[r]), float(sc[r]), bool(fin[r]))
                 for r in range(cnt.value)]
+
+    def serve(self, prompts, max_new, eos=2, chunk=16):
+        """ti_engine_serve (continuous batching): each request's new tokens, in request order."""
+        flat = np.ascontiguousarray([t for p in prompts for t in p], np.int32)
+        offs = np.ascontiguousarray(np.cumsum([0] + [len(p) for p in prompts]), np.int32)
+        out = np.zeros((len(prompts), max_new), np.int32)
+        n = np.zeros(len(prompts), np.int32)
+        check(lib().ti_engine_serve(self.h, len(prompts), _ptr(flat), _ptr(offs), max_new, eos, chunk, _ptr(out),
+                                    _ptr(n)))
+        return [out[r, : n[r]].tolist() for r in range(len(prompts))]
 
     def set_prefill(self, rows):
         """Prompt tokens per prefill chunk (0 = consume prompts one token per decode step)."""

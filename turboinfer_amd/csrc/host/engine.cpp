@@ -1095,6 +1095,99 @@ int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int len, int max_
   return TI_OK;
 }
 
+// ------------------------------------------------------------------ continuous batching
+// Requests flow through the engine's max_batch stream slots.  Every chunk of the device loop
+// starts with each slot feeding one token at its own position (step_ctr 0, n_in 1): a
+// continuing request its last generated token, a newly admitted one the last token of its
+// prompt, whose other tokens were prefilled into the slot's KV (enqueue_prefill) just before.
+// After the chunk the slots' new tokens are read back (the step feed record + the last
+// argmax); finished requests (EOS, max_new) free their slot for the next queued request.
+int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32_t* offsets, int max_new, int eos,
+                    int chunk, int32_t* out_tokens, int32_t* out_len) {
+  if (!e || !prompts || !offsets || !out_tokens || !out_len || n_req < 1 || max_new < 1 || chunk < 1)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_serve: bad arguments");
+  const ti_engine_config& c = e->c;
+  if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_serve: compat engine");
+  const int B = c.max_batch;
+  const int pf = e->pf_rows > 0 ? e->pf_rows : std::min(e->rows_cap, c.bits == 4 ? TI_GEMM_MAX_ROWS : 16);
+  int max_len = 1;
+  for (int r = 0; r < n_req; ++r) {
+    const int L = offsets[r + 1] - offsets[r];
+    if (L < 1 || L + max_new - 1 > c.max_seq)
+      return ti_set_error(TI_ERR_ARG, "ti_engine_serve: request %d: %d prompt + %d new tokens exceed max_seq %d", r, L,
+                          max_new, c.max_seq);
+    max_len = std::max(max_len, L);
+  }
+  TI_TRY(ensure_io(e, max_len, chunk + 1));
+  for (int i = 0; i < n_req * max_new; ++i) out_tokens[i] = -1;
+  for (int r = 0; r < n_req; ++r) out_len[r] = 0;
+  std::vector<int> slot_req(B, -1), slot_pos(B, 0), slot_tok(B, 0);
+  std::vector<int32_t> in((size_t)B * e->in_cap, 0), nin(B, 1), base(B, 0), outd((size_t)B * e->out_cap);
+  std::vector<unsigned long long> am;
+  int next = 0, live = 0;
+  for (;;) {
+    // admit queued requests into free slots: prefill all but the prompt's last token
+    std::vector<int> fresh;
+    for (int m = 0; m < B && next < n_req; ++m)
+      if (slot_req[m] < 0) {
+        const int r = next++, L = offsets[r + 1] - offsets[r];
+        slot_req[m] = r;
+        slot_pos[m] = L - 1;
+        slot_tok[m] = prompts[offsets[r] + L - 1];
+        fresh.push_back(m);
+        ++live;
+      }
+    if (live == 0) break;
+    if (!fresh.empty()) {
+      for (int m : fresh) {
+        const int r = slot_req[m], L = offsets[r + 1] - offsets[r];
+        std::memcpy(&in[(size_t)m * e->in_cap], prompts + offsets[r], (size_t)L * 4);
+      }
+      TI_TRY(ti_memcpy_h2d(e->in_tokens, in.data(), in.size() * 4, e->s));
+      for (int m : fresh) {
+        const int L = offsets[slot_req[m] + 1] - offsets[slot_req[m]];
+        for (int t0 = 0; t0 < L - 1; t0 += pf) TI_TRY(enqueue_prefill(e, m, t0, std::min(pf, L - 1 - t0), 0));
+      }
+    }
+    // one chunk: every slot feeds one token at its position; no slot may run past max_seq
+    int S = chunk;
+    for (int m = 0; m < B; ++m) {
+      nin[m] = 1;
+      base[m] = slot_req[m] >= 0 ? slot_pos[m] : 0;
+      in[(size_t)m * e->in_cap] = slot_req[m] >= 0 ? slot_tok[m] : 0;
+      if (slot_req[m] >= 0) S = std::min(S, c.max_seq - slot_pos[m]);
+    }
+    // (stream order: these copies land after the prefill launches have read in_tokens)
+    TI_TRY(ti_memcpy_h2d(e->in_tokens, in.data(), in.size() * 4, e->s));
+    TI_TRY(ti_memcpy_h2d(e->n_in, nin.data(), (size_t)B * 4, e->s));
+    TI_TRY(ti_memcpy_h2d(e->base_pos, base.data(), (size_t)B * 4, e->s));
+    const int32_t zero = 0;
+    TI_TRY(ti_memcpy_h2d(e->step_ctr, &zero, 4, e->s));
+    TI_TRY(run_steps(e, B, 1, S));
+    TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
+    TI_TRY(read_argmax(e, B, am));   // synchronises the stream
+    for (int m = 0; m < B; ++m) {
+      const int r = slot_req[m];
+      if (r < 0) continue;
+      // the token generated at chunk step s: fed back and recorded at step s + 1, the last
+      // one still in the argmax slots
+      for (int s = 0; s < S && slot_req[m] >= 0; ++s) {
+        const int32_t tok = s < S - 1 ? outd[(size_t)m * e->out_cap + s]
+                                      : (int32_t)(0xFFFFFFFFu - (uint32_t)(am[m] & 0xFFFFFFFFull));
+        out_tokens[(size_t)r * max_new + out_len[r]++] = tok;
+        slot_tok[m] = tok;
+        if (out_len[r] >= max_new || tok == eos) {
+          slot_req[m] = -1;
+          --live;
+        }
+      }
+      if (slot_req[m] >= 0) slot_pos[m] += S;
+    }
+    TI_TRY(chain_check(e));
+  }
+  return TI_OK;
+}
+
 int ti_engine_set_prefill(ti_engine* e, int rows) {
   if (!e || e->c.compat || rows < 0 || rows > e->rows_cap || (rows > 0 && rows > (e->c.bits == 4 ? TI_GEMM_MAX_ROWS : 16)))
     return ti_set_error(TI_ERR_ARG, "ti_engine_set_prefill: rows %d", rows);
