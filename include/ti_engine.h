@@ -127,6 +127,12 @@ int ti_engine_set_chain(ti_engine* e, int on, int* active);
  * on = 0/1 sets both, -1 leaves them; *active (nullable) receives whether 1-stream steps fold. */
 int ti_engine_set_fold(ti_engine* e, int on, int* active);
 
+/* QKV projection + attention of single-stream steps in one launch (ti_hip.h
+ * ti_qkv_attn_fused): applies on top of the fold and the attention partials (both on), int4
+ * weights, heads == kv_heads, head_dim 64/128.  on = 1 (or env TI_QKV_ATTN=1) / 0 / -1 leaves
+ * it; *active (nullable) receives whether 1-stream steps use it. */
+int ti_engine_set_qkv_attn(ti_engine* e, int on, int* active);
+
 /* One decode step: token[s] at position pos[s] for each stream; logits [n][vocab] to host
  * (used for non-greedy sampling and per-step parity). */
 int ti_engine_step(ti_engine* e, int n_streams, const int32_t* tokens, const int32_t* pos, float* logits);

@@ -252,6 +252,17 @@ int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, const uint1
                             int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
                             int kv_heads, int head_dim, int splits, uint16_t* part_o, float* part_ml,
                             ti_stream_t s);
+/* The QKV projection and ti_attn_decode_partials of one stream in ONE launch (int4 weights,
+ * heads == kv_heads, head_dim 64/128): x is TI_X_F16_FOLDED (epi->ss_in / n_ss as for
+ * ti_gemm_wq_a16), epi a TI_EPI_QKV_ROPE_KV epilogue (q to epi->out, K/V row appended at
+ * pos).  Workgroup (head h, split s) computes tile s of head h in q, k and v, hands them to
+ * the head's other workgroups through `counters` (per head 16 words, zero before the first
+ * call and left zero by every call) and runs split s of head h's attention; partials as
+ * ti_attn_decode_partials with splits = head_dim / 16.  A hand-off wait longer than ~20 ms
+ * sets *abort_flag. */
+int ti_qkv_attn_fused(const void* tiles, const uint16_t* scales, const uint16_t* x, float eps, int K,
+                      const ti_epilogue* epi, uint16_t* part_o, float* part_ml, uint32_t* counters,
+                      uint32_t* abort_flag, ti_stream_t s);
 /* One launch of a chain (ti_chain): the same attention; K/V, q and pos read with sc1 loads
  * after the wait, out stored write-through. */
 int ti_attn_decode_chained(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,

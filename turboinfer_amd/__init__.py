@@ -79,7 +79,7 @@ EXPORTED = [
     "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token", "ti_gemm_wq_a16_chained", "ti_gemm_chainable",
     "ti_attn_decode_chained", "ti_step_begin_chained", "ti_engine_set_chain", "ti_gemm_grid", "ti_engine_set_fold",
     "ti_attn_decode_partials", "ti_sample_device", "ti_sample_step", "ti_engine_generate_sampled",
-    "ti_engine_beam_search", "ti_engine_serve",
+    "ti_engine_beam_search", "ti_engine_serve", "ti_qkv_attn_fused", "ti_engine_set_qkv_attn",
 ]
 
 _lib = None
@@ -133,6 +133,9 @@ def lib() -> C.CDLL:
                                                 C.POINTER(C.c_int)]
         if hasattr(L, "ti_attn_decode_partials"):
             L.ti_attn_decode_partials.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
+        if hasattr(L, "ti_qkv_attn_fused"):
+            L.ti_qkv_attn_fused.argtypes = [vp, vp, vp, f32, i32, C.POINTER(Epilogue), vp, vp, vp, vp, vp]
+            L.ti_engine_set_qkv_attn.argtypes = [vp, i32, C.POINTER(C.c_int)]
         L.ti_step_begin.argtypes = [C.POINTER(StepArgs), vp]
         L.ti_matmul_f32.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, vp]
         L.ti_rms_norm_f32.argtypes = [vp, vp, vp, i32, i32, f32, vp]
@@ -369,6 +372,13 @@ class Engine:
         """Folded rms_norm hand-off on/off (None: query); returns whether 1-stream steps use it."""
         act = C.c_int(0)
         check(lib().ti_engine_set_fold(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
+        return bool(act.value)
+
+    def set_qkv_attn(self, on=None) -> bool:
+        """QKV projection + attention in one launch on/off (None: query); returns whether
+        1-stream steps use it (needs the fold and the attention partials)."""
+        act = C.c_int(0)
+        check(lib().ti_engine_set_qkv_attn(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
         return bool(act.value)
 
     def step(self, tokens, pos):

@@ -98,6 +98,10 @@ struct ti_engine {
   // single-stream attention leaves its split merge to the O projection (ti_attn_decode_partials
   // + TI_X_ATTN_SPLITS): no arrival-ticket hand-off at the end of the attention launch
   bool part_on = true;         // TI_ATTN_PART=0 turns it off
+  // QKV projection + attention in one launch (ti_qkv_attn_fused) when the step folds and
+  // hands partials over: ti_engine_set_qkv_attn / TI_QKV_ATTN
+  bool qa_on = false;
+  uint32_t* qa_ctr = nullptr;  // [heads][16], zero between launches
   uint16_t* part_o = nullptr;  // [heads][TI_ATTN_MAX_PART_SPLITS][head_dim]
   float* part_ml = nullptr;    // [heads][TI_ATTN_MAX_PART_SPLITS][2]
   // on-device sampling (ti_engine_generate_sampled): the step graph ends with ti_sample_step
@@ -403,6 +407,14 @@ bool part_usable(ti_engine* e, int M) {
          e->qd() <= 4096;
 }
 
+// QKV + attention fused (ti_qkv_attn_fused): on top of the fold and the partials, int4,
+// heads == kv_heads, head_dim 64 / 128.
+bool qa_usable(ti_engine* e, int M) {
+  const ti_engine_config& c = e->c;
+  return e->qa_on && e->qa_ctr && e->part_on && e->part_o && fold_usable(e, M) && c.bits == 4 &&
+         c.heads == c.kv_heads && (c.head_dim == 64 || c.head_dim == 128) && e->qd() <= 4096;
+}
+
 // One decode step for streams [0, M) on e->s.  Graph-capturable (no host sync / alloc).
 int enqueue_step(ti_engine* e, int M, int advance) {
   const ti_engine_config& c = e->c;
@@ -424,7 +436,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   sa.step_ctr = e->step_ctr;
   const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
   // fold (M == 1): every rms_norm input is handed over as fx + ss partials by its producer
-  const bool fold = fold_usable(e, M), part = part_usable(e, M);
+  const bool fold = fold_usable(e, M), part = part_usable(e, M), qa = qa_usable(e, M);
   auto next_norm = [&](int l) -> const float* { return l < c.layers ? e->layer[l].attn_norm : e->out_norm; };
   if (fold) {
     sa.fold_w = next_norm(0);
@@ -472,14 +484,22 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     ep.k_cache = L.kc;
     ep.v_cache = L.vc;
     ep.kv_stream_stride = e->kv_stride;
-    TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));
-
     ti_epilogue eo{};
     eo.kind = TI_EPI_RESID_F32;
     eo.ldo = H;
     eo.out = e->h;
     fold_into(eo, L.ffn_norm);
-    if (part) {   // the O projection merges the attention's splits while staging its input
+    if (qa) {   // one launch: QKV tiles of a head, hand-off within the head, its attention splits
+      ep.ss_in = e->ss;
+      ep.n_ss = n_ss;
+      TI_TRY(ti_qkv_attn_fused(L.qkv.tiles, L.qkv.scales, e->fx, c.eps, H, &ep, e->part_o, e->part_ml, e->qa_ctr,
+                               e->chain_abort, e->s));
+      eo.ss_in = e->part_ml;
+      eo.n_ss = c.head_dim / 16;
+      eo.head_dim = c.head_dim;
+      TI_TRY(gemm(L.o, e->part_o, TI_X_ATTN_SPLITS, qd, 2, nullptr, eo, 4, false));
+    } else if (part) {   // the O projection merges the attention's splits while staging its input
+      TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));
       TI_TRY(ti_attn_decode_partials(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M, c.heads, c.kv_heads,
                                      c.head_dim, e->splits_for(M), e->part_o, e->part_ml, e->s));
       eo.ss_in = e->part_ml;
@@ -487,6 +507,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
       eo.head_dim = c.head_dim;
       TI_TRY(gemm(L.o, e->part_o, TI_X_ATTN_SPLITS, qd, 2, nullptr, eo, 4, false));
     } else {
+      TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));
       TI_TRY(ti_attn_decode(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M, c.heads, c.kv_heads, c.head_dim,
                             e->splits_for(M), e->ws, e->attn, e->s));
       TI_TRY(gemm(L.o, e->attn, TI_X_F16, qd, 2, nullptr, eo, 4, false));
@@ -703,6 +724,8 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
       return fail(rc);
     if (const char* env = getenv("TI_ATTN_PART")) e->part_on = atoi(env) != 0;
     if (const char* env = getenv("TI_FOLD")) e->fold_on = atoi(env) != 0;
+    if ((rc = e->alloc_t(&e->qa_ctr, (size_t)c.heads * 16))) return fail(rc);
+    if (const char* env = getenv("TI_QKV_ATTN")) e->qa_on = atoi(env) != 0;
     e->chain_slots = 2 + 5 * c.layers;
     e->chain_cum.assign((size_t)e->chain_slots, 0u);
     if ((rc = e->alloc_t(&e->chain_ctr, (size_t)e->chain_slots * TI_CHAIN_SHARDS)) || (rc = e->alloc_t(&e->chain_abort, (size_t)1)))
@@ -1293,6 +1316,18 @@ int ti_engine_set_fold(ti_engine* e, int on, int* active) {
     e->fold_on = e->part_on = on != 0;
   }
   if (active) *active = fold_usable(e, 1) ? 1 : 0;
+  return TI_OK;
+}
+
+int ti_engine_set_qkv_attn(ti_engine* e, int on, int* active) {
+  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_qkv_attn: null");
+  if (on >= 0 && (on != 0) != e->qa_on) {
+    TI_TRY(ti_stream_sync(e->s));   // captured step graphs bake the setting in
+    for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
+    e->graphs.clear();
+    e->qa_on = on != 0;
+  }
+  if (active) *active = qa_usable(e, 1) ? 1 : 0;
   return TI_OK;
 }
 

@@ -111,8 +111,12 @@ __device__ __forceinline__ float groups_sum(float v) {
 
 // CH: one launch of a chain (ti_chain): wait first, then pos, q and K/V with sc1 loads, the
 // output stored write-through in fp16 pairs, and every workgroup signals once.
-template <int HD, int G, int R, bool HP, bool CH = false>   // HP: head-parallel lanes (G >= 4, HD / (64 / G) == 8; see below)
+// EARLY (CH, not HP): pos was written before this launch, so a split whose range does not hold
+// the fresh row at pos issues its K/V ring before the wait (only q comes from the producer);
+// the split holding it waits first.
+template <int HD, int G, int R, bool HP, bool CH = false, bool EARLY = false>   // HP: head-parallel lanes (G >= 4, HD / (64 / G) == 8; see below)
 __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, int kvh, int m, unsigned flat_block) {
+  static_assert(!EARLY || (CH && !HP), "EARLY: chained, lane-group layout");
   static_assert(!HP || (G >= 4 && HD / (64 / G) == 8), "head-parallel layout: 8 dims per lane");
   constexpr int LPK = HD / 8;       // lanes per key row
   constexpr int KPW = 64 / LPK;     // keys per slot (wave-load)
@@ -125,8 +129,8 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int dl = lane % LPK, kg = lane / LPK;
-  if constexpr (CH) chain_wait(a.chain);
-  const int L = (CH ? (int)__builtin_amdgcn_readfirstlane(ld_sc1_u32(a.pos + m)) : a.pos[m]) + 1;
+  if constexpr (CH && !EARLY) chain_wait(a.chain);
+  const int L = (CH && !EARLY ? (int)__builtin_amdgcn_readfirstlane(ld_sc1_u32(a.pos + m)) : a.pos[m]) + 1;
   // K/V of this workgroup's (stream, kv-head): [max_seq][HD] fp16 from wg_off
   const int64_t wg_off = (int64_t)m * a.stride + (int64_t)kvh * a.max_seq * HD;
   const __amdgpu_buffer_rsrc_t rk = sc1_rsrc(a.kc + wg_off), rv = sc1_rsrc(a.vc + wg_off), rq = sc1_rsrc(a.q);
@@ -255,8 +259,15 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
       kr[s] = ld_k((int64_t)key * HD + dl * 8);
       vr[s] = ld_v((int64_t)key * HD + dl * 8);
     };
+    const bool fresh_here = s1 == L && s1 > s0;   // workgroup-uniform
+    if constexpr (EARLY) {
+      if (fresh_here) chain_wait(a.chain);
+    }
   #pragma unroll
     for (int s = 0; s < R; ++s) refill(s);
+    if constexpr (EARLY) {
+      if (!fresh_here) chain_wait(a.chain);
+    }
 
     float q[G][8];
   #pragma unroll

@@ -27,6 +27,7 @@
 #include <stdlib.h>
 
 #include "common.hpp"
+#include "attention_body.hpp"
 
 namespace ti {
 
@@ -378,12 +379,14 @@ __device__ __forceinline__ void lds_barrier() {
 //          (max, sum) pairs (XM_ATTN), else NULL
 //   p_mgk: M | grid << 6 | epilogue kind << 18 | head_dim / 64 << 21 (XM_ATTN)
 //   p_kx:  K | (ldx, or n_ss for XM_F16F, or splits for XM_ATTN) << 16
-template <int BITS, int XM, bool CH = false>
-__global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
-                                                                   const void* p_x, const float* p_aux, int p_mgk,
-                                                                   int p_N, int p_kx, int p_ldo, const float* p_pre,
-                                                                   const GemvArgs a_in) {
-  GemvArgs a = a_in;
+// The body is a device function: gemv_wq_kernel runs it over workgroup blockIdx.x's contiguous
+// tile range; STR (the fused QKV + attention launch below) over ntl_in tiles t0_in + i * tstr_in
+// chosen by the caller, bid standing in for blockIdx.x (argmax slot, counter shard, fold slot).
+template <int BITS, int XM, bool CH, bool STR>
+__device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* p_scales, const void* p_x,
+                                          const float* p_aux, int p_mgk, int p_N, int p_kx, int p_ldo,
+                                          const float* p_pre, GemvArgs a, const unsigned bid, const int t0_in,
+                                          const int ntl_in, const int tstr_in) {
   a.tiles = p_tiles;
   a.scales = p_scales;
   a.x = p_x;
@@ -401,9 +404,9 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   const int KT = a.K >> 7, xs = a.K + 8, NT = a.N >> 4, K8 = a.K >> 3;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: counters live in SGPRs
-  const int t0 = (int)(blockIdx.x * (unsigned)NT / (unsigned)p_grid);   // NT * grid < 2^32
-  const int t1 = (int)((blockIdx.x + 1) * (unsigned)NT / (unsigned)p_grid);
-  const int ntl = t1 - t0;
+  const int tstr = STR ? tstr_in : 1;             // tile stride
+  const int t0 = STR ? t0_in : (int)(bid * (unsigned)NT / (unsigned)p_grid);   // NT * grid < 2^32
+  const int ntl = STR ? ntl_in : (int)((bid + 1) * (unsigned)NT / (unsigned)p_grid) - t0;
   const int KW = wave < KT ? (KT - wave + kGemvWaves - 1) / kGemvWaves : 0;   // k-tiles per tile, this wave
   const int total = ntl * KW;
   const GemvLds L = gemv_lds_layout(a.M, a.K, ntl);
@@ -418,6 +421,11 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   // ---- 1. small inputs into registers, ahead of the ring
   const int n_sc = BITS == 16 ? 0 : ntl * KT * 2;  // u32x4 pieces of scales
   const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16);
+  auto sc_off = [&](int i) -> int {                // piece i of the dense [ntl][KT][2] image
+    if constexpr (!STR) return i;
+    const int tl = i / (2 * KT);
+    return i + tl * (tstr - 1) * 2 * KT;
+  };
   u32x4 sc_reg = {0u, 0u, 0u, 0u};
 #if TI_GEMV_EXP & 8   // diagnostic: no dependency on x / scales (constants instead of loads)
   const int nx16 = a.M * K8;
@@ -428,7 +436,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   auto load_x = [&]() {};
   if (false) {
 #else
-  if constexpr (BITS != 16) sc_reg = ld_w(sg + (tid < n_sc ? tid : 0));
+  if constexpr (BITS != 16) sc_reg = ld_w(sg + sc_off(tid < n_sc ? tid : 0));
 
   const int nx16 = a.M * K8;
   float4 v0, v1, w0, w1;
@@ -489,7 +497,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   {
     const int idx = tid < n_res ? tid : 0;
     const int tl = idx / (a.M * 16), rem = idx - tl * a.M * 16, m = rem >> 4, n = rem & 15;
-    pre_p = kind == TI_EPI_RESID_F32 ? p_pre + (size_t)m * ldo + (t0 + tl) * 16 + n
+    pre_p = kind == TI_EPI_RESID_F32 ? p_pre + (size_t)m * ldo + (t0 + tl * tstr) * 16 + n
             : kind == TI_EPI_QKV_ROPE_KV ? p_pre + (tid < a.M ? tid : 0) : p_pre;
   }
   float pre = 0.0f;
@@ -511,10 +519,10 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   // items past the end re-load the last item (no branch around loads); coordinates advance
   // by counters (no integer division in the stream).
   const u32x4* tb = a.tiles + (size_t)t0 * KT * (kWave * C) + lane;
-  const size_t last_off = total > 0 ? ((size_t)(ntl - 1) * KT + wave + kGemvWaves * (KW - 1)) * (kWave * C) : 0;
+  const size_t last_off = total > 0 ? ((size_t)(ntl - 1) * tstr * KT + wave + kGemvWaves * (KW - 1)) * (kWave * C) : 0;
   int rt = 0, rk = 0, rj = 0;                      // refill cursor: tile, k index, item
   auto refill_off = [&]() -> size_t {
-    const size_t o = rj < total ? ((size_t)rt * KT + wave + kGemvWaves * rk) * (kWave * C) : last_off;
+    const size_t o = rj < total ? ((size_t)rt * tstr * KT + wave + kGemvWaves * rk) * (kWave * C) : last_off;
     ++rj;
     if (++rk == KW) { rk = 0; ++rt; }
     return o;
@@ -526,7 +534,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
 #ifndef TI_CHAIN_R0
 #define TI_CHAIN_R0 2   // chained: ring slots issued before the wait (x loads queue behind them)
 #endif
-  constexpr int R0 = CH ? (TI_CHAIN_R0 < R ? TI_CHAIN_R0 : R) : (R >= 8 ? 4 : R);
+  constexpr int R0 = CH && !STR ? (TI_CHAIN_R0 < R ? TI_CHAIN_R0 : R) : (R >= 8 ? 4 : R);
   u32x4 ring[R][C];
 #if TI_GEMV_RING_DELAY > 0   // A/B knob: hold the ring back (x 64 clocks) behind the small loads
   __builtin_amdgcn_s_sleep(TI_GEMV_RING_DELAY);
@@ -608,7 +616,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   }
   // rare shapes: what the register prefetch did not cover (these loads wait behind the ring)
   if constexpr (BITS != 16) {
-    for (int i = tid + kGemvThreads; i < n_sc; i += kGemvThreads) ((u32x4*)sl)[i] = sg[i];
+    for (int i = tid + kGemvThreads; i < n_sc; i += kGemvThreads) ((u32x4*)sl)[i] = sg[sc_off(i)];
   }
   if constexpr (XM == XM_F16 || XM == XM_F16F) {
     if (nx16 > XPF * kGemvThreads) stage_x_generic<XM, CH>(a, xl, red, XPF * kGemvThreads);
@@ -747,7 +755,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   // inputs past the one-per-thread prefetch (ntl * M * 16 or M * head_dim > 512): loaded now
   for (int i = tid + kGemvThreads; i < n_res; i += kGemvThreads) {
     const int tl = i / (a.M * 16), rem = i - tl * a.M * 16, m = rem >> 4, n = rem & 15;
-    const float* pp = p_pre + (size_t)m * ldo + (t0 + tl) * 16 + n;
+    const float* pp = p_pre + (size_t)m * ldo + (t0 + tl * tstr) * 16 + n;
     if constexpr (CH) es[i] = ld_sc1_f32(pp);
     else es[i] = *pp;
     if (fold) es[n_res + i] = a.epi.fold_w[(size_t)t0 * 16 + i];
@@ -782,7 +790,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       for (int w = 1; w < kGemvWaves; ++w) v += sp[w * kWave];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (i < a.M) epilogue<CH>(a, t0 + tl, tl, n, i, XM == XM_F16F ? v[i] / rms : v[i], es, best[i], ok, fw_l, ssacc);
+        if (i < a.M) epilogue<CH>(a, t0 + tl * tstr, tl, n, i, XM == XM_F16F ? v[i] / rms : v[i], es, best[i], ok, fw_l, ssacc);
     }
   } else {
     const int i4 = wave & 3;
@@ -791,7 +799,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       float v = 0.0f;
 #pragma unroll
       for (int w = 0; w < kGemvWaves; ++w) v += sp[w * kWave * 4];
-      epilogue<CH>(a, t0 + tl, tl, lane, i4, v, es, best[0], true, fw_l, ssacc);
+      epilogue<CH>(a, t0 + tl * tstr, tl, lane, i4, v, es, best[0], true, fw_l, ssacc);
     }
   }
   if (a.epi.kind == TI_EPI_LOGITS_ARGMAX) {
@@ -805,16 +813,17 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
     }
     if (a.M <= 4) {
       if ((lane & 15) == 0)
-        for (int i = 0; i < a.M; ++i)
-          if (best[i]) atomicMax(best_l + i, best[i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)   // constant bounds: best[] stays in registers
+          if (i < a.M && best[i]) atomicMax(best_l + i, best[i]);
     } else {
       const int m = 4 * (lane >> 4) + (wave & 3);
       if ((lane & 15) == 0 && m < a.M && best[0]) atomicMax(best_l + m, best[0]);
     }
     lds_barrier();
     if (tid < a.M && best_l[tid])
-      atomicMax(a.epi.argmax + (size_t)tid * TI_ARGMAX_SLOTS + (blockIdx.x & (TI_ARGMAX_SLOTS - 1)), best_l[tid]);
-    if (a.epi.step_ctr && blockIdx.x == 0 && tid == 0) {
+      atomicMax(a.epi.argmax + (size_t)tid * TI_ARGMAX_SLOTS + (bid & (TI_ARGMAX_SLOTS - 1)), best_l[tid]);
+    if (a.epi.step_ctr && bid == 0 && tid == 0) {
       if constexpr (CH) __hip_atomic_fetch_add(a.epi.step_ctr, a.epi.advance, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else *a.epi.step_ctr += a.epi.advance;
     }
@@ -828,11 +837,64 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       float t = 0.0f;
 #pragma unroll
       for (int w = 0; w < kGemvWaves; ++w) t += red2[w];
-      a.epi.fold_ss[blockIdx.x] = t;
+      a.epi.fold_ss[bid] = t;
     }
   }
-  if constexpr (CH) chain_signal(a.chain, blockIdx.x);
+  if constexpr (CH) chain_signal(a.chain, bid);
   GEMV_TS(4);
+}
+
+template <int BITS, int XM, bool CH = false>
+__global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
+                                                                   const void* p_x, const float* p_aux, int p_mgk,
+                                                                   int p_N, int p_kx, int p_ldo, const float* p_pre,
+                                                                   const GemvArgs a_in) {
+  gemv_body<BITS, XM, CH, false>(p_tiles, p_scales, p_x, p_aux, p_mgk, p_N, p_kx, p_ldo, p_pre, a_in, blockIdx.x, 0, 0, 1);
+}
+
+// ============================================================ QKV + attention, one launch
+// ti_qkv_attn_fused (one stream, int4, kv_heads == heads): workgroup (head h, split s) of the
+// heads x S grid (S = HD / 16) first computes tile s of head h in each of the q, k and v
+// projections (tiles h*S + s + {0, 1, 2} * q_dim/16 of the folded-input QKV GEMV, RoPE + KV
+// append epilogue stored write-through), so the head's S workgroups together produce its q
+// row and its K/V row at pos; it then signals the head's counter, waits for the head's other
+// workgroups (chain_wait on the S shards) and runs split s of that head's attention in
+// partials mode (the O projection merges, TI_X_ATTN_SPLITS).  The launch boundary between
+// the QKV GEMV and the attention becomes a hand-off between the S workgroups of one head.
+// Counters: per head 8 shards + one pass count; the S-th workgroup past the wait re-arms them,
+// so they are zero between launches (zeroed once by the caller).
+#ifndef TI_QA_RING
+#define TI_QA_RING 4   // K/V slots per wave, issued before the hand-off wait
+#endif
+template <int HD>
+__global__ __launch_bounds__(kGemvThreads, 1) void qkv_attn_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
+                                                                    const void* p_x, const float* p_aux, int p_mgk,
+                                                                    int p_N, int p_kx, int p_ldo, const float* p_pre,
+                                                                    const GemvArgs ga, const AttnArgs aa,
+                                                                    uint32_t* ctr) {
+  constexpr int S = HD / 16;
+  static_assert(S <= TI_CHAIN_SHARDS, "one counter shard per split");
+  const unsigned h = blockIdx.x / S, s = blockIdx.x - h * S;
+  uint32_t* hc = ctr + h * 16;
+  {
+    GemvArgs g = ga;
+    g.chain.wait_ctr = nullptr;
+    g.chain.signal_ctr = hc;
+    gemv_body<4, XM_F16F, true, true>(p_tiles, p_scales, p_x, p_aux, p_mgk, p_N, p_kx, p_ldo, p_pre, g, s, h * S + s, 3,
+                                      p_N / 48);
+  }
+  AttnArgs at = aa;
+  at.chain.wait_ctr = hc;
+  at.chain.signal_ctr = nullptr;
+  at.chain.wait_target = S;
+  attn_split_body<HD, 1, TI_QA_RING, false, true, true>(at, s, h, 0, blockIdx.x);
+  if (threadIdx.x == 0) {
+    const uint32_t n = __hip_atomic_fetch_add(hc + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n == S - 1) {
+#pragma unroll
+      for (int i = 0; i <= 8; ++i) st_sc1_u32(hc + i, 0u);
+    }
+  }
 }
 
 
@@ -1528,6 +1590,69 @@ extern "C" int ti_gemm_chainable(int bits, int x_kind, int M, int N, int K) {
   if (xm != XM_F16 && xm != XM_NORM1) return 0;
   const int grid = gemv_grid(M, N, K, query_cus());
   return gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid) <= 160 * 1024 ? 1 : 0;
+}
+
+extern "C" int ti_qkv_attn_fused(const void* tiles, const uint16_t* scales, const uint16_t* x, float eps, int K,
+                                 const ti_epilogue* epi, uint16_t* part_o, float* part_ml, uint32_t* counters,
+                                 uint32_t* abort_flag, ti_stream_t stream) {
+  using namespace ti;
+  if (!tiles || !scales || !x || !epi || !epi->out || !part_o || !part_ml || !counters || !abort_flag)
+    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_fused: null pointer");
+  const int hd = epi->head_dim, qd = epi->q_dim, N = qd + 2 * epi->kv_dim;
+  if (epi->kind != TI_EPI_QKV_ROPE_KV || !epi->pos || !epi->rope_cs || !epi->k_cache || !epi->v_cache ||
+      (hd != 64 && hd != 128) || epi->kv_dim != qd || qd % hd || epi->ldo < qd || epi->max_seq < 1 ||
+      epi->kv_stream_stride < (int64_t)qd * epi->max_seq)
+    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_fused: needs a QKV_ROPE_KV epilogue with kv_dim == q_dim, head_dim 64/128");
+  if (!epi->ss_in || epi->n_ss < 1 || epi->n_ss > 256)
+    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_fused: x is TI_X_F16_FOLDED: ss_in and 1 <= n_ss <= 256 required");
+  if (K < 128 || (K & 127) || K > 0xffff) return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_fused: bad K %d", K);
+  if (((uintptr_t)epi->out & 3) || ((uintptr_t)epi->k_cache & 3) || ((uintptr_t)epi->v_cache & 3))
+    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_fused: outputs must be 4-byte aligned");
+  if ((int64_t)epi->max_seq * hd * 2 >= 0x7fffffffLL)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_fused: a head's cache exceeds 2 GiB");
+  const int S = hd / 16, heads = qd / hd, grid = heads * S;
+  const int lds = gemv_lds_bytes_tiles(1, K, 3);
+  if (lds > 96 * 1024 || grid > 0xfff)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_fused: K %d / heads %d too large", K, heads);
+  GemvArgs a{};
+  a.tiles = (const u32x4*)tiles;
+  a.scales = scales;
+  a.x = x;
+  a.norm_w = nullptr;
+  a.eps = eps;
+  a.x_kind = TI_X_F16_FOLDED;
+  a.ldx = K;
+  a.M = 1;
+  a.N = N;
+  a.K = K;
+  a.epi = *epi;
+  a.chain = ChainDev{nullptr, nullptr, abort_flag, 0u, 0u};
+  AttnArgs t{};
+  t.q = (const float*)epi->out;
+  t.kc = epi->k_cache;
+  t.vc = epi->v_cache;
+  t.pos = epi->pos;
+  t.stride = epi->kv_stream_stride;
+  t.max_seq = epi->max_seq;
+  t.M = 1;
+  t.heads = heads;
+  t.kv_heads = heads;
+  t.splits = S;
+  t.scale = 1.0f / sqrtf((float)hd);   // tensor_engine.cpp:1288
+  t.chain = ChainDev{nullptr, nullptr, abort_flag, 0u, 0u};
+  t.part_o = part_o;
+  t.part_ml = part_ml;
+  const int mgk = 1 | (grid << 6) | (TI_EPI_QKV_ROPE_KV << 18);
+  const int kx = K | (epi->n_ss << 16);
+  hipStream_t s = (hipStream_t)stream;
+  if (hd == 128)
+    hipLaunchKernelGGL((qkv_attn_kernel<128>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, epi->ss_in,
+                       mgk, N, kx, epi->ldo, (const float*)epi->pos, a, t, counters);
+  else
+    hipLaunchKernelGGL((qkv_attn_kernel<64>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, epi->ss_in,
+                       mgk, N, kx, epi->ldo, (const float*)epi->pos, a, t, counters);
+  TI_LAUNCH_CHECK("qkv_attn_kernel");
+  return TI_OK;
 }
 
 extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x,
