@@ -15,6 +15,21 @@ template <bool CH>
 __global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a, const ChainDev chain) {
   __shared__ int s_tok;
   const int m = blockIdx.x, tid = threadIdx.x;
+  // Unchained with hidden % 8 == 0 (<= 8192): the embedding row moves in 16-byte pieces, all
+  // of a thread's loads in flight together; the fold weights (independent of the token) are
+  // loaded before the token is decided.
+  constexpr int kPT = 4;   // pieces of 8 per thread
+  const int H8 = a.hidden >> 3;
+  const bool vec = !CH && (a.hidden & 7) == 0 && H8 <= 256 * kPT && a.placeholder_first < 0;
+  float4 fw[kPT][2];
+  if (vec && a.fold_x) {
+#pragma unroll
+    for (int p = 0; p < kPT; ++p) {
+      const int i8 = min(tid + 256 * p, H8 - 1);
+      fw[p][0] = *(const float4*)(a.fold_w + 8 * i8);
+      fw[p][1] = *(const float4*)(a.fold_w + 8 * i8 + 4);
+    }
+  }
   if constexpr (CH) chain_wait(chain);
   const int s = CH ? (int)ld_sc1_u32(a.step_ctr) : *a.step_ctr;
   const int nin = a.n_in ? a.n_in[m] : 0;
@@ -59,6 +74,39 @@ __global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a, c
       const float v = 0.1f * (float)((off + (size_t)i) % 100);
       if constexpr (CH) st_sc1_f32(h + i, v);
       else h[i] = v;
+    }
+  } else if (vec) {
+    const uint16_t* e = a.emb + (size_t)s_tok * a.hidden;
+    f16x8 ev[kPT];
+#pragma unroll
+    for (int p = 0; p < kPT; ++p) ev[p] = *(const f16x8*)(e + 8 * min(tid + 256 * p, H8 - 1));
+    float ss = 0.0f;
+#pragma unroll
+    for (int p = 0; p < kPT; ++p) {
+      const int i8 = tid + 256 * p;
+      if (i8 >= H8) break;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)ev[p][j];
+      *(float4*)(h + 8 * i8) = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)(h + 8 * i8 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      if (a.fold_x) {   // the first projection's TI_X_F16_FOLDED input (ti_hip.h)
+        const float w[8] = {fw[p][0].x, fw[p][0].y, fw[p][0].z, fw[p][0].w, fw[p][1].x, fw[p][1].y, fw[p][1].z, fw[p][1].w};
+        f16x8 fx;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          fx[j] = (f16)(v[j] * w[j]);
+          ss = fmaf(v[j], v[j], ss);
+        }
+        *(f16x8*)(a.fold_x + (size_t)m * a.hidden + 8 * i8) = fx;
+      }
+    }
+    if (a.fold_x) {
+      __shared__ float s_red4[4];
+      ss = group_sum<64>(ss);
+      if ((tid & 63) == 0) s_red4[tid >> 6] = ss;
+      __syncthreads();
+      if (tid == 0) a.fold_ss[m] = (s_red4[0] + s_red4[1]) + (s_red4[2] + s_red4[3]);
     }
   } else {
     const uint16_t* e = a.emb + (size_t)s_tok * a.hidden;
