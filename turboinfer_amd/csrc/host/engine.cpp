@@ -972,6 +972,8 @@ int ti_engine_generate_sampled(ti_engine* e, int n, const int32_t* prompts, cons
 // a candidate's next-token distribution is its last position's logits, computed on the device
 // by a full forward pass over the candidate's tokens (prefill + one step), as the reference
 // recomputes each candidate from scratch.
+}  // extern "C" (the helpers below are C++)
+
 namespace {
 struct Beam {
   std::vector<int32_t> tokens;
@@ -1029,6 +1031,8 @@ std::vector<float> beam_top_p(const std::vector<float>& probs, float p) {
   return f;
 }
 }  // namespace
+
+extern "C" {
 
 int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int len, int max_new, int beam_size, float temperature,
                           int top_k, float top_p, float length_penalty, int eos, int32_t* out_tokens,

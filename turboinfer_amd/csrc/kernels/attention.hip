@@ -54,6 +54,9 @@ static int launch_attn(const AttnArgs& a, hipStream_t s, const ti_chain* chain) 
     if (!long_range) return launch_one<HD, G, TI_ATTN_RING_HP, true>(a, s, chain);   // head-parallel lanes
   }
   if (long_range) return launch_one<HD, G, TI_ATTN_RING_LONG, false>(a, s, chain);
+  if constexpr (G == 1) {   // one stream, MHA (the 7B decode): 3 slots (bench A/B 745 vs 741 tok/s)
+    if (a.M == 1) return launch_one<HD, G, TI_ATTN_RING_M1, false>(a, s, chain);
+  }
   return launch_one<HD, G, TI_ATTN_RING, false>(a, s, chain);
 }
 

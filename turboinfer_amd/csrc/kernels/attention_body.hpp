@@ -33,6 +33,9 @@ struct AttnArgs {
 // range for a GQA group (Llama-3-8B, 32 streams x 8192 keys: 236 -> 197 us per layer).
 #define TI_ATTN_RING 2
 #endif
+#ifndef TI_ATTN_RING_M1
+#define TI_ATTN_RING_M1 3   // one stream, one q-head per kv-head (tools/ab_attn_ring.sh)
+#endif
 #ifndef TI_ATTN_RING_HP
 #define TI_ATTN_RING_HP 8   // keys in flight per wave in the head-parallel layout
 #endif
