@@ -72,6 +72,10 @@ class ModelLoader {
   static bool validate_file(const std::string& file_path);
   static ModelMetadata get_model_info(const std::string& file_path);
   static bool validate_model(const ModelData& model_data, const ModelMetadata& metadata);
+
+ private:
+  // GGUF v3 (reference model_loader.hpp:216); turboinfer_amd/csrc/api/gguf.cpp
+  static ModelData load_gguf(const std::string& file_path);
 };
 
 const char* format_to_string(ModelFormat format);

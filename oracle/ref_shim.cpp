@@ -6,7 +6,10 @@
 // Nothing here is part of the product and nothing here re-implements reference
 // arithmetic: every call lands in the reference's own TensorEngine / Quantizer /
 // InferenceEngine.
+#include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <fstream>
 #include <cstdint>
 #include <cstring>
 #include <exception>
@@ -15,6 +18,7 @@
 
 #include "turboinfer/core/tensor_engine.hpp"
 #include "turboinfer/model/inference_engine.hpp"
+#include "turboinfer/model/model_loader.hpp"
 #include "turboinfer/optimize/quantization.hpp"
 
 using turboinfer::core::ComputeDevice;
@@ -51,6 +55,32 @@ int guard(F&& f) {
   }
 }
 }  // namespace
+
+// ModelData -> <out>.meta (text) + <out>.data (the tensors' raw bytes in the .meta order):
+// the dump tests/test_gguf.py compares between this library, the reference and the oracle.
+static void dump_model_data(const turboinfer::model::ModelData& md, const std::string& out) {
+  const auto& m = md.metadata();
+  std::ofstream meta(out + ".meta"), data(out + ".data", std::ios::binary);
+  char rope[32];
+  std::snprintf(rope, sizeof rope, "%.9g", (double)m.rope_theta);
+  meta << m.name << "\n" << m.architecture << "\n" << m.version << "\n" << m.vocab_size << " " << m.hidden_size << " "
+       << m.num_layers << " " << m.num_heads << " " << m.intermediate_size << " " << rope << "\n";
+  std::vector<std::string> keys;
+  for (const auto& kv : m.extra_params) keys.push_back(kv.first);
+  std::sort(keys.begin(), keys.end());
+  meta << keys.size() << "\n";
+  for (const auto& k : keys) meta << k << "\t" << m.extra_params.at(k) << "\n";
+  const auto names = md.tensor_names();
+  meta << names.size() << "\n";
+  for (const auto& n : names) {
+    const auto* t = md.get_tensor(n);
+    const bool h = t->dtype() == turboinfer::core::DataType::kFloat16;
+    meta << n << " " << (h ? 3 : 0) << " " << t->shape().ndim();
+    for (size_t d : t->shape().dimensions()) meta << " " << d;
+    meta << "\n";
+    if (t->byte_size()) data.write((const char*)t->data(), (std::streamsize)t->byte_size());
+  }
+}
 
 extern "C" {
 
@@ -314,6 +344,15 @@ int ref_tinq_save(const char* path, int qtype, int symmetric, int n, const char*
     qc.symmetric = symmetric != 0;
     turboinfer::optimize::Quantizer qz(qc);
     qz.save_quantized_model(qz.quantize_model(md), path);
+    return 0;
+  });
+}
+
+// ModelLoader::load (model_loader.cpp:710-873 for .gguf) of a file written by
+// tests/golden/gen_gguf.py, dumped as api_check's gguf_load does.
+int ref_gguf_dump(const char* in, const char* out) {
+  return guard([&] {
+    dump_model_data(turboinfer::model::ModelLoader::load(in), out);
     return 0;
   });
 }

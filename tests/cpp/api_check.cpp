@@ -12,6 +12,8 @@
 //                                                     Quantizer::quantize_model + save_quantized_model
 //   api_check tinq_load <in.tinq> <out_dir>           Quantizer::load_quantized_model -> meta.txt,
 //                                                     names.txt and <i>.bin in the file's order
+//   api_check gguf_load <in.gguf> <out>               ModelLoader::load -> <out>.meta + <out>.data
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -222,6 +224,37 @@ static int tinq_save(const std::string& dir, int bits, int sym, const std::strin
   return 0;
 }
 
+// ModelData -> <out>.meta (text) + <out>.data (the tensors' raw bytes in the .meta order):
+// the dump tests/test_gguf.py compares between this library, the reference and the oracle.
+static void dump_model_data(const turboinfer::model::ModelData& md, const std::string& out) {
+  const auto& m = md.metadata();
+  std::ofstream meta(out + ".meta"), data(out + ".data", std::ios::binary);
+  char rope[32];
+  std::snprintf(rope, sizeof rope, "%.9g", (double)m.rope_theta);
+  meta << m.name << "\n" << m.architecture << "\n" << m.version << "\n" << m.vocab_size << " " << m.hidden_size << " "
+       << m.num_layers << " " << m.num_heads << " " << m.intermediate_size << " " << rope << "\n";
+  std::vector<std::string> keys;
+  for (const auto& kv : m.extra_params) keys.push_back(kv.first);
+  std::sort(keys.begin(), keys.end());
+  meta << keys.size() << "\n";
+  for (const auto& k : keys) meta << k << "\t" << m.extra_params.at(k) << "\n";
+  const auto names = md.tensor_names();
+  meta << names.size() << "\n";
+  for (const auto& n : names) {
+    const auto* t = md.get_tensor(n);
+    const bool h = t->dtype() == turboinfer::core::DataType::kFloat16;
+    meta << n << " " << (h ? 3 : 0) << " " << t->shape().ndim();
+    for (size_t d : t->shape().dimensions()) meta << " " << d;
+    meta << "\n";
+    if (t->byte_size()) data.write((const char*)t->data(), (std::streamsize)t->byte_size());
+  }
+}
+
+static int gguf_load(const std::string& in, const std::string& out) {
+  dump_model_data(model::ModelLoader::load(in), out);
+  return 0;
+}
+
 static int tinq_load(const std::string& in, const std::string& dir) {
   const model::ModelData md = optimize::Quantizer::load_quantized_model(in);
   const auto& m = md.metadata();
@@ -245,6 +278,7 @@ int main(int argc, char** argv) {
     if (mode == "op" && argc >= 5) return op(argc, argv);
     if (mode == "tinq_save" && argc == 6) return tinq_save(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argv[5]);
     if (mode == "tinq_load" && argc == 4) return tinq_load(argv[2], argv[3]);
+    if (mode == "gguf_load" && argc == 4) return gguf_load(argv[2], argv[3]);
     if (mode == "generate" && argc == 8)
       return generate(argv[2], argv[3], std::atoi(argv[4]), std::atoi(argv[5]), std::atoi(argv[6]), argv[7]);
     throw std::runtime_error("bad arguments for mode " + mode);

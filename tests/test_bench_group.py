@@ -3,6 +3,7 @@ two ranks under torchrun share only a gloo barrier and the max over ranks of the
 from __future__ import annotations
 
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -23,7 +24,8 @@ def test_two_rank_barrier_and_max():
            os.path.join(ROOT, "tests", "helpers", "group_probe.py")]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
-    lines = [l for l in r.stdout.splitlines() if l.startswith("rank ")]
-    assert len(lines) == 2, r.stdout + r.stderr
-    for l in lines:
-        assert "world 2" in l and "max 11.0" in l and "tokens 14" in l
+    # the two ranks share the launcher's stdout: their lines may interleave without a newline
+    found = re.findall(r"rank (\d+) world (\d+) max ([0-9.]+) tokens (\d+)", r.stdout)
+    assert sorted(f[0] for f in found) == ["0", "1"], r.stdout + r.stderr
+    for _, world, mx, tokens in found:
+        assert (world, mx, tokens) == ("2", "11.0", "14")

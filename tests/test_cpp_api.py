@@ -311,3 +311,86 @@ def test_tinq_load_reads_reference_file(api_check, tmp_path, case):
         got = read(out / f"{names.index(name)}.bin")
         assert got.dtype == data.dtype and got.shape == data.shape, name
         np.testing.assert_array_equal(got, data)
+
+
+# ---------------------------------------------------------------------------- GGUF (CPU)
+def _read_dump(prefix):
+    """<prefix>.meta / .data as written by api_check gguf_load and ref_shim ref_gguf_dump."""
+    lines = open(str(prefix) + ".meta").read().split("\n")
+    nums = lines[3].split()
+    meta = lines[:3] + [int(v) for v in nums[:5]] + [np.float32(float(nums[5]))]
+    ne = int(lines[4])
+    extras = dict(ln.split("\t", 1) for ln in lines[5:5 + ne])
+    data, off, tensors = open(str(prefix) + ".data", "rb").read(), 0, {}
+    for ln in lines[6 + ne:6 + ne + int(lines[5 + ne])]:
+        p = ln.split()
+        code, nd = int(p[1]), int(p[2])
+        shape = tuple(int(v) for v in p[3:3 + nd])
+        dt = np.dtype(np.float16 if code == 3 else np.float32)
+        n = int(np.prod(shape))
+        tensors[p[0]] = (code, shape, np.frombuffer(data, dt, n, off).reshape(shape))
+        off += n * dt.itemsize
+    return meta, extras, tensors
+
+
+def _gguf_oracle():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import gguf_oracle
+    return gguf_oracle
+
+
+def _same_model(got, want):
+    gm, ge, gt = got
+    wm, we, wt = want
+    assert gm == wm and ge == we
+    assert sorted(gt) == sorted(wt)
+    for name, (code, shape, arr) in wt.items():
+        c, s, a = gt[name]
+        assert (c, s) == (code, shape), name
+        assert a.dtype == arr.dtype and np.array_equal(a.view(np.uint8), np.ascontiguousarray(arr).view(np.uint8)), name
+
+
+@pytest.mark.parametrize("case", ["gguf_ref_pin", "gguf_mixed"])
+def test_gguf_load_matches_oracle(api_check, tmp_path, case):
+    """ModelLoader::load on the fixtures against gguf_oracle.gguf_read: metadata fields and
+    extra_params text as the reference maps them, tensor names / shapes (row-major) / dtypes,
+    and values bit for bit -- F32 / F16 kept, BF16 widened, Q4_0 / Q4_1 / Q8_0 dequantized."""
+    path = os.path.join(GOLDEN, case + ".gguf")
+    api_check("gguf_load", path, tmp_path / "ours")
+    _same_model(_read_dump(tmp_path / "ours"), _gguf_oracle().gguf_read(path))
+
+
+def test_gguf_container_walk_matches_reference(api_check, tmp_path):
+    """Pins the walk (header, every scalar key/value type, the ModelMetadata mapping, tensor
+    info, dims reversed, data placement) on the compiled reference's own ModelLoader
+    (model_loader.cpp:710-873), on the file it reads correctly."""
+    import ctypes as C
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libti_ref.so")
+    if not os.path.exists(ref_so):
+        pytest.skip("compiled reference not present (build container only)")
+    path = os.path.join(GOLDEN, "gguf_ref_pin.gguf")
+    ref = C.CDLL(ref_so)
+    assert ref.ref_gguf_dump(path.encode(), str(tmp_path / "ref").encode()) == 0
+    api_check("gguf_load", path, tmp_path / "ours")
+    _same_model(_read_dump(tmp_path / "ours"), _read_dump(tmp_path / "ref"))
+
+
+def test_gguf_rejects_bad_files(api_check, tmp_path):
+    G = _gguf_oracle()
+    good = open(os.path.join(GOLDEN, "gguf_mixed.gguf"), "rb").read()
+    cases = {"magic": b"GGUX" + good[4:], "version": good[:4] + (2).to_bytes(4, "little") + good[8:],
+             "truncated": good[: len(good) - 100]}
+    # an unsupported ggml type (Q5_0 = 6) in the first tensor info
+    G.gguf_write(tmp_path / "q5.gguf", [("general.name", G.STR, "q5")],
+                 [("w", np.zeros((2, 32), np.float32), G.T_F32)])
+    raw = bytearray(open(tmp_path / "q5.gguf", "rb").read())
+    i = raw.index(b"w") + 1 + 4 + 16   # name, n_dims, two dims
+    raw[i:i + 4] = (6).to_bytes(4, "little")
+    cases["type"] = bytes(raw)
+    for name, data in cases.items():
+        p = tmp_path / f"bad_{name}.gguf"
+        p.write_bytes(data)
+        r = subprocess.run([BIN, "gguf_load", str(p), str(tmp_path / "x")], capture_output=True, text=True, timeout=60)
+        assert r.returncode != 0, name
+        assert ("GGUF" in r.stderr + r.stdout) or ("tensor data" in r.stderr + r.stdout), (name, r.stderr)

@@ -2,6 +2,7 @@
 // ModelLoader entry points.  Container semantics follow the reference's
 // src/model/model_loader.cpp:186-311; file parsing is SURVEY.md 8(f) rank 3 (not built).
 #include <algorithm>
+#include <fstream>
 #include <sstream>
 #include <stdexcept>
 
@@ -89,10 +90,36 @@ bool ends_with(const std::string& s, const std::string& suffix) {
 }
 }  // namespace
 
-ModelData ModelLoader::load(const std::string& file_path) { loader_off_path("load(" + file_path + ")"); }
-ModelData ModelLoader::load(const std::string& file_path, ModelFormat) { loader_off_path("load(" + file_path + ")"); }
+// load (reference model_loader.cpp load/:load(path, format)): GGUF is read (gguf.cpp); the
+// other formats stay outside this library.
+ModelData ModelLoader::load(const std::string& file_path) { return load(file_path, detect_format(file_path)); }
+ModelData ModelLoader::load(const std::string& file_path, ModelFormat format) {
+  if (format == ModelFormat::kGGUF) return load_gguf(file_path);
+  loader_off_path("load(" + file_path + ")");
+}
+// get_model_info (reference model_loader.cpp:596-633): for GGUF the header is checked and the
+// reference's fixed defaults are returned (it does not parse the key/value pairs there).
 ModelMetadata ModelLoader::get_model_info(const std::string& file_path) {
-  loader_off_path("get_model_info(" + file_path + ")");
+  if (detect_format(file_path) != ModelFormat::kGGUF) loader_off_path("get_model_info(" + file_path + ")");
+  std::ifstream f(file_path, std::ios::binary);
+  if (!f.is_open()) throw std::runtime_error("Failed to extract model metadata: Could not open GGUF file for metadata reading");
+  char magic[4] = {0, 0, 0, 0};
+  uint32_t version = 0;
+  f.read(magic, 4);
+  f.read(reinterpret_cast<char*>(&version), 4);
+  if (std::string(magic, 4) != "GGUF") throw std::runtime_error("Failed to extract model metadata: Invalid GGUF magic number");
+  ModelMetadata m;
+  const std::string base = file_path.substr(file_path.find_last_of('/') + 1);
+  m.name = base.substr(0, base.rfind('.'));
+  m.architecture = "GGUF";
+  m.version = std::to_string(version);
+  m.vocab_size = 32000;
+  m.hidden_size = 4096;
+  m.num_layers = 32;
+  m.num_heads = 32;
+  m.intermediate_size = 11008;
+  m.rope_theta = 10000.0f;
+  return m;
 }
 
 ModelFormat ModelLoader::detect_format(const std::string& file_path) {
