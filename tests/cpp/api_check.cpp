@@ -13,6 +13,8 @@
 //   api_check tinq_load <in.tinq> <out_dir>           Quantizer::load_quantized_model -> meta.txt,
 //                                                     names.txt and <i>.bin in the file's order
 //   api_check gguf_load <in.gguf> <out>               ModelLoader::load -> <out>.meta + <out>.data
+//   api_check generate_gguf <in.gguf> <prompts> <n_new> <top_k> <weight_bits> <out>
+//                                                     generate_batch on a model read from a GGUF file
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -170,6 +172,9 @@ static int op(int argc, char** argv) {
 }
 
 // model_dir/manifest.txt: "meta vocab hidden layers heads inter rope_theta" then "<name> <file>" lines
+static int run_generate(const model::ModelData& md, const std::string& prompts_file, int n_new, int top_k, int bits,
+                        const std::string& out);
+
 static int generate(const std::string& dir, const std::string& prompts_file, int n_new, int top_k, int bits,
                     const std::string& out) {
   model::ModelData md;
@@ -182,6 +187,17 @@ static int generate(const std::string& dir, const std::string& prompts_file, int
   md.metadata().architecture = "llama";
   std::string name, file;
   while (man >> name >> file) md.add_tensor(name, read_array(dir + "/" + file));
+  return run_generate(md, prompts_file, n_new, top_k, bits, out);
+}
+
+// the same from a GGUF file (ModelLoader::load; llama.cpp tensor names)
+static int generate_gguf(const std::string& path, const std::string& prompts_file, int n_new, int top_k, int bits,
+                         const std::string& out) {
+  return run_generate(model::ModelLoader::load(path), prompts_file, n_new, top_k, bits, out);
+}
+
+static int run_generate(const model::ModelData& md, const std::string& prompts_file, int n_new, int top_k, int bits,
+                        const std::string& out) {
   const Tensor pt = read_array(prompts_file);   // i32 [n][len]
   const size_t n = pt.shape().size(0), len = pt.shape().size(1);
   std::vector<std::vector<int>> prompts(n);
@@ -279,6 +295,8 @@ int main(int argc, char** argv) {
     if (mode == "tinq_save" && argc == 6) return tinq_save(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argv[5]);
     if (mode == "tinq_load" && argc == 4) return tinq_load(argv[2], argv[3]);
     if (mode == "gguf_load" && argc == 4) return gguf_load(argv[2], argv[3]);
+    if (mode == "generate_gguf" && argc == 8)
+      return generate_gguf(argv[2], argv[3], std::atoi(argv[4]), std::atoi(argv[5]), std::atoi(argv[6]), argv[7]);
     if (mode == "generate" && argc == 8)
       return generate(argv[2], argv[3], std::atoi(argv[4]), std::atoi(argv[5]), std::atoi(argv[6]), argv[7]);
     throw std::runtime_error("bad arguments for mode " + mode);

@@ -394,3 +394,52 @@ def test_gguf_rejects_bad_files(api_check, tmp_path):
         r = subprocess.run([BIN, "gguf_load", str(p), str(tmp_path / "x")], capture_output=True, text=True, timeout=60)
         assert r.returncode != 0, name
         assert ("GGUF" in r.stderr + r.stdout) or ("tensor data" in r.stderr + r.stdout), (name, r.stderr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ttype", ["f32", "f16"])
+def test_inference_engine_runs_gguf_checkpoint(api_check, golden, oracle, tmp_path, ttype):
+    """A Llama written as a llama.cpp GGUF (blk.N.* names, [out][in] linear weights; F32, or
+    F16 linears and embedding) and read by ModelLoader::load drives InferenceEngine: its greedy
+    tokens equal those of the same values given under the reference's names ([in][out])."""
+    from pyoracle import OracleModel
+    G = _gguf_oracle()
+    d = golden("decode_mini_gqa_w4")
+    cfg = json.loads(str(d["cfg"]))
+    m = OracleModel(oracle, cfg, int(d["seed"][0]), float(d["jitter"][0]))
+    w = m.weights()
+    m.close()
+    if ttype == "f16":   # both sides see the fp16-rounded values
+        w = {k: (v.astype(np.float16).astype(f32) if v.ndim == 2 else v) for k, v in w.items()}
+    lin = G.T_F16 if ttype == "f16" else G.T_F32
+    names = {"attention.q_proj.weight": "attn_q", "attention.k_proj.weight": "attn_k",
+             "attention.v_proj.weight": "attn_v", "attention.o_proj.weight": "attn_output",
+             "feed_forward.w3.weight": "ffn_gate", "feed_forward.w1.weight": "ffn_up",
+             "feed_forward.w2.weight": "ffn_down", "attention_norm.weight": "attn_norm", "ffn_norm.weight": "ffn_norm"}
+    tensors = [("token_embd.weight", w["token_embeddings.weight"], lin),
+               ("output_norm.weight", w["norm.weight"], G.T_F32),
+               ("output.weight", np.ascontiguousarray(w["lm_head.weight"].T), lin)]
+    for l in range(cfg["layers"]):
+        for ref, gg in names.items():
+            v = w[f"layers.{l}.{ref}"]
+            tensors.append((f"blk.{l}.{gg}.weight", np.ascontiguousarray(v.T) if v.ndim == 2 else v,
+                            lin if v.ndim == 2 else G.T_F32))
+    kvs = [("general.architecture", G.STR, "llama"), ("llama.vocab_size", G.U32, cfg["vocab"]),
+           ("llama.embedding_length", G.U32, cfg["hidden"]), ("llama.block_count", G.U32, cfg["layers"]),
+           ("llama.attention.head_count", G.U32, cfg["heads"]),
+           ("llama.attention.head_count_kv", G.U32, cfg["kv_heads"]),
+           ("llama.feed_forward_length", G.U32, cfg["inter"]), ("llama.rope.theta", G.F32, float(cfg["rope_theta"])),
+           ("tokenizer.ggml.tokens", G.ARR, (G.STR, ["<unk>", "<s>", "</s>"]))]
+    G.gguf_write(tmp_path / "m.gguf", kvs, tensors)
+    mdir = tmp_path / "ref"
+    mdir.mkdir()
+    lines = [f"meta {cfg['vocab']} {cfg['hidden']} {cfg['layers']} {cfg['heads']} {cfg['inter']} {cfg['rope_theta']!r}"]
+    for j, (k, v) in enumerate(w.items()):
+        write(mdir / f"t{j}.bin", v.astype(f32))
+        lines.append(f"{k} t{j}.bin")
+    (mdir / "manifest.txt").write_text("\n".join(lines) + "\n")
+    prompts = write(tmp_path / "p.bin", np.array([d["prompt"].tolist()] * 2, np.int32))
+    api_check("generate", mdir, prompts, 12, 1, cfg["bits"], tmp_path / "a.bin")
+    api_check("generate_gguf", tmp_path / "m.gguf", prompts, 12, 1, cfg["bits"], tmp_path / "b.bin")
+    a, b = read(tmp_path / "a.bin"), read(tmp_path / "b.bin")
+    assert a.shape == b.shape and np.array_equal(a, b)

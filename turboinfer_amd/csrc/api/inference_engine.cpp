@@ -42,6 +42,51 @@ const core::Tensor* layer_tensor(const ModelData& m, size_t l, const char* hf, c
   return find(m, {a + hf, b + meta, b + hf});
 }
 
+// A ModelData read from a llama GGUF (ModelLoader::load) carries llama.cpp's
+// tensor names and [out][in] linear weights; the engine takes the reference's names and [in][out]
+// (ti_engine.h slots).  llama.cpp's q / k rows are already ordered for adjacent-pair RoPE, the
+// rotation apply_rope implements (tensor_engine.cpp:1602-1612), so only names and the transpose
+// change.  A file without output.weight ties the lm_head to the embedding.
+bool gguf_named(const ModelData& m) { return m.get_tensor("blk.0.ffn_up.weight") != nullptr; }
+
+core::Tensor transposed_f32(const core::Tensor& t) {
+  if (t.shape().ndim() != 2) throw std::runtime_error("InferenceEngine: GGUF linear weight is not 2-D");
+  const size_t r = t.shape().size(0), c = t.shape().size(1);
+  const std::vector<float> v = api::to_f32(t);
+  core::Tensor o(core::TensorShape({c, r}), core::DataType::kFloat32);
+  float* d = o.data_ptr<float>();
+  for (size_t i = 0; i < r; ++i)
+    for (size_t j = 0; j < c; ++j) d[j * r + i] = v[i * c + j];
+  return o;
+}
+
+ModelData from_gguf_names(const ModelData& g) {
+  ModelData m;
+  m.metadata() = g.metadata();
+  auto need = [&](const std::string& n) -> const core::Tensor& {
+    const core::Tensor* t = g.get_tensor(n);
+    if (!t) throw std::runtime_error("InferenceEngine: GGUF model lacks " + n);
+    return *t;
+  };
+  m.add_tensor("token_embeddings.weight", need("token_embd.weight"));
+  m.add_tensor("norm.weight", need("output_norm.weight"));
+  const core::Tensor* out = g.get_tensor("output.weight");
+  m.add_tensor("lm_head.weight", transposed_f32(out ? *out : need("token_embd.weight")));
+  for (size_t l = 0; l < g.metadata().num_layers; ++l) {
+    const std::string b = "blk." + std::to_string(l) + ".", r = "layers." + std::to_string(l) + ".";
+    m.add_tensor(r + "attention.q_proj.weight", transposed_f32(need(b + "attn_q.weight")));
+    m.add_tensor(r + "attention.k_proj.weight", transposed_f32(need(b + "attn_k.weight")));
+    m.add_tensor(r + "attention.v_proj.weight", transposed_f32(need(b + "attn_v.weight")));
+    m.add_tensor(r + "attention.o_proj.weight", transposed_f32(need(b + "attn_output.weight")));
+    m.add_tensor(r + "feed_forward.w3.weight", transposed_f32(need(b + "ffn_gate.weight")));
+    m.add_tensor(r + "feed_forward.w1.weight", transposed_f32(need(b + "ffn_up.weight")));
+    m.add_tensor(r + "feed_forward.w2.weight", transposed_f32(need(b + "ffn_down.weight")));
+    m.add_tensor(r + "attention_norm.weight", need(b + "attn_norm.weight"));
+    m.add_tensor(r + "ffn_norm.weight", need(b + "ffn_norm.weight"));
+  }
+  return m;
+}
+
 bool is_int(const core::Tensor& t) {
   return t.dtype() == core::DataType::kInt8 || t.dtype() == core::DataType::kInt32 ||
          t.dtype() == core::DataType::kInt16 || t.dtype() == core::DataType::kUInt8;
@@ -92,6 +137,7 @@ class InferenceEngineImpl {
   }
 
   void build(const ModelData& m, const InferenceConfig& c) {
+    if (gguf_named(m)) return build(from_gguf_names(m), c);
     const ModelMetadata& md = m.metadata();
     const size_t H = md.hidden_size, L = md.num_layers, nh = md.num_heads, V = md.vocab_size;
     size_t I = md.intermediate_size;
