@@ -247,7 +247,9 @@ int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_ca
  * zero row.  The O projection merges them while staging its input (TI_X_ATTN_SPLITS), so the
  * attention launch ends without the arrival-ticket hand-off.  2 <= splits <=
  * TI_ATTN_MAX_PART_SPLITS; no workspace. */
+#ifndef TI_ATTN_MAX_PART_SPLITS
 #define TI_ATTN_MAX_PART_SPLITS 8
+#endif
 int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
                             int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
                             int kv_heads, int head_dim, int splits, uint16_t* part_o, float* part_ml,

@@ -174,11 +174,12 @@ struct ti_engine {
     weight_bytes += tb + sb;
     return TI_OK;
   }
+  int attn_target = 256;   // attention workgroups aimed at (env TI_ATTN_TARGET, A/B knob)
   int splits_for(int M) const {
     if (c.attn_splits > 0) return c.attn_splits;
     // one 8-wave attention workgroup per CU: a second round of workgroups costs a whole
     // workgroup latency (load, merge hand-off) for little bandwidth (tools/probe_attn.hip)
-    const int target = 256;
+    const int target = attn_target;
     int sp = (target + c.kv_heads * M - 1) / (c.kv_heads * M);
     const int cap = std::max(1, c.max_seq / 64);
     return std::max(1, std::min(sp, std::min(cap, 64)));
@@ -709,6 +710,7 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     for (int p = 0; p < c.max_seq; ++p) pv[p] = (float)p;
     if ((rc = ti_rope_table(pv.data(), c.max_seq, hd, c.rope_theta, cs.data()))) return fail(rc);
     if ((rc = ti_memcpy_h2d(e->rope_cs, cs.data(), cs.size() * 4, e->s))) return fail(rc);
+    if (const char* env = getenv("TI_ATTN_TARGET")) e->attn_target = std::max(1, atoi(env));
     e->splits_max = e->splits_for(1);
     e->pf_rows = c.bits == 4 ? TI_GEMM_MAX_ROWS : 16;
     e->rows_cap = std::max(B, e->pf_rows);
