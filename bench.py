@@ -101,9 +101,11 @@ def cpu_baseline(m, L):
     layer_s, head_s = ref.time_decode(H, nh, I, V, L, weight_kind=1, n_layers=1)
     tok_s = layers * layer_s + head_s
     return {"value": round(1.0 / tok_s, 6), "unit": "tokens/s", "cores": 1, "kind": "reference",
+            "cpu_model": cpu_info(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "sample": f"1 decode layer ({layer_s:.2f} s) x {layers} + lm_head ({head_s:.2f} s) at L={L}, "
                       f"INT4 held as int32 (reference quantized path), 1 stream; matmul_3d_2d is single-threaded "
-                      f"(tensor_engine.cpp:620-633); host {os.uname().machine}, {os.cpu_count()} logical CPUs"}
+                      f"(tensor_engine.cpp:620-633, no OpenMP on the decode path, so OMP_NUM_THREADS does not "
+                      f"change it); host {os.uname().machine}, {os.cpu_count()} logical CPUs"}
 
 
 def pmc_traffic(kernel: str):
@@ -121,9 +123,64 @@ def pmc_traffic(kernel: str):
         return None, None
 
 
+def dry_run(g: "Group", args) -> int:
+    """The replica path without a GPU: every rank takes part in the same two barriers and the
+    max over ranks as a real run, with a fixed per-rank duration in place of the timed steps."""
+    g.barrier()
+    dt = g.max(0.001 * (g.rank + 1))
+    g.barrier()
+    if g.rank == 0:
+        print(json.dumps({"metric": "decode tokens/s/GPU, Llama-7B-shape INT4 @2048 ctx; % HBM-read roofline",
+                          "value": None, "dry_run": True, "n_gpus": g.world, "max_rank_s": dt,
+                          "config": {"global_batch": args.batch * g.world, "parallelism": f"replicas{g.world}"}}))
+    g.close()
+    return 0
+
+
+def cpu_info() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_replicas(n: int, argv: list) -> int:
+    """`--gpus N` without a launcher: start N ranks of this script (one per GPU) as child
+    processes and wait for them.  This process never touches a GPU (nothing here makes a HIP
+    call), so no program is exec'd after GPU initialisation.  The children do the same
+    barrier / max-over-ranks timing as under torch.distributed.run; rank 0's JSON line is
+    passed through."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out, _ = procs[0].communicate()
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    sys.stdout.write(out.decode())
+    sys.stdout.flush()
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="replicas, one process per GPU (spawned here when no "
+                                                        "launcher has set WORLD_SIZE)")
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--batch", type=int, default=1, help="decode streams per GPU")
@@ -133,11 +190,24 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
     ap.add_argument("--attn-splits", type=int, default=0, help="0 = the engine's policy")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU-only rehearsal of the replica launch / barrier / max-over-ranks path: no GPU, "
+                         "no engine; prints the JSON line with value null (tests)")
     args = ap.parse_args()
+
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return spawn_replicas(args.gpus, sys.argv[1:])
+    if world_env is not None and int(world_env) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} ranks", file=sys.stderr)
+        return 2
+
+    g = Group()
+    if args.dry_run:
+        return dry_run(g, args)
 
     import turboinfer_amd as T
 
-    g = Group()
     T.init(g.local_rank)
     m = MODELS[args.model]
     V, H, layers, nh, nkv, hd, I, bits, theta = m
@@ -165,11 +235,14 @@ def main() -> int:
     ms_per_step = dt / args.steps * 1000.0
     sb, wb = step_bytes(m, B, L)
 
-    # Dominant kernel: the W4 decode GEMM (gemv_wq_kernel<4>), ~76 % of a step's bytes.
-    # Live timing: each linear class launched back to back between two HIP events on the
-    # engine stream, cycling through the layers so the weights come from HBM as in a step
-    # (per-launch time includes the ~1.2-1.5 us dependent-launch boundary); a step issues
-    # layers x (qkv, o, gate/up, down) + lm_head launches, weighted accordingly.
+    # Dominant kernel: the W4 decode GEMM family (gemv_wq_kernel<4, *>), ~76 % of a step's
+    # bytes.  Live timing on the engine stream: each linear class as the step runs it (same
+    # kernel, x mode and epilogue), `kernel_reps` launches cycling through the layers so the
+    # weights come from HBM, captured into a graph and replayed back to back for several ms
+    # between two HIP events (ti_engine_time_kernel).  A step issues layers x (qkv, o,
+    # gate/up, down) + lm_head launches, weighted accordingly: achieved = sum(bytes) /
+    # sum(time) over those launches, which is what profiles/*_kernel_stats.txt gives as
+    # sum(calls x bytes) / total time over the gemv_wq_kernel<4, *> rows.
     names = ["qkv", "o", "gate_up", "down", "lm_head"]
     per = {}
     gemv_bytes = gemv_us = 0.0

@@ -29,3 +29,28 @@ def test_two_rank_barrier_and_max():
     assert sorted(f[0] for f in found) == ["0", "1"], r.stdout + r.stderr
     for _, world, mx, tokens in found:
         assert (world, mx, tokens) == ("2", "11.0", "14")
+
+
+def test_bench_spawns_replicas_without_launcher():
+    """`bench.py --gpus 2` with no WORLD_SIZE in the environment starts its own two ranks (child
+    processes, before any GPU call) and rank 0 reports n_gpus 2 after the shared barriers and the
+    max over ranks (--dry-run: the same launch/timing path with no engine)."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--batch", "64", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["dry_run"] is True
+    assert out["config"]["global_batch"] == 128
+    assert abs(out["max_rank_s"] - 0.002) < 1e-12   # rank 1's duration wins the max
+
+
+def test_bench_rejects_mismatched_launcher_world():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr

@@ -1406,9 +1406,6 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
   TI_TRY(setup(e->layer[0], W, x, xk, ldx, nw, ep));
   std::vector<int32_t> base(n, kv_len - 1);
   TI_TRY(ti_memcpy_h2d(e->pos, base.data(), (size_t)n * 4, e->s));
-  hipEvent_t a, b;
-  E_CHECK(hipEventCreate(&a), "hipEventCreate");
-  E_CHECK(hipEventCreate(&b), "hipEventCreate");
   auto launch = [&]() -> int {
     DevLayer& L = e->layer[cur];
     cur = (cur + 1) % c.layers;
@@ -1422,20 +1419,43 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
                             e->splits_for(n), e->ws, e->attn, e->s);
     return gemm_rows(e, *W, n, x, xk, ldx, nw, ep, which == 2 ? 2 : 4, false);
   };
-  int rc = launch();   // warm
-  if (rc == TI_OK) {
-    hipEventRecord(a, e->s);
-    for (int r = 0; r < reps && rc == TI_OK; ++r) rc = launch();
-    hipEventRecord(b, e->s);
-    hipEventSynchronize(b);
+  // The `reps` launches are captured once into a graph and the graph is replayed `rounds`
+  // times between two HIP events: no host launch cost inside the timed region (eager
+  // launches of ~10 us kernels can go host-bound on a slow host and read 2x long), and
+  // several milliseconds of back-to-back work, so the clocks are those of a running step.
+  TI_TRY(ti_gemm_prepare());
+  TI_TRY(ti_stream_sync(e->s));
+  E_CHECK(hipStreamBeginCapture(e->s, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+  int rc = TI_OK;
+  for (int r = 0; r < reps && rc == TI_OK; ++r) rc = launch();
+  hipGraph_t graph = nullptr;
+  const hipError_t ec = hipStreamEndCapture(e->s, &graph);
+  if (rc != TI_OK) {
+    if (graph) hipGraphDestroy(graph);
+    return rc;
   }
+  E_CHECK(ec, "hipStreamEndCapture");
+  hipGraphExec_t gx = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&gx, graph, nullptr, nullptr, 0);
+  hipGraphDestroy(graph);
+  E_CHECK(ei, "hipGraphInstantiate");
+  const int rounds = std::max(4, 4096 / reps);
+  hipEvent_t a, b;
+  E_CHECK(hipEventCreate(&a), "hipEventCreate");
+  E_CHECK(hipEventCreate(&b), "hipEventCreate");
+  hipError_t el = hipGraphLaunch(gx, e->s);   // warm (code objects, caches, clocks)
+  if (el == hipSuccess) el = hipEventRecord(a, e->s);
+  for (int r = 0; r < rounds && el == hipSuccess; ++r) el = hipGraphLaunch(gx, e->s);
+  if (el == hipSuccess) el = hipEventRecord(b, e->s);
+  if (el == hipSuccess) el = hipEventSynchronize(b);
   float ms = 0.0f;
-  hipEventElapsedTime(&ms, a, b);
+  if (el == hipSuccess) el = hipEventElapsedTime(&ms, a, b);
   hipEventDestroy(a);
   hipEventDestroy(b);
-  TI_TRY(rc);
+  hipGraphExecDestroy(gx);
+  E_CHECK(el, "ti_engine_time_kernel: graph replay");
   // per projection (all row chunks of it, and the rms_norm prep of the batched path)
-  *avg_us = (double)ms * 1000.0 / (double)reps;
+  *avg_us = (double)ms * 1000.0 / ((double)reps * rounds);
   if (which == 5) {
     *bytes = 2.0 * n * (double)kvd * kv_len * 2.0 + (double)n * qd * (4 + 2);
   } else {
