@@ -22,6 +22,7 @@ _i8p = np.ctypeslib.ndpointer(np.int8, flags="C_CONTIGUOUS")
 _u16p = np.ctypeslib.ndpointer(np.uint16, flags="C_CONTIGUOUS")
 _u64p = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
 SZ = C.c_size_t
+_FWD = C.CFUNCTYPE(C.c_size_t, C.c_void_p, C.POINTER(C.c_int32), C.c_size_t, C.POINTER(C.POINTER(C.c_float)))
 
 
 def build_oracle() -> None:
@@ -87,6 +88,13 @@ class Oracle:
         L.or_plumbing_generate.restype = SZ
         L.or_sample_token.argtypes = [_f32p, SZ, C.c_float, SZ, C.c_float, C.c_float, C.POINTER(C.c_float)]
         L.or_sample_token.restype = C.c_int
+        L.or_sample_probs.argtypes = [_f32p, SZ, C.c_float, SZ, C.c_float, _f32p]
+        L.or_sample_probs.restype = None
+        L.or_beam_search.argtypes = [_FWD, C.c_void_p, _i32p, SZ, SZ, SZ, C.c_float, SZ, C.c_float, C.c_float,
+                                     C.c_int, _i32p, _i32p, _f32p, _f32p, _i32p, C.POINTER(C.c_float)]
+        L.or_beam_search.restype = C.c_int
+        L.or_plumbing_forward_rows.argtypes = [SZ, SZ, SZ, SZ, _f32p]
+        L.or_plumbing_forward_rows.restype = None
         L.or_half_to_float.argtypes = [C.c_uint16]
         L.or_half_to_float.restype = C.c_float
         L.or_float_to_half.argtypes = [C.c_float]
@@ -217,6 +225,42 @@ class Oracle:
         t = self.lib.or_sample_token(lg, lg.size, temperature, top_k, top_p, u, C.byref(lp))
         return t, lp.value
 
+    def sample_probs(self, logits, temperature=1.0, top_k=1, top_p=0.9):
+        lg = f32(logits).reshape(-1)
+        pr = np.empty(lg.size, np.float32)
+        self.lib.or_sample_probs(lg, lg.size, temperature, top_k, top_p, pr)
+        return pr
+
+    def beam_search(self, forward, prompt, max_new, beam, temperature=1.0, top_k=0, top_p=1.0,
+                    length_penalty=1.0, eos=2):
+        """or_beam_search (beam_search_decode restated) over forward(tokens) -> logits:
+        ([(new tokens, log_prob, normalised score, finished)] best first, smallest decision gap)."""
+        keep = {}
+
+        def cb(_ctx, toks, n, out):
+            lg = np.ascontiguousarray(forward([toks[i] for i in range(n)]), np.float32)
+            keep["lg"] = lg
+            out[0] = lg.ctypes.data_as(C.POINTER(C.c_float))
+            return lg.size
+
+        fn = _FWD(cb)
+        p = np.ascontiguousarray(prompt, np.int32)
+        toks = np.zeros(beam * max(max_new, 1), np.int32)
+        nt, fin = np.zeros(beam, np.int32), np.zeros(beam, np.int32)
+        lp, sc, gap = np.zeros(beam, np.float32), np.zeros(beam, np.float32), C.c_float()
+        n = self.lib.or_beam_search(fn, None, p, p.size, max_new, beam, temperature, top_k, top_p, length_penalty,
+                                    eos, toks, nt, lp, sc, fin, C.byref(gap))
+        if n < 0:
+            raise RuntimeError(f"or_beam_search: {n}")
+        m = max(max_new, 1)
+        return ([(toks[r * m: r * m + nt[r]].tolist(), float(lp[r]), float(sc[r]), bool(fin[r])) for r in range(n)],
+                gap.value)
+
+    def plumbing_forward_rows(self, vocab, hidden, layers, n):
+        out = np.empty(n * vocab, np.float32)
+        self.lib.or_plumbing_forward_rows(vocab, hidden, layers, n, out)
+        return out
+
     def plumbing_generate(self, vocab, hidden, layers, prompt, max_new, max_seq=2048):
         p = np.ascontiguousarray(prompt, np.int32)
         out = np.zeros(len(prompt) + max_new, np.int32)
@@ -303,6 +347,10 @@ class Reference:
         L.ref_quantize.argtypes = [_f32p, C.c_uint64, C.c_int, C.c_int, _i32p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.ref_dequantize.argtypes = [_i32p, C.c_uint64, C.c_int, C.c_float, C.c_float, _f32p]
         L.ref_plumbing_generate.argtypes = [C.c_uint64] * 3 + [_i32p, C.c_uint64, C.c_uint64, _i32p, C.POINTER(C.c_uint64)]
+        L.ref_plumbing_generate_sampled.argtypes = [C.c_uint64] * 3 + [_i32p, C.c_uint64, C.c_uint64, C.c_float,
+                                                    C.c_uint64, C.c_float, _i32p, _f32p, C.POINTER(C.c_uint64)]
+        L.ref_plumbing_beam_search.argtypes = [C.c_uint64] * 3 + [_i32p] + [C.c_uint64] * 3 + [
+            C.c_float, C.c_uint64, C.c_float, C.c_float, _i32p, _i32p, _i32p, _f32p, C.POINTER(C.c_uint64)]
         L.ref_time_decode.argtypes = [C.c_uint64] * 5 + [C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
 
     def _chk(self, rc):
@@ -398,6 +446,31 @@ class Reference:
         n = C.c_uint64()
         self._chk(self.lib.ref_plumbing_generate(vocab, hidden, layers, p, p.size, max_new, out, C.byref(n)))
         return out[: n.value].tolist()
+
+    def plumbing_generate_sampled(self, vocab, hidden, layers, prompt, max_new, temperature, top_k, top_p):
+        """The reference's generate(..., include_logprobs=true) with a sampling config: (all
+        tokens, log-prob of each sampled token)."""
+        p = np.ascontiguousarray(prompt, np.int32)
+        out = np.zeros(len(prompt) + max_new + 1, np.int32)
+        lp = np.zeros(max_new + 1, np.float32)
+        n = C.c_uint64()
+        k = self.lib.ref_plumbing_generate_sampled(vocab, hidden, layers, p, p.size, max_new, temperature, top_k,
+                                                   top_p, out, lp, C.byref(n))
+        self._chk(k)
+        return out[: n.value].tolist(), lp[:k].copy()
+
+    def plumbing_beam_search(self, vocab, hidden, layers, prompt, max_new, beam, temperature, top_k, top_p,
+                             length_penalty):
+        """The reference's generate_beam_search(include_logprobs=true): [(new tokens, finished,
+        per-token log-prob)] in result order."""
+        p = np.ascontiguousarray(prompt, np.int32)
+        toks = np.zeros(beam * max_new, np.int32)
+        nt, fin = np.zeros(beam, np.int32), np.zeros(beam, np.int32)
+        lp = np.zeros(beam, np.float32)
+        n = C.c_uint64()
+        self._chk(self.lib.ref_plumbing_beam_search(vocab, hidden, layers, p, p.size, max_new, beam, temperature,
+                                                    top_k, top_p, length_penalty, toks, nt, fin, lp, C.byref(n)))
+        return [(toks[r * max_new: r * max_new + nt[r]].tolist(), bool(fin[r]), float(lp[r])) for r in range(n.value)]
 
     def time_decode(self, H, heads, inter, vocab, L, weight_kind=1, n_layers=1):
         ls, hs = C.c_double(), C.c_double()

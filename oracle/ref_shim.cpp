@@ -194,10 +194,9 @@ int ref_dequantize(const int32_t* q, uint64_t n, int bits, float scale, float zp
 
 // InferenceEngine::generate on the benchmark's synthetic model
 // (benchmarks/benchmark_inference.cpp:145-225 fill patterns), greedy (top_k = 1).
-int ref_plumbing_generate(uint64_t vocab, uint64_t hidden, uint64_t layers, const int32_t* prompt,
-                          uint64_t n_prompt, uint64_t max_new, int32_t* tokens_out,
-                          uint64_t* n_out) {
-  return guard([&] {
+namespace {
+// benchmark_inference.cpp:145-225 create_test_model fill patterns (data, not algorithm).
+turboinfer::model::ModelData plumbing_model(uint64_t vocab, uint64_t hidden, uint64_t layers) {
     using namespace turboinfer::model;
     ModelMetadata md{};
     md.name = "synthetic_test_model";
@@ -243,6 +242,16 @@ int ref_plumbing_generate(uint64_t vocab, uint64_t hidden, uint64_t layers, cons
         lm.data_ptr<float>()[i] = (static_cast<float>(i % 500) / 500.0f - 0.5f) * 0.01f;
       data.add_tensor("lm_head.weight", std::move(lm));
     }
+    return data;
+}
+}  // namespace
+
+int ref_plumbing_generate(uint64_t vocab, uint64_t hidden, uint64_t layers, const int32_t* prompt,
+                          uint64_t n_prompt, uint64_t max_new, int32_t* tokens_out,
+                          uint64_t* n_out) {
+  return guard([&] {
+    using namespace turboinfer::model;
+    ModelData data = plumbing_model(vocab, hidden, layers);
     InferenceConfig cfg;
     cfg.top_k = 1;
     cfg.temperature = 1.0f;
@@ -253,6 +262,64 @@ int ref_plumbing_generate(uint64_t vocab, uint64_t hidden, uint64_t layers, cons
     for (size_t i = 0; i < r.tokens.size(); ++i) tokens_out[i] = r.tokens[i];
     *n_out = r.tokens.size();
     return static_cast<int>(r.tokens.size());
+  });
+}
+
+// The reference's generate() with a sampling configuration and include_logprobs = true on the
+// plumbing model: every step runs the reference's own sample_next_token
+// (inference_engine.cpp:1554-1673) with its clock-seeded mt19937 draw (:470-473), and the
+// GenerationResult carries std::log(probs[token]) of each sampled token.  The draw is not
+// observable; the (token, log-prob) pairs pin temperature, top-k (with tied logits: the
+// plumbing lm_head repeats every 500 columns), softmax and top-p renormalisation.
+int ref_plumbing_generate_sampled(uint64_t vocab, uint64_t hidden, uint64_t layers, const int32_t* prompt,
+                                  uint64_t n_prompt, uint64_t max_new, float temperature, uint64_t top_k,
+                                  float top_p, int32_t* tokens_out, float* logprobs_out, uint64_t* n_out) {
+  return guard([&] {
+    using namespace turboinfer::model;
+    ModelData data = plumbing_model(vocab, hidden, layers);
+    InferenceConfig cfg;
+    cfg.top_k = top_k;
+    cfg.top_p = top_p;
+    cfg.temperature = temperature;
+    cfg.device = ComputeDevice::kCPU;
+    InferenceEngine eng(data, cfg);
+    std::vector<int> p(prompt, prompt + n_prompt);
+    GenerationResult r = eng.generate(p, max_new, true);
+    for (size_t i = 0; i < r.tokens.size(); ++i) tokens_out[i] = r.tokens[i];
+    for (size_t i = 0; i < r.logprobs.size(); ++i) logprobs_out[i] = r.logprobs[i];
+    *n_out = r.tokens.size();
+    return static_cast<int>(r.logprobs.size());
+  });
+}
+
+// The reference's generate_beam_search (inference_engine.cpp:830-871 over beam_search_decode
+// :1912-2069) on the plumbing model: deterministic (no draws).  Per result r: its new tokens
+// (out_tokens[r * max_new ..], -1 padded, count in out_ntok[r]), finished flag, and the
+// per-token log-prob the result carries (candidate.log_prob / n_new, :862-865).
+int ref_plumbing_beam_search(uint64_t vocab, uint64_t hidden, uint64_t layers, const int32_t* prompt,
+                             uint64_t n_prompt, uint64_t max_new, uint64_t beam_size, float temperature,
+                             uint64_t top_k, float top_p, float length_penalty, int32_t* out_tokens, int32_t* out_ntok,
+                             int32_t* out_finished, float* out_logprob, uint64_t* n_out) {
+  return guard([&] {
+    using namespace turboinfer::model;
+    ModelData data = plumbing_model(vocab, hidden, layers);
+    InferenceConfig cfg;
+    cfg.top_k = top_k;
+    cfg.top_p = top_p;
+    cfg.temperature = temperature;
+    cfg.length_penalty = length_penalty;
+    cfg.device = ComputeDevice::kCPU;
+    InferenceEngine eng(data, cfg);
+    std::vector<int> p(prompt, prompt + n_prompt);
+    std::vector<GenerationResult> rs = eng.generate_beam_search(p, max_new, beam_size, true);
+    for (size_t r = 0; r < rs.size(); ++r) {
+      out_ntok[r] = static_cast<int32_t>(rs[r].tokens.size());
+      for (size_t t = 0; t < max_new; ++t) out_tokens[r * max_new + t] = t < rs[r].tokens.size() ? rs[r].tokens[t] : -1;
+      out_finished[r] = rs[r].finished ? 1 : 0;
+      out_logprob[r] = rs[r].logprobs.empty() ? 0.0f : rs[r].logprobs[0];
+    }
+    *n_out = rs.size();
+    return static_cast<int>(rs.size());
   });
 }
 

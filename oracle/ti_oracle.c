@@ -604,3 +604,22 @@ size_t or_plumbing_generate(size_t V, size_t H, size_t layers, const int* prompt
   free(up); free(down); free(lm); free(row); free(logits);
   return n;
 }
+
+/* forward_pass on the plumbing model (:1429-1491): row r starts from the placeholder
+ * 0.1f*(i%100) at flat index i = r*H + h (:1444-1448); all rows' logits are returned, as the
+ * reference returns the full [1, n, V] tensor (:1486-1489). */
+void or_plumbing_forward_rows(size_t V, size_t H, size_t layers, size_t n, float* logits) {
+  const size_t I = 4 * H;
+  float** up = (float**)malloc(sizeof(float*) * layers);
+  float** down = (float**)malloc(sizeof(float*) * layers);
+  for (size_t l = 0; l < layers; ++l) { up[l] = (float*)malloc(sizeof(float) * H * I); down[l] = (float*)malloc(sizeof(float) * I * H); }
+  float* lm = (float*)malloc(sizeof(float) * H * V);
+  plumb_fill(V, H, layers, up, down, lm);
+  float* row = (float*)malloc(sizeof(float) * H);
+  for (size_t r = 0; r < n; ++r) {
+    for (size_t h = 0; h < H; ++h) row[h] = 0.1f * (float)((r * H + h) % 100);
+    plumb_row(V, H, layers, up, down, lm, row, logits + r * V);
+  }
+  for (size_t l = 0; l < layers; ++l) { free(up[l]); free(down[l]); }
+  free(up); free(down); free(lm); free(row);
+}

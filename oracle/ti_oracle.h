@@ -96,6 +96,16 @@ float or_synth_unit(uint64_t seed, uint32_t tensor_id, uint64_t idx);
 
 /* sample_next_token with the uniform draw u supplied (the reference draws it from a
  * clock-seeded mt19937).  Greedy = top_k 1.  ti_oracle_sample.cpp. */
+/* beam_search_decode (inference_engine.cpp:1912-2069) over a caller-supplied forward pass:
+ * fwd(ctx, tokens, n, &logits) returns the distribution's length and points at its logits. */
+typedef size_t (*or_forward_fn)(void* ctx, const int32_t* tokens, size_t n, const float** logits);
+int or_beam_search(or_forward_fn fwd, void* ctx, const int32_t* prompt, size_t len, size_t max_new, size_t beam_size,
+                   float temperature, size_t top_k, float top_p, float length_penalty, int eos, int32_t* out_tokens,
+                   int32_t* out_ntok, float* out_log_prob, float* out_score, int32_t* out_finished, float* min_gap);
+/* forward_pass (:1429-1491) of the plumbing model: all n rows' logits [n][V] */
+void or_plumbing_forward_rows(size_t V, size_t H, size_t layers, size_t n, float* logits);
+/* sample_next_token's distribution (temperature, top-k, softmax, top-p renormalised), probs[V] */
+void or_sample_probs(const float* logits, size_t V, float temperature, size_t top_k, float top_p, float* probs);
 int or_sample_token(const float* logits, size_t V, float temperature, size_t top_k, float top_p,
                     float u, float* logprob_out);
 

@@ -17,8 +17,9 @@
 
 #include "ti_oracle.h"
 
-extern "C" int or_sample_token(const float* logits_in, size_t V, float temperature, size_t top_k,
-                               float top_p, float u, float* logprob_out) {
+// The distribution sample_next_token draws from (everything before :1651), into probs[V].
+extern "C" void or_sample_probs(const float* logits_in, size_t V, float temperature, size_t top_k, float top_p,
+                                float* probs_out) {
   std::vector<float> logits(logits_in, logits_in + V);
   if (temperature != 1.0f && temperature > 0.0f)                       // :1594-1599
     for (float& l : logits) l /= temperature;
@@ -52,6 +53,13 @@ extern "C" int or_sample_token(const float* logits_in, size_t V, float temperatu
     if (ns > 0.0f)
       for (float& p : probs) p /= ns;
   }
+  std::copy(probs.begin(), probs.end(), probs_out);
+}
+
+extern "C" int or_sample_token(const float* logits_in, size_t V, float temperature, size_t top_k,
+                               float top_p, float u, float* logprob_out) {
+  std::vector<float> probs(V);
+  or_sample_probs(logits_in, V, temperature, top_k, top_p, probs.data());
   float cum = 0.0f;                                                    // :1654-1672
   for (size_t i = 0; i < V; ++i) {
     cum += probs[i];

@@ -44,6 +44,16 @@ def ti():
     return T
 
 
+@pytest.fixture(scope="session")
+def ti_host():
+    """The native library for its host-only entry points (no device bound): CPU tests."""
+    import turboinfer_amd as T
+    if not os.path.exists(T.LIB_PATH):
+        T.build()
+    T.lib()
+    return T
+
+
 def inp(seed: int, shape, scale: float = 1.0) -> np.ndarray:
     """Same seeded inputs as tests/golden/gen_golden.py."""
     return (np.random.RandomState(seed).standard_normal(shape) * scale).astype(np.float32)

@@ -139,6 +139,36 @@ for i, p in enumerate([[1, 15, 25, 35], [1, 10, 20, 30, 40, 50], [1, 5, 15, 25, 
 save("plumbing_generate", "InferenceEngine::generate, benchmark_inference create_test_model(1000,256,4), top_k=1, "
      "20 new tokens (BASELINE config 1)", **cases)
 
+# The reference's own sampler through its public generate() (include_logprobs = true): one
+# realisation of its clock-seeded draws per config, (token, log-prob) per sampled step.
+cases = {}
+SAMPLE_CFGS = [(1.0, 50, 0.9), (0.7, 40, 0.9), (1.3, 0, 0.95), (1.0, 3, 1.0), (0.5, 1000, 0.5), (2.0, 7, 0.99),
+               (1.0, 2, 1.0), (0.9, 9, 1.0)]
+for i, (T, k, p) in enumerate(SAMPLE_CFGS):
+    toks, lps = ref.plumbing_generate_sampled(1000, 256, 4, [1, 15, 25, 35], 12, T, k, p)
+    cases[f"cfg{i}"] = np.array([T, k, p], f32)
+    cases[f"tokens{i}"], cases[f"logprobs{i}"] = np.array(toks, np.int32), lps
+save("sample_plumbing", "InferenceEngine::generate(include_logprobs) with sampling configs (temperature, top_k, top_p) "
+     "on create_test_model(1000,256,4), prompt 1 15 25 35, 12 new tokens; the draws are the reference's clock-seeded "
+     "mt19937 (one realisation)", n=np.array([len(SAMPLE_CFGS)]), **cases)
+
+# The reference's generate_beam_search on the plumbing model (deterministic: no draws).  Its
+# forward_pass returns all seq_len x vocab logits and beam_search_decode reads them as one
+# distribution (:1961-1966), so token ids run past the vocabulary; ties everywhere (the lm_head
+# repeats every 500 columns) exercise its std::sort / priority_queue orders.
+cases = {}
+BEAM_CFGS = [(3, 2, 1.0, 0, 1.0, 1.0), (4, 3, 1.0, 50, 0.9, 1.0), (3, 4, 0.7, 0, 1.0, 0.6), (2, 2, 1.0, 2, 1.0, 1.0),
+             (3, 3, 1.5, 7, 0.95, 1.3)]
+for i, (mn, beam, T, k, p, lpen) in enumerate(BEAM_CFGS):
+    res = ref.plumbing_beam_search(1000, 256, 4, [1, 15, 25, 35], mn, beam, T, k, p, lpen)
+    cases[f"cfg{i}"] = np.array([mn, beam, T, k, p, lpen], f32)
+    cases[f"tokens{i}"] = np.array([t + [-1] * (mn - len(t)) for t, _, _ in res], np.int32)
+    cases[f"finished{i}"] = np.array([f for _, f, _ in res], np.int32)
+    cases[f"logprob{i}"] = np.array([lp for _, _, lp in res], f32)
+save("beam_plumbing", "InferenceEngine::generate_beam_search(include_logprobs) on create_test_model(1000,256,4), "
+     "prompt 1 15 25 35; cfg = (max_new, beam, temperature, top_k, top_p, length_penalty)",
+     n=np.array([len(BEAM_CFGS)]), **cases)
+
 # -------------------------------------------- reference-composed decode step (O2)
 def synth_model(cfg, seed, jitter):
     """The weights or_model_synth builds, materialised in numpy (data for the reference)."""

@@ -1,11 +1,13 @@
 """Decode-engine parity (ti_engine.h) against the reference-composed decode (golden vectors
 from the compiled reference) and the oracle.
 
-Bars (BASELINE north_star): greedy token ids bit-exact; logits within 1e-2 relative
-(|gpu - ref| <= 1e-2 * max|ref| per step).  Greedy equality is asserted on every step whose
-reference top-2 margin exceeds the logits tolerance (reported margins are printed); the
-fp16 activation / fp16 KV path cannot promise equality on a near-tie, the reference's own
-order of equal logits being libstdc++'s sort (hard part 2).
+Bars.  north_star: greedy token ids bit-exact; logits within 1e-2 relative.  The tests hold
+the logits to TOL = 2e-3 * max|ref| per step, 5x tighter: the measured error is 5.6e-4 ..
+8.4e-4 * max|ref| at every BASELINE config shape, one stream and 64 / 32 streams alike
+(tools/parity_probe.py, round 2).  Greedy equality is then implied wherever the reference's
+top-2 margin exceeds 2 * TOL; every checked step is asserted to have a margin above 3 * TOL
+(seeds, prompts and streams chosen offline with tools/margin_search.py), and its token is
+asserted equal -- no step is skipped (hard part 2).
 """
 from __future__ import annotations
 
@@ -17,7 +19,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 f32 = np.float32
-REL = 1e-2
+TOL = 2e-3
 
 
 def engine_for(ti, cfg, max_batch=1, max_seq=None, splits=0):
@@ -32,9 +34,19 @@ def margin(lg):
 
 
 def assert_logits_close(got, ref):
-    tol = REL * float(np.max(np.abs(ref)))
+    tol = TOL * float(np.max(np.abs(ref)))
     err = float(np.max(np.abs(got.astype(np.float64) - ref)))
     assert err <= tol, f"logit error {err} > {tol}"
+
+
+def assert_greedy(got, ref, ref_logits, what=""):
+    """Every step: the reference margin is wide (so the logits bound decides the token), and
+    the tokens are equal."""
+    assert len(got) == len(ref)
+    for i, (g, r) in enumerate(zip(got, ref)):
+        m, mx = margin(ref_logits[i]), float(np.max(np.abs(ref_logits[i])))
+        assert m > 3 * TOL * mx, f"{what} step {i}: reference margin {m:.4g} <= 3 * TOL * {mx:.4g} (re-pick the seed)"
+        assert g == r, f"{what} token {i}: gpu {g} ref {r} (margin {m})"
 
 
 @pytest.mark.parametrize("name", ["mini_gqa_w4", "mini_hd128_w8"])
@@ -59,13 +71,7 @@ def test_engine_greedy_tokens_match_reference(ti, golden, name):
     e = engine_for(ti, cfg)
     e.synth(int(d["seed"][0]), float(d["jitter"][0]))
     got = e.generate([prompt], len(ref_new))[0].tolist()
-    margins = [margin(d["logits"][len(prompt) - 1 + i]) for i in range(len(ref_new))]
-    tol = [REL * float(np.max(np.abs(d["logits"][len(prompt) - 1 + i]))) for i in range(len(ref_new))]
-    print("margins", margins, "tol", tol)
-    for i, (g, r) in enumerate(zip(got, ref_new)):
-        if margins[i] <= tol[i]:
-            break                      # near-tie: later tokens legitimately diverge
-        assert g == r, f"token {i}: gpu {g} ref {r} (margin {margins[i]})"
+    assert_greedy(got, ref_new, d["logits"][len(prompt) - 1:], name)
     e.close()
 
 
@@ -100,12 +106,8 @@ def test_engine_gqa8_long_context_vs_oracle(ti, oracle):
     e.synth(seed, jit)
     e.fill_kv(0, fill, kv_seed)
     got, lg = e.generate([prompt], 6, start_pos=[fill], want_logits=True)
-    for i, (g, r) in enumerate(zip(got[0].tolist(), ref)):
-        if margin(ref_logits[i]) <= REL * np.max(np.abs(ref_logits[i])):
-            break
-        assert g == r, (i, got, ref)
-    if got[0].tolist() == ref:
-        assert_logits_close(lg[0], ref_logits[-1])
+    assert_greedy(got[0].tolist(), ref, ref_logits)
+    assert_logits_close(lg[0], ref_logits[-1])
     e.close()
 
 
@@ -118,10 +120,7 @@ def test_engine_batched_streams_independent(ti, oracle):
     e.synth(seed, jit)
     got = e.generate(prompts, 5)
     for b, (ref, ref_logits) in enumerate(single):
-        for i, (g, r) in enumerate(zip(got[b].tolist(), ref)):
-            if margin(ref_logits[i]) <= REL * np.max(np.abs(ref_logits[i])):
-                break
-            assert g == r, (b, i, got[b], ref)
+        assert_greedy(got[b].tolist(), ref, ref_logits, f"stream {b}")
     e.close()
 
 
@@ -141,28 +140,80 @@ def test_engine_replay_fixed_position(ti, oracle):
         got = int(e.last_tokens(1)[0])
         m.fill_kv(L - 1, kv_seed)          # slot L-1 is rewritten every replay step
         ref, lg = m.step(tok)
-        if margin(lg) > REL * np.max(np.abs(lg)):
-            assert got == ref, (step, got, ref)
+        assert_greedy([got], [ref], [lg], f"replay step {step}")
         tok = got
     m.close()
     e.close()
 
 
-def test_engine_7b_shape_two_layers(ti, oracle):
-    """Llama-2-7B layer shapes (H 4096, I 11008, 32 heads x 128, vocab 32000, INT4 g128),
-    two layers, 2047 synthetic cache slots: the real kernel shapes of the benchmark."""
-    cfg = dict(vocab=32000, hidden=4096, layers=2, heads=32, kv_heads=32, head_dim=128, inter=11008,
-               rope_theta=10000.0, eps=1e-5, bits=4, group=128, max_seq=2048)
-    seed, kv_seed, fill = 2025, 3, 2047
-    ref, ref_logits = _oracle_tokens(oracle, cfg, seed, 0.0, [seed % 32000], 1, fill, kv_seed)
-    e = engine_for(ti, cfg)
+# BASELINE config shapes, two layers each (parity probe + margin search, round 2)
+CFG_7B = dict(vocab=32000, hidden=4096, layers=2, heads=32, kv_heads=32, head_dim=128, inter=11008,
+              rope_theta=10000.0, eps=1e-5, bits=4, group=128, max_seq=2048)
+CFG_TL = dict(vocab=32000, hidden=2048, layers=2, heads=32, kv_heads=4, head_dim=64, inter=5632,
+              rope_theta=10000.0, eps=1e-5, bits=8, group=128, max_seq=2048)
+CFG_L3 = dict(vocab=128256, hidden=4096, layers=2, heads=32, kv_heads=8, head_dim=128, inter=14336,
+              rope_theta=500000.0, eps=1e-5, bits=4, group=128, max_seq=8192)
+
+
+def _stream_params(seed, b, V):
+    """Stream b of a synthetic batch: its first token and KV seed (tools/margin_search.py)."""
+    return (seed * 7 + 13 * b) % V, 100 + b
+
+
+def _full_shape_streams(ti, oracle, cfg, seed, B, checked, n_steps, slot_of=None):
+    """B streams, each with its own synthetic cache of max_seq - n_steps slots and its own first
+    token, decode n_steps tokens (the last at position max_seq - 1).  `checked` streams (logical
+    indices; slot_of maps them to engine slots, default identity) are compared with the oracle:
+    per-step logits through ti_engine_step (teacher-forced with the oracle's tokens) and the greedy
+    tokens of ti_engine_generate (the device loop with argmax feedback)."""
+    from pyoracle import OracleModel
+    V, fill = cfg["vocab"], cfg["max_seq"] - n_steps
+    slot_of = slot_of or (lambda b: b)
+    m = OracleModel(oracle, cfg, seed, 0.0)
+    ref = {}
+    for b in checked:
+        tok0, kvs = _stream_params(seed, b, V)
+        m.fill_kv(fill, kvs)
+        toks, lgs, t = [], [], tok0
+        for _ in range(n_steps):
+            t, lg = m.step(t)
+            toks.append(t)
+            lgs.append(lg)
+        ref[b] = (tok0, toks, lgs)
+    m.close()
+    logical = {slot_of(b): b for b in checked}
+    params = [_stream_params(seed, logical.get(s, s), V) for s in range(B)]
+    e = engine_for(ti, cfg, max_batch=B)
     e.synth(seed, 0.0)
-    e.fill_kv(0, fill, kv_seed)
-    got, lg = e.generate([[seed % 32000]], 1, start_pos=[fill], want_logits=True)
-    assert_logits_close(lg[0], ref_logits[0])
-    if margin(ref_logits[0]) > REL * np.max(np.abs(ref_logits[0])):
-        assert int(got[0, 0]) == ref[0]
+    for s in range(B):
+        e.fill_kv(s, fill, params[s][1])
+    feed = [p[0] for p in params]
+    for step in range(n_steps):
+        lg = e.step(feed, [fill + step] * B)
+        for s, b in logical.items():
+            assert_logits_close(lg[s], ref[b][2][step])
+        feed = [int(t) for t in np.argmax(lg, axis=1)]
+        for s, b in logical.items():
+            feed[s] = ref[b][1][step]
+    for s in range(B):
+        e.fill_kv(s, fill, params[s][1])
+    got = e.generate([[p[0]] for p in params], n_steps, start_pos=[fill] * B)
     e.close()
+    for s, b in logical.items():
+        assert_greedy(got[s].tolist(), ref[b][1], ref[b][2], f"stream {b}")
+
+
+def test_engine_7b_shape_two_layers(ti, oracle):
+    """BASELINE configs[2] shapes: Llama-2-7B layers (H 4096, I 11008, 32 heads x 128, vocab
+    32000, INT4 g128), two layers, one stream decoding positions 2044..2047."""
+    _full_shape_streams(ti, oracle, CFG_7B, 2025, 1, [1], 4, slot_of=lambda b: 0)
+
+
+def test_engine_7b_64_streams(ti, oracle):
+    """BASELINE configs[3] per GPU: 64 streams of Llama-2-7B shape (batch 512 over 8 replicas),
+    each with its own 2044-slot cache and first token, four steps to position 2047: five streams
+    spread over the batch (both 32-row GEMM chunks) against the oracle."""
+    _full_shape_streams(ti, oracle, CFG_7B, 2025, 64, [1, 17, 35, 49, 63], 4)
 
 
 def test_engine_compat_plumbing_matches_reference_generate(ti, oracle, golden):
@@ -198,32 +249,22 @@ def test_engine_compat_plumbing_matches_reference_generate(ti, oracle, golden):
     e.close()
 
 
-def _full_shape_step(ti, oracle, cfg, seed, fill, kv_seed):
-    ref, ref_logits = _oracle_tokens(oracle, cfg, seed, 0.0, [seed % cfg["vocab"]], 1, fill, kv_seed)
-    e = engine_for(ti, cfg)
-    e.synth(seed, 0.0)
-    e.fill_kv(0, fill, kv_seed)
-    got, lg = e.generate([[seed % cfg["vocab"]]], 1, start_pos=[fill], want_logits=True)
-    assert_logits_close(lg[0], ref_logits[0])
-    if margin(ref_logits[0]) > REL * np.max(np.abs(ref_logits[0])):
-        assert int(got[0, 0]) == ref[0]
-    e.close()
-
-
 def test_engine_tinyllama_int8_shape(ti, oracle):
-    """BASELINE config 2 shapes: TinyLlama-1.1B (H 2048, 32 q / 4 kv heads x 64, I 5632,
-    vocab 32000) with INT8 g128 weights, two layers, 2047 cached slots."""
-    cfg = dict(vocab=32000, hidden=2048, layers=2, heads=32, kv_heads=4, head_dim=64, inter=5632,
-               rope_theta=10000.0, eps=1e-5, bits=8, group=128, max_seq=2048)
-    _full_shape_step(ti, oracle, cfg, 1101, 2047, 11)
+    """BASELINE configs[1] shapes: TinyLlama-1.1B (H 2048, 32 q / 4 kv heads x 64, I 5632,
+    vocab 32000) with INT8 g128 weights, two layers, one stream decoding positions 2044..2047."""
+    _full_shape_streams(ti, oracle, CFG_TL, 1101, 1, [1], 4, slot_of=lambda b: 0)
 
 
 def test_engine_llama3_8b_gqa_long_context_shape(ti, oracle):
-    """BASELINE config 5 shapes: Llama-3-8B (H 4096, 32 q / 8 kv heads x 128, I 14336,
-    vocab 128256, rope theta 5e5) INT4 g128, two layers, 8191 cached slots (8192-token KV)."""
-    cfg = dict(vocab=128256, hidden=4096, layers=2, heads=32, kv_heads=8, head_dim=128, inter=14336,
-               rope_theta=500000.0, eps=1e-5, bits=4, group=128, max_seq=8192)
-    _full_shape_step(ti, oracle, cfg, 808, 8191, 5)
+    """BASELINE configs[4] shapes: Llama-3-8B (H 4096, 32 q / 8 kv heads x 128, I 14336,
+    vocab 128256, rope theta 5e5) INT4 g128, two layers, one stream at positions 8189..8191."""
+    _full_shape_streams(ti, oracle, CFG_L3, 808, 1, [8], 3, slot_of=lambda b: 0)
+
+
+def test_engine_llama3_32_streams_8192(ti, oracle):
+    """BASELINE configs[4]: 32 streams of Llama-3-8B GQA shape, each with its own 8189-slot
+    cache (8192-token KV), three steps to position 8191: five streams against the oracle."""
+    _full_shape_streams(ti, oracle, CFG_L3, 808, 32, [2, 8, 19, 24, 31], 3)
 
 
 def test_engine_batch_beyond_one_gemm_chunk(ti, oracle):
@@ -237,7 +278,4 @@ def test_engine_batch_beyond_one_gemm_chunk(ti, oracle):
     e.close()
     for b in (0, 7, 16, 19):
         ref, ref_logits = _oracle_tokens(oracle, MID, seed, jit, prompts[b], 3)
-        for i, (g, r) in enumerate(zip(got[b].tolist(), ref)):
-            if margin(ref_logits[i]) <= REL * np.max(np.abs(ref_logits[i])):
-                break
-            assert g == r, (b, i, got[b], ref)
+        assert_greedy(got[b].tolist(), ref, ref_logits, f"stream {b}")

@@ -15,6 +15,8 @@ import ctypes as C
 import numpy as np
 import pytest
 
+from test_gpu_engine import TOL
+
 pytestmark = pytest.mark.gpu
 
 f16 = np.float16
@@ -91,8 +93,8 @@ CFGS = {
 @pytest.mark.parametrize("name", list(CFGS))
 def test_engine_fold_matches_unfolded_steps(ti, name):
     """Fold on vs off on twin engines fed the same tokens step by step: logits within the
-    decode tolerance (1e-2 of max |logit|) every step, greedy argmax equal wherever the top-2
-    margin exceeds it; then greedy generate() from the same prompt agrees on those steps."""
+    decode tolerance (TOL of max |logit|, test_gpu_engine.py) every step, greedy argmax equal
+    wherever the top-2 margin exceeds twice it (which the bound implies); then greedy generate() from the same prompt agrees on those steps."""
     v, h, l, nh, nkv, hd, inter, bits = CFGS[name]
     eng = {}
     for fold in (True, False):
@@ -105,10 +107,10 @@ def test_engine_fold_matches_unfolded_steps(ti, name):
     for pos in range(20):
         lf = eng[True].step([toks[pos]], [pos])[0].astype(np.float64)
         lu = eng[False].step([toks[pos]], [pos])[0].astype(np.float64)
-        tol = 1e-2 * float(np.max(np.abs(lu)))
+        tol = TOL * float(np.max(np.abs(lu)))
         assert float(np.max(np.abs(lf - lu))) <= tol, pos
         srt = np.sort(lu)
-        if srt[-1] - srt[-2] > tol:
+        if srt[-1] - srt[-2] > 2 * tol:      # then the bound above decides the argmax
             assert int(np.argmax(lf)) == int(np.argmax(lu)), pos
         if pos + 1 >= len(toks):
             toks.append(int(np.argmax(lu)))

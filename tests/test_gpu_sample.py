@@ -1,12 +1,15 @@
 """On-device sampling (ti_hip.h ti_sample_device / ti_sample_step, ti_engine_generate_sampled)
-against the product's host sampler ti_sample_token, which follows the reference's
-sample_next_token (inference_engine.cpp:1554-1673) line by line with the uniform draw given.
+against the ORACLE's sampler (oracle/ti_oracle_sample.cpp: sample_next_token,
+inference_engine.cpp:1554-1673, with the uniform draw given), which tests/test_sampling_oracle.py
+pins to the compiled reference's own generate(include_logprobs) output.
 
 Same logits and draw -> same token: the device sums the survivors' probabilities in index
 order exactly as the reference's loops over all V do (the rest add exact zeros).  Its exp/log
 are the device's (<= 1 ulp from glibc), so log-probabilities agree to 1e-5 and a token could
 only differ when a draw lies within ~1e-6 of a cumulative boundary (not hit by these seeds).
-Ties at the top-k / top-p cut (unspecified in the reference's std::sort) are not exercised.
+Equal logits at the top-k cut: the device keeps the lowest indices, the reference whatever
+libstdc++'s std::sort leaves there; test_device_sampler_tied_logits checks every setting where
+the two agree and counts the ones where the reference's tie order differs.
 """
 from __future__ import annotations
 
@@ -27,7 +30,7 @@ def dev(ti, a):
 @pytest.mark.parametrize("V", [1000, 32000, 128256])
 @pytest.mark.parametrize("T,k,p", [(1.0, 1, 1.0), (0.7, 40, 0.9), (1.0, 50, 1.0), (1.3, 1024, 0.95),
                                    (0.0, 8, 0.5), (1.0, 200, 0.0)])
-def test_device_sampler_matches_host_sampler(ti, V, T, k, p):
+def test_device_sampler_matches_oracle(ti, oracle, V, T, k, p):
     if k > V:
         pytest.skip("top_k above vocab")
     M = 6
@@ -42,12 +45,42 @@ def test_device_sampler_matches_host_sampler(ti, V, T, k, p):
     ti.sync()
     got_t, got_lp = tok_d.download(np.int32, M), lp_d.download(f32, M)
     for m in range(M):
-        want_t, want_lp = ti.sample_token(logits[m], T, k, p, float(draws[m]))
+        want_t, want_lp = oracle.sample_token(logits[m], T, k, p, float(draws[m]))
         assert int(got_t[m]) == want_t, (m, int(got_t[m]), want_t)
         if np.isfinite(want_lp):
             assert abs(float(got_lp[m]) - want_lp) <= 1e-5 * max(1.0, abs(want_lp)), (m, got_lp[m], want_lp)
         else:
             assert not np.isfinite(got_lp[m])
+
+
+def test_device_sampler_tied_logits(ti, oracle):
+    """The reference's plumbing logits (every value twice: lm_head repeats every 500 columns)."""
+    V = 1000
+    lg = np.stack([oracle.plumbing_generate(V, 256, 4, [1, 15, 25, 35], s + 1)[1] for s in range(2)])
+    ld = dev(ti, lg)
+    agree = differ = 0
+    for T, k, p in [(1.0, 2, 1.0), (1.0, 3, 1.0), (0.7, 40, 0.9), (2.0, 7, 0.99), (0.9, 9, 1.0), (1.0, 50, 0.9),
+                    (1.3, 0, 0.95), (0.5, 1000, 0.5)]:
+        if k == 0:
+            continue                                     # the device sampler needs 1 <= k
+        # survivors under lowest-index-first ties vs the reference's std::sort order
+        low = [set(np.lexsort((np.arange(V), -row))[:k].tolist()) for row in lg]
+        ref = [set(np.flatnonzero(np.isfinite(np.log(oracle.sample_probs(row, 1.0, k, 1.0)))).tolist()) for row in lg]
+        if low != ref:
+            differ += 1
+            continue
+        draws = np.array([0.3, 0.8], f32)
+        tok_d, lp_d = ti.DeviceBuffer(2 * 4), ti.DeviceBuffer(2 * 4)
+        ti.check(ti.lib().ti_sample_device(ld.ptr, V, 2, V, T, k, p, dev(ti, draws).ptr, tok_d.ptr, lp_d.ptr, None))
+        ti.sync()
+        got_t, got_lp = tok_d.download(np.int32, 2), lp_d.download(f32, 2)
+        for m in range(2):
+            want_t, want_lp = oracle.sample_token(lg[m], T, k, p, float(draws[m]))
+            assert int(got_t[m]) == want_t, (T, k, p, m, int(got_t[m]), want_t)
+            assert abs(float(got_lp[m]) - want_lp) <= 1e-5 * max(1.0, abs(want_lp))
+        agree += 1
+    print(f"tied logits: {agree} settings compared, {differ} with a reference tie order other than lowest-index")
+    assert agree >= 4
 
 
 def test_device_sampler_rejects_unsupported_top_k(ti):
@@ -66,9 +99,9 @@ CFGS = {
 
 
 @pytest.mark.parametrize("name", list(CFGS))
-def test_engine_sampled_generate_matches_host_loop(ti, name):
+def test_engine_sampled_generate_matches_host_loop(ti, oracle, name):
     """The device loop with on-device sampling against ti_engine_step (the same kernels, logits
-    to the host) + the host sampler, fed the same draws: identical tokens and log-probs.  With
+    to the host) + the oracle's sampler, fed the same draws: identical tokens and log-probs.  With
     prefill the prompt's KV comes from the batched kernels (rounding within the decode
     tolerance): the same tokens up to the first draw that lands across a moved boundary."""
     v, h, l, nh, nkv, hd, inter, bits = CFGS[name]
@@ -88,7 +121,7 @@ def test_engine_sampled_generate_matches_host_loop(ti, name):
     for pos in range(len(prompt) + new - 1):
         lg = ref.step([toks[pos]], [pos])[0]
         if pos >= len(prompt) - 1:
-            t, lp = ti.sample_token(lg, T, k, p, float(draws[len(want)]))
+            t, lp = oracle.sample_token(lg, T, k, p, float(draws[len(want)]))
             want.append(t)
             want_lp.append(lp)
             toks.append(t)

@@ -3,8 +3,8 @@ requests admitted (prefilled) into slots that finished, the rest continuing at t
 positions.
 
 Each request must decode as if it ran alone: against the oracle's reference-composed decode
-of that prompt (greedy equality up to the first near-tie, as test_gpu_engine.py's batched
-test), and -- since the batched kernels compute every row from its own inputs -- bit for bit
+of that prompt (greedy equality on every step, prompts chosen with every reference margin
+above 3 x the logits tolerance, as in test_gpu_engine.py), and -- since the batched kernels compute every row from its own inputs -- bit for bit
 the same whatever the chunking of the device loop (which changes which requests share a
 chunk and when slots turn over).  An EOS ends a request early and frees its slot.
 """
@@ -13,11 +13,11 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from test_gpu_engine import MID, REL, _oracle_tokens, engine_for, margin
+from test_gpu_engine import MID, _oracle_tokens, assert_greedy, engine_for
 
 pytestmark = pytest.mark.gpu
 
-PROMPTS = [[1, 2, 3], [400], [7, 8, 9, 10, 11], [5, 6], [100, 200, 300, 400, 500, 600, 700], [9], [42, 43, 44]]
+PROMPTS = [[1, 2, 3], [400], [7, 8, 9, 10, 11], [5, 7], [100, 200, 300, 400, 500, 600, 700], [12], [42, 43, 44]]
 
 
 def test_serve_requests_decode_independently(ti, oracle):
@@ -32,10 +32,7 @@ def test_serve_requests_decode_independently(ti, oracle):
     for p, g in zip(PROMPTS, got):
         assert len(g) == new
         ref, ref_logits = _oracle_tokens(oracle, MID, seed, jit, p, new)
-        for i, (a, b) in enumerate(zip(g, ref)):
-            if margin(ref_logits[i]) <= REL * np.max(np.abs(ref_logits[i])):
-                break
-            assert a == b, (p, i, g, ref)
+        assert_greedy(g, ref, ref_logits, f"request {p}")
 
 
 def test_serve_eos_frees_the_slot(ti):
