@@ -84,7 +84,10 @@ int ti_engine_generate_sampled(ti_engine* e, int n_streams, const int32_t* promp
  * reference's beam loop (max-heap on log-probability, expansion by the beam_size most probable
  * tokens after temperature / softmax / top-k / top-p renormalisation (:1798-1910), length-
  * normalised ranking log_prob / len^length_penalty, early stop at beam_size finished beams),
- * with each candidate's next-token distribution from a device forward pass over its tokens.
+ * with each candidate's next-token distribution from its last position's logits.  Every live
+ * beam owns a stream slot holding its KV cache: one batched decode step per expansion round, a
+ * fork copies the parent's cache prefix (the reference recomputes each candidate, :1961), so
+ * beam_size <= max_batch.  max_new = 0 returns the prompt as one finished beam (no tokens).
  * Results best first: out_tokens [beam_size][max_new] (new tokens, -1 padded), out_log_prob,
  * out_score (normalised), out_finished [beam_size] (nullable), *out_count beams returned. */
 int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int prompt_len, int max_new, int beam_size,

@@ -105,6 +105,13 @@ int ti_fill_uniform_f32(uint64_t seed, uint32_t tensor_id, uint64_t n, float mul
                         float* dst, ti_stream_t s);
 /* Synthetic KV for one stream of one layer: slots [0, n) of dst ([kv_heads][max_seq][head_dim]
  * fp16) from the oracle's [pos][kv_heads*head_dim] uniform stream (or_model_fill_kv). */
+/* Beam search's fork (no reference counterpart: the reference recomputes every candidate,
+ * inference_engine.cpp:1961): copy a cache prefix between stream slots.  tab: device array of
+ * n_tab fp16 cache base pointers (layer K / V); per cache, `rows` rows of row_elems elements
+ * (pitch row_pitch) from element offset src_off to dst_off.  row_elems, row_pitch and the
+ * offsets are multiples of 8. */
+int ti_kv_copy_slots(uint16_t* const* tab, int n_tab, int64_t src_off, int64_t dst_off, int rows, int64_t row_pitch,
+                     int64_t row_elems, ti_stream_t s);
 int ti_fill_kv_uniform(uint64_t seed, uint32_t tensor_id, int n, int kv_heads, int head_dim, int max_seq,
                        uint16_t* dst, ti_stream_t s);
 

@@ -1,19 +1,19 @@
-"""Beam search (ti_engine_beam_search, C++ InferenceEngine::generate_beam_search) against a
-restatement of the reference's beam_search_decode (inference_engine.cpp:1912-2069) and its
-softmax / apply_top_k_filtering / apply_top_p_filtering helpers (:1798-1910), driven by the
-same engine's forward passes (the last position's logits of each candidate, computed by
-generate(candidate, 1)).
+"""Beam search (ti_engine_beam_search, C++ InferenceEngine::generate_beam_search) against the
+ORACLE's beam search (oracle/ti_oracle_beam.cpp: beam_search_decode, inference_engine.cpp:
+1912-2069, with its softmax / top-k / top-p helpers :1798-1910), which tests/test_beam_oracle.py
+pins to the compiled reference's own generate_beam_search.  The oracle is driven by the
+oracle's reference-composed decode (each candidate recomputed from scratch, its last
+position's logits: the documented deviation from the reference's seq_len x vocab read).
 
-The restatement is float32 numpy in the reference's operation order (sequential sums via
-cumsum); numpy's exp may differ from glibc's by an ulp, so beams must match exactly and
-log-probabilities / scores to 1e-5 relative.  (The reference itself reads seq_len x vocab
-logits of its full-sequence forward pass as one distribution, a bug not reproduced; its
-llama forward pass is broken anyway)
+The engine keeps every live beam in a KV stream slot and decodes all beams in one batched step
+per round, forking a parent's cache prefix into a free slot (ti_kv_copy_slots).  Its logits are
+the decode path's (within TOL of the oracle, test_gpu_engine.py), so the comparison is only
+meaningful where no ranking decision is a near-tie: each case asserts the oracle's smallest
+decision gap (expansion cut and keep / drop cut, in log-probability / score units) exceeds 0.03
+-- prompts and settings chosen offline -- and then requires the same beams in the same order,
+the same finished flags, and log-probabilities / scores within 0.02 per token.
 """
 from __future__ import annotations
-
-import heapq
-import math
 
 import numpy as np
 import pytest
@@ -21,105 +21,77 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 f32 = np.float32
+CFG = dict(vocab=512, hidden=256, layers=2, heads=4, kv_heads=2, head_dim=64, inter=512, rope_theta=10000.0,
+           eps=1e-5, bits=4, group=128, max_seq=64)
+SEED, JIT = 0x7157, 0.1
 
 
-def _softmax(lg):
-    mx = lg.max()
-    p = np.exp((lg - mx).astype(f32)).astype(f32)
-    s = np.cumsum(p, dtype=f32)[-1]
-    return (p / s).astype(f32) if s > 0 else p
+def _engine(ti, max_batch=8):
+    c = CFG
+    e = ti.Engine(c["vocab"], c["hidden"], c["layers"], c["heads"], c["kv_heads"], c["head_dim"], c["inter"],
+                  bits=c["bits"], max_seq=c["max_seq"], max_batch=max_batch)
+    e.synth(SEED, JIT)
+    return e
 
 
-def _renorm(f):
-    s = np.cumsum(f, dtype=f32)[-1]
-    return (f / s).astype(f32) if s > 0 else f
+@pytest.fixture(scope="module")
+def oracle_forward(oracle):
+    from pyoracle import OracleModel
+    m = OracleModel(oracle, CFG, SEED, JIT)
+
+    def forward(toks):                  # a candidate's last-position logits, from scratch
+        m.fill_kv(0, 0)
+        lg = None
+        for t in toks:
+            _, lg = m.step(t)
+        return lg
+
+    yield forward
+    m.close()
 
 
-def _order(p):            # std::sort descending by probability (ties: lower index first here)
-    return sorted(range(len(p)), key=lambda i: (-float(p[i]), i))
+CASES = [([357, 248, 21, 296, 77], 4, 2, 1.0, 0, 1.0, 1.0), ([357, 248, 21, 296, 77], 5, 2, 1.2, 8, 1.0, 1.5),
+         ([4, 39], 4, 3, 0.8, 50, 0.95, 0.6), ([170, 20], 4, 2, 1.0, 0, 1.0, 1.0), ([4, 39], 3, 3, 1.0, 0, 0.9, 1.0),
+         ([231], 3, 4, 1.0, 20, 1.0, 1.0)]
 
 
-def _top_k(p, k):
-    if k >= len(p):
-        return p
-    f = p.copy()
-    for i in _order(p)[k:]:
-        f[i] = 0
-    return _renorm(f)
-
-
-def _top_p(p, top_p):
-    if top_p >= 1.0:
-        return p
-    cum, keep = f32(0), np.zeros(len(p), bool)
-    for i in _order(p):
-        cum = f32(cum + p[i])
-        keep[i] = True
-        if cum >= f32(top_p):
-            break
-    f = np.where(keep, p, f32(0)).astype(f32)
-    return _renorm(f)
-
-
-def ref_beam_search(forward, prompt, max_new, beam_size, T, top_k, top_p, lp_pow, eos):
-    heap, tie = [], 0
-    heapq.heappush(heap, (-0.0, tie, list(prompt), f32(0), f32(0), False))
-    done = []
-    for _ in range(max_new):
-        cur = []
-        while heap:
-            cur.append(heapq.heappop(heap))
-        if not cur:
-            break
-        nxt = []
-        for (_, _, toks, lpb, _, fin) in cur:
-            if fin:
-                done.append((toks, lpb, f32(0), fin))
-                continue
-            lg = forward(toks).astype(f32)
-            if T != 1.0:
-                lg = (lg / f32(T)).astype(f32)
-            p = _softmax(lg)
-            if 0 < top_k < len(p):
-                p = _top_k(p, top_k)
-            if top_p < 1.0:
-                p = _top_p(p, top_p)
-            cands = [i for i in _order(p) if p[i] > 0][:beam_size]
-            for i in cands:
-                nt = toks + [i]
-                nl = f32(lpb + f32(math.log(float(p[i]))))
-                nxt.append([nt, nl, f32(0), i == eos or len(nt) >= len(prompt) + max_new])
-        for c in nxt:
-            c[2] = f32(c[1] / f32(len(c[0]) ** lp_pow))
-        nxt.sort(key=lambda c: -float(c[2]))
-        for c in nxt[:beam_size]:
-            if c[3]:
-                done.append(tuple(c))
-            else:
-                tie += 1
-                heapq.heappush(heap, (-float(c[1]), tie, c[0], c[1], c[2], False))
-        if len(done) >= beam_size:
-            break
-    while heap:
-        _, _, toks, lpb, sc, _ = heapq.heappop(heap)
-        done.append((toks, lpb, sc, True))
-    done.sort(key=lambda c: -float(c[2]))
-    return [(c[0][len(prompt):], float(c[1]), float(c[2]), bool(c[3])) for c in done[:beam_size]]
-
-
-@pytest.mark.parametrize("beam,T,k,p,lp", [(3, 1.0, 0, 1.0, 1.0), (4, 0.8, 50, 0.95, 0.6), (2, 1.2, 8, 1.0, 1.5)])
-def test_beam_search_matches_reference_logic(ti, beam, T, k, p, lp):
-    e = ti.Engine(512, 256, 2, 4, 2, 64, 512, bits=4, max_seq=64, max_batch=1)
-    e.synth(0x7157, 0.1)
-    prompt, new = [3, 17, 99, 5], 6
-
-    def forward(toks):
-        return e.generate([toks], 1, want_logits=True)[1][0]
-
-    want = ref_beam_search(forward, prompt, new, beam, T, k, p, lp, 2)
+@pytest.mark.parametrize("prompt,new,beam,T,k,p,lp", CASES)
+def test_beam_search_matches_oracle(ti, oracle, oracle_forward, prompt, new, beam, T, k, p, lp):
+    want, gap = oracle.beam_search(oracle_forward, prompt, new, beam, T, k, p, lp, eos=2)
+    assert gap > 0.03, f"oracle decision gap {gap}: near-tie, re-pick the case"
+    e = _engine(ti)
     got = e.beam_search(prompt, new, beam, T, k, p, lp, 2)
     e.close()
     assert len(got) == len(want)
     for (gt, gl, gs, gf), (wt, wl, ws, wf) in zip(got, want):
-        assert gt == wt and gf == wf
-        assert abs(gl - wl) <= 1e-5 * max(1.0, abs(wl)) and abs(gs - ws) <= 1e-5 * max(1.0, abs(ws))
+        assert gt == wt and gf == wf, (got, want)
+        n = max(1, len(wt))
+        assert abs(gl - wl) <= 0.02 * n and abs(gs - ws) <= 0.02 * n, (gl, wl, gs, ws)
+
+
+def test_beam_search_reuses_slots_across_rounds(ti, oracle, oracle_forward):
+    """Forks every round (beam 4, 6 new tokens): the slots' caches stay consistent with the
+    candidates' sequences -- each returned beam's log-probability equals the sum of the
+    oracle's log-probabilities of its tokens recomputed from scratch (within 0.02 per token)."""
+    prompt, new, beam = [4, 39], 6, 4
+    e = _engine(ti)
+    got = e.beam_search(prompt, new, beam, 1.0, 0, 1.0, 1.0, 2)
+    e.close()
+    assert len(got) == beam
+    for toks, lpb, _, _ in got:
+        seq, total = list(prompt), 0.0
+        for t in toks:
+            lg = oracle_forward(seq).astype(np.float64)
+            total += float(lg[t] - lg.max() - np.log(np.sum(np.exp(lg - lg.max()))))
+            seq.append(t)
+        assert abs(lpb - total) <= 0.02 * len(toks), (toks, lpb, total)
+
+
+def test_beam_search_edges(ti):
+    e = _engine(ti, max_batch=2)
+    # max_new = 0: the prompt comes back as one finished beam without tokens (:1937, :2052-2057)
+    assert e.beam_search([5, 6], 0, 3) == [([], 0.0, 0.0, True)]
+    # more beams than stream slots: refused before any work
+    with pytest.raises(ti.TiError):
+        e.beam_search([5, 6], 2, 3)
+    e.close()

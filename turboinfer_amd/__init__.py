@@ -69,7 +69,7 @@ EXPORTED = [
     "ti_memcpy_d2h", "ti_memcpy_d2d", "ti_memset", "ti_stream_create", "ti_stream_destroy", "ti_stream_sync",
     "ti_device_sync", "ti_event_create", "ti_event_destroy", "ti_event_record", "ti_event_elapsed_ms",
     "ti_wpack_tile_bytes", "ti_wpack_scale_bytes", "ti_wpack_host", "ti_wsynth_device", "ti_fill_uniform_f16",
-    "ti_fill_uniform_f32", "ti_fill_kv_uniform", "ti_gemm_wq_a16", "ti_gemm_lds_bytes", "ti_gemm_prepare",
+    "ti_fill_uniform_f32", "ti_fill_kv_uniform", "ti_kv_copy_slots", "ti_gemm_wq_a16", "ti_gemm_lds_bytes", "ti_gemm_prepare",
     "ti_gemm_max_rows", "ti_rmsnorm_f16",
     "ti_attn_workspace_bytes", "ti_attn_decode", "ti_step_begin", "ti_matmul_f32", "ti_rms_norm_f32",
     "ti_rope_f32", "ti_silu_f32", "ti_relu_f32", "ti_add_f32", "ti_mul_f32", "ti_softmax_f32", "ti_attention_f32",
@@ -116,6 +116,7 @@ def lib() -> C.CDLL:
         L.ti_fill_uniform_f16.argtypes = [u64, C.c_uint32, u64, f32, vp, vp]
         L.ti_fill_uniform_f32.argtypes = [u64, C.c_uint32, u64, f32, f32, vp, vp]
         L.ti_fill_kv_uniform.argtypes = [u64, C.c_uint32, i32, i32, i32, i32, vp, vp]
+        L.ti_kv_copy_slots.argtypes = [vp, i32, C.c_int64, C.c_int64, i32, C.c_int64, C.c_int64, vp]
         L.ti_gemm_wq_a16.argtypes = [vp, vp, i32, vp, i32, i32, vp, f32, i32, i32, i32, C.POINTER(Epilogue), vp]
         L.ti_gemm_lds_bytes.argtypes = [i32, i32, i32]
         L.ti_gemm_max_rows.argtypes = [i32, i32, i32, i32]

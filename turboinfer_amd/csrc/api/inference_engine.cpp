@@ -461,8 +461,9 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
 }
 
 // generate_beam_search (inference_engine.cpp:830-871): the beam loop runs in ti_engine_beam_search
-// (device forward passes, the reference's host ranking); results keep only the new tokens and,
-// with include_logprobs, the beam's average log-probability per token.
+// (beams as KV stream slots, one batched device step per round, the reference's host ranking);
+// results keep only the new tokens and, with include_logprobs, the beam's average log-probability
+// per token.  max_new_tokens = 0 gives the prompt back as one finished result with no tokens.
 std::vector<GenerationResult> InferenceEngine::generate_beam_search(const std::vector<int>& input_tokens,
                                                                    size_t max_new_tokens, size_t beam_size,
                                                                    bool include_logprobs) {
@@ -471,7 +472,6 @@ std::vector<GenerationResult> InferenceEngine::generate_beam_search(const std::v
   InferenceEngineImpl& im = *impl_;
   if (im.compat) off_path("generate_beam_search on the reference_compat plumbing model", "rank 4");
   std::vector<GenerationResult> results;
-  if (max_new_tokens == 0) return results;
   const int nb = (int)beam_size, mn = (int)max_new_tokens;
   std::vector<int32_t> prompt(input_tokens.begin(), input_tokens.end()), out((size_t)nb * mn);
   std::vector<float> lp(nb);

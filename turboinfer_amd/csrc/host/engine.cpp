@@ -128,6 +128,7 @@ struct ti_engine {
   int in_cap = 0, out_cap = 0;
   int splits_max = 1;
   int64_t kv_stride = 0;
+  uint16_t** kv_tab = nullptr;   // device [2 * layers]: every layer's K then V cache base (ti_kv_copy_slots)
   size_t weight_bytes = 0, kv_bytes = 0;
   std::map<std::pair<int, int>, hipGraphExec_t> graphs;  // (M, advance | sampled << 1)
   int replay_M = 0;
@@ -736,6 +737,11 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     std::vector<int32_t> ones(e->pf_rows, 1);
     if ((rc = ti_memcpy_h2d(e->pf_ones, ones.data(), ones.size() * 4, e->s)) || (rc = ti_memset(e->pf_zero, 0, 4, e->s)))
       return fail(rc);
+    std::vector<uint16_t*> tab;
+    for (auto& L : e->layer) tab.push_back(L.kc);
+    for (auto& L : e->layer) tab.push_back(L.vc);
+    if ((rc = e->alloc_t(&e->kv_tab, tab.size())) || (rc = ti_memcpy_h2d(e->kv_tab, tab.data(), tab.size() * sizeof(void*), e->s)))
+      return fail(rc);
   }
   const int R = std::max(B, e->rows_cap);
   if ((rc = e->alloc_t(&e->h, (size_t)R * H)) || (rc = e->alloc_t(&e->logits, (size_t)B * V)) ||
@@ -969,11 +975,14 @@ int ti_engine_generate_sampled(ti_engine* e, int n, const int32_t* prompts, cons
 // InferenceEngine::generate_beam_search / beam_search_decode (inference_engine.cpp:830-871,
 // 1912-2069) with the reference's control flow, scoring and container orders (max-heap on
 // log_prob, std::sort on probabilities and normalised scores) and its helpers softmax /
-// apply_top_k_filtering / apply_top_p_filtering (:1798-1910).  One deviation: the reference
-// reads seq_len x vocab "logits" of its full-sequence forward pass as one distribution; here
-// a candidate's next-token distribution is its last position's logits, computed on the device
-// by a full forward pass over the candidate's tokens (prefill + one step), as the reference
-// recomputes each candidate from scratch.
+// apply_top_k_filtering / apply_top_p_filtering (:1798-1910).
+// Where the reference recomputes every candidate from scratch with a full forward pass (:1961),
+// here every live beam owns a stream slot whose KV cache holds its sequence: one batched decode
+// step per expansion round gives all beams' next-token logits at once, and a beam that forks
+// copies its parent's cache prefix into a free slot (ti_kv_copy_slots) -- the first child
+// keeps the parent's slot.  One deviation from the reference's numbers: the reference reads
+// seq_len x vocab "logits" of its full-sequence forward pass as one distribution; here a
+// candidate's next-token distribution is its last position's logits.
 }  // extern "C" (the helpers below are C++)
 
 namespace {
@@ -982,6 +991,7 @@ struct Beam {
   float log_prob = 0.0f;
   float normalized_score = 0.0f;
   bool finished = false;
+  int slot = -1;      // stream slot whose cache holds tokens[0 .. size-2] (its parent's, until forked)
 };
 
 std::vector<float> beam_softmax(const std::vector<float>& lg) {
@@ -1032,6 +1042,13 @@ std::vector<float> beam_top_p(const std::vector<float>& probs, float p) {
     for (auto& x : f) x /= sum;
   return f;
 }
+
+// Copy slot `src`'s cache positions [0, n) into slot `dst`, every layer, K and V.
+int fork_slot(ti_engine* e, int src, int dst, int n) {
+  const ti_engine_config& c = e->c;
+  return ti_kv_copy_slots(e->kv_tab, 2 * c.layers, (int64_t)src * e->kv_stride, (int64_t)dst * e->kv_stride,
+                          c.kv_heads, (int64_t)c.max_seq * c.head_dim, (int64_t)n * c.head_dim, e->s);
+}
 }  // namespace
 
 extern "C" {
@@ -1039,26 +1056,27 @@ extern "C" {
 int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int len, int max_new, int beam_size, float temperature,
                           int top_k, float top_p, float length_penalty, int eos, int32_t* out_tokens,
                           float* out_log_prob, float* out_score, int32_t* out_finished, int* out_count) {
-  if (!e || !prompt || !out_tokens || !out_count || len < 1 || max_new < 1)
+  if (!e || !prompt || !out_count || len < 1 || max_new < 0 || (max_new > 0 && !out_tokens))
     return ti_set_error(TI_ERR_ARG, "ti_engine_beam_search: bad arguments");
   if (beam_size < 1) return ti_set_error(TI_ERR_ARG, "ti_engine_beam_search: Beam size must be greater than 0");
   const ti_engine_config& c = e->c;
   if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_beam_search: compat engine");
   if (len + max_new - 1 > c.max_seq)
     return ti_set_error(TI_ERR_ARG, "ti_engine_beam_search: %d + %d tokens exceed max_seq %d", len, max_new, c.max_seq);
+  if (max_new > 0 && beam_size > c.max_batch)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_beam_search: beam_size %d exceeds the engine's %d stream slots",
+                        beam_size, c.max_batch);
   const size_t V = (size_t)c.vocab;
-  std::vector<float> logits(V);
-  auto forward = [&](const std::vector<int32_t>& toks) -> int {   // last position's logits
-    int32_t n = (int32_t)toks.size(), tok = 0;
-    return ti_engine_generate(e, 1, toks.data(), &n, n, nullptr, 1, &tok, logits.data());
-  };
+  std::vector<float> logits((size_t)c.max_batch * V);
   auto cmp = [](const Beam& a, const Beam& b) { return a.log_prob < b.log_prob; };
   std::priority_queue<Beam, std::vector<Beam>, decltype(cmp)> beam(cmp);
   Beam init;
   init.tokens.assign(prompt, prompt + len);
+  init.slot = 0;
   beam.push(init);
   std::vector<Beam> done;
   const size_t bs = (size_t)beam_size, target = (size_t)len + (size_t)max_new;
+  std::vector<int32_t> feed(c.max_batch), pos(c.max_batch);
   for (int step = 0; step < max_new; ++step) {
     std::vector<Beam> cur;
     while (!beam.empty()) {
@@ -1066,14 +1084,30 @@ int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int len, int max_
       beam.pop();
     }
     if (cur.empty()) break;
+    // next-token logits of every live beam: the prompt's prefill + first step into slot 0, then
+    // one batched decode step over the slots (each feeds its last token at its own position;
+    // slots no beam owns decode a dummy token into their own, unused cache)
+    if (step == 0) {
+      int32_t tok = 0;
+      TI_TRY(ti_engine_generate(e, 1, prompt, &len, len, nullptr, 1, &tok, logits.data()));
+    } else {
+      int M = 0;
+      for (const auto& cand : cur) M = std::max(M, cand.slot + 1);
+      std::fill(feed.begin(), feed.end(), 0);
+      std::fill(pos.begin(), pos.end(), 0);
+      for (const auto& cand : cur) {
+        feed[cand.slot] = cand.tokens.back();
+        pos[cand.slot] = (int32_t)cand.tokens.size() - 1;
+      }
+      TI_TRY(ti_engine_step(e, M, feed.data(), pos.data(), logits.data()));
+    }
     std::vector<Beam> next;
     for (const auto& cand : cur) {
       if (cand.finished) {
         done.push_back(cand);
         continue;
       }
-      TI_TRY(forward(cand.tokens));
-      std::vector<float> lg = logits;
+      std::vector<float> lg(logits.begin() + (size_t)cand.slot * V, logits.begin() + (size_t)(cand.slot + 1) * V);
       if (temperature != 1.0f)
         for (auto& x : lg) x /= temperature;
       std::vector<float> probs = beam_softmax(lg);
@@ -1096,6 +1130,22 @@ int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int len, int max_
     for (auto& b : next) b.normalized_score = b.log_prob / std::pow((float)b.tokens.size(), length_penalty);
     std::sort(next.begin(), next.end(), [](const Beam& a, const Beam& b) { return a.normalized_score > b.normalized_score; });
     const size_t keep = std::min(bs, next.size());
+    // slots of the surviving beams: the first survivor of each parent keeps the parent's slot,
+    // the others fork the parent's cache (positions 0 .. parent length - 1) into a free slot
+    std::vector<char> owned(c.max_batch, 0);
+    std::vector<size_t> forks;
+    for (size_t i = 0; i < keep; ++i) {
+      if (next[i].finished) continue;
+      if (!owned[next[i].slot]) owned[next[i].slot] = 1;
+      else forks.push_back(i);
+    }
+    int free_slot = 0;
+    for (size_t i : forks) {
+      while (owned[free_slot]) ++free_slot;   // a free slot exists: at most beam_size <= max_batch survivors
+      TI_TRY(fork_slot(e, next[i].slot, free_slot, (int)next[i].tokens.size() - 1));
+      owned[free_slot] = 1;
+      next[i].slot = free_slot;
+    }
     for (size_t i = 0; i < keep; ++i) {
       if (next[i].finished) done.push_back(next[i]);
       else beam.push(next[i]);

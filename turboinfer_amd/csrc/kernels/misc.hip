@@ -236,6 +236,21 @@ __global__ void fill_kv_kernel(uint64_t stream, int n, int kv_heads, int hd, int
   }
 }
 
+// --------------------------------------------------------------- KV slot copy
+// Beam search (ti_engine_beam_search): a beam that forks copies its parent's cache prefix into
+// a free stream slot.  For each of n_tab caches (layer K / V base pointers in `tab`), `rows`
+// rows (kv heads) of `row_elems` fp16 each, row pitch `row_pitch`, from element offset
+// src_off to dst_off.  16 bytes per thread (row_elems % 8 == 0, 16-byte aligned rows).
+__global__ __launch_bounds__(256) void kv_copy_kernel(uint16_t* const* tab, int64_t src_off, int64_t dst_off,
+                                                      int64_t row_pitch, int64_t row_chunks) {
+  uint16_t* base = tab[blockIdx.z];
+  const int64_t r = blockIdx.y;
+  for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < row_chunks; c += (int64_t)gridDim.x * 256) {
+    const uint4 v = *(const uint4*)(base + src_off + r * row_pitch + 8 * c);
+    *(uint4*)(base + dst_off + r * row_pitch + 8 * c) = v;
+  }
+}
+
 }  // namespace ti
 
 extern "C" int ti_step_begin(const ti_step_args* a, ti_stream_t stream) {
@@ -333,5 +348,20 @@ extern "C" int ti_fill_uniform_f32(uint64_t seed, uint32_t tensor_id, uint64_t n
   hipLaunchKernelGGL(fill_uniform_f32_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                      synth_stream(seed, tensor_id), n, mul, add, dst);
   TI_LAUNCH_CHECK("fill_uniform_f32_kernel");
+  return TI_OK;
+}
+
+extern "C" int ti_kv_copy_slots(uint16_t* const* tab, int n_tab, int64_t src_off, int64_t dst_off, int rows,
+                                int64_t row_pitch, int64_t row_elems, ti_stream_t stream) {
+  using namespace ti;
+  if (!tab || n_tab < 1 || n_tab > 65535 || rows < 1 || rows > 65535 || row_elems < 0 || (row_elems & 7) ||
+      row_pitch < row_elems || (row_pitch & 7) || (src_off & 7) || (dst_off & 7) || src_off < 0 || dst_off < 0)
+    return ti_set_error(TI_ERR_ARG, "ti_kv_copy_slots: bad arguments");
+  if (row_elems == 0 || src_off == dst_off) return TI_OK;
+  const int64_t chunks = row_elems / 8;
+  const unsigned bx = (unsigned)((chunks + 255) / 256 < 64 ? (chunks + 255) / 256 : 64);
+  hipLaunchKernelGGL(kv_copy_kernel, dim3(bx, rows, n_tab), dim3(256), 0, (hipStream_t)stream, tab, src_off, dst_off,
+                     row_pitch, chunks);
+  TI_LAUNCH_CHECK("kv_copy_kernel");
   return TI_OK;
 }
