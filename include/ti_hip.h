@@ -153,7 +153,17 @@ typedef struct ti_chain {
  * epi->n_ss = splits (<= TI_ATTN_MAX_PART_SPLITS) and epi->head_dim; the launch merges the
  * splits (max-rescaled, sum-weighted, as the attention's own merge) while staging x.
  * Epilogue (all outputs of one call): */
-enum ti_x_kind { TI_X_F16 = 0, TI_X_F32 = 1, TI_X_F32_RMSNORM = 2, TI_X_F16_FOLDED = 3, TI_X_ATTN_SPLITS = 4 };
+enum ti_x_kind { TI_X_F16 = 0, TI_X_F32 = 1, TI_X_F32_RMSNORM = 2, TI_X_F16_FOLDED = 3, TI_X_ATTN_SPLITS = 4,
+                 TI_X_F16_PACKED = 5 };
+/* TI_X_F16_PACKED: fp16 rows in the batched-rows kernel's fragment order, so every load of its
+ * MFMA operands is one contiguous KiB per wave (bits 4).  Element (m, k) of an M x K operand
+ * (K % 128 == 0) sits at TI_PACKED_INDEX(m, k, K / 128); the buffer holds ceil(M / 16) * 16
+ * rows (16-row blocks of 16 * K elements, block b at b * 16 * K).  Producers: ti_rmsnorm_f16_packed,
+ * ti_attn_decode_packed, and the batched epilogues TI_EPI_STORE_F16 / TI_EPI_SILU_MUL_F16 with
+ * out_packed set. */
+#define TI_PACKED_INDEX(m, k, kt)                                                                        \
+  ((((((size_t)((m) >> 4) * (size_t)(kt) + (size_t)((k) >> 7)) * 4 + (size_t)(((k) >> 3) & 3)) * 64 +    \
+     (size_t)((((k) >> 5) & 3) * 16 + ((m) & 15))) * 8 + (size_t)((k) & 7)))
 enum ti_epilogue_kind {
   TI_EPI_STORE_F32 = 0,      /* out_f32[m*ldo + n] = y                                  */
   TI_EPI_STORE_F16 = 1,      /* out_f16[m*ldo + n] = fp16(y)                             */
@@ -196,6 +206,9 @@ typedef struct ti_epilogue {
   const float* fold_w;
   uint16_t* fold_x;
   float* fold_ss;
+  /* TI_EPI_STORE_F16 / TI_EPI_SILU_MUL_F16 of the batched-rows kernels (M > 16 or packed x):
+   * write the fp16 output in TI_X_F16_PACKED order (K = ldo, ldo % 128 == 0) */
+  int32_t out_packed;
 } ti_epilogue;
 
 int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind,
@@ -210,12 +223,15 @@ int ti_gemm_lds_bytes(int M, int N, int K);
  * and is used above TI_GEMM_FUSED_ROWS (env, default 2) rows.  An int4 caller with more rows
  * than this returns for TI_X_F32_RMSNORM should normalise them with ti_rmsnorm_f16 and pass
  * TI_X_F16 rows.  0 = shape unsupported. */
-#define TI_GEMM_MAX_ROWS 32
+#define TI_GEMM_MAX_ROWS 64
 int ti_gemm_max_rows(int bits, int x_kind, int N, int K);
 /* y[m][0:K] = fp16(rms_norm(x[m][0:K]) * w), tensor_engine.cpp:1452-1508 (the batched path's
  * activation prep; the same arithmetic as the fused TI_X_F32_RMSNORM prologue). */
 int ti_rmsnorm_f16(const float* x, int ldx, const float* w, float eps, uint16_t* y, int ldy, int M, int K,
                    ti_stream_t s);
+/* ti_rmsnorm_f16 writing y in TI_X_F16_PACKED order (K % 128 == 0). */
+int ti_rmsnorm_f16_packed(const float* x, int ldx, const float* w, float eps, uint16_t* y, int M, int K,
+                          ti_stream_t s);
 /* The same GEMM as one launch of a chain (see ti_chain): M == 1, fused kernel only
  * (TI_ERR_UNSUPPORTED otherwise, nothing launched). */
 int ti_gemm_wq_a16_chained(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind,
@@ -248,6 +264,12 @@ int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_ca
                    int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
                    int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
                    ti_stream_t s);
+/* ti_attn_decode writing out in TI_X_F16_PACKED order (K = heads * head_dim, a multiple of 128):
+ * the batched O projection's operand. */
+int ti_attn_decode_packed(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                          int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
+                          int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
+                          ti_stream_t s);
 /* The same attention with the split merge left to the consumer: split s of (stream m, head h)
  * writes its normalised row part_o[((m*heads + h)*splits + s)*head_dim + d] (fp16) and
  * (max, sum) at part_ml[2*((m*heads + h)*splits + s)]; an empty split writes (-inf, 0) and a

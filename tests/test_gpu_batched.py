@@ -28,7 +28,9 @@ def run(ti, tiles, scales, x16, M, N, K, ep):
 # workgroup (N/16 not a multiple of the grid), a last k-chunk of fewer than 8 k-tiles,
 # more tiles than 5 per workgroup (grid grows)
 @pytest.mark.parametrize("M,K,N", [(17, 1024, 64), (32, 4096, 4096 + 48), (24, 1152, 4000), (8, 11008, 256),
-                                   (3, 14336, 96), (20, 4096, 25600), (32, 384, 16)])
+                                   (3, 14336, 96), (20, 4096, 25600), (32, 384, 16), (64, 4096, 12288),
+                                   (48, 11008, 4096 + 16), (33, 1152, 4000), (64, 384, 16), (64, 14336, 256),
+                                   (40, 4096, 32000)])
 def test_batched_store(ti, oracle, M, K, N):
     rng = np.random.RandomState(M * 7 + K + N)
     w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
@@ -45,7 +47,7 @@ def test_batched_store(ti, oracle, M, K, N):
 
 
 def test_batched_resid_silu_logits(ti, oracle):
-    M, K = 21, 2048
+    M, K = 57, 2048
     rng = np.random.RandomState(5)
     x = rng.standard_normal((M, K)).astype(f16)
     xd, xa = dev(ti, x), x.astype(np.float64)
@@ -92,7 +94,7 @@ def test_batched_resid_silu_logits(ti, oracle):
 
 @pytest.mark.parametrize("hd,nh,nkv", [(128, 4, 4), (64, 8, 2)])
 def test_batched_qkv_rope_kv_append(ti, oracle, hd, nh, nkv):
-    M, H, max_seq, theta = 19, 512, 40, 10000.0
+    M, H, max_seq, theta = 45, 512, 40, 10000.0
     qd, kvd = nh * hd, nkv * hd
     N = qd + 2 * kvd
     rng = np.random.RandomState(hd + nh)
@@ -154,3 +156,71 @@ def test_rmsnorm_f16_matches_fused_prologue(ti, oracle):
         ti.sync()
         outs.append(od.download(f32, (M, N)))
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+# ------------------------------------------------------- fragment-packed operands (M > 16)
+def test_packed_operands_match_row_major(ti, oracle):
+    """TI_X_F16_PACKED: rms_norm prep, GEMM input, SiLU*up output and attention output in the
+    batched-rows kernel's fragment order give the bit-identical numbers of the row-major forms
+    (the same arithmetic; only addresses differ)."""
+    L = ti.lib()
+    rng = np.random.RandomState(11)
+    M, K, N = 45, 1152, 512
+    x32 = rng.standard_normal((M, K)).astype(f32)
+    w = (rng.standard_normal(K) * 0.1 + 1).astype(f32)
+    xd, wd = dev(ti, x32), dev(ti, w)
+    Mp = (M + 15) // 16 * 16
+    rm, pk = ti.DeviceBuffer(M * K * 2), ti.DeviceBuffer(Mp * K * 2)
+    ti.check(L.ti_rmsnorm_f16(xd.ptr, K, wd.ptr, 1e-5, rm.ptr, K, M, K, None))
+    ti.check(L.ti_rmsnorm_f16_packed(xd.ptr, K, wd.ptr, 1e-5, pk.ptr, M, K, None))
+    ti.sync()
+    rows = rm.download(np.uint16, (M, K))
+    np.testing.assert_array_equal(ti.unpack_rows(pk.download(np.uint16, Mp * K), M, K), rows)
+    # GEMM on both forms: store, and SiLU*up written packed
+    wt = (rng.standard_normal((K, N)) * 0.03).astype(f32)
+    tiles, scales = ti.wpack_host(wt, 4)
+    td, sd = dev(ti, tiles), dev(ti, scales)
+    outs = []
+    for xk, xb in ((ti.X_F16, rm), (ti.X_F16_PACKED, pk)):
+        yd = ti.DeviceBuffer(M * N * 4)
+        ep = ti.Epilogue()
+        ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F32, N, yd.ptr
+        ti.check(L.ti_gemm_wq_a16(td.ptr, sd.ptr, 4, xb.ptr, xk, K, None, 1e-5, M, N, K, C.byref(ep), None))
+        ti.sync()
+        outs.append(yd.download(f32, (M, N)))
+    np.testing.assert_array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+    I = 256
+    g = (rng.standard_normal((K, I)) * 0.05).astype(f32)
+    u = (rng.standard_normal((K, I)) * 0.05).astype(f32)
+    tg, sg = ti.wpack_host(g, 4, n_total=2 * I, row_map=ti.ROWS_INTERLEAVE8, row_offset=0)
+    ti.wpack_host(u, 4, n_total=2 * I, row_map=ti.ROWS_INTERLEAVE8, row_offset=8, tiles=tg, scales=sg)
+    tgd, sgd = dev(ti, tg), dev(ti, sg)        # (held: a temporary's buffer would be freed before the launch)
+    acts = []
+    for packed in (0, 1):
+        yd = ti.DeviceBuffer(Mp * I * 2)
+        ep = ti.Epilogue()
+        ep.kind, ep.ldo, ep.out, ep.out_packed = ti.EPI_SILU_MUL_F16, I, yd.ptr, packed
+        ti.check(L.ti_gemm_wq_a16(tgd.ptr, sgd.ptr, 4, pk.ptr, ti.X_F16_PACKED, K, None, 1e-5, M, 2 * I, K,
+                                  C.byref(ep), None))
+        ti.sync()
+        a = yd.download(np.uint16, Mp * I)
+        acts.append(ti.unpack_rows(a, M, I) if packed else a[: M * I].reshape(M, I))
+    np.testing.assert_array_equal(acts[0], acts[1])
+    # attention output, both layouts
+    heads, kvh, hd, max_seq = 4, 2, 64, 48
+    q = rng.standard_normal((M, heads * hd)).astype(f32)
+    kc = (rng.standard_normal((M, kvh, max_seq, hd)) * 0.5).astype(np.float16)
+    vc = (rng.standard_normal((M, kvh, max_seq, hd)) * 0.5).astype(np.float16)
+    pos = rng.randint(0, max_seq, size=M).astype(np.int32)
+    qd_, kd, vd, pd = dev(ti, q), dev(ti, kc), dev(ti, vc), dev(ti, pos)
+    ws = ti.DeviceBuffer(L.ti_attn_workspace_bytes(M, heads, hd, 4))
+    ws.zero()
+    o_rm, o_pk = ti.DeviceBuffer(M * heads * hd * 2), ti.DeviceBuffer(Mp * heads * hd * 2)
+    stride = kvh * max_seq * hd
+    ti.check(L.ti_attn_decode(qd_.ptr, kd.ptr, vd.ptr, stride, max_seq, pd.ptr, M, heads, kvh, hd, 4, ws.ptr,
+                              o_rm.ptr, None))
+    ti.check(L.ti_attn_decode_packed(qd_.ptr, kd.ptr, vd.ptr, stride, max_seq, pd.ptr, M, heads, kvh, hd, 4, ws.ptr,
+                                     o_pk.ptr, None))
+    ti.sync()
+    np.testing.assert_array_equal(ti.unpack_rows(o_pk.download(np.uint16, Mp * heads * hd), M, heads * hd),
+                                  o_rm.download(np.uint16, (M, heads * hd)))

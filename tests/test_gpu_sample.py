@@ -70,8 +70,8 @@ def test_device_sampler_tied_logits(ti, oracle):
             differ += 1
             continue
         draws = np.array([0.3, 0.8], f32)
-        tok_d, lp_d = ti.DeviceBuffer(2 * 4), ti.DeviceBuffer(2 * 4)
-        ti.check(ti.lib().ti_sample_device(ld.ptr, V, 2, V, T, k, p, dev(ti, draws).ptr, tok_d.ptr, lp_d.ptr, None))
+        tok_d, lp_d, dd = ti.DeviceBuffer(2 * 4), ti.DeviceBuffer(2 * 4), dev(ti, draws)
+        ti.check(ti.lib().ti_sample_device(ld.ptr, V, 2, V, T, k, p, dd.ptr, tok_d.ptr, lp_d.ptr, None))
         ti.sync()
         got_t, got_lp = tok_d.download(np.int32, 2), lp_d.download(f32, 2)
         for m in range(2):

@@ -23,11 +23,11 @@ ROOT = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("TI_LIB") or os.path.join(HERE, "lib", "libturboinfer_amd.so")
 
 TI_OK = 0
-X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED, X_ATTN_SPLITS = 0, 1, 2, 3, 4
+X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED, X_ATTN_SPLITS, X_F16_PACKED = 0, 1, 2, 3, 4, 5
 ATTN_MAX_PART_SPLITS = 8           # TI_ATTN_MAX_PART_SPLITS (include/ti_hip.h)
 EPI_STORE_F32, EPI_STORE_F16, EPI_RESID_F32, EPI_SILU_MUL_F16, EPI_QKV_ROPE_KV, EPI_LOGITS_ARGMAX = range(6)
 ARGMAX_SLOTS = 32
-GEMM_MAX_ROWS = 32                 # TI_GEMM_MAX_ROWS (include/ti_hip.h)   # TI_ARGMAX_SLOTS (include/ti_hip.h)
+GEMM_MAX_ROWS = 64                 # TI_GEMM_MAX_ROWS (include/ti_hip.h)   # TI_ARGMAX_SLOTS (include/ti_hip.h)
 SCALE_GROUP, SCALE_TENSOR, SCALE_UNIT = 0, 1, 2
 ROWS_CONCAT, ROWS_INTERLEAVE8 = 0, 1
 (W_Q, W_K, W_V, W_O, W_GATE, W_UP, W_DOWN, W_LM_HEAD, V_ATTN_NORM, V_FFN_NORM, V_OUT_NORM, E_EMBED) = range(12)
@@ -43,7 +43,7 @@ class Epilogue(C.Structure):
                 ("pos", C.c_void_p), ("rope_cs", C.c_void_p), ("k_cache", C.c_void_p), ("v_cache", C.c_void_p),
                 ("kv_stream_stride", C.c_int64), ("argmax", C.c_void_p), ("step_ctr", C.c_void_p),
                 ("advance", C.c_int32), ("n_ss", C.c_int32), ("ss_in", C.c_void_p),
-                ("fold_w", C.c_void_p), ("fold_x", C.c_void_p), ("fold_ss", C.c_void_p)]
+                ("fold_w", C.c_void_p), ("fold_x", C.c_void_p), ("fold_ss", C.c_void_p), ("out_packed", C.c_int32)]
 
 
 class StepArgs(C.Structure):
@@ -70,7 +70,7 @@ EXPORTED = [
     "ti_device_sync", "ti_event_create", "ti_event_destroy", "ti_event_record", "ti_event_elapsed_ms",
     "ti_wpack_tile_bytes", "ti_wpack_scale_bytes", "ti_wpack_host", "ti_wsynth_device", "ti_fill_uniform_f16",
     "ti_fill_uniform_f32", "ti_fill_kv_uniform", "ti_kv_copy_slots", "ti_gemm_wq_a16", "ti_gemm_lds_bytes", "ti_gemm_prepare",
-    "ti_gemm_max_rows", "ti_rmsnorm_f16",
+    "ti_gemm_max_rows", "ti_rmsnorm_f16", "ti_rmsnorm_f16_packed", "ti_attn_decode_packed",
     "ti_attn_workspace_bytes", "ti_attn_decode", "ti_step_begin", "ti_matmul_f32", "ti_rms_norm_f32",
     "ti_rope_f32", "ti_silu_f32", "ti_relu_f32", "ti_add_f32", "ti_mul_f32", "ti_softmax_f32", "ti_attention_f32",
     "ti_argmax_f32", "ti_engine_create", "ti_engine_destroy", "ti_engine_get_stream", "ti_engine_memory", "ti_engine_set_tensor",
@@ -121,9 +121,11 @@ def lib() -> C.CDLL:
         L.ti_gemm_lds_bytes.argtypes = [i32, i32, i32]
         L.ti_gemm_max_rows.argtypes = [i32, i32, i32, i32]
         L.ti_rmsnorm_f16.argtypes = [vp, i32, vp, f32, vp, i32, i32, i32, vp]
+        L.ti_rmsnorm_f16_packed.argtypes = [vp, i32, vp, f32, vp, i32, i32, vp]
         L.ti_attn_workspace_bytes.argtypes = [i32, i32, i32, i32]
         L.ti_attn_workspace_bytes.restype = sz
         L.ti_attn_decode.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
+        L.ti_attn_decode_packed.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
         if hasattr(L, "ti_sample_device"):
             L.ti_sample_device.argtypes = [vp, i32, i32, i32, f32, i32, f32, vp, vp, vp, vp]
             L.ti_engine_generate_sampled.argtypes = [vp, i32, vp, vp, i32, vp, i32, f32, i32, f32, vp, vp, vp]
@@ -255,6 +257,27 @@ def wpack_host(w: np.ndarray, bits: int, n_total: int | None = None, scale_mode:
     check(L.ti_wpack_host(_ptr(w), K, N, n_total, bits, scale_mode, row_map, row_offset, _ptr(tiles),
                           _ptr(scales) if bits != 16 else None))
     return tiles, scales
+
+
+def packed_index(m, k, K):
+    """TI_PACKED_INDEX (include/ti_hip.h): element (m, k) of a TI_X_F16_PACKED operand (numpy arrays ok)."""
+    kt = K // 128
+    return (((((m >> 4) * kt + (k >> 7)) * 4 + ((k >> 3) & 3)) * 64 + ((k >> 5) & 3) * 16 + (m & 15)) * 8 + (k & 7))
+
+
+def pack_rows(x):
+    """Row-major [M][K] -> TI_X_F16_PACKED order (rows padded to a multiple of 16)."""
+    M, K = x.shape
+    Mp = (M + 15) // 16 * 16
+    out = np.zeros(Mp * K, x.dtype)
+    mm, kk = np.meshgrid(np.arange(M), np.arange(K), indexing="ij")
+    out[packed_index(mm, kk, K)] = x
+    return out
+
+
+def unpack_rows(p, M, K):
+    mm, kk = np.meshgrid(np.arange(M), np.arange(K), indexing="ij")
+    return p[packed_index(mm, kk, K)]
 
 
 def rope_table(pos, head_dim: int, theta: float) -> np.ndarray:

@@ -213,6 +213,11 @@ int validate(const ti_engine_config& c) {
   return TI_OK;
 }
 
+// Rows of the batched-rows kernel (int4, M > 16) take their fp16 operands in fragment order
+// (TI_X_F16_PACKED): the rms_norm prep, the attention output and the SiLU*up output are written
+// that way, so every operand load of the kernel is one contiguous KiB per wave.
+bool packed_rows(const ti_engine* e, int M) { return e->c.bits == 4 && M > 16; }
+
 // One projection for rows [0, M): the fused kernel in chunks of the rows its LDS image
 // holds, or -- int4, when the rows do not fit -- rms_norm into fp16 rows once (e->xn) and
 // the batched-rows kernel in chunks of TI_GEMM_MAX_ROWS.  Graph-capturable.
@@ -220,7 +225,13 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
               const ti_epilogue& epi, size_t out_elem, bool last_gets_ctr) {
   const ti_engine_config& c = e->c;
   int rows = ti_gemm_max_rows(c.bits, x_kind, W.N, W.K);
-  if (x_kind == TI_X_F32_RMSNORM && rows < M && c.bits == 4 && e->xn) {
+  if (x_kind == TI_X_F32_RMSNORM && packed_rows(e, M) && e->xn) {
+    TI_TRY(ti_rmsnorm_f16_packed(static_cast<const float*>(x), ldx, nw, c.eps, e->xn, M, W.K, e->s));
+    x = e->xn;
+    x_kind = TI_X_F16_PACKED;
+    ldx = W.K;
+    rows = ti_gemm_max_rows(c.bits, x_kind, W.N, W.K);
+  } else if (x_kind == TI_X_F32_RMSNORM && rows < M && c.bits == 4 && e->xn) {
     TI_TRY(ti_rmsnorm_f16(static_cast<const float*>(x), ldx, nw, c.eps, e->xn, W.K, M, W.K, e->s));
     x = e->xn;
     x_kind = TI_X_F16;
@@ -228,7 +239,7 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
     rows = ti_gemm_max_rows(c.bits, x_kind, W.N, W.K);
   }
   if (rows < 1) return ti_set_error(TI_ERR_UNSUPPORTED, "engine: no GEMM kernel for N=%d K=%d", W.N, W.K);
-  const size_t x_elem = x_kind == TI_X_F16 || x_kind == TI_X_F16_FOLDED ? 2 : 4;
+  const size_t x_elem = x_kind == TI_X_F16 || x_kind == TI_X_F16_FOLDED || x_kind == TI_X_F16_PACKED ? 2 : 4;
   for (int m0 = 0; m0 < M; m0 += rows) {
     const int mm = std::min(rows, M - m0);
     ti_epilogue ep = epi;
@@ -438,7 +449,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   sa.step_ctr = e->step_ctr;
   const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
   // fold (M == 1): every rms_norm input is handed over as fx + ss partials by its producer
-  const bool fold = fold_usable(e, M), part = part_usable(e, M), qa = qa_usable(e, M);
+  const bool fold = fold_usable(e, M), part = part_usable(e, M), qa = qa_usable(e, M), pk = packed_rows(e, M);
   auto next_norm = [&](int l) -> const float* { return l < c.layers ? e->layer[l].attn_norm : e->out_norm; };
   if (fold) {
     sa.fold_w = next_norm(0);
@@ -510,15 +521,17 @@ int enqueue_step(ti_engine* e, int M, int advance) {
       TI_TRY(gemm(L.o, e->part_o, TI_X_ATTN_SPLITS, qd, 2, nullptr, eo, 4, false));
     } else {
       TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));
-      TI_TRY(ti_attn_decode(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M, c.heads, c.kv_heads, c.head_dim,
-                            e->splits_for(M), e->ws, e->attn, e->s));
-      TI_TRY(gemm(L.o, e->attn, TI_X_F16, qd, 2, nullptr, eo, 4, false));
+      TI_TRY((pk ? ti_attn_decode_packed : ti_attn_decode)(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M,
+                                                           c.heads, c.kv_heads, c.head_dim, e->splits_for(M), e->ws,
+                                                           e->attn, e->s));
+      TI_TRY(gemm(L.o, e->attn, pk ? TI_X_F16_PACKED : TI_X_F16, qd, 2, nullptr, eo, 4, false));
     }
 
     ti_epilogue eg{};
     eg.kind = TI_EPI_SILU_MUL_F16;
     eg.ldo = I;
     eg.out = e->act;
+    eg.out_packed = pk;
     TI_TRY(gemm(L.gu, e->h, TI_X_F32_RMSNORM, H, 4, L.ffn_norm, eg, 2, false));
 
     ti_epilogue ed{};
@@ -526,7 +539,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     ed.ldo = H;
     ed.out = e->h;
     fold_into(ed, next_norm(l + 1));
-    TI_TRY(gemm(L.down, e->act, TI_X_F16, I, 2, nullptr, ed, 4, false));
+    TI_TRY(gemm(L.down, e->act, pk ? TI_X_F16_PACKED : TI_X_F16, I, 2, nullptr, ed, 4, false));
   }
   ti_epilogue el{};
   el.kind = TI_EPI_LOGITS_ARGMAX;
@@ -588,23 +601,26 @@ int enqueue_prefill(ti_engine* e, int m, int t0, int rows, int base) {
     ep.v_cache = vc;
     ep.kv_stream_stride = 0;
     TI_TRY(gemm_rows(e, L.qkv, rows, e->h, TI_X_F32_RMSNORM, H, L.attn_norm, ep, 4, false));
-    TI_TRY(ti_attn_decode(e->q, kc, vc, 0, c.max_seq, e->pos, rows, c.heads, c.kv_heads, c.head_dim,
-                          e->splits_for(rows), e->ws, e->attn, e->s));
+    const bool pk = packed_rows(e, rows);
+    TI_TRY((pk ? ti_attn_decode_packed : ti_attn_decode)(e->q, kc, vc, 0, c.max_seq, e->pos, rows, c.heads,
+                                                         c.kv_heads, c.head_dim, e->splits_for(rows), e->ws, e->attn,
+                                                         e->s));
     ti_epilogue eo{};
     eo.kind = TI_EPI_RESID_F32;
     eo.ldo = H;
     eo.out = e->h;
-    TI_TRY(gemm_rows(e, L.o, rows, e->attn, TI_X_F16, qd, nullptr, eo, 4, false));
+    TI_TRY(gemm_rows(e, L.o, rows, e->attn, pk ? TI_X_F16_PACKED : TI_X_F16, qd, nullptr, eo, 4, false));
     ti_epilogue eg{};
     eg.kind = TI_EPI_SILU_MUL_F16;
     eg.ldo = I;
     eg.out = e->act;
+    eg.out_packed = pk;
     TI_TRY(gemm_rows(e, L.gu, rows, e->h, TI_X_F32_RMSNORM, H, L.ffn_norm, eg, 2, false));
     ti_epilogue ed{};
     ed.kind = TI_EPI_RESID_F32;
     ed.ldo = H;
     ed.out = e->h;
-    TI_TRY(gemm_rows(e, L.down, rows, e->act, TI_X_F16, I, nullptr, ed, 4, false));
+    TI_TRY(gemm_rows(e, L.down, rows, e->act, pk ? TI_X_F16_PACKED : TI_X_F16, I, nullptr, ed, 4, false));
   }
   return TI_OK;
 }
@@ -716,8 +732,9 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     e->pf_rows = c.bits == 4 ? TI_GEMM_MAX_ROWS : 16;
     e->rows_cap = std::max(B, e->pf_rows);
     const int R = e->rows_cap;
-    if ((rc = e->alloc_t(&e->q, (size_t)R * qd)) || (rc = e->alloc_t(&e->attn, (size_t)R * qd)) ||
-        (rc = e->alloc_t(&e->act, (size_t)R * I)) || (rc = e->alloc_t(&e->xn, (size_t)R * H)) ||
+    const int Rp = (R + 15) / 16 * 16;   // packed operands hold whole 16-row blocks
+    if ((rc = e->alloc_t(&e->q, (size_t)R * qd)) || (rc = e->alloc_t(&e->attn, (size_t)Rp * qd)) ||
+        (rc = e->alloc_t(&e->act, (size_t)Rp * I)) || (rc = e->alloc_t(&e->xn, (size_t)Rp * std::max(H, I))) ||
         (rc = e->alloc(reinterpret_cast<void**>(&e->ws), ti_attn_workspace_bytes(R, c.heads, hd, e->splits_max))) ||
         (rc = e->alloc_t(&e->pf_ones, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->pf_zero, (size_t)1)) ||
         (rc = e->alloc_t(&e->pf_base, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->fx, (size_t)H)) ||
@@ -1439,6 +1456,8 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
         ep.head_dim = c.head_dim;
       }
     }
+    if (packed_rows(e, n) && (which == 1 || which == 3)) xk = TI_X_F16_PACKED;   // enqueue_step's operands
+    if (packed_rows(e, n) && which == 2) ep.out_packed = 1;
     if (fold && xk == TI_X_F32_RMSNORM) {   // the step's consumer form (enqueue_step)
       x = e->fx;
       xk = TI_X_F16_FOLDED;
@@ -1465,8 +1484,9 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
       return ti_attn_decode_partials(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, n, c.heads, c.kv_heads,
                                      c.head_dim, e->splits_for(n), e->part_o, e->part_ml, e->s);
     if (which == 5)
-      return ti_attn_decode(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, n, c.heads, c.kv_heads, c.head_dim,
-                            e->splits_for(n), e->ws, e->attn, e->s);
+      return (packed_rows(e, n) ? ti_attn_decode_packed : ti_attn_decode)(e->q, L.kc, L.vc, e->kv_stride, c.max_seq,
+                                                                           e->pos, n, c.heads, c.kv_heads, c.head_dim,
+                                                                           e->splits_for(n), e->ws, e->attn, e->s);
     return gemm_rows(e, *W, n, x, xk, ldx, nw, ep, which == 2 ? 2 : 4, false);
   };
   // The `reps` launches are captured once into a graph and the graph is replayed `rounds`

@@ -86,7 +86,7 @@ extern "C" size_t ti_attn_workspace_bytes(int M, int heads, int head_dim, int sp
 static int attn_impl(const float* q, const uint16_t* k_cache, const uint16_t* v_cache, int64_t kv_stream_stride,
                      int max_seq, const int32_t* pos, int M, int heads, int kv_heads, int head_dim, int splits,
                      float* workspace, uint16_t* out, ti_chain* chain, ti_stream_t stream,
-                     uint16_t* part_o = nullptr, float* part_ml = nullptr) {
+                     uint16_t* part_o = nullptr, float* part_ml = nullptr, bool packed = false) {
   using namespace ti;
   if (!q || !k_cache || !v_cache || !pos || ((!workspace || !out) && !part_o))
     return ti_set_error(TI_ERR_ARG, "ti_attn_decode: null pointer");
@@ -103,7 +103,11 @@ static int attn_impl(const float* q, const uint16_t* k_cache, const uint16_t* v_
   // splits only shape the work (results agree to rounding); the merge stages all partials
   // of a kv-head group in LDS, which bounds them.
   if (!part_o) splits = std::min(splits, std::max(1, ti::attn_max_splits(G, head_dim)));
+  if (packed && (((heads * head_dim) & 127) || chain || part_o))
+    return ti_set_error(TI_ERR_ARG, "ti_attn_decode_packed: heads * head_dim %d not a multiple of 128",
+                        heads * head_dim);
   AttnArgs a;
+  a.out_kt = packed ? heads * head_dim / 128 : 0;
   a.part_o = part_o;
   a.part_ml = part_ml;
   a.q = q;
@@ -138,6 +142,14 @@ extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uin
                               ti_stream_t stream) {
   return attn_impl(q, k_cache, v_cache, kv_stream_stride, max_seq, pos, M, heads, kv_heads, head_dim, splits, workspace,
                    out, nullptr, stream);
+}
+
+extern "C" int ti_attn_decode_packed(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
+                                     int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
+                                     int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
+                                     ti_stream_t stream) {
+  return attn_impl(q, k_cache, v_cache, kv_stream_stride, max_seq, pos, M, heads, kv_heads, head_dim, splits, workspace,
+                   out, nullptr, stream, nullptr, nullptr, true);
 }
 
 extern "C" int ti_attn_decode_chained(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,

@@ -25,6 +25,7 @@ struct AttnArgs {
   // (max, sum) and the merge is left to the consumer (the O projection's x staging)
   uint16_t* part_o;   // [M][heads][splits][HD] fp16, nullptr = merge in this launch
   float* part_ml;     // [M][heads][splits][2]
+  int32_t out_kt;     // > 0: out in TI_X_F16_PACKED order with K / 128 = out_kt (ti_attn_decode_packed)
 };
 
 #ifndef TI_ATTN_RING
@@ -171,6 +172,10 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
   };
   // fp16 output element idx (thread parity == idx parity): chained, lane pairs store 4 bytes
   auto store_out = [&](size_t idx, float val) {
+    if (a.out_kt > 0) {   // packed: row m = idx / K, column idx % K (parity kept: pairs stay adjacent)
+      const int K = a.heads * HD, m = (int)(idx / (size_t)K), k = (int)(idx - (size_t)m * K);
+      idx = TI_PACKED_INDEX(m, k, a.out_kt);
+    }
     const uint32_t hv = f2h(val);
     if constexpr (CH) {
       const uint32_t hp = (uint32_t)__shfl_xor((int)hv, 1, kWave);

@@ -55,9 +55,16 @@ __device__ unsigned long long g_gemv_ts[4096 * 8];
 __device__ unsigned long long g_gemv_wts[4096 * 8];   // per-wave end of stream
 #define GEMV_WTS() \
   do { if ((threadIdx.x & 63) == 0) g_gemv_wts[blockIdx.x * 8 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+__device__ unsigned long long g_rows_ts[4096 * 8 * 8];   // [wg][wave][phase] (gemm_rows_kernel)
+#define ROWS_TS(k)                                                                                     \
+  do {                                                                                                 \
+    if ((threadIdx.x & 63) == 0)                                                                       \
+      g_rows_ts[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();   \
+  } while (0)
 #else
 #define GEMV_WTS() do { } while (0)
 #define GEMV_TS(k) do { } while (0)
+#define ROWS_TS(k) do { } while (0)
 #endif
 
 constexpr int kGemvWaves = 8;
@@ -943,7 +950,8 @@ __device__ __forceinline__ void epilogue_mb(const GemvArgs& a, int nt, int m, in
       if (live) ((float*)e.out)[(size_t)m * e.ldo + ng] = v;
       break;
     case TI_EPI_STORE_F16:
-      if (live) ((uint16_t*)e.out)[(size_t)m * e.ldo + ng] = f2h(v);
+      if (live)
+        ((uint16_t*)e.out)[e.out_packed ? TI_PACKED_INDEX(m, ng, e.ldo >> 7) : (size_t)m * e.ldo + ng] = f2h(v);
       break;
     case TI_EPI_RESID_F32:
       if (live) {
@@ -955,7 +963,8 @@ __device__ __forceinline__ void epilogue_mb(const GemvArgs& a, int nt, int m, in
       const float up = __shfl_down(v, 8, kWave);
       if (live && n < 8) {
         const float s = v / (1.0f + expf(-v));
-        ((uint16_t*)e.out)[(size_t)m * e.ldo + nt * 8 + n] = f2h(up * s);
+        const int j = nt * 8 + n;
+        ((uint16_t*)e.out)[e.out_packed ? TI_PACKED_INDEX(m, j, e.ldo >> 7) : (size_t)m * e.ldo + j] = f2h(up * s);
       }
       break;
     }
@@ -1251,6 +1260,164 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_mbr_kernel(const GemvArg
     *a.epi.step_ctr += a.epi.advance;
 }
 
+// ------------------------------------------------------------- rows kernel (17..64 rows)
+// Batched decode at configs[3] / [4] scale (64 / 32 streams): the weights are still read once
+// per launch, but every weight fragment now meets up to 64 rows.  Register operands, no LDS in
+// the stream: the 8 waves form RG row groups of 8 / RG waves; a group owns MB 16-row blocks
+// and splits the k-tiles over its waves (k-tile w, w + 8 / RG, ...).  Per item a wave holds
+// the packed weights of the workgroup's NTL tiles at that k-tile (a WD-slot ring, issued
+// WD - 1 items ahead: HBM latency) and its rows' x fragments (two slots, one item ahead: L2
+// latency).  The item count is padded to a multiple of WD with zero-scale clamped items, so
+// the loop body has no branches (no vmcnt(0) at a join).  After the stream the partial blocks
+// of the group's waves are summed in a fixed order through LDS and the epilogue runs.
+template <int MB, int NTL, int RG, bool XP = false>
+struct RowsCfg {
+  static constexpr int kGroupWaves = kGemvWaves / RG;
+  static constexpr int kWD = MB * NTL <= 3 ? 4 : 3;   // ring slots (VGPR budget: no spills)
+};
+__host__ __device__ inline int rows_slab_bytes(int mb_total, int ntl) {
+  return align16(ntl * mb_total * kGemvWaves * kWave * 16);
+}
+__host__ __device__ inline int rows_lds_bytes(int mb_total, int ntl, int K) {
+  return rows_slab_bytes(mb_total, ntl) + align16(ntl * (K >> 7) * 32);
+}
+
+template <int MB, int NTL, int RG, bool XP>
+__global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvArgs a, int grid) {
+  constexpr int GW = RowsCfg<MB, NTL, RG>::kGroupWaves, WD = RowsCfg<MB, NTL, RG>::kWD;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int KT = a.K >> 7, NT = a.N >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, kq = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave / GW, gw = wave % GW;
+  const int t0 = (int)(blockIdx.x * (unsigned)NT / (unsigned)grid);
+  const int t1 = (int)((blockIdx.x + 1) * (unsigned)NT / (unsigned)grid);
+  const int ntl = t1 - t0;                           // NTL or NTL - 1
+  const int NI = (KT + GW - 1) / GW, NIP = (NI + WD - 1) / WD * WD;
+  ROWS_TS(0);
+  f32x4* slab = (f32x4*)smem;                        // after the stream: [NTL][RG * MB][8][64]
+  uint16_t* sl = (uint16_t*)(smem + rows_slab_bytes(RG * MB, NTL));   // [ntl][KT][16]
+
+  // the workgroup's group scales (ntl * KT <= 512: two 16-byte pieces per thread), first
+  const int n_sc = ntl * KT * 2;
+  const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16);
+  const u32x4 sc0 = ld_w(sg + (tid < n_sc ? tid : 0));
+  const u32x4 sc1 = ld_w(sg + (tid + kGemvThreads < n_sc ? tid + kGemvThreads : 0));
+
+  const f16* xg = (const f16*)a.x;
+  const u32x4* tb = a.tiles + lane;
+  auto kt_of = [&](int it) { return min(gw + GW * it, KT - 1); };
+  auto load_w = [&](u32x4 (&w)[NTL], int it) {
+#if TI_GEMV_EXP & 128   // diagnostic: no weight traffic after the first ring
+    it = it < WD ? it : it % WD;
+#endif
+    const int kt = kt_of(it);
+#pragma unroll
+    for (int tl = 0; tl < NTL; ++tl) w[tl] = ld_w(tb + ((size_t)(t0 + min(tl, ntl - 1)) * KT + kt) * kWave);
+  };
+  auto load_x = [&](f16x8 (&x)[MB][4], int it) {
+#if TI_GEMV_EXP & 256   // diagnostic: no activation traffic after the first ring
+    it = it < WD ? it : it % WD;
+#endif
+    const int kt = kt_of(it);
+#pragma unroll
+    for (int b = 0; b < MB; ++b) {
+      if constexpr (XP) {   // TI_X_F16_PACKED: one contiguous KiB per (block, s4)
+        const int bb = min(grp * MB + b, (a.M - 1) >> 4);
+        const f16* xp = xg + ((size_t)(bb * KT + kt) * 4) * 512 + lane * 8;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) x[b][s4] = *(const f16x8*)(xp + s4 * 512);
+      } else {
+        const int m = min((grp * MB + b) * 16 + r, a.M - 1);
+        const f16* xr = xg + (size_t)m * a.ldx + kt * 128 + kq * 32;   // the tile's k order (A fragments)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) x[b][s4] = *(const f16x8*)(xr + s4 * 8);
+      }
+    }
+  };
+  u32x4 W[WD][NTL];
+  f16x8 X[WD][MB][4];
+#pragma unroll
+  for (int u = 0; u < WD - 1; ++u) {
+    load_w(W[u], u);
+    load_x(X[u], u);
+  }
+  if (tid < n_sc) ((u32x4*)sl)[tid] = sc0;
+  if (tid + kGemvThreads < n_sc) ((u32x4*)sl)[tid + kGemvThreads] = sc1;
+  lds_barrier();
+  ROWS_TS(1);
+
+  f32x4 acc[NTL][MB];
+#pragma unroll
+  for (int t = 0; t < NTL; ++t)
+#pragma unroll
+    for (int b = 0; b < MB; ++b) acc[t][b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+  uint32_t magic;
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
+  auto compute = [&](const u32x4 (&w)[NTL], const f16x8 (&x)[MB][4], int it) {
+    const int kt = gw + GW * it;
+    const bool kvalid = kt < KT;
+    const int ktc = kvalid ? kt : KT - 1;
+#pragma unroll
+    for (int tl = 0; tl < NTL; ++tl) {
+      f32x4 t[MB];
+#pragma unroll
+      for (int b = 0; b < MB; ++b) t[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const f16x8 bf = deq_int4_signed(w[tl][s4], magic);
+#pragma unroll
+        for (int b = 0; b < MB; ++b) t[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(x[b][s4], bf, t[b], 0, 0, 0);
+      }
+      const float sc = kvalid ? h2f(sl[(min(tl, ntl - 1) * KT + ktc) * 16 + r]) : 0.0f;
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        acc[tl][b][0] = fmaf(sc, t[b][0], acc[tl][b][0]);
+        acc[tl][b][1] = fmaf(sc, t[b][1], acc[tl][b][1]);
+        acc[tl][b][2] = fmaf(sc, t[b][2], acc[tl][b][2]);
+        acc[tl][b][3] = fmaf(sc, t[b][3], acc[tl][b][3]);
+      }
+    }
+  };
+  for (int i = 0; i < NIP; i += WD) {
+#pragma unroll
+    for (int u = 0; u < WD; ++u) {
+      load_w(W[(u + WD - 1) % WD], i + u + WD - 1);  // WD - 1 items ahead (clamped past the end)
+      load_x(X[(u + WD - 1) % WD], i + u + WD - 1);
+      compute(W[u], X[u], i + u);
+#if TI_GEMV_EXP & 4
+      if (i + u == 0) ROWS_TS(2);
+#endif
+    }
+  }
+  ROWS_TS(3);
+
+  // ---- sum each group's waves in a fixed order, then the epilogue
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ROWS_TS(4);
+#pragma unroll
+  for (int tl = 0; tl < NTL; ++tl)
+#pragma unroll
+    for (int b = 0; b < MB; ++b) slab[((tl * RG * MB + grp * MB + b) * kGemvWaves + wave) * kWave + lane] = acc[tl][b];
+  lds_barrier();
+  const int n = lane & 15, nblk = ntl * RG * MB * 4;
+  const int nblk_pad = (nblk + kGemvWaves - 1) / kGemvWaves * kGemvWaves;
+  for (int cb = wave; cb < nblk_pad; cb += kGemvWaves) {   // wave-uniform trip count (shuffles inside)
+    const bool ok = cb < nblk;
+    const int cbc = ok ? cb : 0, tl = cbc / (RG * MB * 4), bb = (cbc >> 2) % (RG * MB), i = cbc & 3;
+    const int g = bb / MB;
+    const float* sp = (const float*)(slab + (tl * RG * MB + bb) * kGemvWaves * kWave + lane) + i;
+    float v = 0.0f;
+#pragma unroll
+    for (int w = 0; w < GW; ++w) v += sp[(g * GW + w) * kWave * 4];
+    const int m = bb * 16 + 4 * (lane >> 4) + i;
+    epilogue_mb(a, t0 + tl, m, n, v, ok && m < a.M);
+  }
+  ROWS_TS(5);
+  if (a.epi.kind == TI_EPI_LOGITS_ARGMAX && a.epi.step_ctr && blockIdx.x == 0 && tid == 0)
+    *a.epi.step_ctr += a.epi.advance;
+}
+
 static int g_num_cus = 0;
 
 __host__ inline int gemv_xmode(int x_kind, int M, int K) {
@@ -1298,7 +1465,7 @@ static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid, cons
 // rms_norm rows into fp16 (the batched path's activation prep): the same arithmetic as the
 // fused XM_NORM staging above (per-thread k8 pieces, wave sums, 8 waves in order).
 __global__ __launch_bounds__(kGemvThreads) void rmsnorm_f16_kernel(const float* x, int ldx, const float* w, float eps,
-                                                                    uint16_t* y, int ldy, int K) {
+                                                                    uint16_t* y, int ldy, int K, int pk_kt) {
   __shared__ float red[kGemvWaves];
   const int m = blockIdx.x, tid = threadIdx.x, K8 = K >> 3;
   const float* xr = x + (size_t)m * ldx;
@@ -1323,7 +1490,7 @@ __global__ __launch_bounds__(kGemvThreads) void rmsnorm_f16_kernel(const float* 
     h[2] = (f16)((v0.z / rms) * w0.z); h[3] = (f16)((v0.w / rms) * w0.w);
     h[4] = (f16)((v1.x / rms) * w1.x); h[5] = (f16)((v1.y / rms) * w1.y);
     h[6] = (f16)((v1.z / rms) * w1.z); h[7] = (f16)((v1.w / rms) * w1.w);
-    *(f16x8*)(y + (size_t)m * ldy + 8 * k8) = h;
+    *(f16x8*)(y + (pk_kt > 0 ? TI_PACKED_INDEX(m, 8 * k8, pk_kt) : (size_t)m * ldy + 8 * k8)) = h;
   }
 }
 
@@ -1385,6 +1552,62 @@ static int launch_mb(const GemvArgs& a, int MB, int grid, int ntl, int lds, hipS
     default: return launch_mb_t<1, 8>(a, grid, lds, s);
   }
 }
+// Rows kernel (M > 16): RG row groups x MB blocks per group, NTL tiles per workgroup.
+// TI_GEMM_ROWS=0 keeps the older 16/32-row kernels (A/B knob); TI_GEMM_ROWS_RG forces RG.
+static int g_rows_on = -1, g_rows_rg = -1;
+static bool rows_on() {
+  if (g_rows_on < 0) {
+    const char* s = getenv("TI_GEMM_ROWS");
+    g_rows_on = s ? (atoi(s) != 0) : 1;
+    const char* r = getenv("TI_GEMM_ROWS_RG");
+    g_rows_rg = r && (atoi(r) == 1 || atoi(r) == 2) ? atoi(r) : 0;
+  }
+  return g_rows_on == 1;
+}
+__host__ inline void rows_shape(int M, int* MB, int* RG) {
+  const int rg = M > 32 ? 2 : (g_rows_rg > 0 ? g_rows_rg : 1);   // 64 rows: two groups of 32
+  const int mb = (M + 16 * rg - 1) / (16 * rg);
+  *MB = mb;
+  *RG = rg;
+}
+__host__ inline int rows_tiles_cap(int MB, int K) {
+  const int lim = MB >= 2 ? 3 : 4, cap = 512 / (K >> 7);   // VGPR budget: no spills
+  return cap < 1 ? 1 : (cap > lim ? lim : cap);
+}
+__host__ inline int rows_grid(int MB, int N, int K, int num_cus, int* ntl_out) {
+  const int NT = N >> 4, cap = rows_tiles_cap(MB, K);
+  int grid = NT < num_cus ? NT : num_cus;
+  if ((NT + grid - 1) / grid > cap) grid = (NT + cap - 1) / cap;
+  *ntl_out = (NT + grid - 1) / grid;
+  return grid;
+}
+template <int MB, int RG, bool XP>
+static int launch_rows_t(const GemvArgs& a, int ntl, int grid, int lds, hipStream_t s) {
+  if (ntl == 1) hipLaunchKernelGGL((gemm_rows_kernel<MB, 1, RG, XP>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
+  else if (ntl == 2) hipLaunchKernelGGL((gemm_rows_kernel<MB, 2, RG, XP>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
+  else if (ntl == 3) hipLaunchKernelGGL((gemm_rows_kernel<MB, 3, RG, XP>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
+  else if constexpr (MB < 2) hipLaunchKernelGGL((gemm_rows_kernel<MB, 4, RG, XP>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
+  else return ti_set_error(TI_ERR_ARG, "gemm_rows_kernel: %d tiles per workgroup at MB %d", ntl, MB);
+  TI_LAUNCH_CHECK("gemm_rows_kernel");
+  return TI_OK;
+}
+template <bool XP>
+static int launch_rows_x(const GemvArgs& a, int MB, int RG, int ntl, int grid, int lds, hipStream_t s) {
+  if (RG == 2) return MB == 1 ? launch_rows_t<1, 2, XP>(a, ntl, grid, lds, s) : launch_rows_t<2, 2, XP>(a, ntl, grid, lds, s);
+  return MB == 1 ? launch_rows_t<1, 1, XP>(a, ntl, grid, lds, s) : launch_rows_t<2, 1, XP>(a, ntl, grid, lds, s);
+}
+static int launch_rows(const GemvArgs& a, int MB, int RG, int ntl, int grid, int lds, hipStream_t s) {
+  return a.x_kind == TI_X_F16_PACKED ? launch_rows_x<true>(a, MB, RG, ntl, grid, lds, s)
+                                     : launch_rows_x<false>(a, MB, RG, ntl, grid, lds, s);
+}
+#define TI_ROWS_FNS1(MB, RG, XP)                                                                          \
+  (const void*)gemm_rows_kernel<MB, 1, RG, XP>, (const void*)gemm_rows_kernel<MB, 2, RG, XP>,                \
+      (const void*)gemm_rows_kernel<MB, 3, RG, XP>
+#define TI_ROWS_FNS2(XP)                                                                                 \
+  TI_ROWS_FNS1(1, 1, XP), TI_ROWS_FNS1(2, 1, XP), TI_ROWS_FNS1(1, 2, XP), TI_ROWS_FNS1(2, 2, XP),         \
+      (const void*)gemm_rows_kernel<1, 4, 1, XP>, (const void*)gemm_rows_kernel<1, 4, 2, XP>
+#define TI_ROWS_FNS TI_ROWS_FNS2(false), TI_ROWS_FNS2(true)
+
 #define TI_MB_FNS1(K)                                                                                \
   (const void*)K<1, 1>, (const void*)K<1, 2>, (const void*)K<1, 3>, (const void*)K<1, 4>, (const void*)K<1, 5>, \
       (const void*)K<1, 6>, (const void*)K<1, 7>, (const void*)K<1, 8>
@@ -1426,7 +1649,7 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<16, XM_F16, true>, (const void*)gemv_wq_kernel<16, XM_NORM1, true>,
       (const void*)gemv_wq_kernel<4, XM_F16F>, (const void*)gemv_wq_kernel<8, XM_F16F>,
       (const void*)gemv_wq_kernel<16, XM_F16F>, (const void*)gemv_wq_kernel<4, XM_ATTN>,
-      (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS};
+      (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS, TI_ROWS_FNS};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
@@ -1461,7 +1684,8 @@ static bool use_batched(int bits, int x_kind, int M, int N, int K) {
 
 extern "C" int ti_gemm_max_rows(int bits, int x_kind, int N, int K) {
   if (N < 16 || K < 128) return 0;
-  if (bits == 4 && x_kind == TI_X_F16) return TI_GEMM_MAX_ROWS;
+  if (bits == 4 && (x_kind == TI_X_F16 || x_kind == TI_X_F16_PACKED)) return TI_GEMM_MAX_ROWS;
+  if (x_kind == TI_X_F16_PACKED) return 0;
   int m = fused_rows_pref(bits);
   while (m > 1 && !fused_fits(m, N, K)) --m;
   return fused_fits(m, N, K) ? m : 0;
@@ -1473,7 +1697,18 @@ extern "C" int ti_rmsnorm_f16(const float* x, int ldx, const float* w, float eps
   if (M < 1 || K < 8 || (K & 7) || ldx < K || ldy < K)
     return ti_set_error(TI_ERR_ARG, "ti_rmsnorm_f16: bad shape (M=%d K=%d ldx=%d ldy=%d)", M, K, ldx, ldy);
   hipLaunchKernelGGL(ti::rmsnorm_f16_kernel, dim3(M), dim3(ti::kGemvThreads), 0, (hipStream_t)stream, x, ldx, w, eps,
-                     y, ldy, K);
+                     y, ldy, K, 0);
+  TI_LAUNCH_CHECK("rmsnorm_f16_kernel");
+  return TI_OK;
+}
+
+extern "C" int ti_rmsnorm_f16_packed(const float* x, int ldx, const float* w, float eps, uint16_t* y, int M, int K,
+                                     ti_stream_t stream) {
+  if (!x || !w || !y) return ti_set_error(TI_ERR_ARG, "ti_rmsnorm_f16_packed: null pointer");
+  if (M < 1 || K < 128 || (K & 127) || ldx < K)
+    return ti_set_error(TI_ERR_ARG, "ti_rmsnorm_f16_packed: bad shape (M=%d K=%d ldx=%d)", M, K, ldx);
+  hipLaunchKernelGGL(ti::rmsnorm_f16_kernel, dim3(M), dim3(ti::kGemvThreads), 0, (hipStream_t)stream, x, ldx, w, eps,
+                     y, K, K, K >> 7);
   TI_LAUNCH_CHECK("rmsnorm_f16_kernel");
   return TI_OK;
 }
@@ -1490,8 +1725,10 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: M must be in [1,%d] (got %d)", TI_GEMM_MAX_ROWS, M);
   if (K <= 0 || (K & 127) || N <= 0 || (N & 15))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: K %% 128 and N %% 16 must be 0 (K=%d N=%d)", K, N);
-  if (x_kind < TI_X_F16 || x_kind > TI_X_ATTN_SPLITS)
+  if (x_kind < TI_X_F16 || x_kind > TI_X_F16_PACKED)
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: bad x_kind %d", x_kind);
+  if (x_kind == TI_X_F16_PACKED && (bits != 4 || chain))
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: TI_X_F16_PACKED needs bits 4 (batched-rows kernel)");
   if (x_kind == TI_X_ATTN_SPLITS &&
       (M != 1 || chain || !epi->ss_in || epi->n_ss < 1 || epi->n_ss > TI_ATTN_MAX_PART_SPLITS ||
        (epi->head_dim != 64 && epi->head_dim != 128) || K % epi->head_dim || K > 4096))
@@ -1525,15 +1762,26 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     default:
       return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: unknown epilogue %d", epi->kind);
   }
-  const bool batched = use_batched(bits, x_kind, M, N, K);
+  const bool packed_x = x_kind == TI_X_F16_PACKED;
+  const bool batched = packed_x || use_batched(bits, x_kind, M, N, K);
+  if (epi->out_packed && (!batched || (epi->kind != TI_EPI_STORE_F16 && epi->kind != TI_EPI_SILU_MUL_F16) ||
+                          (epi->ldo & 127)))
+    return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: out_packed needs the batched-rows kernel, a fp16 store / SiLU "
+                        "epilogue and ldo %% 128 == 0");
   if (batched && epi->kind == TI_EPI_RESID_F32 && epi->fold_x)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: fold_x needs the fused kernel");
-  if (batched && !(bits == 4 && x_kind == TI_X_F16))
+  if (batched && !(bits == 4 && (x_kind == TI_X_F16 || packed_x)))
     return ti_set_error(TI_ERR_UNSUPPORTED,
                         "ti_gemm_wq_a16: M=%d K=%d exceeds the fused kernel (ti_gemm_max_rows); the batched-rows "
                         "kernel needs bits 4 and fp16 rows (normalise with ti_rmsnorm_f16)", M, K);
-  int grid = 0, lds = 0, ntl = 0;
-  if (batched) {
+  int grid = 0, lds = 0, ntl = 0, rMB = 0, rRG = 0;
+  const bool rows = batched && (packed_x || M > 32 || (M > 16 && rows_on()));
+  if (rows) {
+    rows_on();
+    rows_shape(M, &rMB, &rRG);
+    grid = rows_grid(rMB, N, K, query_cus(), &ntl);
+    lds = rows_lds_bytes(rRG * rMB, ntl, K);
+  } else if (batched) {
     const int MB = M > 16 ? 2 : 1;
     grid = mb_grid(MB, N, K, query_cus(), &ntl);
     lds = mb_use_lds(MB) ? mb_lds_bytes(MB, ntl, K) : mbr_lds_bytes(MB, ntl, K);
@@ -1571,6 +1819,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   a.chain = chain_dev(chain);
   if (chain) chain->signaled = (uint32_t)grid;
   hipStream_t s = (hipStream_t)stream;
+  if (rows) return launch_rows(a, rMB, rRG, ntl, grid, lds, s);
   if (batched) return launch_mb(a, M > 16 ? 2 : 1, grid, ntl, lds, s);
   if (bits == 4) return launch_gemv<4>(a, lds, s, grid, chain);
   if (bits == 8) return launch_gemv<8>(a, lds, s, grid, chain);
