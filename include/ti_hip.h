@@ -223,8 +223,12 @@ int ti_gemm_lds_bytes(int M, int N, int K);
  * and is used above TI_GEMM_FUSED_ROWS (env, default 2) rows.  An int4 caller with more rows
  * than this returns for TI_X_F32_RMSNORM should normalise them with ti_rmsnorm_f16 and pass
  * TI_X_F16 rows.  0 = shape unsupported. */
-#define TI_GEMM_MAX_ROWS 64
+#define TI_GEMM_MAX_ROWS 256
 int ti_gemm_max_rows(int bits, int x_kind, int N, int K);
+/* 1 when M rows of an int4 GEMM go to the batched-rows kernel (17 .. 64 rows): its fp16
+ * operands are best given as TI_X_F16_PACKED.  From 65 rows (TI_GEMM_TILE_ROWS, env, <= 65) on
+ * the LDS-tiled kernel takes TI_X_F16 rows. */
+int ti_gemm_packed_rows(int bits, int M);
 /* y[m][0:K] = fp16(rms_norm(x[m][0:K]) * w), tensor_engine.cpp:1452-1508 (the batched path's
  * activation prep; the same arithmetic as the fused TI_X_F32_RMSNORM prologue). */
 int ti_rmsnorm_f16(const float* x, int ldx, const float* w, float eps, uint16_t* y, int ldy, int M, int K,

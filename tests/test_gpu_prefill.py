@@ -71,3 +71,18 @@ def test_prefill_start_pos_and_cache_contents(ti, oracle):
     assert_greedy(got[0].tolist(), ref, ref_logits)
     assert_logits_close(lg[0], ref_logits[-1])
     e.close()
+
+
+def test_prefill_tile_chunk_vs_oracle(ti, oracle):
+    """A 300-token prompt: one 256-row chunk through the LDS-tiled GEMM (ti_gemm_packed_rows
+    says row-major there) and a 43-row chunk through the batched-rows kernel (packed)."""
+    cfg = dict(MID, max_seq=512)
+    seed, jit = 21, 0.1
+    prompt = np.random.RandomState(9).randint(0, cfg["vocab"], size=300).tolist()
+    ref, ref_logits = _oracle_tokens(oracle, cfg, seed, jit, prompt, 3)
+    e = engine_for(ti, cfg)
+    e.synth(seed, jit)
+    got, lg = e.generate([prompt], 3, want_logits=True)
+    assert_greedy(got[0].tolist(), ref, ref_logits)
+    assert_logits_close(lg[0], ref_logits[-1])
+    e.close()

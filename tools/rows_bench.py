@@ -15,7 +15,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import turboinfer_amd as T  # noqa: E402
 
-XK = T.X_F16 if os.environ.get("ROWS_X") == "rowmajor" else T.X_F16_PACKED
+ROWMAJOR = os.environ.get("ROWS_X") == "rowmajor"
 Ms = [int(a) for a in sys.argv[1:]] or [32, 64]
 T.init(0)
 L = T.lib()
@@ -33,6 +33,7 @@ for name, K, N in shapes:
         T.check(L.ti_wsynth_device(1, 7 + c, K, N, N, 4, 0, 0, tiles.ptr, scales.ptr, None))
         W.append((tiles, scales))
     for M in Ms:
+        XK = T.X_F16 if ROWMAJOR or not T.lib().ti_gemm_packed_rows(4, M) else T.X_F16_PACKED
         x16 = T.DeviceBuffer.from_array(np.random.RandomState(0).standard_normal((M, K)).astype(np.float16))
         y = T.DeviceBuffer(M * N * 4)
         ep = T.Epilogue()

@@ -27,7 +27,7 @@ X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED, X_ATTN_SPLITS, X_F16_PACKED = 0, 1, 2
 ATTN_MAX_PART_SPLITS = 8           # TI_ATTN_MAX_PART_SPLITS (include/ti_hip.h)
 EPI_STORE_F32, EPI_STORE_F16, EPI_RESID_F32, EPI_SILU_MUL_F16, EPI_QKV_ROPE_KV, EPI_LOGITS_ARGMAX = range(6)
 ARGMAX_SLOTS = 32
-GEMM_MAX_ROWS = 64                 # TI_GEMM_MAX_ROWS (include/ti_hip.h)   # TI_ARGMAX_SLOTS (include/ti_hip.h)
+GEMM_MAX_ROWS = 256                 # TI_GEMM_MAX_ROWS (include/ti_hip.h)   # TI_ARGMAX_SLOTS (include/ti_hip.h)
 SCALE_GROUP, SCALE_TENSOR, SCALE_UNIT = 0, 1, 2
 ROWS_CONCAT, ROWS_INTERLEAVE8 = 0, 1
 (W_Q, W_K, W_V, W_O, W_GATE, W_UP, W_DOWN, W_LM_HEAD, V_ATTN_NORM, V_FFN_NORM, V_OUT_NORM, E_EMBED) = range(12)
@@ -70,7 +70,7 @@ EXPORTED = [
     "ti_device_sync", "ti_event_create", "ti_event_destroy", "ti_event_record", "ti_event_elapsed_ms",
     "ti_wpack_tile_bytes", "ti_wpack_scale_bytes", "ti_wpack_host", "ti_wsynth_device", "ti_fill_uniform_f16",
     "ti_fill_uniform_f32", "ti_fill_kv_uniform", "ti_kv_copy_slots", "ti_gemm_wq_a16", "ti_gemm_lds_bytes", "ti_gemm_prepare",
-    "ti_gemm_max_rows", "ti_rmsnorm_f16", "ti_rmsnorm_f16_packed", "ti_attn_decode_packed",
+    "ti_gemm_max_rows", "ti_gemm_packed_rows", "ti_rmsnorm_f16", "ti_rmsnorm_f16_packed", "ti_attn_decode_packed",
     "ti_attn_workspace_bytes", "ti_attn_decode", "ti_step_begin", "ti_matmul_f32", "ti_rms_norm_f32",
     "ti_rope_f32", "ti_silu_f32", "ti_relu_f32", "ti_add_f32", "ti_mul_f32", "ti_softmax_f32", "ti_attention_f32",
     "ti_argmax_f32", "ti_engine_create", "ti_engine_destroy", "ti_engine_get_stream", "ti_engine_memory", "ti_engine_set_tensor",
@@ -120,6 +120,7 @@ def lib() -> C.CDLL:
         L.ti_gemm_wq_a16.argtypes = [vp, vp, i32, vp, i32, i32, vp, f32, i32, i32, i32, C.POINTER(Epilogue), vp]
         L.ti_gemm_lds_bytes.argtypes = [i32, i32, i32]
         L.ti_gemm_max_rows.argtypes = [i32, i32, i32, i32]
+        L.ti_gemm_packed_rows.argtypes = [i32, i32]
         L.ti_rmsnorm_f16.argtypes = [vp, i32, vp, f32, vp, i32, i32, i32, vp]
         L.ti_rmsnorm_f16_packed.argtypes = [vp, i32, vp, f32, vp, i32, i32, vp]
         L.ti_attn_workspace_bytes.argtypes = [i32, i32, i32, i32]

@@ -216,7 +216,7 @@ int validate(const ti_engine_config& c) {
 // Rows of the batched-rows kernel (int4, M > 16) take their fp16 operands in fragment order
 // (TI_X_F16_PACKED): the rms_norm prep, the attention output and the SiLU*up output are written
 // that way, so every operand load of the kernel is one contiguous KiB per wave.
-bool packed_rows(const ti_engine* e, int M) { return e->c.bits == 4 && M > 16; }
+bool packed_rows(const ti_engine* e, int M) { return ti_gemm_packed_rows(e->c.bits, M) != 0; }
 
 // One projection for rows [0, M): the fused kernel in chunks of the rows its LDS image
 // holds, or -- int4, when the rows do not fit -- rms_norm into fp16 rows once (e->xn) and

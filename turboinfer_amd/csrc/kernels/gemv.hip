@@ -1418,6 +1418,131 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
     *a.epi.step_ctr += a.epi.advance;
 }
 
+// ------------------------------------------------------------- tile kernel (>= 128 rows)
+// Prefill (forward_pass over a prompt chunk, inference_engine.cpp:1429-1491) and very large
+// batches: a classic LDS-tiled MFMA GEMM, compute-bound at these row counts.  One workgroup
+// computes a 128-row x 128-column block; its 8 waves form 2 (rows) x 4 (columns) and each owns
+// 64 rows x 2 weight tiles.  Per 128-k group: the activation block (128 rows x 128 k fp16,
+// 32 KiB) arrives in LDS by LDS-DMA one group ahead (double buffer) -- each DMA instruction
+// fetches 4 contiguous 256-byte row segments, its lanes' 16-byte chunks XOR-swizzled by row so
+// the A-fragment reads are bank-conflict free -- and the waves' packed weights come straight
+// into VGPRs from a ring three groups ahead.  Group scales of the workgroup's tiles sit in LDS.
+// Per group and wave: 2 tiles dequantized (offset-free int4 -> fp16), 16 A fragments read,
+// 32 v_mfma_f32_16x16x32_f16, then the fp32 group-scale FMA.  The workgroup grid is ordered so
+// that the row blocks sharing a column block run on one XCD (blockIdx % 8), where its L2
+// serves their common weight stream.
+constexpr int kTileBM = 128, kTileWR = 4;   // rows per workgroup (x 128 columns), weight ring
+__host__ __device__ inline int tile_lds_bytes(int K) { return 2 * kTileBM * 256 + align16(8 * (K >> 7) * 32); }
+
+template <int UNUSED>
+__global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int KT = a.K >> 7, NT = a.N >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, kq = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wave >> 2, wn = wave & 3;
+  // blockIdx -> (row block, column block): the n_rb row blocks of a column block share an XCD
+  const int b8 = blockIdx.x & 7, rest = blockIdx.x >> 3;
+  const int rb = rest % n_rb, cb = (rest / n_rb) * 8 + b8;
+  if (cb >= n_cb) return;
+  const int m0 = rb * kTileBM, t0 = cb * 8;
+  f16* xb = (f16*)smem;                                       // [2][128 rows][128 k] swizzled
+  uint16_t* sl = (uint16_t*)(smem + 2 * kTileBM * 256);       // [8 tiles][KT][16]
+  const int n_sc = 8 * KT * 2;                                // 16-byte pieces
+  const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16);
+  const int ntile_ok = min(8, NT - t0);
+  for (int i = tid; i < n_sc; i += kGemvThreads)
+    ((u32x4*)sl)[i] = i < ntile_ok * KT * 2 ? ld_w(sg + i) : (u32x4){0u, 0u, 0u, 0u};
+
+  const f16* xg = (const f16*)a.x;
+  auto issue_x = [&](int kg) {   // 32 DMA instructions per group, 4 per wave
+    f16* dst = xb + (kg & 1) * kTileBM * 128;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = wave * 4 + q, row = 4 * j + (lane >> 4), p = lane & 15, c = p ^ (row & 15);
+      const int m = min(m0 + row, a.M - 1);
+      dma_1k(xg + (size_t)m * a.ldx + kg * 128 + c * 8, dst + j * 512);
+    }
+  };
+  const u32x4* tb = a.tiles + lane;
+  auto load_w = [&](u32x4 (&w)[2], int kg) {
+    kg = min(kg, KT - 1);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) w[t] = ld_w(tb + ((size_t)min(t0 + wn * 2 + t, NT - 1) * KT + kg) * kWave);
+  };
+  u32x4 W[kTileWR][2];
+  issue_x(0);
+#pragma unroll
+  for (int u = 0; u < kTileWR - 1; ++u) load_w(W[u], u);
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[t][b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+  uint32_t magic;
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
+  auto compute = [&](const u32x4 (&w)[2], int kg) {
+    const f16* xr = xb + (kg & 1) * kTileBM * 128 + (wm * 64 + r) * 128;
+    f16x8 xf[4][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) xf[b][s4] = *(const f16x8*)(xr + b * 16 * 128 + (((kq * 4 + s4) ^ r) * 8));
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x4 tmp[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) tmp[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const f16x8 bf = deq_int4_signed(w[t][s4], magic);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) tmp[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[b][s4], bf, tmp[b], 0, 0, 0);
+      }
+      const float sc = h2f(sl[((wn * 2 + t) * KT + kg) * 16 + r]);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        acc[t][b][0] = fmaf(sc, tmp[b][0], acc[t][b][0]);
+        acc[t][b][1] = fmaf(sc, tmp[b][1], acc[t][b][1]);
+        acc[t][b][2] = fmaf(sc, tmp[b][2], acc[t][b][2]);
+        acc[t][b][3] = fmaf(sc, tmp[b][3], acc[t][b][3]);
+      }
+    }
+  };
+  // Per group kg: x(kg) and W(kg) were issued earlier; issue x(kg + 1) and W(kg + WR - 1),
+  // wait until only those weight loads are younger than x(kg + 1)... (see below), compute kg.
+  const int KTP = (KT + kTileWR - 1) / kTileWR * kTileWR;
+  for (int k0 = 0; k0 < KTP; k0 += kTileWR) {
+#pragma unroll
+    for (int u = 0; u < kTileWR; ++u) {
+      const int kg = k0 + u;
+      // x(kg) landed (the loads younger than it: W(kg + WR - 2), 2 instructions) and every
+      // wave is past compute(kg - 1), so buffer (kg + 1) & 1 is free
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      lds_barrier();
+      if (kg < KT) {
+        if (kg + 1 < KT) issue_x(kg + 1);
+        load_w(W[(u + kTileWR - 1) % kTileWR], kg + kTileWR - 1);
+        compute(W[u], kg);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // epilogue straight from the accumulators (16 x 4 outputs per lane pattern of the MFMA)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int tn = t0 + wn * 2 + t;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 64 + b * 16 + 4 * (lane >> 4) + i;
+        epilogue_mb(a, tn < NT ? tn : NT - 1, m, r, acc[t][b][i], tn < NT && m < a.M);
+      }
+  }
+  if (a.epi.kind == TI_EPI_LOGITS_ARGMAX && a.epi.step_ctr && blockIdx.x == 0 && tid == 0)
+    *a.epi.step_ctr += a.epi.advance;
+}
+
 static int g_num_cus = 0;
 
 __host__ inline int gemv_xmode(int x_kind, int M, int K) {
@@ -1570,6 +1695,16 @@ __host__ inline void rows_shape(int M, int* MB, int* RG) {
   *MB = mb;
   *RG = rg;
 }
+// Tile kernel from this many rows on (TI_GEMM_TILE_ROWS in [17, 65], default 65: the rows
+// kernel takes at most 64 rows).
+static int g_tile_rows = 0;
+static int tile_rows() {
+  if (g_tile_rows <= 0) {
+    const char* s = getenv("TI_GEMM_TILE_ROWS");
+    g_tile_rows = s && atoi(s) > 16 && atoi(s) <= 65 ? atoi(s) : 65;
+  }
+  return g_tile_rows;
+}
 __host__ inline int rows_tiles_cap(int MB, int K) {
   const int lim = MB >= 2 ? 3 : 4, cap = 512 / (K >> 7);   // VGPR budget: no spills
   return cap < 1 ? 1 : (cap > lim ? lim : cap);
@@ -1649,7 +1784,8 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<16, XM_F16, true>, (const void*)gemv_wq_kernel<16, XM_NORM1, true>,
       (const void*)gemv_wq_kernel<4, XM_F16F>, (const void*)gemv_wq_kernel<8, XM_F16F>,
       (const void*)gemv_wq_kernel<16, XM_F16F>, (const void*)gemv_wq_kernel<4, XM_ATTN>,
-      (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS, TI_ROWS_FNS};
+      (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS, TI_ROWS_FNS,
+      (const void*)gemm_tile_kernel<0>};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
@@ -1681,6 +1817,8 @@ static bool use_batched(int bits, int x_kind, int M, int N, int K) {
   const bool mb_ok = bits == 4 && x_kind == TI_X_F16;
   return !fused_fits(M, N, K) || (mb_ok && M > fused_rows_pref(bits));
 }
+
+extern "C" int ti_gemm_packed_rows(int bits, int M) { return bits == 4 && M > 16 && M < ti::tile_rows() ? 1 : 0; }
 
 extern "C" int ti_gemm_max_rows(int bits, int x_kind, int N, int K) {
   if (N < 16 || K < 128) return 0;
@@ -1775,8 +1913,15 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
                         "ti_gemm_wq_a16: M=%d K=%d exceeds the fused kernel (ti_gemm_max_rows); the batched-rows "
                         "kernel needs bits 4 and fp16 rows (normalise with ti_rmsnorm_f16)", M, K);
   int grid = 0, lds = 0, ntl = 0, rMB = 0, rRG = 0;
-  const bool rows = batched && (packed_x || M > 32 || (M > 16 && rows_on()));
-  if (rows) {
+  const bool tile = batched && x_kind == TI_X_F16 && M >= tile_rows();
+  const bool rows = !tile && batched && (packed_x || M > 32 || (M > 16 && rows_on()));
+  int n_cb = 0, n_rb = 0;
+  if (tile) {
+    n_cb = ((N >> 4) + 7) / 8;
+    n_rb = (M + kTileBM - 1) / kTileBM;
+    grid = (n_cb + 7) / 8 * 8 * n_rb;
+    lds = tile_lds_bytes(K);
+  } else if (rows) {
     rows_on();
     rows_shape(M, &rMB, &rRG);
     grid = rows_grid(rMB, N, K, query_cus(), &ntl);
@@ -1819,6 +1964,11 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   a.chain = chain_dev(chain);
   if (chain) chain->signaled = (uint32_t)grid;
   hipStream_t s = (hipStream_t)stream;
+  if (tile) {
+    hipLaunchKernelGGL(gemm_tile_kernel<0>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
+    TI_LAUNCH_CHECK("gemm_tile_kernel");
+    return TI_OK;
+  }
   if (rows) return launch_rows(a, rMB, rRG, ntl, grid, lds, s);
   if (batched) return launch_mb(a, M > 16 ? 2 : 1, grid, ntl, lds, s);
   if (bits == 4) return launch_gemv<4>(a, lds, s, grid, chain);
