@@ -12,8 +12,12 @@
 // decode engine of include/ti_engine.h on one MI355X: packed INT4/INT8/fp16 weights and a
 // fp16 KV cache in HBM, the whole decode step captured in a hipGraph.  Greedy requests
 // (top_k == 1) run their token loop on the device; other sampling settings and logprobs
-// take the logits to the host each step.  Prompts are consumed one token per decode step
-// (prefill is SURVEY.md 8(f) rank 1).
+// take the logits to the host each step unless the device sampler runs them.  Prompts are
+// prefilled in chunks of up to 256 rows through the batched GEMM.
+//
+// Binary layout: InferenceConfig carries two trailing fields (weight_bits, gpu_index) that the
+// reference's struct does not have, so this header is a source drop-in, not a layout drop-in:
+// code compiled against the reference's header must be recompiled against this one.
 //
 // Model forms accepted (reference weight names, inference_engine.cpp:483-563):
 //   * llama: token_embeddings / embed_tokens, per-layer q/k/v/o, gate/up/down, both norms,

@@ -15,6 +15,10 @@
 #include "model/model_loader.hpp"
 #include "optimize/quantization.hpp"
 
+// The reference's umbrella header also pulls in util/profiler.hpp, hence <chrono>; reference
+// programs rely on that transitively (tests/test_inference_engine.cpp, examples/basic_inference.cpp).
+#include <chrono>
+
 namespace turboinfer {
 
 struct Version {

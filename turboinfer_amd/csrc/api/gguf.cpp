@@ -17,7 +17,7 @@
 //     block, an fp16 scale d (and min m), y = (q - 8) d, q d + m, q d); the reference declares
 //     these types fp32 and reads the packed bytes as floats (:165-182, 817-829).  BF16 is
 //     widened to fp32.  Other types raise.
-// The CPU restatement is oracle/pyoracle.py gguf_read (tests/test_gguf.py).
+// The CPU restatement is oracle/gguf_oracle.py (tests/test_cpp_api.py gguf cases).
 #include <algorithm>
 #include <cstring>
 #include <filesystem>

@@ -69,6 +69,9 @@ ModelData from_gguf_names(const ModelData& g) {
     return *t;
   };
   m.add_tensor("token_embeddings.weight", need("token_embd.weight"));
+  // older converters omit llama.vocab_size: the embedding's rows are the vocabulary
+  const core::Tensor& emb = need("token_embd.weight");
+  if (m.metadata().vocab_size == 0 && emb.shape().ndim() == 2) m.metadata().vocab_size = emb.shape().size(0);
   m.add_tensor("norm.weight", need("output_norm.weight"));
   const core::Tensor* out = g.get_tensor("output.weight");
   m.add_tensor("lm_head.weight", transposed_f32(out ? *out : need("token_embd.weight")));
@@ -536,9 +539,17 @@ std::unique_ptr<InferenceEngine> create_engine(const std::string& model_path, co
   return std::make_unique<InferenceEngine>(model_path, config);
 }
 
-std::string quick_generate(const std::string& model_path, const std::string&, size_t, float) {
-  (void)ModelLoader::load(model_path);   // throws: checkpoint ingestion is SURVEY.md 8(f) rank 3
-  return std::string();
+// Reference inference_engine.cpp:2075-2082: build an engine from the checkpoint, then
+// generate(prompt) and decode().  The checkpoint loads (GGUF); the string prompt
+// needs the tokenizer, which is out of scope, so this throws from generate(std::string) rather
+// than returning text it cannot produce.
+std::string quick_generate(const std::string& model_path, const std::string& prompt, size_t max_tokens,
+                           float temperature) {
+  InferenceConfig config;
+  config.temperature = temperature;
+  InferenceEngine engine(model_path, config);
+  auto result = engine.generate(prompt, max_tokens);
+  return engine.decode(result.tokens);
 }
 
 }  // namespace model
