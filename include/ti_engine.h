@@ -135,6 +135,16 @@ int ti_engine_set_fold(ti_engine* e, int on, int* active);
  * weights, heads == kv_heads, head_dim 64/128.  on = 1 (or env TI_QKV_ATTN=1) / 0 / -1 leaves
  * it; *active (nullable) receives whether 1-stream steps use it. */
 int ti_engine_set_qkv_attn(ti_engine* e, int on, int* active);
+/* Single-stream steps run every decode layer in ONE persistent launch (ti_pds_decode) when on
+ * and the model qualifies (INT4, heads == kv_heads, head_dim 128, 8 splits, hidden = 128 *
+ * heads, fold and split partials on); bit-identical to the per-layer launches.  -1 leaves the
+ * setting; *active (nullable) receives whether single-stream steps use it.  Env TI_PDS. */
+int ti_engine_set_pds(ti_engine* e, int on, int* active);
+/* Bit 0: a persistent launch's hand-off wait timed out (its results are undefined). */
+int ti_engine_pds_error(ti_engine* e, uint32_t* err);
+/* Diagnostic (engine created with env TI_PDS_TS=1): the last persistent launch's phase
+ * timestamps, [256][layers][5][8] s_memrealtime ticks (100 MHz), n entries at most. */
+int ti_engine_pds_timestamps(ti_engine* e, unsigned long long* out, size_t n);
 
 /* One decode step: token[s] at position pos[s] for each stream; logits [n][vocab] to host
  * (used for non-greedy sampling and per-step parity). */

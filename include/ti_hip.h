@@ -298,6 +298,48 @@ int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, const uint1
 int ti_qkv_attn_fused(const void* tiles, const uint16_t* scales, const uint16_t* x, float eps, int K,
                       const ti_epilogue* epi, uint16_t* part_o, float* part_ml, uint32_t* counters,
                       uint32_t* abort_flag, ti_stream_t s);
+
+/* ----------------------------------------------------- persistent decode layers
+ * All n_layers decode layers of ONE stream in one persistent launch (pds.hip): replaces the
+ * per-layer QKV / attention / O / gate-up / down launches of forward_pass_incremental
+ * (inference_engine.cpp:1493-1552, TransformerLayer::forward_incremental :203-279) for INT4
+ * group-128 weights, heads == kv_heads, head_dim 128, grid = heads * 8 workgroups (<= the CU
+ * count, one per CU) and hidden = 16 * grid.  Input: h, fx / ss as ti_step_begin leaves them
+ * with the layer-0 fold (n_ss0 partials); output: h and fx / ss folded with out_norm (n_ss =
+ * grid partials) for the lm_head's TI_X_F16_FOLDED input.  Same arithmetic, bit for bit, as
+ * the per-layer launches with the fold and split-partials hand-offs.  ctr (n_layers * 5 * 256
+ * words) and launches (grid words) start zeroed and must not be touched between calls; *err
+ * gets bit 0 when a hand-off wait exceeded ~50 ms (results then undefined). */
+typedef struct ti_pds_layer {
+  const void* tiles[4];              /* packed INT4 tiles: qkv, o, gate/up (interleaved), down */
+  const uint16_t* scales[4];
+  const float* attn_norm;
+  const float* ffn_norm;
+  uint16_t* k_cache;                 /* [kv_heads][max_seq][head_dim] fp16, stream 0 */
+  uint16_t* v_cache;
+} ti_pds_layer;
+typedef struct ti_pds_args {
+  const ti_pds_layer* layers;        /* device array [n_layers] */
+  int32_t n_layers, grid, H, I, qd, heads, kv_heads, head_dim, max_seq, n_ss0;
+  float eps;
+  const int32_t* pos;                /* [1] this step's position */
+  const float* rope_cs;              /* [max_seq][head_dim] (cos, sin) */
+  const float* out_norm;
+  float* h;
+  uint16_t* fx;
+  float* ss;                         /* [grid] */
+  float* q;
+  uint16_t* act;
+  uint16_t* part_o;                  /* [heads][8][head_dim] */
+  float* part_ml;                    /* [heads][8][2] */
+  uint32_t* ctr;
+  uint32_t* launches;
+  uint32_t* err;
+  const void* zero;                  /* >= 2 KiB of readable memory, never written */
+  unsigned long long* ts;            /* diagnostic phase timestamps [grid][n_layers][5][8], or NULL */
+} ti_pds_args;
+#define TI_PDS_CTR_WORDS_PER_LAYER (5 * 8 * 32)
+int ti_pds_decode(const ti_pds_args* a, ti_stream_t s);
 /* One launch of a chain (ti_chain): the same attention; K/V, q and pos read with sc1 loads
  * after the wait, out stored write-through. */
 int ti_attn_decode_chained(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,

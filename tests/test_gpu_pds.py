@@ -1,0 +1,71 @@
+"""Persistent decode layers (ti_pds_decode, pds.hip) against the per-layer launches.
+
+The persistent launch runs every decode layer of a single-stream step with the same arithmetic,
+item for item, as the per-layer launches with the folded rms_norm and split-partials hand-offs,
+so twin engines fed the same tokens must give bit-identical logits at every step (positions
+crossing the 8 attention splits' boundaries, position 0 included), identical greedy tokens, and
+no hand-off timeout.  The per-layer path itself is held to the oracle by test_gpu_engine.py.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CFGS = {
+    # name: vocab, hidden, layers, heads, kv_heads, head_dim, inter   (hidden = 128 * heads)
+    "small": (512, 256, 2, 2, 2, 128, 512),
+    "l2_shape": (32000, 4096, 2, 32, 32, 128, 11008),
+}
+
+
+def _twins(ti, name, max_seq):
+    v, h, l, nh, nkv, hd, inter = CFGS[name]
+    eng = {}
+    for on in (True, False):
+        e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=4, max_seq=max_seq, max_batch=1, attn_splits=8)
+        e.synth(0x7157, 0.1)
+        e.set_prefill(0)
+        assert e.set_fold(True)
+        assert e.set_pds(on) is on
+        eng[on] = e
+    return eng
+
+
+@pytest.mark.parametrize("name", list(CFGS))
+def test_pds_steps_bit_identical(ti, name):
+    eng = _twins(ti, name, 256)
+    toks = [3, 17, 99, 5]
+    for pos in range(40):
+        a = eng[True].step([toks[pos]], [pos])[0]
+        b = eng[False].step([toks[pos]], [pos])[0]
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), pos
+        if pos + 1 >= len(toks):
+            toks.append(int(np.argmax(b)))
+    assert eng[True].pds_error() == 0
+    ga = eng[True].generate([[1, 2, 3]], 12)
+    gb = eng[False].generate([[1, 2, 3]], 12)
+    assert np.array_equal(np.asarray(ga), np.asarray(gb))
+    assert eng[True].pds_error() == 0
+    for e in eng.values():
+        e.close()
+
+
+def test_pds_long_context_replay(ti):
+    """7B layer shape over a 2048-slot synthetic KV cache (the bench's configuration, 2 layers):
+    replayed steps at position 2047 give the same argmax token with the persistent launch on and
+    off, and repeated launches (monotonic hand-off counters) never time out."""
+    v, h, l, nh, nkv, hd, inter = CFGS["l2_shape"]
+    toks = {}
+    for on in (True, False):
+        e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=4, max_seq=2048, max_batch=1)
+        e.synth(0x7157, 0.1)
+        assert e.set_pds(on) is on
+        e.fill_kv(0, 2047, 0x5eed)
+        e.replay_prepare(1, 2048, 7)
+        e.replay_run(64)
+        e.sync()
+        toks[on] = e.last_tokens(1)
+        if on:
+            assert e.pds_error() == 0
+        e.close()
+    assert np.array_equal(toks[True], toks[False])

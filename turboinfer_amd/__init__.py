@@ -80,6 +80,7 @@ EXPORTED = [
     "ti_attn_decode_chained", "ti_step_begin_chained", "ti_engine_set_chain", "ti_gemm_grid", "ti_engine_set_fold",
     "ti_attn_decode_partials", "ti_sample_device", "ti_sample_step", "ti_engine_generate_sampled",
     "ti_engine_beam_search", "ti_engine_serve", "ti_qkv_attn_fused", "ti_engine_set_qkv_attn",
+    "ti_pds_decode", "ti_engine_set_pds", "ti_engine_pds_error", "ti_engine_pds_timestamps",
 ]
 
 _lib = None
@@ -140,6 +141,10 @@ def lib() -> C.CDLL:
         if hasattr(L, "ti_qkv_attn_fused"):
             L.ti_qkv_attn_fused.argtypes = [vp, vp, vp, f32, i32, C.POINTER(Epilogue), vp, vp, vp, vp, vp]
             L.ti_engine_set_qkv_attn.argtypes = [vp, i32, C.POINTER(C.c_int)]
+        if hasattr(L, "ti_engine_set_pds"):
+            L.ti_engine_set_pds.argtypes = [vp, i32, C.POINTER(C.c_int)]
+            L.ti_engine_pds_error.argtypes = [vp, C.POINTER(C.c_uint32)]
+            L.ti_engine_pds_timestamps.argtypes = [vp, vp, C.c_size_t]
         L.ti_step_begin.argtypes = [C.POINTER(StepArgs), vp]
         L.ti_matmul_f32.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, vp]
         L.ti_rms_norm_f32.argtypes = [vp, vp, vp, i32, i32, f32, vp]
@@ -405,6 +410,19 @@ class Engine:
         act = C.c_int(0)
         check(lib().ti_engine_set_qkv_attn(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
         return bool(act.value)
+
+    def set_pds(self, on=None) -> bool:
+        """All decode layers of a single-stream step in one persistent launch on/off (None:
+        query); returns whether 1-stream steps use it (ti_engine_set_pds)."""
+        act = C.c_int(0)
+        check(lib().ti_engine_set_pds(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
+        return bool(act.value)
+
+    def pds_error(self) -> int:
+        """Bit 0: a persistent launch's hand-off wait timed out."""
+        err = C.c_uint32(0)
+        check(lib().ti_engine_pds_error(self.h, C.byref(err)))
+        return int(err.value)
 
     def step(self, tokens, pos):
         t = np.ascontiguousarray(tokens, np.int32)

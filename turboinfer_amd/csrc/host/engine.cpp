@@ -140,6 +140,15 @@ struct ti_engine {
   uint32_t* chain_ctr = nullptr;
   uint32_t* chain_abort = nullptr;
   std::vector<uint32_t> chain_cum;
+  // all decode layers of a single-stream step in one persistent launch (ti_pds_decode,
+  // pds.hip): ti_engine_set_pds / TI_PDS; needs the fold and the split partials
+  bool pds_on = false;
+  ti_pds_layer* pds_layers = nullptr;   // device [layers]
+  uint32_t* pds_ctr = nullptr;          // [layers * TI_PDS_CTR_WORDS_PER_LAYER], monotonic
+  uint32_t* pds_launches = nullptr;     // [256]
+  uint32_t* pds_err = nullptr;
+  void* pds_zero = nullptr;             // 4 KiB of zeros, never written
+  unsigned long long* pds_ts = nullptr; // TI_PDS_TS=1: phase timestamps of the last launch
 
   int qd() const { return c.heads * c.head_dim; }
   int kvd() const { return c.kv_heads * c.head_dim; }
@@ -428,6 +437,22 @@ bool qa_usable(ti_engine* e, int M) {
          c.heads == c.kv_heads && (c.head_dim == 64 || c.head_dim == 128) && e->qd() <= 4096;
 }
 
+// Persistent decode layers (ti_pds_decode): one stream with the fold and the split partials,
+// INT4, MHA with head_dim 128, heads * 8 == hidden / 16 <= the CU count (Llama-2-7B: 256).
+int g_pds_cus = 0;
+bool pds_usable(ti_engine* e, int M) {
+  const ti_engine_config& c = e->c;
+  if (!e->pds_on || !e->pds_layers || M != 1 || c.bits != 4 || c.compat) return false;
+  if (!fold_usable(e, M) || !part_usable(e, M) || e->splits_for(M) != 8) return false;
+  if (c.heads != c.kv_heads || c.head_dim != 128 || c.heads * 8 != c.hidden / 16 || c.heads * 8 > 256) return false;
+  if (g_pds_cus == 0) {
+    int dev = 0, n = 0;
+    g_pds_cus = (hipGetDevice(&dev) == hipSuccess &&
+                 hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) ? n : -1;
+  }
+  return g_pds_cus >= c.heads * 8;
+}
+
 // One decode step for streams [0, M) on e->s.  Graph-capturable (no host sync / alloc).
 int enqueue_step(ti_engine* e, int M, int advance) {
   const ti_engine_config& c = e->c;
@@ -482,7 +507,40 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     return TI_OK;
   };
 
-  for (int l = 0; l < c.layers; ++l) {
+  const bool pds = pds_usable(e, M);
+  if (pds) {   // every layer in one persistent launch; the lm_head stages its fold (grid partials)
+    ti_pds_args pa{};
+    pa.layers = e->pds_layers;
+    pa.n_layers = c.layers;
+    pa.grid = c.heads * 8;
+    pa.H = H;
+    pa.I = I;
+    pa.qd = qd;
+    pa.heads = c.heads;
+    pa.kv_heads = c.kv_heads;
+    pa.head_dim = c.head_dim;
+    pa.max_seq = c.max_seq;
+    pa.n_ss0 = n_ss;
+    pa.eps = c.eps;
+    pa.pos = e->pos;
+    pa.rope_cs = e->rope_cs;
+    pa.out_norm = e->out_norm;
+    pa.h = e->h;
+    pa.fx = e->fx;
+    pa.ss = e->ss;
+    pa.q = e->q;
+    pa.act = e->act;
+    pa.part_o = e->part_o;
+    pa.part_ml = e->part_ml;
+    pa.ctr = e->pds_ctr;
+    pa.launches = e->pds_launches;
+    pa.err = e->pds_err;
+    pa.zero = e->pds_zero;
+    pa.ts = e->pds_ts;
+    TI_TRY(ti_pds_decode(&pa, e->s));
+    n_ss = pa.grid;
+  }
+  for (int l = 0; l < (pds ? 0 : c.layers); ++l) {
     DevLayer& L = e->layer[l];
     ti_epilogue ep{};
     ep.kind = TI_EPI_QKV_ROPE_KV;
@@ -759,6 +817,30 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     for (auto& L : e->layer) tab.push_back(L.vc);
     if ((rc = e->alloc_t(&e->kv_tab, tab.size())) || (rc = ti_memcpy_h2d(e->kv_tab, tab.data(), tab.size() * sizeof(void*), e->s)))
       return fail(rc);
+    if (c.bits == 4) {   // persistent decode layers (pds_usable decides per step)
+      std::vector<ti_pds_layer> pl((size_t)c.layers);
+      for (int l = 0; l < c.layers; ++l) {
+        DevLayer& L = e->layer[l];
+        const DevLinear* lin[4] = {&L.qkv, &L.o, &L.gu, &L.down};
+        for (int i = 0; i < 4; ++i) {
+          pl[l].tiles[i] = lin[i]->tiles;
+          pl[l].scales[i] = lin[i]->scales;
+        }
+        pl[l].attn_norm = L.attn_norm;
+        pl[l].ffn_norm = L.ffn_norm;
+        pl[l].k_cache = L.kc;
+        pl[l].v_cache = L.vc;
+      }
+      if ((rc = e->alloc(reinterpret_cast<void**>(&e->pds_layers), pl.size() * sizeof(ti_pds_layer))) ||
+          (rc = ti_memcpy_h2d(e->pds_layers, pl.data(), pl.size() * sizeof(ti_pds_layer), e->s)) ||
+          (rc = e->alloc_t(&e->pds_ctr, (size_t)c.layers * TI_PDS_CTR_WORDS_PER_LAYER)) ||
+          (rc = e->alloc_t(&e->pds_launches, (size_t)256)) || (rc = e->alloc_t(&e->pds_err, (size_t)1)) ||
+          (rc = e->alloc(&e->pds_zero, 4096)))
+        return fail(rc);
+      if (const char* env = getenv("TI_PDS")) e->pds_on = atoi(env) != 0;
+      if (const char* env = getenv("TI_PDS_TS"))
+        if (atoi(env) != 0 && (rc = e->alloc_t(&e->pds_ts, (size_t)256 * c.layers * 5 * 8))) return fail(rc);
+    }
   }
   const int R = std::max(B, e->rows_cap);
   if ((rc = e->alloc_t(&e->h, (size_t)R * H)) || (rc = e->alloc_t(&e->logits, (size_t)B * V)) ||
@@ -1401,6 +1483,36 @@ int ti_engine_set_qkv_attn(ti_engine* e, int on, int* active) {
     e->qa_on = on != 0;
   }
   if (active) *active = qa_usable(e, 1) ? 1 : 0;
+  return TI_OK;
+}
+
+int ti_engine_set_pds(ti_engine* e, int on, int* active) {
+  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_pds: null");
+  if (on >= 0 && (on != 0) != e->pds_on) {
+    TI_TRY(ti_stream_sync(e->s));   // captured step graphs bake the setting in
+    for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
+    e->graphs.clear();
+    e->pds_on = on != 0;
+  }
+  if (active) *active = pds_usable(e, 1) ? 1 : 0;
+  return TI_OK;
+}
+
+int ti_engine_pds_timestamps(ti_engine* e, unsigned long long* out, size_t n) {
+  if (!e || !out) return ti_set_error(TI_ERR_ARG, "ti_engine_pds_timestamps: null");
+  if (!e->pds_ts) return ti_set_error(TI_ERR_ARG, "ti_engine_pds_timestamps: engine built without TI_PDS_TS=1");
+  const size_t have = (size_t)256 * e->c.layers * 5 * 8;
+  TI_TRY(ti_stream_sync(e->s));
+  E_CHECK(hipMemcpy(out, e->pds_ts, std::min(n, have) * 8, hipMemcpyDeviceToHost), "hipMemcpy(pds_ts)");
+  return TI_OK;
+}
+
+int ti_engine_pds_error(ti_engine* e, uint32_t* err) {
+  if (!e || !err) return ti_set_error(TI_ERR_ARG, "ti_engine_pds_error: null");
+  *err = 0;
+  if (!e->pds_err) return TI_OK;
+  TI_TRY(ti_stream_sync(e->s));
+  E_CHECK(hipMemcpy(err, e->pds_err, 4, hipMemcpyDeviceToHost), "hipMemcpy(pds_err)");
   return TI_OK;
 }
 

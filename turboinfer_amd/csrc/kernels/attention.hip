@@ -50,7 +50,10 @@ static int launch_one(const AttnArgs& a, hipStream_t s, const ti_chain* chain) {
 template <int HD, int G>
 static int launch_attn(const AttnArgs& a, hipStream_t s, const ti_chain* chain) {
   const bool long_range = G >= 4 && a.max_seq / a.splits >= 1024;   // keys per split (upper bound)
-  if constexpr (G >= 4 && HD / (64 / G) == 8) {
+#ifndef TI_ATTN_HP
+#define TI_ATTN_HP 1   // head-parallel lanes for GQA groups of 4-8 over short ranges
+#endif
+  if constexpr (TI_ATTN_HP && G >= 4 && HD / (64 / G) == 8) {
     if (!long_range) return launch_one<HD, G, TI_ATTN_RING_HP, true>(a, s, chain);   // head-parallel lanes
   }
   if (long_range) return launch_one<HD, G, TI_ATTN_RING_LONG, false>(a, s, chain);
