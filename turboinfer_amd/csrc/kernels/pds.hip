@@ -41,11 +41,11 @@
 namespace ti {
 
 #ifndef TI_PDS_RING
-#define TI_PDS_RING 6   // units (2 KiB per wave each) in flight per consumer wave
+#define TI_PDS_RING 8   // units (2 KiB per wave each) in flight per consumer wave
 #endif
 constexpr int kPdsRing = TI_PDS_RING;
 constexpr int kPdsC = 8;                         // consumer waves
-constexpr int kPdsThreads = (kPdsC + 1) * kWave;
+constexpr int kPdsThreads = kPdsC * kWave;      // wave 7 is also the control wave
 constexpr int kPdsCThreads = kPdsC * kWave;
 constexpr int kPdsSplits = 8;
 constexpr int kPdsHd = 128;
@@ -160,14 +160,15 @@ __device__ __forceinline__ u32x4 ld_sc1_b128(const void* base, uint32_t byte_off
   return __builtin_amdgcn_raw_buffer_load_b128(sc1_rsrc(base), byte_off, 0, kAuxSc1Load);
 }
 
-// Every phase of a consumer wave is padded to whole blocks of RING units (dummy units load the
-// zero page and are consumed as nothing), so each phase starts at ring slot 0 and the slot
-// indices stay static (VGPRs, not scratch).  Blocks before the last refill from the phase's own
-// cursor; the last block refills from the NEXT phase's cursor, so that phase starts with RING
-// units already in flight.
-template <class C, class R0, class R1>
-__device__ __forceinline__ void pds_blocks(u32x4 (&ring)[kPdsRing][2], int nblk, C& consume, R0& refill_in,
-                                           R1& refill_next) {
+// Every phase of a consumer wave is padded to whole blocks of RING units (dummy units are not
+// loaded and are consumed as nothing), so each phase starts at ring slot 0 and the slot indices
+// stay static (VGPRs, not scratch).  Blocks before the last refill from the phase's own cursor;
+// after the last block the wave passes the phase's closing barrier and only then issues the NEXT
+// phase's first RING units (the control wave after its signal), so the issue stalls of a full
+// memory queue stay off the phase's critical path and the next phase starts with RING units
+// already landed.
+template <class C, class R0>
+__device__ __forceinline__ void pds_blocks(u32x4 (&ring)[kPdsRing][2], int nblk, C& consume, R0& refill_in) {
   for (int b = 0; b + 1 < nblk; ++b) {
 #pragma unroll
     for (int k = 0; k < kPdsRing; ++k) {
@@ -176,10 +177,7 @@ __device__ __forceinline__ void pds_blocks(u32x4 (&ring)[kPdsRing][2], int nblk,
     }
   }
 #pragma unroll
-  for (int k = 0; k < kPdsRing; ++k) {
-    consume(ring[k]);
-    refill_next(ring[k]);
-  }
+  for (int k = 0; k < kPdsRing; ++k) consume(ring[k]);   // the next phase refills after the barrier
 }
 __device__ __forceinline__ int pds_nblk(int units) { return units > 0 ? (units + kPdsRing - 1) / kPdsRing : 1; }
 
@@ -213,7 +211,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bid = blockIdx.x, grid = gridDim.x;
-  const bool is_x = wave == kPdsC;
+  const bool is_x = wave == kPdsC - 1;   // control wave (also a consumer)
   const int H = a.H, I = a.I, qd = a.qd, HD = kPdsHd;
   const int pos = __builtin_amdgcn_readfirstlane(gptr(a.pos)[0]);
   const int L = pos + 1;
@@ -222,7 +220,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
   const int chunk = (L + kPdsSplits - 1) / kPdsSplits;
   const int s0 = sp * chunk, s1 = min(L, s0 + chunk);
   const int nslot = s1 > s0 ? (s1 - s0 + 3) / 4 : 0;
-  const int cw = is_x ? 0 : wave;
+  const int cw = wave;
   const int att_units = cw < nslot ? (nslot - cw + kPdsC - 1) / kPdsC : 0;
   const int64_t kv_off = (int64_t)kvh * a.max_seq * HD;
   // GEMV partitions (the same for every layer)
@@ -253,6 +251,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
     return q;
   };
   auto grefill = [&](GCur& c, u32x4 (&slot)[2]) {
+    if (c.t >= c.ntl) return;   // dummy unit: nothing to load (consumed as nothing)
     const u32x4* p0 = gnext(c);
     const u32x4* p1 = gnext(c);
     slot[0] = pds_ld_w(p0);
@@ -273,21 +272,22 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
     // the row at pos is written by this launch's QKV epilogue: never stream it (its stale
     // line must not sit in a cache ahead of the sc1 load after the hand-off)
     const bool ok = c.key0 + du < s1 && c.key0 + du != pos;
+    ++c.u;
+    if (kPdsC * 4 * (c.u - 1) + s0 + cw * 4 >= s1) return;   // no key of the wave's slot: dummy unit
     const u32x4* pk = ok ? (const u32x4*)(c.kb + (size_t)du * HD) : zero_l;
     const u32x4* pv = ok ? (const u32x4*)(c.vb + (size_t)du * HD) : zero_l + kWave;
     slot[0] = pds_ld_w(pk);
     slot[1] = pds_ld_w(pv);
-    ++c.u;
   };
 
   u32x4 ring[kPdsRing][2];
+#pragma unroll
+  for (int s = 0; s < kPdsRing; ++s) ring[s][0] = ring[s][1] = (u32x4){0u, 0u, 0u, 0u};
   GCur gc{};   // the current GEMV phase's cursor (started by the previous phase's last block)
   ACur ac{};
-  if (!is_x) {
-    gc = gcur(0, PH_QKV);
+  gc = gcur(0, PH_QKV);
 #pragma unroll
-    for (int s = 0; s < kPdsRing; ++s) grefill(gc, ring[s]);
-  }
+  for (int s = 0; s < kPdsRing; ++s) grefill(gc, ring[s]);
 
   // ---------------------------------------------------------------- X wave: setup
   uint32_t epoch = 0;
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
 
   // C waves: consume one GEMV phase of partition p (acc per tile into the slab); the last
   // block refills from the next phase (rnext)
-  auto gemv_phase = [&](const PdsLin& p, auto& rnext) {
+  auto gemv_phase = [&](const PdsLin& p) {
     const f16* xrow = xl + kq * 32;
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     int ct = 0, ck = 0, j = 0;
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       item(u[1]);
     };
     auto rin = [&](u32x4 (&slot)[2]) { grefill(gc, slot); };
-    pds_blocks(ring, pds_nblk(p.n_units), consume, rin, rnext);
+    pds_blocks(ring, pds_nblk(p.n_units), consume, rin);
     if (p.KW == 0)
       for (int tl = 0; tl < p.ntl; ++tl)
         if (lane < 16) slab[(tl * kPdsC + cw) * 16 + lane] = 0.0f;
@@ -432,24 +432,20 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       if (is_x) ts(l, PH_QKV, 0);
       if (is_x && l > 0) pds_poll(ctr_of(l - 1, PH_DN), target, a.err, lane, dead);
       if (is_x) ts(l, PH_QKV, 1);
-      if (!is_x) stage_scales(p, ly.scales[0]);   // constant: before the hand-off
+      stage_scales(p, ly.scales[0]);   // constant: before the hand-off
       pds_barrier();
       float rms = 1.0f;
-      if (!is_x) {
-        stage_f16(a.fx, H);
-      } else {
-        rms = fold_rms(l == 0 ? a.n_ss0 : grid, H);
-      }
+      stage_f16(a.fx, H);
+      if (is_x) rms = fold_rms(l == 0 ? a.n_ss0 : grid, H);
       pds_barrier();
       if (is_x) ts(l, PH_QKV, 2);
-      if (!is_x) {
-        ac = acur(l);   // the attention's first block is issued during QKV's last
-        auto rn = [&](u32x4 (&slot)[2]) { arefill(ac, slot); };
-        gemv_phase(p, rn);
-      }
+      ac = acur(l);   // the attention's first block: issued after the closing barrier
+      gemv_phase(p);
       if (wave == 0) ts(l, PH_QKV, 3);
       pds_barrier();
       if (is_x) ts(l, PH_QKV, 4);
+      if (!is_x) {   // the control wave issues these after its signal
+      }
       if (is_x) {
         // outputs (tl, n) = lane (ntl <= 4): gemv epilogue TI_EPI_QKV_ROPE_KV, M = 1
         const int tl = lane >> 4, n = lane & 15;
@@ -481,6 +477,11 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
         pds_signal(cl + PH_QKV * kPdsShards * kPdsShardWords, bid, lane);
         ts(l, PH_QKV, 5);
       }
+      // the next phase's first units: issued once the epilogue's stores have drained (they
+      // would queue behind these in the CU's memory pipeline)
+      pds_barrier();
+#pragma unroll
+      for (int s = 0; s < kPdsRing; ++s) arefill(ac, ring[s]);
     }
 
     // ---------------- attention split (kvh, sp): partials as ti_attn_decode_partials
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       pds_barrier();
       pds_barrier();
       if (is_x) ts(l, PH_ATT, 2);
-      if (!is_x) {
+      {
         const int dl = lane & 15, kg = lane >> 4;
         float qv[8];
 #pragma unroll
@@ -514,7 +515,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
           const int key = s0 + (cw + kPdsC * ci) * 4 + kg;
           ++ci;
           const bool valid = key < s1;
-          u32x4 kv = u[0], vv = u[1];
+          u32x4 kv = u[0], vv = valid ? u[1] : (u32x4){0u, 0u, 0u, 0u};   // dummy units hold stale data
           if (valid && key == pos) {
             kv = *(const u32x4*)(kf_l + dl * 8);
             vv = *(const u32x4*)(vf_l + dl * 8);
@@ -537,8 +538,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
         };
         gc = gcur(l, PH_O);
         auto rin = [&](u32x4 (&slot)[2]) { arefill(ac, slot); };
-        auto rn = [&](u32x4 (&slot)[2]) { grefill(gc, slot); };
-        pds_blocks(ring, pds_nblk(att_units), consume, rin, rn);
+        pds_blocks(ring, pds_nblk(att_units), consume, rin);
         // merge the lane groups of the wave (attn_split_body, LPK = 16)
         const float mx = groups_max<16>(mrun);
         const float f = mrun == -INFINITY ? 0.0f : __expf(mrun - mx);
@@ -581,6 +581,11 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
         pds_signal(cl + PH_ATT * kPdsShards * kPdsShardWords, bid, lane);
         ts(l, PH_ATT, 5);
       }
+      // the next phase's first units: issued once the epilogue's stores have drained (they
+      // would queue behind these in the CU's memory pipeline)
+      pds_barrier();
+#pragma unroll
+      for (int s = 0; s < kPdsRing; ++s) grefill(gc, ring[s]);
     }
 
     // ---------------- O: x = the splits merged (gemv XM_ATTN staging), residual + fold (ffn_norm)
@@ -589,38 +594,31 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       if (is_x) ts(l, PH_O, 0);
       if (is_x) pds_poll(ctr_of(l, PH_ATT), target, a.err, lane, dead);
       if (is_x) ts(l, PH_O, 1);
-      if (!is_x) stage_scales(p, ly.scales[1]);
+      stage_scales(p, ly.scales[1]);
       pds_barrier();
-      if (!is_x) {
+      {
         const int K8 = qd >> 3;
         for (int i0 = 0; i0 < K8; i0 += kPdsCThreads) {
           const int idx = i0 + tid;
           float part = 0.0f;
           if (idx < K8) {
             const int hh = (8 * idx) >> 7, d = (8 * idx) & 127;
-            // two batches of 4 splits in flight (register pressure: the ring is live here);
-            // the same order of operations as the one-pass merge
             float2 pml[kPdsSplits];
+            u32x4 po[kPdsSplits];
 #pragma unroll
-            for (int s = 0; s < kPdsSplits; ++s)
+            for (int s = 0; s < kPdsSplits; ++s) {
               pml[s] = __builtin_bit_cast(float2, ld_sc1_u64((const unsigned long long*)(a.part_ml + 2 * (hh * kPdsSplits + s))));
-            u32x4 po[4];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) po[s] = ld_sc1_b128(a.part_o, (uint32_t)(((size_t)(hh * kPdsSplits + s) * HD + d) * 2));
+              po[s] = ld_sc1_b128(a.part_o, (uint32_t)(((size_t)(hh * kPdsSplits + s) * HD + d) * 2));
+            }
             float mx = -INFINITY;
 #pragma unroll
             for (int s = 0; s < kPdsSplits; ++s) mx = fmaxf(mx, pml[s].x);
             float num[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, den = 0.0f;
 #pragma unroll
             for (int s = 0; s < kPdsSplits; ++s) {
-              if (s == 4) {
-#pragma unroll
-                for (int s2 = 0; s2 < 4; ++s2)
-                  po[s2] = ld_sc1_b128(a.part_o, (uint32_t)(((size_t)(hh * kPdsSplits + 4 + s2) * HD + d) * 2));
-              }
               const float f = pml[s].x != -INFINITY ? pml[s].y * __expf(pml[s].x - mx) : 0.0f;
               den += f;
-              const f16x8 o = __builtin_bit_cast(f16x8, po[s & 3]);
+              const f16x8 o = __builtin_bit_cast(f16x8, po[s]);
 #pragma unroll
               for (int e = 0; e < 8; ++e) num[e] = fmaf(f, (float)o[e], num[e]);
             }
@@ -640,12 +638,8 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       }
       pds_barrier();
       if (is_x) ts(l, PH_O, 2);
-      if (!is_x) {
-        GCur gnx = gcur(l, PH_GU);
-        auto rn = [&](u32x4 (&slot)[2]) { grefill(gnx, slot); };
-        gemv_phase(p, rn);
-        gc = gnx;
-      }
+      GCur gnx = gcur(l, PH_GU);
+      gemv_phase(p);
       if (wave == 0) ts(l, PH_O, 3);
       pds_barrier();
       if (is_x) ts(l, PH_O, 4);
@@ -654,6 +648,12 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
         pds_signal(cl + PH_O * kPdsShards * kPdsShardWords, bid, lane);
         ts(l, PH_O, 5);
       }
+      // the next phase's first units: issued once the epilogue's stores have drained (they
+      // would queue behind these in the CU's memory pipeline)
+      pds_barrier();
+#pragma unroll
+      for (int s = 0; s < kPdsRing; ++s) grefill(gnx, ring[s]);
+      gc = gnx;
     }
 
     // ---------------- gate/up: x = fx (fold of O), SiLU * up
@@ -662,22 +662,15 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       if (is_x) ts(l, PH_GU, 0);
       if (is_x) pds_poll(ctr_of(l, PH_O), target, a.err, lane, dead);
       if (is_x) ts(l, PH_GU, 1);
-      if (!is_x) stage_scales(p, ly.scales[2]);
+      stage_scales(p, ly.scales[2]);
       pds_barrier();
       float rms = 1.0f;
-      if (!is_x) {
-        stage_f16(a.fx, H);
-      } else {
-        rms = fold_rms(grid, H);
-      }
+      stage_f16(a.fx, H);
+      if (is_x) rms = fold_rms(grid, H);
       pds_barrier();
       if (is_x) ts(l, PH_GU, 2);
-      if (!is_x) {
-        GCur gnx = gcur(l, PH_DN);
-        auto rn = [&](u32x4 (&slot)[2]) { grefill(gnx, slot); };
-        gemv_phase(p, rn);
-        gc = gnx;
-      }
+      GCur gnx = gcur(l, PH_DN);
+      gemv_phase(p);
       if (wave == 0) ts(l, PH_GU, 3);
       pds_barrier();
       if (is_x) ts(l, PH_GU, 4);
@@ -694,6 +687,12 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
         pds_signal(cl + PH_GU * kPdsShards * kPdsShardWords, bid, lane);
         ts(l, PH_GU, 5);
       }
+      // the next phase's first units: issued once the epilogue's stores have drained (they
+      // would queue behind these in the CU's memory pipeline)
+      pds_barrier();
+#pragma unroll
+      for (int s = 0; s < kPdsRing; ++s) grefill(gnx, ring[s]);
+      gc = gnx;
     }
 
     // ---------------- down: x = act, residual + fold (next layer's attention_norm / final norm)
@@ -702,17 +701,13 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       if (is_x) ts(l, PH_DN, 0);
       if (is_x) pds_poll(ctr_of(l, PH_GU), target, a.err, lane, dead);
       if (is_x) ts(l, PH_DN, 1);
-      if (!is_x) stage_scales(p, ly.scales[3]);
+      stage_scales(p, ly.scales[3]);
       pds_barrier();
-      if (!is_x) stage_f16(a.act, I);
+      stage_f16(a.act, I);
       pds_barrier();
       if (is_x) ts(l, PH_DN, 2);
-      if (!is_x) {
-        GCur gnx = gcur(l + 1, PH_QKV);
-        auto rn = [&](u32x4 (&slot)[2]) { grefill(gnx, slot); };
-        gemv_phase(p, rn);
-        gc = gnx;
-      }
+      GCur gnx = gcur(l + 1, PH_QKV);
+      gemv_phase(p);
       if (wave == 0) ts(l, PH_DN, 3);
       pds_barrier();
       if (is_x) ts(l, PH_DN, 4);
@@ -721,6 +716,12 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
         pds_signal(cl + PH_DN * kPdsShards * kPdsShardWords, bid, lane);
         ts(l, PH_DN, 5);
       }
+      // the next phase's first units: issued once the epilogue's stores have drained (they
+      // would queue behind these in the CU's memory pipeline)
+      pds_barrier();
+#pragma unroll
+      for (int s = 0; s < kPdsRing; ++s) grefill(gnx, ring[s]);
+      gc = gnx;
     }
   }
   if (is_x && lane < 16) gptr_w(a.h)[t0o * 16 + lane] = h_l[lane];
