@@ -118,7 +118,9 @@ def pmc_traffic(kernel: str):
         return None, None
     try:
         d = json.load(open(files[-1]))
-        return int(d["kernels"][kernel]["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+        k = d["kernels"][kernel]
+        v = k.get("step_weighted_traffic_bytes_per_launch", k["traffic_bytes_per_launch"])
+        return int(v), os.path.relpath(files[-1], ROOT)
     except (KeyError, ValueError, OSError):
         return None, None
 

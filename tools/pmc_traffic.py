@@ -29,6 +29,24 @@ def main():
     for k, v in fam.items():
         out["kernels"][k] = {"dispatches": len(v), "traffic_bytes_per_launch": round(sum(v) / len(v)),
                              "min": round(min(v)), "max": round(max(v))}
+    # The pass mixes the decode steps with the bench's per-class timing launches, so the plain
+    # mean depends on that mixture.  Step-weighted: each dispatch is assigned to the projection
+    # class whose algorithmic bytes are nearest (7B shapes), the per-class means are weighted by
+    # the step's own mixture (32 x QKV, O, gate/up, down + 1 lm_head), comparable to the bench
+    # line's bytes_per_launch.
+    algo = {"qkv": 25960448, "o": 8658944, "gate_up": 46505984, "down": 23270912, "lm_head": 67592192}
+    per = defaultdict(list)
+    for b in fam.get("gemv_wq_kernel<4>", []):
+        per[min(algo, key=lambda c: abs(algo[c] - b))].append(b)
+    if len(per) == len(algo):
+        n = {"qkv": 32, "o": 32, "gate_up": 32, "down": 32, "lm_head": 1}
+        cls = {c: {"dispatches": len(per[c]), "traffic_bytes": round(sum(per[c]) / len(per[c])), "algorithmic_bytes": algo[c],
+                   "ratio": round(sum(per[c]) / len(per[c]) / algo[c], 4)} for c in algo}
+        tw = sum(n[c] * cls[c]["traffic_bytes"] for c in algo) / sum(n.values())
+        aw = sum(n[c] * algo[c] for c in algo) / sum(n.values())
+        out["kernels"]["gemv_wq_kernel<4>"].update({"classes": cls, "step_weighted_traffic_bytes_per_launch": round(tw),
+                                                    "step_weighted_algorithmic_bytes_per_launch": round(aw),
+                                                    "step_weighted_ratio": round(tw / aw, 4)})
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out))
 

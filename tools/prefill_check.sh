@@ -1,0 +1,7 @@
+# Prefill: parity tests and timing
+set -e
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_prefill.py tests/test_gpu_batched.py -x -q --timeout 120 --timeout-method thread > gpurun_out/prefill_tests.log 2>&1
+timeout -k 10 200 python3 tools/prefill_bench.py > gpurun_out/prefill.txt 2>&1

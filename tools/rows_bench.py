@@ -55,5 +55,5 @@ for name, K, N in shapes:
         T.check(L.ti_event_elapsed_ms(ev0, ev1, C.byref(ms)))
         us = ms.value * 1e3 / reps
         by = tb + sb + M * K * 2
-        print(f"M={M:3d} {name:11s} K={K:6d} N={N:6d} {us:8.2f} us  {by / us / 1e3:8.1f} GB/s", flush=True)
+        print(f"M={M:3d} {name:11s} K={K:6d} N={N:6d} {us:8.2f} us  {by / us / 1e3:8.1f} GB/s  {2 * M * K * N / us / 1e6:7.1f} TFLOP/s", flush=True)
     del W
