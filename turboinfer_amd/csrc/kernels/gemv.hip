@@ -1386,7 +1386,9 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
 constexpr int kTileBM = 128, kTileWR = 4;   // rows per workgroup (x 128 columns), weight ring
 __host__ __device__ inline int tile_lds_bytes(int K) { return 2 * kTileBM * 256 + align16(8 * (K >> 7) * 32); }
 
-template <int UNUSED>
+// TPW: weight tiles per wave (2: 128 columns per workgroup; 1: 64 columns, twice the workgroups
+// for the narrow N = 4096 projections, which otherwise fill only 64 of 256 CUs at 256 rows).
+template <int TPW>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KT = a.K >> 7, NT = a.N >> 4;
@@ -1396,12 +1398,12 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   const int b8 = blockIdx.x & 7, rest = blockIdx.x >> 3;
   const int rb = rest % n_rb, cb = (rest / n_rb) * 8 + b8;
   if (cb >= n_cb) return;
-  const int m0 = rb * kTileBM, t0 = cb * 8;
+  const int m0 = rb * kTileBM, t0 = cb * 4 * TPW;
   f16* xb = (f16*)smem;                                       // [2][128 rows][128 k] swizzled
-  uint16_t* sl = (uint16_t*)(smem + 2 * kTileBM * 256);       // [8 tiles][KT][16]
-  const int n_sc = 8 * KT * 2;                                // 16-byte pieces
+  uint16_t* sl = (uint16_t*)(smem + 2 * kTileBM * 256);       // [4 TPW tiles][KT][16]
+  const int n_sc = 4 * TPW * KT * 2;                          // 16-byte pieces
   const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16);
-  const int ntile_ok = min(8, NT - t0);
+  const int ntile_ok = min(4 * TPW, NT - t0);
   for (int i = tid; i < n_sc; i += kGemvThreads)
     ((u32x4*)sl)[i] = i < ntile_ok * KT * 2 ? ld_w(sg + i) : (u32x4){0u, 0u, 0u, 0u};
 
@@ -1416,23 +1418,23 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
     }
   };
   const u32x4* tb = a.tiles + lane;
-  auto load_w = [&](u32x4 (&w)[2], int kg) {
+  auto load_w = [&](u32x4 (&w)[TPW], int kg) {
     kg = min(kg, KT - 1);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) w[t] = ld_w(tb + ((size_t)min(t0 + wn * 2 + t, NT - 1) * KT + kg) * kWave);
+    for (int t = 0; t < TPW; ++t) w[t] = ld_w(tb + ((size_t)min(t0 + wn * TPW + t, NT - 1) * KT + kg) * kWave);
   };
-  u32x4 W[kTileWR][2];
+  u32x4 W[kTileWR][TPW];
   issue_x(0);
 #pragma unroll
   for (int u = 0; u < kTileWR - 1; ++u) load_w(W[u], u);
-  f32x4 acc[2][4];
+  f32x4 acc[TPW][4];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < TPW; ++t)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[t][b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
   uint32_t magic;
   asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
-  auto compute = [&](const u32x4 (&w)[2], int kg) {
+  auto compute = [&](const u32x4 (&w)[TPW], int kg) {
     const f16* xr = xb + (kg & 1) * kTileBM * 128 + (wm * 64 + r) * 128;
     f16x8 xf[4][4];
 #pragma unroll
@@ -1440,7 +1442,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) xf[b][s4] = *(const f16x8*)(xr + b * 16 * 128 + (((kq * 4 + s4) ^ r) * 8));
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < TPW; ++t) {
       f32x4 tmp[4];
 #pragma unroll
       for (int b = 0; b < 4; ++b) tmp[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
@@ -1450,7 +1452,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #pragma unroll
         for (int b = 0; b < 4; ++b) tmp[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[b][s4], bf, tmp[b], 0, 0, 0);
       }
-      const float sc = h2f(sl[((wn * 2 + t) * KT + kg) * 16 + r]);
+      const float sc = h2f(sl[((wn * TPW + t) * KT + kg) * 16 + r]);
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         acc[t][b][0] = fmaf(sc, tmp[b][0], acc[t][b][0]);
@@ -1467,9 +1469,9 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #pragma unroll
     for (int u = 0; u < kTileWR; ++u) {
       const int kg = k0 + u;
-      // x(kg) landed (the loads younger than it: W(kg + WR - 2), 2 instructions) and every
+      // x(kg) landed (the loads younger than it: W(kg + WR - 2), TPW instructions) and every
       // wave is past compute(kg - 1), so buffer (kg + 1) & 1 is free
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TPW) : "memory");
       lds_barrier();
       if (kg < KT) {
         if (kg + 1 < KT) issue_x(kg + 1);
@@ -1481,8 +1483,8 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // epilogue straight from the accumulators (16 x 4 outputs per lane pattern of the MFMA)
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int tn = t0 + wn * 2 + t;
+  for (int t = 0; t < TPW; ++t) {
+    const int tn = t0 + wn * TPW + t;
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
@@ -1496,6 +1498,15 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 }
 
 static int g_num_cus = 0;
+// TI_TILE_NARROW=0 keeps 128-column workgroups for every shape (A/B knob)
+static int g_tile_narrow = -1;
+__host__ inline bool tile_narrow_on() {
+  if (g_tile_narrow < 0) {
+    const char* e = getenv("TI_TILE_NARROW");
+    g_tile_narrow = e ? atoi(e) != 0 : 1;
+  }
+  return g_tile_narrow != 0;
+}
 
 __host__ inline int gemv_xmode(int x_kind, int M, int K) {
   if (x_kind == TI_X_F16) return XM_F16;
@@ -1737,7 +1748,7 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<4, XM_F16F>, (const void*)gemv_wq_kernel<8, XM_F16F>,
       (const void*)gemv_wq_kernel<16, XM_F16F>, (const void*)gemv_wq_kernel<4, XM_ATTN>,
       (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS, TI_ROWS_FNS,
-      (const void*)gemm_tile_kernel<0>};
+      (const void*)gemm_tile_kernel<2>, (const void*)gemm_tile_kernel<1>};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
@@ -1867,10 +1878,12 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   int grid = 0, lds = 0, ntl = 0, rMB = 0, rRG = 0;
   const bool tile = batched && x_kind == TI_X_F16 && M >= tile_rows();
   const bool rows = !tile && batched && (packed_x || M > 32 || (M > 16 && rows_on()));
-  int n_cb = 0, n_rb = 0;
+  int n_cb = 0, n_rb = 0, tpw = 2;
   if (tile) {
-    n_cb = ((N >> 4) + 7) / 8;
     n_rb = (M + kTileBM - 1) / kTileBM;
+    // 64-column workgroups when 128-column ones would leave CUs idle (tile_tpw())
+    tpw = (((N >> 4) + 7) / 8) * n_rb < query_cus() && tile_narrow_on() ? 1 : 2;
+    n_cb = ((N >> 4) + 4 * tpw - 1) / (4 * tpw);
     grid = (n_cb + 7) / 8 * 8 * n_rb;
     lds = tile_lds_bytes(K);
   } else if (rows) {
@@ -1917,7 +1930,8 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   if (chain) chain->signaled = (uint32_t)grid;
   hipStream_t s = (hipStream_t)stream;
   if (tile) {
-    hipLaunchKernelGGL(gemm_tile_kernel<0>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
+    if (tpw == 1) hipLaunchKernelGGL(gemm_tile_kernel<1>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
+    else hipLaunchKernelGGL(gemm_tile_kernel<2>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
     TI_LAUNCH_CHECK("gemm_tile_kernel");
     return TI_OK;
   }
