@@ -54,6 +54,11 @@ int ti_engine_memory(ti_engine* e, size_t* weight_bytes, size_t* kv_bytes);
 /* Upload one tensor given in the reference layout (fp32 host memory); linear weights are
  * quantized + packed per the engine's bits (scale_mode: ti_hip.h TI_SCALE_*). */
 int ti_engine_set_tensor(ti_engine* e, int slot, int layer, const float* data, int scale_mode);
+/* Engines created with bits = 4 or 8 | TI_BITS_G32 (ti_hip.h: group-32 weights, GGUF Q4_0 /
+ * Q8_0 blocks): a linear weight given exactly, q int8 [K][N] (reference layout) and fp16 block
+ * scales d [K/32][N], weight = d * q -- no re-quantization.  ti_engine_set_tensor on such an
+ * engine quantizes fp32 weights per 32-block (absmax / 7 or / 127). */
+int ti_engine_set_tensor_q(ti_engine* e, int slot, int layer, const int8_t* q, const uint16_t* d);
 /* Synthetic model of SURVEY 8(d) generated on the device (bit-identical to the oracle's
  * or_model_synth for the same seed / jitter). */
 int ti_engine_synth(ti_engine* e, uint64_t seed, float norm_jitter);

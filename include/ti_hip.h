@@ -76,7 +76,7 @@ int ti_event_elapsed_ms(void* start, void* stop, float* ms); /* synchronises on 
  * tiles ordered [N/16][K/128]; inside a tile, 1 KiB chunk c holds for lane l (0..63)
  * at byte 1024*c + 16*l the k-run of output row (l & 15) starting at
  * k = 32*(l >> 4) + c*(32/chunks) -- one coalesced dwordx4 per lane per chunk.
- * Group scales (bits 4/8): fp16, [N/16][K/128][16].
+ * Group scales (bits 4/8): fp16, [N/16][K/128][16].  bits may carry TI_BITS_G32 (below).
  * K must be a multiple of 128 and N a multiple of 16. */
 enum ti_scale_mode { TI_SCALE_GROUP = 0, TI_SCALE_TENSOR = 1, TI_SCALE_UNIT = 2 };
 enum ti_row_map { TI_ROWS_CONCAT = 0, TI_ROWS_INTERLEAVE8 = 1 };
@@ -92,6 +92,19 @@ size_t ti_wpack_scale_bytes(int bits, int K, int N);
  * group), one per-tensor scale (reference Quantizer), or unit (reference raw cast). */
 int ti_wpack_host(const float* w, int K, int N_src, int N_total, int bits, int scale_mode,
                   int row_map, int row_offset, void* tiles, uint16_t* scales);
+
+/* Group-32 weights (GGUF Q4_0 / Q8_0 blocks, model_loader.cpp:165-182 / ggml's formats): bits
+ * 4 or 8 with TI_BITS_G32 set.  Tiles as above except the k order inside a tile: lane l's
+ * 16 bytes (int4; int8: 8 bytes per MFMA step in chunk s4 / 2) hold, for MFMA step s4, the
+ * 8 weights k = 32*s4 + 8*(l >> 4) + e, so every 32-weight block is one MFMA's reduction.
+ * Scales fp16 [N/16][K/128][4][16] (one per output row and 32-k block).  Runs on the fused
+ * kernel only (M <= ti_gemm_max_rows, no packed rows). */
+#define TI_BITS_G32 32
+/* Pack exact integer weights: q int8 [K][N_src] (int4: -8..7, int8: -127..127) with fp16 block
+ * scales d [K/32][N_src]: weight(k, c) = d[k/32][c] * q[k][c] exactly, as ggml dequantizes a
+ * Q4_0 / Q8_0 block (bits = 4 or 8, TI_BITS_G32 implied; rows mapped as in ti_wpack_host). */
+int ti_wpack_q_host(const int8_t* q, const uint16_t* d, int K, int N_src, int N_total, int bits, int row_map,
+                    int row_offset, void* tiles, uint16_t* scales);
 
 /* The synthetic model of SURVEY 8(d) generated straight into device tiles:
  * element (k, c) of tensor `tensor_id` = u(seed, tensor_id, k*N_src + c) * amp,

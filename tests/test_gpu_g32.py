@@ -1,0 +1,148 @@
+"""Group-32 weights (TI_BITS_G32): GGUF Q4_0 / Q8_0 blocks consumed as they are, no re-quantization.
+
+ggml dequantizes a Q4_0 block as d * (q - 8) and a Q8_0 block as d * q (32 weights, one fp16 d;
+reference model_loader.cpp:165-182 names the types, ggml's block formats define them).  The
+weights here are such products -- random integer q and fp16 d -- so w = d * q is exact in fp32,
+and the device must reproduce y = x . w up to fp32 summation order (the bound of
+test_gpu_kernels.py: 2e-5 * sum |x w|).  The engine test replaces the oracle model's linear
+weights by the same products and holds the decode logits to the engine tests' bar.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+f16 = np.float16
+f32 = np.float32
+
+
+def g32_weight(rng, K, N, bits):
+    lo, hi = (-8, 7) if bits == 4 else (-127, 127)
+    q = rng.randint(lo, hi + 1, size=(K, N)).astype(np.int8)
+    amp = 0.3 / np.sqrt(K) / (4.0 if bits == 4 else 64.0)
+    d = (rng.uniform(0.5, 1.5, size=(K // 32, N)) * amp).astype(f16)
+    w = np.repeat(d.astype(f32), 32, axis=0) * q.astype(f32)   # exact
+    return q, d, w
+
+
+def pack_g32(ti, q, d, bits):
+    L = ti.lib()
+    K, N = q.shape
+    tiles = np.zeros(L.ti_wpack_tile_bytes(bits | ti.BITS_G32, K, N), np.uint8)
+    scales = np.zeros(L.ti_wpack_scale_bytes(bits | ti.BITS_G32, K, N) // 2, np.uint16)
+    qa, da = np.ascontiguousarray(q), np.ascontiguousarray(d).view(np.uint16)
+    ti.check(L.ti_wpack_q_host(qa.ctypes.data, da.ctypes.data, K, N, N, bits, 0, 0, tiles.ctypes.data,
+                               scales.ctypes.data))
+    return ti.DeviceBuffer.from_array(tiles), ti.DeviceBuffer.from_array(scales)
+
+
+def run_gemm(ti, td, sd, bits, x, x_kind, M, N, K, norm=None):
+    yd = ti.DeviceBuffer(M * N * 4)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F32, N, yd.ptr
+    xd = ti.DeviceBuffer.from_array(np.ascontiguousarray(x))
+    nd = ti.DeviceBuffer.from_array(norm) if norm is not None else None
+    ti.check(ti.lib().ti_gemm_wq_a16(td.ptr, sd.ptr, bits | ti.BITS_G32, xd.ptr, x_kind, K, nd.ptr if nd else None,
+                                     1e-5, M, N, K, C.byref(ep), None))
+    ti.sync()
+    return yd.download(f32, (M, N))
+
+
+def assert_close_dot(y, xa, w, rel=2e-5):
+    ref = xa.astype(np.float64) @ w.astype(np.float64)
+    bound = rel * (np.abs(xa).astype(np.float64) @ np.abs(w).astype(np.float64)) + 1e-6
+    err = np.abs(y.astype(np.float64) - ref)
+    assert np.all(err <= bound), f"max err {err.max()} vs bound {bound[err > bound][:4]}"
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+@pytest.mark.parametrize("M,K,N", [(1, 128, 16), (1, 4096, 256), (3, 384, 80), (16, 1024, 64), (2, 11008, 32)])
+def test_gemm_g32_matches_exact_blocks(ti, bits, M, K, N):
+    rng = np.random.RandomState(K + N + M + bits)
+    q, d, w = g32_weight(rng, K, N, bits)
+    td, sd = pack_g32(ti, q, d, bits)
+    x = rng.standard_normal((M, K)).astype(f32)
+    y = run_gemm(ti, td, sd, bits, x, ti.X_F32, M, N, K)
+    assert_close_dot(y, x.astype(f16).astype(f32), w)
+    x16 = x.astype(f16)
+    y16 = run_gemm(ti, td, sd, bits, x16, ti.X_F16, M, N, K)
+    assert_close_dot(y16, x16.astype(f32), w)
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+@pytest.mark.parametrize("M", [1, 3])
+def test_gemm_g32_rmsnorm_prologue(ti, oracle, bits, M):
+    K, N = 2048, 64
+    rng = np.random.RandomState(31 + M)
+    q, d, w = g32_weight(rng, K, N, bits)
+    td, sd = pack_g32(ti, q, d, bits)
+    x = (rng.standard_normal((M, K)) * 3).astype(f32)
+    nw = (1 + 0.1 * rng.standard_normal(K)).astype(f32)
+    y = run_gemm(ti, td, sd, bits, x, ti.X_F32_RMSNORM, M, N, K, norm=nw)
+    xa = oracle.rms_norm(x, nw).astype(f16).astype(f32)
+    bound = (2e-5 + 1e-3) * (np.abs(xa) @ np.abs(w)) + 1e-6   # one fp16 ulp of the normalised row
+    assert np.all(np.abs(y - xa.astype(np.float64) @ w.astype(np.float64)) <= bound)
+
+
+def test_g32_rejects_batched_rows(ti):
+    K, N = 4096, 64
+    rng = np.random.RandomState(5)
+    q, d, _ = g32_weight(rng, K, N, 4)
+    td, sd = pack_g32(ti, q, d, 4)
+    assert ti.lib().ti_gemm_max_rows(4 | ti.BITS_G32, ti.X_F16, N, K) <= 16
+    with pytest.raises(ti.TiError):
+        run_gemm(ti, td, sd, 4, np.zeros((64, K), f16), ti.X_F16, 64, N, K)
+
+
+G32_CFG = dict(vocab=1024, hidden=512, layers=2, heads=8, kv_heads=2, head_dim=64, inter=768, rope_theta=10000.0,
+               eps=1e-5, bits=4, group=128, max_seq=256)
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+def test_engine_g32_decode_vs_oracle(ti, oracle, bits):
+    """A GQA model whose every linear weight is exact group-32 blocks: the engine (bits | G32,
+    weights through ti_engine_set_tensor_q) against the oracle decode with the same weights."""
+    from pyoracle import OracleModel, _OrModel
+    cfg = G32_CFG
+    V, H, NL, I = cfg["vocab"], cfg["hidden"], cfg["layers"], cfg["inter"]
+    qd, kvd = cfg["heads"] * cfg["head_dim"], cfg["kv_heads"] * cfg["head_dim"]
+    m = OracleModel(oracle, cfg, 77, 0.1)
+    base = m.weights()
+    mm = C.cast(m.ptr, C.POINTER(_OrModel)).contents
+    rng = np.random.RandomState(100 + bits)
+    e = ti.Engine(V, H, NL, cfg["heads"], cfg["kv_heads"], cfg["head_dim"], I, bits=bits | ti.BITS_G32,
+                  max_seq=cfg["max_seq"], max_batch=1, rope_theta=cfg["rope_theta"], eps=cfg["eps"])
+    e.set_tensor(ti.E_EMBED, 0, base["token_embeddings.weight"])
+    e.set_tensor(ti.V_OUT_NORM, 0, base["norm.weight"])
+
+    def linear(slot, layer, ptr, K, N):
+        q, d, w = g32_weight(rng, K, N, bits)
+        e.set_tensor_q(slot, layer, q, d)
+        np.ctypeslib.as_array(ptr, shape=(K * N,))[:] = w.reshape(-1)   # the oracle's weight, in place
+
+    linear(ti.W_LM_HEAD, 0, mm.lm_head, H, V)
+    for l in range(NL):
+        p = f"layers.{l}."
+        e.set_tensor(ti.V_ATTN_NORM, l, base[p + "attention_norm.weight"])
+        e.set_tensor(ti.V_FFN_NORM, l, base[p + "ffn_norm.weight"])
+        linear(ti.W_Q, l, mm.wq[l], H, qd)
+        linear(ti.W_K, l, mm.wk[l], H, kvd)
+        linear(ti.W_V, l, mm.wv[l], H, kvd)
+        linear(ti.W_O, l, mm.wo[l], qd, H)
+        linear(ti.W_GATE, l, mm.wg[l], H, I)
+        linear(ti.W_UP, l, mm.wu[l], H, I)
+        linear(ti.W_DOWN, l, mm.wd[l], I, H)
+    e.set_prefill(0)
+    tok = 5
+    for pos in range(12):
+        ref_t, ref_lg = m.step(tok)
+        lg = e.step([tok], [pos])[0]
+        tol = 2e-3 * float(np.max(np.abs(ref_lg)))
+        assert float(np.max(np.abs(lg.astype(np.float64) - ref_lg))) <= tol, pos
+        tok = ref_t
+    m.close()
+    e.close()

@@ -27,7 +27,8 @@ X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED, X_ATTN_SPLITS, X_F16_PACKED = 0, 1, 2
 ATTN_MAX_PART_SPLITS = 8           # TI_ATTN_MAX_PART_SPLITS (include/ti_hip.h)
 EPI_STORE_F32, EPI_STORE_F16, EPI_RESID_F32, EPI_SILU_MUL_F16, EPI_QKV_ROPE_KV, EPI_LOGITS_ARGMAX = range(6)
 ARGMAX_SLOTS = 32
-GEMM_MAX_ROWS = 256                 # TI_GEMM_MAX_ROWS (include/ti_hip.h)   # TI_ARGMAX_SLOTS (include/ti_hip.h)
+GEMM_MAX_ROWS = 256                 # TI_GEMM_MAX_ROWS (include/ti_hip.h)
+BITS_G32 = 32                       # TI_BITS_G32 (include/ti_hip.h): group-32 weights (GGUF Q4_0 / Q8_0)   # TI_ARGMAX_SLOTS (include/ti_hip.h)
 SCALE_GROUP, SCALE_TENSOR, SCALE_UNIT = 0, 1, 2
 ROWS_CONCAT, ROWS_INTERLEAVE8 = 0, 1
 (W_Q, W_K, W_V, W_O, W_GATE, W_UP, W_DOWN, W_LM_HEAD, V_ATTN_NORM, V_FFN_NORM, V_OUT_NORM, E_EMBED) = range(12)
@@ -81,6 +82,7 @@ EXPORTED = [
     "ti_attn_decode_partials", "ti_sample_device", "ti_sample_step", "ti_engine_generate_sampled",
     "ti_engine_beam_search", "ti_engine_serve", "ti_qkv_attn_fused", "ti_engine_set_qkv_attn",
     "ti_pds_decode", "ti_engine_set_pds", "ti_engine_pds_error", "ti_engine_pds_timestamps",
+    "ti_wpack_q_host", "ti_engine_set_tensor_q",
 ]
 
 _lib = None
@@ -161,6 +163,9 @@ def lib() -> C.CDLL:
         L.ti_engine_get_stream.argtypes = [vp, C.POINTER(vp)]
         L.ti_engine_memory.argtypes = [vp, C.POINTER(sz), C.POINTER(sz)]
         L.ti_engine_set_tensor.argtypes = [vp, i32, i32, vp, i32]
+        if hasattr(L, "ti_engine_set_tensor_q"):
+            L.ti_engine_set_tensor_q.argtypes = [vp, i32, i32, vp, vp]
+            L.ti_wpack_q_host.argtypes = [vp, vp, i32, i32, i32, i32, i32, i32, vp, vp]
         L.ti_engine_synth.argtypes = [vp, u64, f32]
         L.ti_engine_fill_kv.argtypes = [vp, i32, i32, u64]
         L.ti_engine_generate.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp]
@@ -324,6 +329,12 @@ class Engine:
             self.close()
         except Exception:
             pass
+
+    def set_tensor_q(self, slot, layer, q, d):
+        """Exact group-32 weight (engine bits 4/8 | BITS_G32): q int8 [K][N], d fp16 [K/32][N]."""
+        qa = np.ascontiguousarray(q, np.int8)
+        da = np.ascontiguousarray(d, np.float16).view(np.uint16)
+        check(lib().ti_engine_set_tensor_q(self.h, slot, layer, qa.ctypes.data, da.ctypes.data))
 
     def set_tensor(self, slot, layer, data, scale_mode=SCALE_GROUP):
         a = np.ascontiguousarray(data, np.float32)

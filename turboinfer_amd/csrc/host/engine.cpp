@@ -213,7 +213,8 @@ int validate(const ti_engine_config& c) {
   const int G = c.heads / c.kv_heads;
   if (G != 1 && G != 2 && G != 4 && G != 8) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_create: GQA group %d", G);
   if (c.head_dim != 64 && c.head_dim != 128) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_create: head_dim %d", c.head_dim);
-  if (c.bits != 4 && c.bits != 8 && c.bits != 16) return ti_set_error(TI_ERR_ARG, "ti_engine_create: bits %d", c.bits);
+  if (c.bits != 4 && c.bits != 8 && c.bits != 16 && c.bits != (4 | TI_BITS_G32) && c.bits != (8 | TI_BITS_G32))
+    return ti_set_error(TI_ERR_ARG, "ti_engine_create: bits %d (4, 8, 16; 4 or 8 | TI_BITS_G32)", c.bits);
   const int qd = c.heads * c.head_dim, kvd = c.kv_heads * c.head_dim;
   if (c.hidden % 128 || qd % 128 || c.inter % 128)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_create: hidden, heads*head_dim and inter must be multiples of 128");
@@ -415,7 +416,8 @@ int run_steps(ti_engine* e, int M, int advance, int n) {
 // the fused kernel with at most 256 workgroups.
 bool fold_usable(ti_engine* e, int M) {
   const ti_engine_config& c = e->c;
-  if (!e->fold_on || M != 1 || c.compat || !e->fx) return false;
+  // (group-32 weights: their launch grid is not ti_gemm_grid's, so no fold hand-off)
+  if (!e->fold_on || M != 1 || c.compat || !e->fx || (c.bits & TI_BITS_G32)) return false;
   const int H = c.hidden, I = c.inter, qd = e->qd();
   const int g_o = ti_gemm_grid(1, H, qd), g_d = ti_gemm_grid(1, H, I);
   return g_o > 0 && g_o <= 256 && g_d > 0 && g_d <= 256 && ti_gemm_max_rows(c.bits, TI_X_F16, H, qd) >= 1;
@@ -931,10 +933,44 @@ int ti_engine_set_tensor(ti_engine* e, int slot, int layer, const float* data, i
   return TI_OK;
 }
 
+// Exact group-32 weights (GGUF Q4_0 / Q8_0 blocks): q [K][N_src] int8 and fp16 block scales
+// d [K/32][N_src], packed without re-quantization (ti_wpack_q_host).
+int ti_engine_set_tensor_q(ti_engine* e, int slot, int layer, const int8_t* q, const uint16_t* d) {
+  if (!e || !q || !d) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q: null");
+  const ti_engine_config& c = e->c;
+  if (!(c.bits & TI_BITS_G32)) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q: engine bits %d lack TI_BITS_G32", c.bits);
+  if (layer < 0 || (slot <= TI_W_DOWN && layer >= c.layers)) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q: layer %d", layer);
+  const int H = c.hidden, I = c.inter, V = c.vocab, qd = e->qd(), kvd = e->kvd();
+  DevLinear* L = nullptr;
+  int K = 0, Nsrc = 0, map = TI_ROWS_CONCAT, off = 0;
+  switch (slot) {
+    case TI_W_Q: L = &e->layer[layer].qkv; K = H; Nsrc = qd; off = 0; break;
+    case TI_W_K: L = &e->layer[layer].qkv; K = H; Nsrc = kvd; off = qd; break;
+    case TI_W_V: L = &e->layer[layer].qkv; K = H; Nsrc = kvd; off = qd + kvd; break;
+    case TI_W_O: L = &e->layer[layer].o; K = qd; Nsrc = H; break;
+    case TI_W_GATE: L = &e->layer[layer].gu; K = H; Nsrc = I; map = TI_ROWS_INTERLEAVE8; off = 0; break;
+    case TI_W_UP: L = &e->layer[layer].gu; K = H; Nsrc = I; map = TI_ROWS_INTERLEAVE8; off = 8; break;
+    case TI_W_DOWN: L = &e->layer[layer].down; K = I; Nsrc = H; break;
+    case TI_W_LM_HEAD: L = &e->lm; K = H; Nsrc = V; break;
+    default: return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q: slot %d is not a linear weight", slot);
+  }
+  const size_t tb = ti_wpack_tile_bytes(c.bits, L->K, L->N), sb = ti_wpack_scale_bytes(c.bits, L->K, L->N);
+  std::vector<uint8_t> th(tb);
+  std::vector<uint16_t> sh(sb / 2 + 1);
+  TI_TRY(ti_memcpy_d2h(th.data(), L->tiles, tb, e->s));
+  TI_TRY(ti_memcpy_d2h(sh.data(), L->scales, sb, e->s));
+  TI_TRY(ti_wpack_q_host(q, d, K, Nsrc, L->N, c.bits, map, off, th.data(), sh.data()));
+  TI_TRY(ti_memcpy_h2d(L->tiles, th.data(), tb, e->s));
+  TI_TRY(ti_memcpy_h2d(L->scales, sh.data(), sb, e->s));
+  return ti_stream_sync(e->s);
+}
+
 int ti_engine_synth(ti_engine* e, uint64_t seed, float norm_jitter) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_synth: null");
   const ti_engine_config& c = e->c;
   if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_synth: compat engines take the reference model");
+  if (c.bits & TI_BITS_G32)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_synth: group-32 engines take their weights from ti_engine_set_tensor[_q]");
   const int H = c.hidden, I = c.inter, V = c.vocab, qd = e->qd(), kvd = e->kvd(), b = c.bits;
   for (int l = 0; l < c.layers; ++l) {
     DevLayer& L = e->layer[l];

@@ -39,18 +39,83 @@ inline uint16_t to_half(float f) {
 
 extern "C" size_t ti_wpack_tile_bytes(int bits, int K, int N) {
   if (K <= 0 || N <= 0) return 0;
-  return (size_t)(N / 16) * (size_t)(K / 128) * 256u * (size_t)bits;
+  return (size_t)(N / 16) * (size_t)(K / 128) * 256u * (size_t)(bits & ~TI_BITS_G32);
 }
 
 extern "C" size_t ti_wpack_scale_bytes(int bits, int K, int N) {
   if (bits == 16 || K <= 0 || N <= 0) return 0;
-  return (size_t)(N / 16) * (size_t)(K / 128) * 16u * sizeof(uint16_t);
+  return (size_t)(N / 16) * (size_t)(K / 128) * 16u * sizeof(uint16_t) * ((bits & TI_BITS_G32) ? 4u : 1u);
+}
+
+namespace {
+
+// One row r of tile (nt, g): the 128 integer weights q of k-group g into the tile's lanes.
+// g32: step s4 of lane kq holds k = 32 s4 + 8 kq + e (each MFMA one 32-block); else k = 32 kq +
+// 8 s4 + e.  int4 nibble p of a word: element 2p at bits 4p, element 2p+1 at bits 16 + 4p, q + 8.
+void pack_row(uint8_t* tile, int bits, bool g32, int r, const int8_t* q) {
+  auto kidx = [&](int kq, int s4, int e) { return g32 ? 32 * s4 + 8 * kq + e : 32 * kq + 8 * s4 + e; };
+  for (int kq = 0; kq < 4; ++kq) {
+    const int lane = kq * 16 + r;
+    if (bits == 4) {
+      uint32_t words[4];
+      for (int s4 = 0; s4 < 4; ++s4) {
+        uint32_t wd = 0;
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t nib = (uint32_t)(q[kidx(kq, s4, e)] + 8) & 0xF;
+          wd |= nib << ((e & 1) ? (16 + 4 * (e >> 1)) : (4 * (e >> 1)));
+        }
+        words[s4] = wd;
+      }
+      std::memcpy(tile + lane * 16, words, 16);
+    } else {   // int8: chunk ch holds steps 2 ch, 2 ch + 1 (8 bytes each)
+      for (int ch = 0; ch < 2; ++ch) {
+        int8_t b[16];
+        for (int h = 0; h < 2; ++h)
+          for (int e = 0; e < 8; ++e) b[8 * h + e] = q[kidx(kq, 2 * ch + h, e)];
+        std::memcpy(tile + ch * 1024 + lane * 16, b, 16);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int ti_wpack_q_host(const int8_t* q, const uint16_t* d, int K, int N_src, int N_total, int bits, int row_map,
+                               int row_offset, void* tiles, uint16_t* scales) {
+  bits &= ~TI_BITS_G32;
+  if (!q || !d || !tiles || !scales) return ti_set_error(TI_ERR_ARG, "ti_wpack_q_host: null pointer");
+  if (bits != 4 && bits != 8) return ti_set_error(TI_ERR_ARG, "ti_wpack_q_host: bits %d (4 or 8)", bits);
+  if (K <= 0 || (K & 127) || N_total <= 0 || (N_total & 15) || N_src <= 0)
+    return ti_set_error(TI_ERR_ARG, "ti_wpack_q_host: K %% 128 / N %% 16 (K=%d N_total=%d)", K, N_total);
+  if (row_map == TI_ROWS_INTERLEAVE8 && (N_src & 7)) return ti_set_error(TI_ERR_ARG, "ti_wpack_q_host: interleave needs N %% 8 == 0");
+  if (map_row(N_src - 1, row_map, row_offset) >= N_total || row_offset < 0)
+    return ti_set_error(TI_ERR_ARG, "ti_wpack_q_host: rows do not fit N_total");
+  const int lo = bits == 4 ? -8 : -127, hi = bits == 4 ? 7 : 127;
+  const int KT = K / 128;
+  const size_t tile_bytes = (size_t)256 * bits;
+  uint8_t* tb = static_cast<uint8_t*>(tiles);
+  int8_t col[128];
+  for (int c = 0; c < N_src; ++c) {
+    const int n = map_row(c, row_map, row_offset), nt = n >> 4, r = n & 15;
+    for (int g = 0; g < KT; ++g) {
+      for (int i = 0; i < 128; ++i) {
+        const int v = q[(size_t)(g * 128 + i) * N_src + c];
+        if (v < lo || v > hi) return ti_set_error(TI_ERR_ARG, "ti_wpack_q_host: weight %d outside [%d, %d]", v, lo, hi);
+        col[i] = (int8_t)v;
+      }
+      for (int s4 = 0; s4 < 4; ++s4) scales[(((size_t)nt * KT + g) * 4 + s4) * 16 + r] = d[(size_t)(g * 4 + s4) * N_src + c];
+      pack_row(tb + ((size_t)nt * KT + g) * tile_bytes, bits, true, r, col);
+    }
+  }
+  return TI_OK;
 }
 
 extern "C" int ti_wpack_host(const float* w, int K, int N_src, int N_total, int bits, int scale_mode, int row_map,
                              int row_offset, void* tiles, uint16_t* scales) {
   if (!w || !tiles) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: null pointer");
-  if (bits != 4 && bits != 8 && bits != 16) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: bits %d", bits);
+  const bool g32 = (bits & TI_BITS_G32) != 0;
+  bits &= ~TI_BITS_G32;
+  if ((bits != 4 && bits != 8 && bits != 16) || (g32 && bits == 16)) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: bits %d", bits);
   if (K <= 0 || (K & 127) || N_total <= 0 || (N_total & 15) || N_src <= 0)
     return ti_set_error(TI_ERR_ARG, "ti_wpack_host: K %% 128 / N %% 16 (K=%d N_total=%d)", K, N_total);
   if (row_map == TI_ROWS_INTERLEAVE8 && (N_src & 7)) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: interleave needs N %% 8 == 0");
@@ -85,36 +150,22 @@ extern "C" int ti_wpack_host(const float* w, int K, int N_src, int N_total, int 
   for (int c = 0; c < N_src; ++c) {
     const int n = map_row(c, row_map, row_offset), nt = n >> 4, r = n & 15;
     for (int g = 0; g < KT; ++g) {
-      float amax = 0.0f;
-      for (int i = 0; i < 128; ++i) {
-        col[i] = w[(size_t)(g * 128 + i) * N_src + c];
-        amax = std::max(amax, std::fabs(col[i]));
-      }
-      const float sc = scale_mode == TI_SCALE_GROUP ? amax / qmax : tensor_scale;
-      scales[((size_t)nt * KT + g) * 16 + r] = to_half(scale_mode == TI_SCALE_UNIT ? 1.0f : sc);
+      for (int i = 0; i < 128; ++i) col[i] = w[(size_t)(g * 128 + i) * N_src + c];
       int8_t q[128];
-      for (int i = 0; i < 128; ++i) {
-        const float v = scale_mode == TI_SCALE_UNIT ? std::round(col[i]) : std::round(col[i] / sc);
-        q[i] = (int8_t)clamp_ref(v, qlo, qmax);
-      }
-      uint8_t* tile = tb + ((size_t)nt * KT + g) * tile_bytes;
-      for (int kq = 0; kq < 4; ++kq) {
-        const int lane = kq * 16 + r;
-        if (bits == 4) {
-          uint32_t words[4];
-          for (int s4 = 0; s4 < 4; ++s4) {
-            uint32_t wd = 0;
-            for (int e = 0; e < 8; ++e) {
-              const uint32_t nib = (uint32_t)(q[kq * 32 + s4 * 8 + e] + 8) & 0xF;
-              wd |= nib << ((e & 1) ? (16 + 4 * (e >> 1)) : (4 * (e >> 1)));
-            }
-            words[s4] = wd;
-          }
-          std::memcpy(tile + lane * 16, words, 16);
-        } else {
-          for (int ch = 0; ch < 2; ++ch) std::memcpy(tile + ch * 1024 + lane * 16, q + kq * 32 + ch * 16, 16);
+      const int gsz = g32 ? 32 : 128;   // weights per scale
+      for (int b0 = 0; b0 < 128; b0 += gsz) {
+        float amax = 0.0f;
+        for (int i = b0; i < b0 + gsz; ++i) amax = std::max(amax, std::fabs(col[i]));
+        const float sc = scale_mode == TI_SCALE_GROUP ? amax / qmax : tensor_scale;
+        const uint16_t sh = to_half(scale_mode == TI_SCALE_UNIT ? 1.0f : sc);
+        if (g32) scales[(((size_t)nt * KT + g) * 4 + b0 / 32) * 16 + r] = sh;
+        else scales[((size_t)nt * KT + g) * 16 + r] = sh;
+        for (int i = b0; i < b0 + gsz; ++i) {
+          const float v = scale_mode == TI_SCALE_UNIT ? std::round(col[i]) : std::round(col[i] / sc);
+          q[i] = (int8_t)clamp_ref(v, qlo, qmax);
         }
       }
+      pack_row(tb + ((size_t)nt * KT + g) * tile_bytes, bits, g32, r, q);
     }
   }
   return TI_OK;

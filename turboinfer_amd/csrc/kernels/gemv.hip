@@ -88,11 +88,11 @@ __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
 // weights in flight), never more than there are 16-row tiles.
 static int g_wg_per_cu = 0;   // TI_GEMV_WG_PER_CU (tuning knob), default 1
 
-__host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_wg);
+__host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_wg, bool g32 = false);
 
 // Tiles per workgroup are bounded by the LDS image (partial slabs and scales grow with
 // them): very wide outputs (a 128k vocabulary) get more workgroups than CUs.
-__host__ inline int gemv_grid(int M, int N, int K, int num_cus) {
+__host__ inline int gemv_grid(int M, int N, int K, int num_cus, bool g32 = false) {
   if (g_wg_per_cu <= 0) {
     const char* s = getenv("TI_GEMV_WG_PER_CU");
     g_wg_per_cu = s && atoi(s) > 0 ? atoi(s) : 1;
@@ -100,14 +100,16 @@ __host__ inline int gemv_grid(int M, int N, int K, int num_cus) {
   const int NT = N >> 4;
   const int g = g_wg_per_cu * (num_cus > 0 ? num_cus : 256);
   int grid = NT < g ? NT : g;
-  while (grid < NT && gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid) > 160 * 1024) grid += grid / 8 + 1;
+  while (grid < NT && gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid, g32) > 160 * 1024) grid += grid / 8 + 1;
   return grid < NT ? grid : NT;
 }
 
 // LDS image of one workgroup (bytes, each region 16-aligned):
 //   x      [M][K + 8] fp16            activation rows (row pad breaks bank aliasing)
-//   scales [ntl][K/128][16] fp16      group scales of the workgroup's tiles
+//   scales [ntl][K/128][16] fp16      group scales of the workgroup's tiles ([ntl][K/128][4][16]
+//                                     with group-32 weights, TI_BITS_G32)
 //   corr   [K/128][16] f32            int4: per (group, row) offset correction (see deq_int4_raw)
+//                                     ([K/32][16] with group-32 weights)
 //   slab   [ntl + 1][8][64] f32x4     per-wave partial tiles (+ one dummy slab)
 //   es     epilogue inputs: residual [ntl][M][16] f32 (+ the fold weights of the same
 //          outputs, TI_EPI_RESID_F32 with fold_x), or RoPE (cos, sin) [M][hd] + pos [M]
@@ -115,20 +117,21 @@ __host__ inline int gemv_grid(int M, int N, int K, int num_cus) {
 struct GemvLds {
   int x, sc, corr, slab, es, best, total;
 };
-__host__ __device__ inline GemvLds gemv_lds_layout(int M, int K, int ntl) {
+__host__ __device__ inline GemvLds gemv_lds_layout(int M, int K, int ntl, bool g32 = false) {
   GemvLds l;
+  const int gm = g32 ? 4 : 1;                  // scale / correction groups per 128 k
   l.x = 0;
   l.sc = l.x + align16(M * (K + 8) * 2);
-  l.corr = l.sc + align16(ntl * (K >> 7) * 32);
-  l.slab = l.corr + (K >> 7) * 16 * 4;         // int4 offset correction [K/128][16 rows] f32
+  l.corr = l.sc + align16(ntl * (K >> 7) * 32 * gm);
+  l.slab = l.corr + (K >> 7) * 16 * 4 * gm;    // int4 offset correction [K/128 (x4)][16 rows] f32
   l.es = l.slab + (ntl + 1) * kGemvWaves * kWave * 16;
   const int es_bytes = 2 * ntl * M * 16 * 4 > M * 128 * 4 + 64 ? 2 * ntl * M * 16 * 4 : M * 128 * 4 + 64;
   l.best = l.es + align16(es_bytes);
   l.total = l.best + 16 * 8;
   return l;
 }
-__host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_wg) {
-  return gemv_lds_layout(M, K, tiles_per_wg).total;
+__host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_wg, bool g32) {
+  return gemv_lds_layout(M, K, tiles_per_wg, g32).total;
 }
 
 // ------------------------------------------------------------- x staging (LDS)
@@ -341,7 +344,10 @@ __device__ __forceinline__ void lds_barrier() {
 // The body is a device function: gemv_wq_kernel runs it over workgroup blockIdx.x's contiguous
 // tile range; STR (the fused QKV + attention launch below) over ntl_in tiles t0_in + i * tstr_in
 // chosen by the caller, bid standing in for blockIdx.x (argmax slot, counter shard, fold slot).
-template <int BITS, int XM, bool CH, bool STR>
+// G32: group-32 weights (TI_BITS_G32, GGUF Q4_0 / Q8_0 blocks): within a tile, lane l holds for
+// MFMA step s4 the 8 k = 32 s4 + 8 (l >> 4) + e, so each v_mfma_f32_16x16x32 reduces exactly one
+// 32-weight block; its scale (and, int4, its offset correction) is applied per step.
+template <int BITS, int XM, bool CH, bool STR, bool G32 = false>
 __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* p_scales, const void* p_x,
                                           const float* p_aux, int p_mgk, int p_N, int p_kx, int p_ldo,
                                           const float* p_pre, GemvArgs a, const unsigned bid, const int t0_in,
@@ -368,7 +374,8 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   const int ntl = STR ? ntl_in : (int)((bid + 1) * (unsigned)NT / (unsigned)p_grid) - t0;
   const int KW = wave < KT ? (KT - wave + kGemvWaves - 1) / kGemvWaves : 0;   // k-tiles per tile, this wave
   const int total = ntl * KW;
-  const GemvLds L = gemv_lds_layout(a.M, a.K, ntl);
+  static_assert(!G32 || (!STR && !CH && BITS != 16), "group-32 weights: int4 / int8, fused kernel only");
+  const GemvLds L = gemv_lds_layout(a.M, a.K, ntl, G32);
   f16* xl = (f16*)(smem + L.x);
   uint16_t* sl = (uint16_t*)(smem + L.sc);
   float* corr = (float*)(smem + L.corr);           // [K/128][16] (int4 only)
@@ -378,8 +385,8 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   float* red = (float*)(smem + L.slab);            // norm reduction scratch (before the stream)
 
   // ---- 1. small inputs into registers, ahead of the ring
-  const int n_sc = BITS == 16 ? 0 : ntl * KT * 2;  // u32x4 pieces of scales
-  const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16);
+  const int n_sc = BITS == 16 ? 0 : ntl * KT * (G32 ? 8 : 2);  // u32x4 pieces of scales
+  const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * (G32 ? 64 : 16));
   auto sc_off = [&](int i) -> int {                // piece i of the dense [ntl][KT][2] image
     if constexpr (!STR) return i;
     const int tl = i / (2 * KT);
@@ -611,8 +618,13 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
         const float hi = ((float)h[2] + (float)h[3]) + ((float)h[6] + (float)h[7]);
         part = 1032.0f * lo + 1152.0f * hi;
       }
-      part = group_sum<16>(part);
-      if (idx < a.M * K8 && (lane & 15) == 0) corr[(k8 >> 4) * 16 + m] = part;
+      if constexpr (G32) {   // one 32-k block = 4 consecutive pieces
+        part = group_sum<4>(part);
+        if (idx < a.M * K8 && (lane & 3) == 0) corr[(k8 >> 2) * 16 + m] = part;
+      } else {
+        part = group_sum<16>(part);
+        if (idx < a.M * K8 && (lane & 15) == 0) corr[(k8 >> 4) * 16 + m] = part;
+      }
     }
     lds_barrier();
   }
@@ -639,9 +651,25 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
     const int kt = wave + kGemvWaves * ck;
     f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
     if constexpr (BITS == 16) t = acc;
+    if constexpr (G32) {
+      const f16* xr32 = xrow - kq * 32 + kq * 8;   // this lane's 8 k of each 32-k block
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const f16x8 bf = dequant_step<BITS>(w, s4, magic);
+        const f16x8 af = *(const f16x8*)(xr32 + kt * 128 + s4 * 32);
+        f32x4 tb = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+        if constexpr (BITS == 4) tb -= *(const f32x4*)(corr + (kt * 4 + s4) * 16 + 4 * kq);
+        const float sc = h2f(sl[((ct * KT + kt) * 4 + s4) * 16 + r]);
+        acc[0] = fmaf(sc, tb[0], acc[0]);
+        acc[1] = fmaf(sc, tb[1], acc[1]);
+        acc[2] = fmaf(sc, tb[2], acc[2]);
+        acc[3] = fmaf(sc, tb[3], acc[3]);
+      }
+    } else {
 #if TI_GEMV_EXP & 1   // diagnostic build (tools/probe_gemv.hip): stream only, no dequant / MFMA
     t[0] += __builtin_bit_cast(float, w[0][0] ^ w[0][1] ^ w[0][2] ^ w[0][3]) + (float)xrow[kt];
 #else
+    (void)t;
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const f16x8 bf = dequant_step<BITS>(w, s4, magic);
@@ -662,6 +690,7 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
       acc[2] = fmaf(sc, t[2], acc[2]);
       acc[3] = fmaf(sc, t[3], acc[3]);
     }
+    }   // !G32
     // the tile's last item lands in its slab, every other item in the dummy slab
     const bool last = ++ck == KW;
     my_slab[(last ? ct : ntl) * kSlabStride] = acc;
@@ -803,12 +832,12 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   GEMV_TS(4);
 }
 
-template <int BITS, int XM, bool CH = false>
+template <int BITS, int XM, bool CH = false, bool G32 = false>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
                                                                    const void* p_x, const float* p_aux, int p_mgk,
                                                                    int p_N, int p_kx, int p_ldo, const float* p_pre,
                                                                    const GemvArgs a_in) {
-  gemv_body<BITS, XM, CH, false>(p_tiles, p_scales, p_x, p_aux, p_mgk, p_N, p_kx, p_ldo, p_pre, a_in, blockIdx.x, 0, 0, 1);
+  gemv_body<BITS, XM, CH, false, G32>(p_tiles, p_scales, p_x, p_aux, p_mgk, p_N, p_kx, p_ldo, p_pre, a_in, blockIdx.x, 0, 0, 1);
 }
 
 // ============================================================ QKV + attention, one launch
@@ -1516,7 +1545,7 @@ __host__ inline int gemv_xmode(int x_kind, int M, int K) {
   return M == 1 && (K >> 3) <= kGemvThreads ? XM_NORM1 : XM_NORM;
 }
 
-template <int BITS>
+template <int BITS, bool G32 = false>
 static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid, const ti_chain* chain) {
   const float* pre = a.epi.kind == TI_EPI_RESID_F32 ? (const float*)a.epi.out
                      : a.epi.kind == TI_EPI_QKV_ROPE_KV ? (const float*)a.epi.pos : (const float*)a.x;
@@ -1539,12 +1568,12 @@ static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid, cons
     return TI_OK;
   }
   switch (xm) {
-    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_ATTN: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_ATTN>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_F16F: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16F>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_ATTN: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_ATTN, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F16F: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16F, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
   }
   TI_LAUNCH_CHECK("gemv_wq_kernel");
   return TI_OK;
@@ -1775,7 +1804,11 @@ static int fused_rows_pref(int bits) {
   }
   return bits == 4 ? g_fused_rows : 16;
 }
-static bool fused_fits(int M, int N, int K) { return M <= 16 && ti_gemm_lds_bytes(M, N, K) <= 160 * 1024; }
+static bool fused_fits(int M, int N, int K, bool g32 = false) {
+  if (M > 16) return false;
+  const int NT = N >> 4, grid = ti::gemv_grid(M, N, K, query_cus(), g32);
+  return ti::gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid, g32) <= 160 * 1024;
+}
 static bool use_batched(int bits, int x_kind, int M, int N, int K) {
   const bool mb_ok = bits == 4 && x_kind == TI_X_F16;
   return !fused_fits(M, N, K) || (mb_ok && M > fused_rows_pref(bits));
@@ -1785,6 +1818,12 @@ extern "C" int ti_gemm_packed_rows(int bits, int M) { return bits == 4 && M > 16
 
 extern "C" int ti_gemm_max_rows(int bits, int x_kind, int N, int K) {
   if (N < 16 || K < 128) return 0;
+  if (bits & TI_BITS_G32) {   // group-32 weights: the fused kernel only
+    if (x_kind == TI_X_F16_PACKED) return 0;
+    int m = 16;
+    while (m > 1 && !fused_fits(m, N, K, true)) --m;
+    return fused_fits(m, N, K, true) ? m : 0;
+  }
   if (bits == 4 && (x_kind == TI_X_F16 || x_kind == TI_X_F16_PACKED)) return TI_GEMM_MAX_ROWS;
   if (x_kind == TI_X_F16_PACKED) return 0;
   int m = fused_rows_pref(bits);
@@ -1819,8 +1858,13 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
                      ti_stream_t stream) {
   using namespace ti;
   if (!tiles || !x || !epi || !epi->out) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: null pointer");
-  if (bits != 4 && bits != 8 && bits != 16)
-    return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: bits must be 4, 8 or 16 (got %d)", bits);
+  const bool g32 = (bits & TI_BITS_G32) != 0;
+  if (g32) bits &= ~TI_BITS_G32;
+  if ((bits != 4 && bits != 8 && bits != 16) || (g32 && bits == 16))
+    return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: bits must be 4, 8 or 16 (+ TI_BITS_G32 for 4 / 8; got %d)", bits);
+  if (g32 && (chain || x_kind == TI_X_F16_PACKED || M > 16 || !fused_fits(M, N, K, true)))
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: group-32 weights run on the fused kernel: M <= "
+                        "ti_gemm_max_rows (M=%d N=%d K=%d), no chain, no packed rows", M, N, K);
   if (bits != 16 && !scales) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: scales required for bits %d", bits);
   if (M < 1 || M > TI_GEMM_MAX_ROWS)
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: M must be in [1,%d] (got %d)", TI_GEMM_MAX_ROWS, M);
@@ -1864,7 +1908,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
       return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: unknown epilogue %d", epi->kind);
   }
   const bool packed_x = x_kind == TI_X_F16_PACKED;
-  const bool batched = packed_x || use_batched(bits, x_kind, M, N, K);
+  const bool batched = !g32 && (packed_x || use_batched(bits, x_kind, M, N, K));
   if (epi->out_packed && (!batched || (epi->kind != TI_EPI_STORE_F16 && epi->kind != TI_EPI_SILU_MUL_F16) ||
                           (epi->ldo & 127)))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: out_packed needs the batched-rows kernel, a fp16 store / SiLU "
@@ -1896,8 +1940,8 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     grid = mb_grid(MB, N, K, query_cus(), &ntl);
     lds = mb_use_lds(MB) ? mb_lds_bytes(MB, ntl, K) : mbr_lds_bytes(MB, ntl, K);
   } else {
-    grid = gemv_grid(M, N, K, query_cus());
-    lds = gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid);
+    grid = gemv_grid(M, N, K, query_cus(), g32);
+    lds = gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid, g32);
   }
   if (lds > 160 * 1024)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: LDS image %d B too large (M=%d N=%d K=%d)", lds, M, N, K);
@@ -1937,6 +1981,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   }
   if (rows) return launch_rows(a, rMB, rRG, ntl, grid, lds, s);
   if (batched) return launch_mb(a, M > 16 ? 2 : 1, grid, ntl, lds, s);
+  if (g32) return bits == 4 ? launch_gemv<4, true>(a, lds, s, grid, chain) : launch_gemv<8, true>(a, lds, s, grid, chain);
   if (bits == 4) return launch_gemv<4>(a, lds, s, grid, chain);
   if (bits == 8) return launch_gemv<8>(a, lds, s, grid, chain);
   return launch_gemv<16>(a, lds, s, grid, chain);
