@@ -445,3 +445,63 @@ def test_inference_engine_runs_gguf_checkpoint(api_check, golden, oracle, tmp_pa
     api_check("generate_gguf", tmp_path / "m.gguf", prompts, 12, 1, cfg["bits"], tmp_path / "b.bin")
     a, b = read(tmp_path / "a.bin"), read(tmp_path / "b.bin")
     assert a.shape == b.shape and np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("qt", ["q4_0", "q8_0"])
+def test_inference_engine_keeps_gguf_q_blocks(api_check, golden, oracle, tmp_path, qt):
+    """A Llama GGUF whose linear weights are Q4_0 / Q8_0 blocks (ggml's quantizers, gguf_oracle)
+    runs on group-32 tiles holding those blocks exactly: with weight_bits 0
+    the loader's dequantized values are recognised as d * q blocks and uploaded as such (the
+    engine reports group-32 blocks), and the greedy tokens equal those of the same dequantized
+    values under the reference's names with weight_bits 4 / 8 | 32 -- the same blocks, reached
+    from fp32 tensors.  (The group-32 kernels themselves: tests/test_gpu_g32.py.)"""
+    from pyoracle import OracleModel
+    G = _gguf_oracle()
+    d = golden("decode_mini_gqa_w4")
+    cfg = json.loads(str(d["cfg"]))
+    m = OracleModel(oracle, cfg, int(d["seed"][0]), float(d["jitter"][0]))
+    w = m.weights()
+    m.close()
+    T, bits = (G.T_Q4_0, 4) if qt == "q4_0" else (G.T_Q8_0, 8)
+
+    def blocks(v_out_in):   # what ggml stores and dequantizes: the [out][in] tensor's 32-blocks
+        a = np.ascontiguousarray(v_out_in, np.float32)
+        raw = (G.quant_q4_0 if T == G.T_Q4_0 else G.quant_q8_0)(a)
+        return G.dequant(raw, T, a.size).reshape(a.shape)
+
+    names = {"attention.q_proj.weight": "attn_q", "attention.k_proj.weight": "attn_k",
+             "attention.v_proj.weight": "attn_v", "attention.o_proj.weight": "attn_output",
+             "feed_forward.w3.weight": "ffn_gate", "feed_forward.w1.weight": "ffn_up",
+             "feed_forward.w2.weight": "ffn_down", "attention_norm.weight": "attn_norm", "ffn_norm.weight": "ffn_norm"}
+    deq = dict(w)
+    deq["lm_head.weight"] = np.ascontiguousarray(blocks(w["lm_head.weight"].T).T)
+    tensors = [("token_embd.weight", w["token_embeddings.weight"], G.T_F32), ("output_norm.weight", w["norm.weight"], G.T_F32),
+               ("output.weight", np.ascontiguousarray(w["lm_head.weight"].T), T)]
+    for l in range(cfg["layers"]):
+        for ref, gg in names.items():
+            v = w[f"layers.{l}.{ref}"]
+            if v.ndim == 2:
+                deq[f"layers.{l}.{ref}"] = np.ascontiguousarray(blocks(v.T).T)
+                tensors.append((f"blk.{l}.{gg}.weight", np.ascontiguousarray(v.T), T))
+            else:
+                tensors.append((f"blk.{l}.{gg}.weight", v, G.T_F32))
+    kvs = [("general.architecture", G.STR, "llama"), ("llama.vocab_size", G.U32, cfg["vocab"]),
+           ("llama.embedding_length", G.U32, cfg["hidden"]), ("llama.block_count", G.U32, cfg["layers"]),
+           ("llama.attention.head_count", G.U32, cfg["heads"]),
+           ("llama.attention.head_count_kv", G.U32, cfg["kv_heads"]),
+           ("llama.feed_forward_length", G.U32, cfg["inter"]), ("llama.rope.theta", G.F32, float(cfg["rope_theta"]))]
+    G.gguf_write(tmp_path / "m.gguf", kvs, tensors)
+    mdir = tmp_path / "ref"
+    mdir.mkdir()
+    lines = [f"meta {cfg['vocab']} {cfg['hidden']} {cfg['layers']} {cfg['heads']} {cfg['inter']} {cfg['rope_theta']!r}"]
+    for j, (k, v) in enumerate(deq.items()):
+        write(mdir / f"t{j}.bin", v.astype(f32))
+        lines.append(f"{k} t{j}.bin")
+    (mdir / "manifest.txt").write_text("\n".join(lines) + "\n")
+    prompts = write(tmp_path / "p.bin", np.array([d["prompt"].tolist()] * 2, np.int32))
+    out_a = api_check("generate", mdir, prompts, 12, 1, bits | 32, tmp_path / "a.bin")
+    out_b = api_check("generate_gguf", tmp_path / "m.gguf", prompts, 12, 1, 0, tmp_path / "b.bin")
+    assert "group-32 blocks" in out_a and "group-32 blocks" in out_b, out_b
+    a, b = read(tmp_path / "a.bin"), read(tmp_path / "b.bin")
+    assert a.shape == b.shape and np.array_equal(a, b)

@@ -8,6 +8,7 @@
 #include "turboinfer/model/inference_engine.hpp"
 
 #include <algorithm>
+#include <map>
 #include <chrono>
 #include <cmath>
 #include <iomanip>
@@ -90,6 +91,68 @@ ModelData from_gguf_names(const ModelData& g) {
   return m;
 }
 
+// GGUF Q4_0 / Q8_0 checkpoints reach the engine as ggml dequantizes them (gguf.cpp): every
+// 32-weight block along K of an output column is d * q with d fp16 and q an integer of
+// [-8, 7] (Q4_0) or [-127, 127] (Q8_0).  Recover (q, d) exactly from the fp32 values so the
+// engine holds the checkpoint's blocks as they are (group-32 tiles, TI_BITS_G32) instead of
+// re-quantizing them per 128.  ggml's quantizers put the block's largest magnitude at q = -8
+// (Q4_0, d = max / -8) or |q| = 127 (Q8_0), so the first candidate nearly always fits.
+bool recover_g32(const std::vector<float>& w, size_t K, size_t N, int bits, std::vector<int8_t>& q,
+                 std::vector<uint16_t>& d) {
+  if (K % 32 || w.size() != K * N) return false;
+  const int lo = bits == 4 ? -8 : -127, hi = bits == 4 ? 7 : 127;
+  q.assign(K * N, 0);
+  d.assign(K / 32 * N, 0);
+  auto half_bits = [](float f) {
+    const _Float16 h = (_Float16)f;
+    uint16_t u;
+    std::memcpy(&u, &h, 2);
+    return u;
+  };
+  auto half_val = [](uint16_t u) {
+    _Float16 h;
+    std::memcpy(&h, &u, 2);
+    return (float)h;
+  };
+  std::vector<float> cand;
+  for (size_t n = 0; n < N; ++n)
+    for (size_t b = 0; b < K / 32; ++b) {
+      float xm = 0.0f;
+      for (size_t k = 32 * b; k < 32 * b + 32; ++k)
+        if (std::fabs(w[k * N + n]) > std::fabs(xm)) xm = w[k * N + n];
+      if (xm == 0.0f) continue;   // all zero: q = 0, d = 0
+      cand.clear();
+      const float sgn = xm > 0.0f ? 1.0f : -1.0f, a = std::fabs(xm);
+      if (bits == 4) {
+        cand.push_back(-sgn * a / 8.0f);
+        for (int j = 7; j >= 1; --j) {
+          cand.push_back(sgn * a / (float)j);
+          cand.push_back(-sgn * a / (float)j);
+        }
+      } else {
+        for (int j = 127; j >= 1; --j) cand.push_back(a / (float)j);
+      }
+      bool found = false;
+      for (float c : cand) {
+        const uint16_t dh = half_bits(c);
+        const float dd = half_val(dh);
+        if (dd == 0.0f || !std::isfinite(dd)) continue;
+        bool ok = true;
+        for (size_t k = 32 * b; k < 32 * b + 32 && ok; ++k) {
+          const float x = w[k * N + n], r = std::rint(x / dd);
+          ok = r >= (float)lo && r <= (float)hi && r * dd == x;
+        }
+        if (!ok) continue;
+        for (size_t k = 32 * b; k < 32 * b + 32; ++k) q[k * N + n] = (int8_t)std::rint(w[k * N + n] / dd);
+        d[b * N + n] = dh;
+        found = true;
+        break;
+      }
+      if (!found) return false;
+    }
+  return true;
+}
+
 bool is_int(const core::Tensor& t) {
   return t.dtype() == core::DataType::kInt8 || t.dtype() == core::DataType::kInt32 ||
          t.dtype() == core::DataType::kInt16 || t.dtype() == core::DataType::kUInt8;
@@ -107,12 +170,51 @@ class InferenceEngineImpl {
   size_t total_generations = 0, total_tokens = 0, total_forward_passes = 0;
   float total_time_ms = 0.0f, peak_tps = 0.0f;
 
+  bool gguf_src = false;  // built from a GGUF-read ModelData (llama.cpp names)
+  // group-32 blocks recovered per linear weight (recover_g32), reused by upload()
+  std::map<const core::Tensor*, std::pair<std::vector<int8_t>, std::vector<uint16_t>>> g32;
+
   InferenceEngineImpl() { rng.seed((unsigned)std::chrono::steady_clock::now().time_since_epoch().count()); }
+
+  // every linear weight of the model is exact group-32 blocks of `bits` (cached on success)
+  bool all_g32(const ModelData& m, size_t L, size_t H, size_t qd, size_t kvd, size_t I, size_t V, int bits) {
+    g32.clear();
+    auto one = [&](const core::Tensor* t, size_t K, size_t N) {
+      if (!t || t->shape().total_size() != K * N) return false;
+      auto& e = g32[t];
+      return recover_g32(api::to_f32(*t), K, N, bits, e.first, e.second);
+    };
+    bool ok = one(find(m, {"lm_head.weight", "output.weight"}), H, V);
+    for (size_t l = 0; l < L && ok; ++l)
+      ok = one(layer_tensor(m, l, "self_attn.q_proj.weight", "attention.q_proj.weight"), H, qd) &&
+           one(layer_tensor(m, l, "self_attn.k_proj.weight", "attention.k_proj.weight"), H, kvd) &&
+           one(layer_tensor(m, l, "self_attn.v_proj.weight", "attention.v_proj.weight"), H, kvd) &&
+           one(layer_tensor(m, l, "self_attn.o_proj.weight", "attention.o_proj.weight"), qd, H) &&
+           one(layer_tensor(m, l, "mlp.gate_proj.weight", "feed_forward.w3.weight"), H, I) &&
+           one(layer_tensor(m, l, "mlp.up_proj.weight", "feed_forward.w1.weight"), H, I) &&
+           one(layer_tensor(m, l, "mlp.down_proj.weight", "feed_forward.w2.weight"), I, H);
+    if (!ok) g32.clear();
+    return ok;
+  }
   ~InferenceEngineImpl() {
     if (eng) ti_engine_destroy(eng);
   }
 
   void upload(int slot, int layer, const core::Tensor& t, size_t K, size_t N, int bits) {
+    if ((bits & TI_BITS_G32) && t.shape().total_size() == K * N) {   // exact blocks when the weight has them
+      auto it = g32.find(&t);
+      std::vector<int8_t> q;
+      std::vector<uint16_t> d;
+      if (it != g32.end()) {
+        q.swap(it->second.first);
+        d.swap(it->second.second);
+        g32.erase(it);
+      }
+      if (!q.empty() || recover_g32(api::to_f32(t), K, N, bits & ~TI_BITS_G32, q, d)) {
+        check(ti_engine_set_tensor_q(eng, slot, layer, q.data(), d.data()), "ti_engine_set_tensor_q");
+        return;
+      }
+    }
     if (t.shape().total_size() != K * N)
       throw std::runtime_error("InferenceEngine: weight for slot " + std::to_string(slot) + " layer " +
                                std::to_string(layer) + " has " + std::to_string(t.shape().total_size()) +
@@ -140,7 +242,10 @@ class InferenceEngineImpl {
   }
 
   void build(const ModelData& m, const InferenceConfig& c) {
-    if (gguf_named(m)) return build(from_gguf_names(m), c);
+    if (gguf_named(m)) {
+      gguf_src = true;
+      return build(from_gguf_names(m), c);
+    }
     const ModelMetadata& md = m.metadata();
     const size_t H = md.hidden_size, L = md.num_layers, nh = md.num_heads, V = md.vocab_size;
     size_t I = md.intermediate_size;
@@ -163,9 +268,14 @@ class InferenceEngineImpl {
         const std::vector<float> v = api::to_f32(*up0);
         for (float x : v)
           if (x < -8.0f || x > 7.0f) bits = 8;
+      } else if (gguf_src && q0) {   // Q4_0 / Q8_0 checkpoint: keep its blocks
+        const size_t kvd = k0 ? k0->shape().total_size() / H : H;
+        if (all_g32(m, L, H, H, kvd, I, V, 4)) bits = 4 | TI_BITS_G32;
+        else if (all_g32(m, L, H, H, kvd, I, V, 8)) bits = 8 | TI_BITS_G32;
       }
     }
-    if (bits != 4 && bits != 8 && bits != 16) throw std::runtime_error("InferenceEngine: weight_bits must be 4, 8 or 16");
+    if (bits != 4 && bits != 8 && bits != 16 && bits != (4 | TI_BITS_G32) && bits != (8 | TI_BITS_G32))
+      throw std::runtime_error("InferenceEngine: weight_bits must be 4, 8, 16 or 4 / 8 | 32 (group-32 blocks)");
     cfg.vocab = (int)V;
     cfg.hidden = (int)H;
     cfg.layers = (int)L;
@@ -529,8 +639,9 @@ std::string InferenceEngine::performance_stats() const {
   if (im.total_time_ms > 0.0f)
     os << "  Average Tokens/Second: " << (im.total_tokens / (im.total_time_ms / 1000.0f)) << "\n";
   os << "  Peak Tokens/Second: " << im.peak_tps << "\n";
-  os << "  Device Memory: " << (memory_usage() / (1024.0 * 1024.0)) << " MB (weights " << im.cfg.bits
-     << "-bit, fp16 KV, " << im.capacity << " stream(s) x " << im.cfg.max_seq << " slots)\n";
+  os << "  Device Memory: " << (memory_usage() / (1024.0 * 1024.0)) << " MB (weights " << (im.cfg.bits & ~TI_BITS_G32)
+     << "-bit" << ((im.cfg.bits & TI_BITS_G32) ? " group-32 blocks" : "") << ", fp16 KV, " << im.capacity
+     << " stream(s) x " << im.cfg.max_seq << " slots)\n";
   os << "  Mode: " << (im.compat ? "reference_compat (plumbing model)" : "llama decode") << "\n";
   return os.str();
 }
