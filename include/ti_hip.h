@@ -236,7 +236,7 @@ int ti_gemm_lds_bytes(int M, int N, int K);
  * and is used above TI_GEMM_FUSED_ROWS (env, default 2) rows.  An int4 caller with more rows
  * than this returns for TI_X_F32_RMSNORM should normalise them with ti_rmsnorm_f16 and pass
  * TI_X_F16 rows.  0 = shape unsupported. */
-#define TI_GEMM_MAX_ROWS 256
+#define TI_GEMM_MAX_ROWS 1024
 int ti_gemm_max_rows(int bits, int x_kind, int N, int K);
 /* 1 when M rows of an int4 GEMM go to the batched-rows kernel (17 .. 64 rows): its fp16
  * operands are best given as TI_X_F16_PACKED.  From 65 rows (TI_GEMM_TILE_ROWS, env, <= 65) on
@@ -275,7 +275,7 @@ int ti_gemm_prepare(void);
  * must be zeroed once before the first call; calls keep its ticket region re-armed.  splits
  * only shapes the work (results agree to rounding) and is capped by what one workgroup can
  * merge in LDS. */
-#define TI_ATTN_MAX_M 256
+#define TI_ATTN_MAX_M 1024
 size_t ti_attn_workspace_bytes(int M, int heads, int head_dim, int splits);
 int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
                    int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
@@ -396,7 +396,7 @@ int ti_step_begin_chained(const ti_step_args* a, ti_chain* chain, ti_stream_t s)
  * survivors in index order (the reference's loops over V add exact zeros elsewhere); exp/log
  * are the device's, equal logits at the k-th place and equal probabilities at the top-p cut
  * go lowest index first.  One 1024-thread workgroup per stream. */
-#define TI_SAMPLE_MAX_K 1024
+#define TI_SAMPLE_MAX_K 4096
 /* logits [M][ldl] fp32, draws [M] -> tokens [M], logprobs [M] (nullable) = log p(token). */
 int ti_sample_device(const float* logits, int ldl, int M, int V, float temperature, int top_k, float top_p,
                      const float* draws, int32_t* tokens, float* logprobs, ti_stream_t s);

@@ -31,7 +31,10 @@ def run(ti, tiles, scales, x16, M, N, K, ep):
                                    (3, 14336, 96), (20, 4096, 25600), (32, 384, 16), (64, 4096, 12288),
                                    (48, 11008, 4096 + 16), (33, 1152, 4000), (64, 384, 16), (64, 14336, 256),
                                    (40, 4096, 32000), (128, 4096, 4096), (200, 1152, 4000 + 16), (256, 11008, 512),
-                                   (129, 384, 16)])
+                                   (129, 384, 16),
+                                   # tile kernel at prefill chunks: 128 / 64 columns per workgroup, ragged tiles and rows
+                                   (512, 4096, 22016), (700, 4096, 12288 + 48), (1000, 1152, 4000 + 16),
+                                   (1024, 384, 16)])
 def test_batched_store(ti, oracle, M, K, N):
     rng = np.random.RandomState(M * 7 + K + N)
     w = (rng.standard_normal((K, N)) * 0.03).astype(f32)

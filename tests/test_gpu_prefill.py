@@ -73,15 +73,19 @@ def test_prefill_start_pos_and_cache_contents(ti, oracle):
     e.close()
 
 
-def test_prefill_tile_chunk_vs_oracle(ti, oracle):
-    """A 300-token prompt: one 256-row chunk through the LDS-tiled GEMM (ti_gemm_packed_rows
-    says row-major there) and a 43-row chunk through the batched-rows kernel (packed)."""
+@pytest.mark.parametrize("rows", [256, None])
+def test_prefill_tile_chunk_vs_oracle(ti, oracle, rows):
+    """A 300-token prompt: with 256-row chunks, one through the LDS-tiled GEMM (ti_gemm_packed_rows
+    says row-major there) and a 43-row chunk through the batched-rows kernel (packed); with the
+    default chunk (TI_GEMM_MAX_ROWS) the prompt runs as one 299-row tile chunk."""
     cfg = dict(MID, max_seq=512)
     seed, jit = 21, 0.1
     prompt = np.random.RandomState(9).randint(0, cfg["vocab"], size=300).tolist()
     ref, ref_logits = _oracle_tokens(oracle, cfg, seed, jit, prompt, 3)
     e = engine_for(ti, cfg)
     e.synth(seed, jit)
+    if rows:
+        e.set_prefill(rows)
     got, lg = e.generate([prompt], 3, want_logits=True)
     assert_greedy(got[0].tolist(), ref, ref_logits)
     assert_logits_close(lg[0], ref_logits[-1])

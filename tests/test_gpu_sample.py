@@ -29,7 +29,8 @@ def dev(ti, a):
 
 @pytest.mark.parametrize("V", [1000, 32000, 128256])
 @pytest.mark.parametrize("T,k,p", [(1.0, 1, 1.0), (0.7, 40, 0.9), (1.0, 50, 1.0), (1.3, 1024, 0.95),
-                                   (0.0, 8, 0.5), (1.0, 200, 0.0)])
+                                   (0.0, 8, 0.5), (1.0, 200, 0.0), (1.0, 1500, 1.0), (0.9, 2500, 0.97),
+                                   (1.0, 4096, 0.9)])
 def test_device_sampler_matches_oracle(ti, oracle, V, T, k, p):
     if k > V:
         pytest.skip("top_k above vocab")
@@ -87,7 +88,7 @@ def test_device_sampler_rejects_unsupported_top_k(ti):
     L = ti.lib()
     rc = L.ti_sample_device(1, 1000, 1, 1000, 1.0, 0, 1.0, 1, 1, None, None)
     assert rc == 3
-    rc = L.ti_sample_device(1, 5000, 1, 5000, 1.0, 2000, 1.0, 1, 1, None, None)
+    rc = L.ti_sample_device(1, 5000, 1, 5000, 1.0, 4097, 1.0, 1, 1, None, None)
     assert rc == 3
 
 

@@ -10,7 +10,8 @@ import turboinfer_amd as T  # noqa: E402
 
 T.init(0)
 L = T.lib()
-for V, k, p in [(32000, 40, 0.9), (32000, 40, 1.0), (32000, 1024, 0.9), (128256, 40, 0.9)]:
+for V, k, p in [(32000, 40, 0.9), (32000, 40, 1.0), (32000, 1024, 0.9), (128256, 40, 0.9), (32000, 2048, 1.0),
+                (32000, 4096, 0.9), (128256, 4096, 0.9)]:
     lg = T.DeviceBuffer.from_array((np.random.RandomState(0).standard_normal(V) * 3).astype(np.float32))
     dr = T.DeviceBuffer.from_array(np.array([0.3], np.float32))
     tok = T.DeviceBuffer(4)

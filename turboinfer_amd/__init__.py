@@ -27,7 +27,7 @@ X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED, X_ATTN_SPLITS, X_F16_PACKED = 0, 1, 2
 ATTN_MAX_PART_SPLITS = 8           # TI_ATTN_MAX_PART_SPLITS (include/ti_hip.h)
 EPI_STORE_F32, EPI_STORE_F16, EPI_RESID_F32, EPI_SILU_MUL_F16, EPI_QKV_ROPE_KV, EPI_LOGITS_ARGMAX = range(6)
 ARGMAX_SLOTS = 32
-GEMM_MAX_ROWS = 256                 # TI_GEMM_MAX_ROWS (include/ti_hip.h)
+GEMM_MAX_ROWS = 1024                # TI_GEMM_MAX_ROWS (include/ti_hip.h)
 BITS_G32 = 32                       # TI_BITS_G32 (include/ti_hip.h): group-32 weights (GGUF Q4_0 / Q8_0)   # TI_ARGMAX_SLOTS (include/ti_hip.h)
 SCALE_GROUP, SCALE_TENSOR, SCALE_UNIT = 0, 1, 2
 ROWS_CONCAT, ROWS_INTERLEAVE8 = 0, 1

@@ -1413,7 +1413,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
 // that the row blocks sharing a column block run on one XCD (blockIdx % 8), where its L2
 // serves their common weight stream.
 constexpr int kTileBM = 128, kTileWR = 4;   // rows per workgroup (x 128 columns), weight ring
-__host__ __device__ inline int tile_lds_bytes(int K) { return 2 * kTileBM * 256 + align16(8 * (K >> 7) * 32); }
+__host__ __device__ inline int tile_lds_bytes(int K, int tpw) { return 2 * kTileBM * 256 + align16(4 * tpw * (K >> 7) * 32); }
 
 // TPW: weight tiles per wave (2: 128 columns per workgroup; 1: 64 columns, twice the workgroups
 // for the narrow N = 4096 projections, which otherwise fill only 64 of 256 CUs at 256 rows).
@@ -1535,6 +1535,13 @@ __host__ inline bool tile_narrow_on() {
     g_tile_narrow = e ? atoi(e) != 0 : 1;
   }
   return g_tile_narrow != 0;
+}
+
+// Weight tiles per wave of the tile kernel: 64-column blocks when 128-column ones would leave
+// CUs idle (TI_TILE_NARROW, on by default), else 128.  (A 256-column block, TPW 4, needs 64
+// VGPRs of weight ring; hipcc put the ring in scratch and it ran 10x slower.)
+__host__ inline int tile_tpw(int N, int n_rb, int cus) {
+  return ((N >> 4) + 7) / 8 * n_rb < cus && tile_narrow_on() ? 1 : 2;
 }
 
 __host__ inline int gemv_xmode(int x_kind, int M, int K) {
@@ -1926,10 +1933,10 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   if (tile) {
     n_rb = (M + kTileBM - 1) / kTileBM;
     // 64-column workgroups when 128-column ones would leave CUs idle (tile_tpw())
-    tpw = (((N >> 4) + 7) / 8) * n_rb < query_cus() && tile_narrow_on() ? 1 : 2;
+    tpw = tile_tpw(N, n_rb, query_cus());
     n_cb = ((N >> 4) + 4 * tpw - 1) / (4 * tpw);
     grid = (n_cb + 7) / 8 * 8 * n_rb;
-    lds = tile_lds_bytes(K);
+    lds = tile_lds_bytes(K, tpw);
   } else if (rows) {
     rows_on();
     rows_shape(M, &rMB, &rRG);

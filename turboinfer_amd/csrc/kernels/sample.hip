@@ -17,7 +17,8 @@
 // select over the whole row, LDS histograms, when there are more than 2048 of them); the
 // survivors (ties lowest index first) are compacted in index order with block scans.  (A
 // radix pass over the row costs ~14 us: one bin takes most keys, so the LDS atomics
-// serialise.)  Differences to the reference: exp / log are the device's (<= 1 ulp from
+// serialise.)  k above 1024 (up to TI_SAMPLE_MAX_K) goes to the radix select directly, and
+// the per-survivor steps stride over the survivors.  Differences to the reference: exp / log are the device's (<= 1 ulp from
 // glibc), and equal logits at the k-th place / equal probabilities at the top-p cut are taken
 // lowest index first (libstdc++'s std::sort leaves their order unspecified).
 #include <math.h>
@@ -88,6 +89,9 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
   __shared__ __attribute__((aligned(16))) float s_p[TI_SAMPLE_MAX_K], s_sorted[TI_SAMPLE_MAX_K];
   __shared__ int s_cut;
   __shared__ int s_idx[TI_SAMPLE_MAX_K];
+  __shared__ int s_rank[TI_SAMPLE_MAX_K];
+  __shared__ unsigned long long s_key[TI_SAMPLE_MAX_K];   // top-p sort keys
+  __shared__ float s_mx[kSampWaves];
   constexpr int kCand = 2048;
   __shared__ uint32_t s_ck[kCand];
   __shared__ int s_ci[kCand];
@@ -193,15 +197,18 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
   // (k elements reach it; for smooth logits a few dozen more).  The k largest candidates,
   // ties lowest index first, are the survivors; with more than kCand candidates the full
   // row goes through the radix select instead.
-  uint32_t tmax = 0u;   // below every finite key
-  own([&](int, uint32_t key, bool ok) { tmax = ok && key > tmax ? key : tmax; });
-  uint32_t tau0;
-  int unused;
-  select_kth([&](auto&& f) { f(tmax); }, k, &tau0, &unused);
-  int ncand = 0;
-  own([&](int, uint32_t key, bool ok) { ncand += ok && key >= tau0; });
-  int tot;
-  const int cbase = wave_base(ncand, &tot);
+  // (k above the thread count: no k-th maximum to bound with, straight to the radix select)
+  int tot = kCand + 1, cbase = 0;
+  uint32_t tau0 = 0u;
+  if (k <= kSampThreads) {
+    uint32_t tmax = 0u;   // below every finite key
+    own([&](int, uint32_t key, bool ok) { tmax = ok && key > tmax ? key : tmax; });
+    int unused;
+    select_kth([&](auto&& f) { f(tmax); }, k, &tau0, &unused);
+    int ncand = 0;
+    own([&](int, uint32_t key, bool ok) { ncand += ok && key >= tau0; });
+    cbase = wave_base(ncand, &tot);
+  }
   const int C_tot = tot;
   int n;
   if (C_tot <= kCand) {
@@ -284,53 +291,94 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
   }
 
   // ---- softmax over the survivors (the others are exp(-inf) = 0 in the reference's loops)
-  float mx = -INFINITY;
-  for (int i = 0; i < n; ++i) mx = fmaxf(mx, s_val[i]);   // every thread, exact in any order
-  if (tid < n) s_p[tid] = expf(s_val[tid] - mx);
+  float mx = -INFINITY;   // exact in any order
+  for (int i = tid; i < n; i += kSampThreads) mx = fmaxf(mx, s_val[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if (lane == 0) s_mx[wv] = mx;
   __syncthreads();
-  // The sequential sums run in one thread (the reference's order), 8 values fetched per step.
-  auto seq_sum = [&](const float* p) {
-    float sum = 0.0f;
-    int i = 0;
-    for (; i + 8 <= n; i += 8) {
-      const float4 x = *(const float4*)(p + i), y = *(const float4*)(p + i + 4);
-      sum += x.x; sum += x.y; sum += x.z; sum += x.w;
-      sum += y.x; sum += y.y; sum += y.z; sum += y.w;
-    }
-    for (; i < n; ++i) sum += p[i];
-    return sum;
-  };
-  // first r (in order) whose running sum reaches `target` (cmp: sum >= target / target <= sum), or -1
-  auto seq_find = [&](const float* p, float target) {
+#pragma unroll
+  for (int w = 0; w < kSampWaves; ++w) mx = fmaxf(mx, s_mx[w]);
+  for (int i = tid; i < n; i += kSampThreads) s_p[i] = expf(s_val[i] - mx);
+  __syncthreads();
+  // The sequential sums run in one thread (the reference's order), 16 values per step with
+  // the next 16 already in flight (the adds are one dependent chain; the LDS latency hides
+  // behind it).
+  auto seq_scan = [&](const float* p, float target, bool find, float* sum_out) {
     float cum = 0.0f;
     int i = 0;
-    for (; i + 8 <= n; i += 8) {
-      const float4 x = *(const float4*)(p + i), y = *(const float4*)(p + i + 4);
-      const float v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+    if (n >= 16) {
+      float4 c[4], nx[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        cum += v[j];
-        if (target <= cum) return i + j;
+      for (int j = 0; j < 4; ++j) c[j] = *(const float4*)(p + 4 * j);
+      for (;; i += 16) {
+        const bool more = i + 32 <= n;
+        if (more) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) nx[j] = *(const float4*)(p + i + 16 + 4 * j);
+        }
+        const float v[16] = {c[0].x, c[0].y, c[0].z, c[0].w, c[1].x, c[1].y, c[1].z, c[1].w,
+                             c[2].x, c[2].y, c[2].z, c[2].w, c[3].x, c[3].y, c[3].z, c[3].w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          cum += v[j];
+          if (find && target <= cum) return i + j;
+        }
+        if (!more) {
+          i += 16;
+          break;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = nx[j];
       }
     }
     for (; i < n; ++i) {
       cum += p[i];
-      if (target <= cum) return i;
+      if (find && target <= cum) return i;
     }
+    *sum_out = cum;
     return -1;
+  };
+  auto seq_sum = [&](const float* p) {
+    float sum;
+    seq_scan(p, 0.0f, false, &sum);
+    return sum;
+  };
+  // first r (in order) whose running sum reaches `target` (cmp: sum >= target / target <= sum), or -1
+  auto seq_find = [&](const float* p, float target) {
+    float sum;
+    return seq_scan(p, target, true, &sum);
   };
   if (tid == 0) s_lp = seq_sum(s_p);
   __syncthreads();
-  if (tid < n) s_p[tid] = s_p[tid] / s_lp;
+  for (int i = tid; i < n; i += kSampThreads) s_p[i] = s_p[i] / s_lp;
   __syncthreads();
 
-  // ---- top-p: rank by probability (descending, lower index first on ties), cut, renormalise
+  // ---- top-p: rank by probability (descending, lower index first on ties), cut, renormalise.
+  // Rank order = ascending (~bits(p), survivor position) for p >= 0: a bitonic sort of those
+  // 64-bit keys in LDS, padded to a power of two with all-ones keys.
   if (a.top_p < 1.0f) {
-    int rank = 0;
-    if (tid < n) {
-      const float p = s_p[tid];
-      for (int j = 0; j < n; ++j) rank += s_p[j] > p || (s_p[j] == p && j < tid);
-      s_sorted[rank] = p;
+    int P = 64;
+    while (P < n) P <<= 1;
+    for (int i = tid; i < P; i += kSampThreads)
+      s_key[i] = i < n ? ((unsigned long long)~__float_as_uint(s_p[i]) << 32) | (uint32_t)i : ~0ull;
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = tid; i < P / 2; i += kSampThreads) {
+          const int lo = 2 * stride * (i / stride) + (i % stride), hi = lo + stride;
+          const unsigned long long x = s_key[lo], y = s_key[hi];
+          if ((x > y) == ((lo & size) == 0)) {
+            s_key[lo] = y;
+            s_key[hi] = x;
+          }
+        }
+        __syncthreads();
+      }
+    for (int r = tid; r < n; r += kSampThreads) {
+      const unsigned long long key = s_key[r];
+      s_sorted[r] = __uint_as_float(~(uint32_t)(key >> 32));
+      s_rank[(uint32_t)key] = r;
     }
     __syncthreads();
     if (tid == 0) {
@@ -338,11 +386,13 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
       s_cut = r < 0 ? n : r + 1;
     }
     __syncthreads();
-    if (tid < n && rank >= s_cut) s_p[tid] = 0.0f;
+    for (int i = tid; i < n; i += kSampThreads)
+      if (s_rank[i] >= s_cut) s_p[i] = 0.0f;
     __syncthreads();
     if (tid == 0) s_lp = seq_sum(s_p);
     __syncthreads();
-    if (tid < n && s_lp > 0.0f) s_p[tid] = s_p[tid] / s_lp;
+    if (s_lp > 0.0f)
+      for (int i = tid; i < n; i += kSampThreads) s_p[i] = s_p[i] / s_lp;
     __syncthreads();
   }
 
