@@ -1,0 +1,82 @@
+"""Prefill attention on MFMA (ti_attn_prefill, prefill_attn.hip): the rows of a prompt chunk
+attend causally to their own stream's cache (forward_pass, inference_engine.cpp:1429-1491 ->
+multi_head_attention, tensor_engine.cpp:1149-1252).
+
+Against the oracle's multi_head_attention per row (the bar of test_gpu_kernels.py's attention
+tests: fp16 output, rtol = atol = 4e-3) and against ti_attn_decode with stream stride 0 (the
+decode kernel the engine used for prefill before; same bar).  Cache rows past the chunk's last
+position hold NaN, as unwritten memory may: they must not reach any output."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from test_gpu_kernels import dev
+
+pytestmark = pytest.mark.gpu
+f16, f32 = np.float16, np.float32
+
+
+def _case(ti, M, nh, nkv, hd, pos, max_seq, seed):
+    rng = np.random.RandomState(seed)
+    kc = rng.standard_normal((nkv, max_seq, hd)).astype(f16)
+    vc = rng.standard_normal((nkv, max_seq, hd)).astype(f16)
+    top = int(pos.max())
+    kc[:, top + 1:] = np.nan
+    vc[:, top + 1:] = np.nan
+    q = rng.standard_normal((M, nh * hd)).astype(f32)
+    kd, vd, qd_, pd = dev(ti, kc), dev(ti, vc), dev(ti, q), dev(ti, pos)
+    L = ti.lib()
+    out = ti.DeviceBuffer(M * nh * hd * 2)
+    ti.check(L.ti_attn_prefill(qd_.ptr, kd.ptr, vd.ptr, max_seq, pd.ptr, M, nh, nkv, hd, out.ptr, None))
+    ref = ti.DeviceBuffer(M * nh * hd * 2)
+    ws = ti.DeviceBuffer(L.ti_attn_workspace_bytes(M, nh, hd, 4))
+    ws.zero()
+    ti.check(L.ti_attn_decode(qd_.ptr, kd.ptr, vd.ptr, 0, max_seq, pd.ptr, M, nh, nkv, hd, 4, ws.ptr, ref.ptr, None))
+    ti.sync()
+    return q, kc, vc, out.download(f16, (M, nh * hd)).astype(f32), ref.download(f16, (M, nh * hd)).astype(f32)
+
+
+@pytest.mark.parametrize("M,nh,nkv,hd,start,max_seq", [
+    (1, 4, 4, 128, 0, 16),          # one row, one key
+    (37, 4, 4, 128, 0, 64),         # partial 16-row block
+    (64, 8, 2, 64, 5, 80),          # GQA 4, hd 64, start past 0
+    (300, 8, 1, 128, 100, 512),     # GQA 8, a cache prefix before the chunk
+    (129, 8, 4, 64, 0, 129),        # prefix ends at max_seq - 1
+])
+def test_prefill_attention_vs_oracle(ti, oracle, M, nh, nkv, hd, start, max_seq):
+    pos = (start + np.arange(M)).astype(np.int32)
+    q, kc, vc, got, dec = _case(ti, M, nh, nkv, hd, pos, max_seq, seed=M + nh + hd)
+    assert np.all(np.isfinite(got))
+    grp = nh // nkv
+    for m in list(range(0, M, max(1, M // 12))) + [M - 1]:
+        S = int(pos[m]) + 1
+        kx = np.repeat(kc[:, :S].astype(f32).transpose(1, 0, 2), grp, axis=1).reshape(1, S, nh * hd)
+        vx = np.repeat(vc[:, :S].astype(f32).transpose(1, 0, 2), grp, axis=1).reshape(1, S, nh * hd)
+        ref = oracle.multi_head_attention(q[m].reshape(1, 1, -1), kx, vx, nh).reshape(-1)
+        np.testing.assert_allclose(got[m], ref, rtol=4e-3, atol=4e-3, err_msg=f"row {m}")
+    np.testing.assert_allclose(got, dec, rtol=4e-3, atol=4e-3)
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+def test_prefill_attention_ragged_positions(ti, hd):
+    """Positions in any order and with gaps (each row's own causal limit, blocks of mixed length)
+    and the 7B chunk shape, against the decode kernel."""
+    rng = np.random.RandomState(hd)
+    pos = rng.permutation(900)[:333].astype(np.int32)
+    _, _, _, got, dec = _case(ti, 333, 8, 2, hd, pos, 1024, seed=hd + 1)
+    assert np.all(np.isfinite(got))
+    np.testing.assert_allclose(got, dec, rtol=4e-3, atol=4e-3)
+
+
+def test_prefill_attention_7b_chunk(ti):
+    pos = np.arange(512, dtype=np.int32)
+    _, _, _, got, dec = _case(ti, 512, 32, 32, 128, pos, 2048, seed=7)
+    np.testing.assert_allclose(got, dec, rtol=4e-3, atol=4e-3)
+
+
+def test_prefill_attention_rejects_bad_sizes(ti):
+    L = ti.lib()
+    assert L.ti_attn_prefill(1, 1, 1, 16, 1, 0, 4, 4, 128, 1, None) != 0
+    assert L.ti_attn_prefill(1, 1, 1, 16, 1, 4, 6, 4, 128, 1, None) != 0
+    assert L.ti_attn_prefill(1, 1, 1, 16, 1, 4, 4, 4, 96, 1, None) != 0

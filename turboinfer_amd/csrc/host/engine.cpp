@@ -620,6 +620,15 @@ int enqueue_step(ti_engine* e, int M, int advance) {
 // batched path that share stream m's KV cache (epilogue / attention stream stride 0: row j
 // appends at its own position and attends to [0, base + t0 + j], causal).  No lm_head: the
 // decode loop takes over at the last prompt token.  Not graph-captured (host position upload).
+// TI_ATTN_PREFILL=0: prefill chunks through the decode attention kernel (A/B knob)
+static bool prefill_attn_on() {
+  static const int on = [] {
+    const char* v = getenv("TI_ATTN_PREFILL");
+    return v ? atoi(v) != 0 : 1;
+  }();
+  return on != 0;
+}
+
 int enqueue_prefill(ti_engine* e, int m, int t0, int rows, int base) {
   const ti_engine_config& c = e->c;
   std::vector<int32_t> bp(rows);
@@ -662,9 +671,12 @@ int enqueue_prefill(ti_engine* e, int m, int t0, int rows, int base) {
     ep.kv_stream_stride = 0;
     TI_TRY(gemm_rows(e, L.qkv, rows, e->h, TI_X_F32_RMSNORM, H, L.attn_norm, ep, 4, false));
     const bool pk = packed_rows(e, rows);
-    TI_TRY((pk ? ti_attn_decode_packed : ti_attn_decode)(e->q, kc, vc, 0, c.max_seq, e->pos, rows, c.heads,
-                                                         c.kv_heads, c.head_dim, e->splits_for(rows), e->ws, e->attn,
-                                                         e->s));
+    if (!pk && prefill_attn_on())   // row-major chunk: one pass over the prefix per 16 rows (MFMA)
+      TI_TRY(ti_attn_prefill(e->q, kc, vc, c.max_seq, e->pos, rows, c.heads, c.kv_heads, c.head_dim, e->attn, e->s));
+    else
+      TI_TRY((pk ? ti_attn_decode_packed : ti_attn_decode)(e->q, kc, vc, 0, c.max_seq, e->pos, rows, c.heads,
+                                                           c.kv_heads, c.head_dim, e->splits_for(rows), e->ws,
+                                                           e->attn, e->s));
     ti_epilogue eo{};
     eo.kind = TI_EPI_RESID_F32;
     eo.ldo = H;

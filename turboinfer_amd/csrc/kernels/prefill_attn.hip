@@ -1,0 +1,190 @@
+// prefill_attn.hip -- causal attention of a prompt chunk over its own stream's cache, on MFMA.
+//
+// The attention of forward_pass over prompt rows (inference_engine.cpp:1429-1491, which calls
+// TensorEngine::multi_head_attention, src/core/tensor_engine.cpp:1149-1252): row m (position
+// pos[m]) attends to keys [0, pos[m]] of the stream's fp16 cache, s_j = (q . k_j) / sqrt(hd),
+// softmax, o = sum_j p_j v_j; q-head h reads kv-head h / (heads / kv_heads).
+//
+// The decode kernel (attention.hip) gives every row its own workgroups, so a chunk of R rows
+// reads the prefix R times.  Here one wave owns 16 query rows of one head and streams the keys
+// once for them in blocks of 16, with fp32 MFMA (v_mfma_f32_16x16x4_f32: the products and sums
+// stay fp32, as in the reference; fp16 K / V convert exactly):
+//   S^T = K Q^T   A = K (lane: key l&15, dims (hd/4)(l>>4) + c), B = Q^T (query l&15, same
+//                 dims), hd/4 steps; D holds S^T[key 4(l>>4)+i][query l&15]
+//   online softmax per query (column): 4 values per lane, two xor-shuffles across the lane
+//                 groups; masked keys (key > pos[query]) get p = 0
+//   O += P V      the key order inside a block is free, so step j takes keys 4(l>>4)+j: lane
+//                 l's own p[j] is the A operand, and B for output tile t is V[key][dim
+//                 (l&15) hd/16 + t], one 16-byte load per j for all tiles
+// Rows of O are rescaled by each block's alpha (read from the lane that owns that query).
+// Queries are dealt longest-prefix first.  Bounded by the MFMA rate: the longest wave runs
+// (R / 16) blocks x (hd/4 + hd/4) MFMAs.
+#include <math.h>
+
+#include "common.hpp"
+
+namespace ti {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int HD>
+struct PfRaw;   // one lane's 16 (K) / hd/16 (V) fp16 values
+template <>
+struct PfRaw<128> {
+  using K = u32x4[4];   // 32 dims
+  using V = u32x4;      // 8 dims
+};
+template <>
+struct PfRaw<64> {
+  using K = u32x4[2];   // 16 dims
+  using V = uint2;      // 4 dims
+};
+
+__device__ __forceinline__ float pf_h(uint32_t w, int hi) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(hi ? (w >> 16) : (w & 0xffffu)));
+}
+
+template <int HD>
+__global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restrict__ q, const uint16_t* __restrict__ kc,
+                                                          const uint16_t* __restrict__ vc, int max_seq,
+                                                          const int32_t* __restrict__ pos, int M, int heads, int G,
+                                                          float scale, uint16_t* __restrict__ out) {
+  constexpr int DG = HD / 4, DV = HD / 16, KW = DG / 8;
+  using KRaw = typename PfRaw<HD>::K;
+  using VRaw = typename PfRaw<HD>::V;
+  const int lane = threadIdx.x, r = lane & 15, g = lane >> 4;
+  const int qb = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, kvh = h / G;
+  const int q0 = qb * 16, qi = min(q0 + r, M - 1);
+  const int p = pos[qi];
+  int kmax = p;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) kmax = max(kmax, __shfl_xor(kmax, o, 64));
+  float qv[DG];
+  {
+    const float* qr = q + ((size_t)qi * heads + h) * HD + g * DG;
+#pragma unroll
+    for (int c = 0; c < DG / 4; ++c) {
+      const float4 t = *(const float4*)(qr + 4 * c);
+      qv[4 * c] = t.x * scale;
+      qv[4 * c + 1] = t.y * scale;
+      qv[4 * c + 2] = t.z * scale;
+      qv[4 * c + 3] = t.w * scale;
+    }
+  }
+  const uint16_t* kb0 = kc + (size_t)kvh * max_seq * HD + g * DG;
+  const uint16_t* vb0 = vc + (size_t)kvh * max_seq * HD + r * DV;
+  auto load = [&](int kb, KRaw& k, VRaw (&v)[4]) {
+    const int kk = min(kb * 16 + r, max_seq - 1);
+#pragma unroll
+    for (int c = 0; c < KW; ++c) k[c] = *(const u32x4*)(kb0 + (size_t)kk * HD + 8 * c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kv = kb * 16 + 4 * g + j;
+      // keys past every row's prefix may be unwritten: zero so that p = 0 times them stays 0
+      v[j] = kv <= kmax ? *(const VRaw*)(vb0 + (size_t)min(kv, max_seq - 1) * HD) : VRaw{};
+    }
+  };
+  f32x4 acc[DV];
+#pragma unroll
+  for (int t = 0; t < DV; ++t) acc[t] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+  float m_run = -INFINITY, l_run = 0.0f;
+  const int nkb = kmax / 16 + 1;
+  KRaw kn;
+  VRaw vn[4];
+  load(0, kn, vn);
+  for (int kb = 0; kb < nkb; ++kb) {
+    KRaw k;
+    VRaw v[4];
+#pragma unroll
+    for (int c = 0; c < KW; ++c) k[c] = kn[c];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = vn[j];
+    if (kb + 1 < nkb) load(kb + 1, kn, vn);
+    f32x4 s = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < DG; ++c) {
+      const uint32_t w = k[c >> 3][(c >> 1) & 3];
+      s = __builtin_amdgcn_mfma_f32_16x16x4f32(pf_h(w, c & 1), qv[c], s, 0, 0, 0);
+    }
+    float pv[4], bm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool ok = kb * 16 + 4 * g + i <= p;
+      pv[i] = ok ? s[i] : -INFINITY;
+      bm = fmaxf(bm, pv[i]);
+    }
+    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m_run, bm);   // finite: key 0 is in every row's prefix
+    const float alpha = m_run == mn ? 1.0f : __expf(m_run - mn);
+    float ps = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pv[i] = pv[i] == -INFINITY ? 0.0f : __expf(pv[i] - mn);
+      ps += pv[i];
+    }
+    l_run = l_run * alpha + ps;
+    m_run = mn;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float ar = __shfl(alpha, 4 * g + i, 64);   // alpha of query 4g + i (row i of O)
+#pragma unroll
+      for (int t = 0; t < DV; ++t) acc[t][i] *= ar;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t vw[DV / 2];
+      if constexpr (HD == 128) {
+        vw[0] = v[j][0]; vw[1] = v[j][1]; vw[2] = v[j][2]; vw[3] = v[j][3];
+      } else {
+        vw[0] = v[j].x; vw[1] = v[j].y;
+      }
+#pragma unroll
+      for (int t = 0; t < DV; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(pv[j], pf_h(vw[t >> 1], t & 1), acc[t], 0, 0, 0);
+    }
+  }
+  float lt = l_run + __shfl_xor(l_run, 16, 64);
+  lt += __shfl_xor(lt, 32, 64);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float inv = 1.0f / __shfl(lt, 4 * g + i, 64);
+    const int row = q0 + 4 * g + i;
+    uint32_t o[DV / 2];
+#pragma unroll
+    for (int t = 0; t < DV / 2; ++t) {
+      const uint16_t lo = __builtin_bit_cast(uint16_t, (_Float16)(acc[2 * t][i] * inv));
+      const uint16_t hi = __builtin_bit_cast(uint16_t, (_Float16)(acc[2 * t + 1][i] * inv));
+      o[t] = lo | ((uint32_t)hi << 16);
+    }
+    if (row < M) {
+      uint16_t* dst = out + ((size_t)row * heads + h) * HD + r * DV;
+      if constexpr (HD == 128) *(ti::u32x4*)dst = (ti::u32x4){o[0], o[1], o[2], o[3]};
+      else *(uint2*)dst = make_uint2(o[0], o[1]);
+    }
+  }
+}
+
+}  // namespace ti
+
+extern "C" int ti_attn_prefill(const float* q, const uint16_t* k_cache, const uint16_t* v_cache, int max_seq,
+                               const int32_t* pos, int M, int heads, int kv_heads, int head_dim, uint16_t* out,
+                               ti_stream_t stream) {
+  if (!q || !k_cache || !v_cache || !pos || !out) return ti_set_error(TI_ERR_ARG, "ti_attn_prefill: null pointer");
+  if (M < 1 || heads < 1 || kv_heads < 1 || heads % kv_heads || max_seq < 1 || (M + 15) / 16 > 65535 || heads > 65535)
+    return ti_set_error(TI_ERR_ARG, "ti_attn_prefill: bad sizes M=%d heads=%d kv_heads=%d max_seq=%d", M, heads,
+                        kv_heads, max_seq);
+  if (head_dim != 64 && head_dim != 128)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_attn_prefill: head_dim %d not in {64,128}", head_dim);
+  const dim3 grid((M + 15) / 16, heads);
+  const float scale = 1.0f / sqrtf((float)head_dim);   // tensor_engine.cpp:1288
+  hipStream_t s = (hipStream_t)stream;
+  if (head_dim == 128)
+    hipLaunchKernelGGL(ti::attn_prefill_kernel<128>, grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq, pos, M, heads,
+                       heads / kv_heads, scale, out);
+  else
+    hipLaunchKernelGGL(ti::attn_prefill_kernel<64>, grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq, pos, M, heads,
+                       heads / kv_heads, scale, out);
+  TI_LAUNCH_CHECK("attn_prefill_kernel");
+  return TI_OK;
+}
