@@ -344,6 +344,7 @@ class Reference:
         L.ref_softmax.argtypes = [_f32p, C.c_uint64, C.c_uint64, C.c_float, _f32p]
         L.ref_attention_fast_incremental.argtypes = [_f32p, _f32p, _f32p, C.c_uint64, C.c_uint64, C.c_uint64, _f32p]
         L.ref_multi_head_attention.argtypes = [_f32p, _f32p, _f32p] + [C.c_uint64] * 4 + [_f32p]
+        L.ref_attention_general.argtypes = [_f32p, _f32p, _f32p, C.c_void_p] + [C.c_uint64] * 5 + [_f32p]
         L.ref_quantize.argtypes = [_f32p, C.c_uint64, C.c_int, C.c_int, _i32p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.ref_dequantize.argtypes = [_i32p, C.c_uint64, C.c_int, C.c_float, C.c_float, _f32p]
         L.ref_plumbing_generate.argtypes = [C.c_uint64] * 3 + [_i32p, C.c_uint64, C.c_uint64, _i32p, C.POINTER(C.c_uint64)]
@@ -419,6 +420,17 @@ class Reference:
         y = np.empty(B * D, np.float32)
         self._chk(self.lib.ref_attention_fast_incremental(q.reshape(-1), k.reshape(-1), v.reshape(-1), B, S, D, y))
         return y.reshape(B, 1, D)
+
+    def attention_general(self, q, k, v, heads=0, mask=None):
+        """TensorEngine::attention (heads 0) / multi_head_attention, any query length, optional mask."""
+        q, k, v = f32(q), f32(k), f32(v)
+        B, Sq, H = q.shape
+        Sk = k.shape[1]
+        m = None if mask is None else f32(mask).reshape(-1)
+        y = np.empty(B * Sq * H, np.float32)
+        self._chk(self.lib.ref_attention_general(q.reshape(-1), k.reshape(-1), v.reshape(-1),
+                                                 None if m is None else m.ctypes.data, B, Sq, Sk, H, heads, y))
+        return y.reshape(B, Sq, H)
 
     def multi_head_attention(self, q, k, v, heads):
         q, k, v = f32(q), f32(k), f32(v)

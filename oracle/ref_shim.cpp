@@ -149,6 +149,21 @@ int ref_multi_head_attention(const float* q, const float* k, const float* v, uin
   });
 }
 
+// TensorEngine::attention (heads 0) / multi_head_attention (heads > 0) with query length Sq
+// and an optional float mask [B][Sq][Sk] (tensor_engine.cpp:1045-1147, 1149-1252).
+int ref_attention_general(const float* q, const float* k, const float* v, const float* mask, uint64_t B,
+                          uint64_t Sq, uint64_t Sk, uint64_t H, uint64_t heads, float* y) {
+  return guard([&] {
+    const uint64_t qd[3] = {B, Sq, H}, kd[3] = {B, Sk, H}, md[3] = {B, Sq, Sk};
+    const uint64_t one[3] = {1, 1, 1};
+    const float zero = 0.0f;
+    Tensor m = mask ? make(mask, 3, md) : make(&zero, 3, one);
+    const Tensor* mp = mask ? &m : nullptr;
+    if (heads == 0) return out(engine().attention(make(q, 3, qd), make(k, 3, kd), make(v, 3, kd), mp), y);
+    return out(engine().multi_head_attention(make(q, 3, qd), make(k, 3, kd), make(v, 3, kd), heads, mp), y);
+  });
+}
+
 // Quantizer: bits 8 / 4, symmetric 0 / 1.  Writes q as int32 (int8 widened), scale, zp.
 int ref_quantize(const float* x, uint64_t n, int bits, int symmetric, int32_t* q, float* scale,
                  float* zp) {

@@ -165,6 +165,13 @@ static int op(int argc, char** argv) {
   else if (name == "softmax") y = te.softmax(in(0), std::stof(argv[5]));
   else if (name == "attention") y = te.attention_fast_incremental(in(0), in(1), in(2));
   else if (name == "mha") y = te.multi_head_attention(in(0), in(1), in(2), (size_t)std::stoul(argv[7]));
+  else if (name == "attn_general") {   // heads (0: TensorEngine::attention), mask file or "-"
+    const size_t heads = (size_t)std::stoul(argv[7]);
+    const bool masked = std::string(argv[8]) != "-";
+    const Tensor mask = masked ? read_array(argv[8]) : Tensor(TensorShape({1}), DataType::kFloat32);
+    const Tensor* mp = masked ? &mask : nullptr;
+    y = heads == 0 ? te.attention(in(0), in(1), in(2), mp) : te.multi_head_attention(in(0), in(1), in(2), heads, mp);
+  }
   else throw std::runtime_error("unknown op " + name);
   (void)argc;
   write_array(out, y);

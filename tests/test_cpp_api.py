@@ -144,6 +144,30 @@ def test_tensor_engine_ops_match_reference_vectors(api_check, golden, tmp_path):
 
 
 @pytest.mark.gpu
+def test_tensor_engine_attention_query_rows_and_mask(api_check, golden, tmp_path):
+    """TensorEngine::attention / multi_head_attention with query length > 1 and float masks
+    (tensor_engine.cpp:1045-1252) against the compiled reference's outputs
+    (tests/golden/gen_attention_prefill.py): batch matmuls, scale, mask and softmax are the
+    reference's arithmetic, so rows of 16+ keys in multiples of 8 (the softmax's exact path)
+    match bit for bit; other lengths to rtol 2e-6.  A query of length 1 takes the incremental
+    path, which ignores the mask as the reference does (rtol 1e-5, the device expf)."""
+    t = tmp_path
+    d = golden("attention_prefill")
+    for i in range(len([k for k in d.files if k.startswith("shape")])):
+        B, Sq, Sk, H, heads = (int(v) for v in d[f"shape{i}"])
+        mask = write(t / "m.bin", d[f"mask{i}"]) if f"mask{i}" in d else "-"
+        api_check("op", "attn_general", t / "y.bin", write(t / "q.bin", d[f"q{i}"]), write(t / "k.bin", d[f"k{i}"]),
+                  write(t / "v.bin", d[f"v{i}"]), heads, mask)
+        got, exp = read(t / "y.bin").reshape(B, Sq, H), d[f"y{i}"]
+        if Sq == 1:
+            np.testing.assert_allclose(got, exp, rtol=1e-5, atol=1e-6)
+        elif Sk >= 16 and Sk % 8 == 0:
+            same_bits(got, exp)
+        else:
+            np.testing.assert_allclose(got, exp, rtol=2e-6, atol=1e-7)
+
+
+@pytest.mark.gpu
 def test_tensor_engine_attention_matches_reference_vectors(api_check, golden, tmp_path):
     """attention_fast_incremental / multi_head_attention: same arithmetic sequence as the
     reference except the device expf (an ulp from glibc's): rtol 1e-5."""

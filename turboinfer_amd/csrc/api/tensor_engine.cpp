@@ -6,6 +6,7 @@
 // the engine stream, download.  No CPU arithmetic path exists.
 #include "turboinfer/core/tensor_engine.hpp"
 
+#include <cmath>
 #include <cstring>
 #include <sstream>
 #include <stdexcept>
@@ -211,21 +212,79 @@ Tensor TensorEngine::apply_rope(const Tensor& input, const Tensor& position_ids,
   return impl_->download(dy, input.shape());
 }
 
+// Query length > 1 (tensor_engine.cpp:1084-1147, per head as multi_head_attention :1149-1252
+// slices the hidden dimension): scores = Q K^T, one matmul per batch entry (the reference's
+// batch_matmul: one fma per k in ascending order = ti_matmul_f32), times 1/sqrt(d) (its scale:
+// ti_mul_f32 by a filled operand), -1e9 added where a float mask is 0 (ti_add_f32 of 0 / -1e9),
+// softmax over the keys (ti_softmax_f32), then P V.  Only the head slicing and the key
+// transpose (the reference's own host loops) run on the host.
+static Tensor attend_rows(TensorEngineImpl& impl, const std::vector<float>& q, const std::vector<float>& k,
+                          const std::vector<float>& v, size_t B, size_t Sq, size_t Sk, size_t H, size_t heads,
+                          const Tensor* mask) {
+  const size_t hd = H / heads, n = B * Sq * Sk;
+  const float scale_factor = 1.0f / std::sqrt(static_cast<float>(hd));   // :1116
+  DeviceBuffer dscale = impl.upload(std::vector<float>(n, scale_factor));
+  DeviceBuffer dmask;
+  const bool masked = mask && mask->dtype() == DataType::kFloat32;   // other mask types: no effect (:1127)
+  if (masked) {
+    const float* md = mask->data_ptr<float>();
+    std::vector<float> add(n);
+    for (size_t i = 0; i < n; ++i) add[i] = md[i] == 0.0f ? -1e9f : 0.0f;   // ATTENTION_MASK_VALUE (:47)
+    dmask = impl.upload(add);
+  }
+  std::vector<float> out(B * Sq * H);
+  std::vector<float> qh(B * Sq * hd), kt(B * hd * Sk), vh(B * Sk * hd);
+  for (size_t h = 0; h < heads; ++h) {
+    for (size_t b = 0; b < B; ++b) {
+      for (size_t s = 0; s < Sq; ++s)
+        std::memcpy(&qh[(b * Sq + s) * hd], &q[(b * Sq + s) * H + h * hd], hd * sizeof(float));
+      for (size_t s = 0; s < Sk; ++s)
+        for (size_t d = 0; d < hd; ++d) {
+          kt[(b * hd + d) * Sk + s] = k[(b * Sk + s) * H + h * hd + d];
+          vh[(b * Sk + s) * hd + d] = v[(b * Sk + s) * H + h * hd + d];
+        }
+    }
+    DeviceBuffer dq = impl.upload(qh), dk = impl.upload(kt), dv = impl.upload(vh);
+    DeviceBuffer ds(n * 4), dp(n * 4), dy(B * Sq * hd * 4);
+    float* fs = (float*)ds.ptr;
+    float* fp = (float*)dp.ptr;
+    for (size_t b = 0; b < B; ++b)
+      check(ti_matmul_f32((const float*)dq.ptr + b * Sq * hd, (const float*)dk.ptr + b * hd * Sk, fs + b * Sq * Sk,
+                          nullptr, (int)Sq, (int)hd, (int)Sk, 0, impl.stream),
+            "ti_matmul_f32");
+    check(ti_mul_f32(fs, (const float*)dscale.ptr, fs, (int64_t)n, impl.stream), "ti_mul_f32");
+    if (masked) check(ti_add_f32(fs, (const float*)dmask.ptr, fs, (int64_t)n, impl.stream), "ti_add_f32");
+    check(ti_softmax_f32(fs, fp, (int)(B * Sq), (int)Sk, 1.0f, impl.stream), "ti_softmax_f32");
+    for (size_t b = 0; b < B; ++b)
+      check(ti_matmul_f32(fp + b * Sq * Sk, (const float*)dv.ptr + b * Sk * hd, (float*)dy.ptr + b * Sq * hd, nullptr,
+                          (int)Sq, (int)Sk, (int)hd, 0, impl.stream),
+            "ti_matmul_f32");
+    const Tensor y = impl.download(dy, TensorShape({B, Sq, hd}));
+    const float* yd = y.data_ptr<float>();
+    for (size_t r = 0; r < B * Sq; ++r) std::memcpy(&out[r * H + h * hd], &yd[r * hd], hd * sizeof(float));
+  }
+  Tensor t(TensorShape({B, Sq, H}), DataType::kFloat32);
+  std::memcpy(t.data(), out.data(), out.size() * sizeof(float));
+  return t;
+}
+
 static Tensor attend(TensorEngineImpl& impl, const Tensor& q, const Tensor& k, const Tensor& v, size_t heads,
                      const Tensor* mask, const char* op) {
   if (q.empty() || k.empty() || v.empty())
     throw std::runtime_error(std::string(op) + ": query, key and value must be non-empty");
-  if (mask) throw std::runtime_error(std::string(op) + ": masked attention is prefill (SURVEY.md 8(f)), not decode");
   const auto& qd = q.shape().dimensions();
   const auto& kd = k.shape().dimensions();
   if (qd.size() != 3 || kd.size() != 3 || v.shape() != k.shape())
-    throw std::runtime_error(std::string(op) + ": expects query [B,1,H] and key/value [B,S,H]");
-  if (qd[1] != 1)
-    throw std::runtime_error(std::string(op) + ": query length " + std::to_string(qd[1]) +
-                             " > 1 is prefill attention (SURVEY.md 8(f)); decode takes one query");
+    throw std::runtime_error(std::string(op) + ": expects query [B,Sq,H] and key/value [B,S,H]");
   const size_t B = qd[0], H = qd[2], S = kd[1];
   if (kd[0] != B || kd[2] != H) throw std::runtime_error(std::string(op) + ": query / key shapes disagree");
   if (heads == 0 || H % heads) throw std::runtime_error(std::string(op) + ": hidden size not divisible by heads");
+  if (qd[1] != 1) {
+    if (mask && mask->shape().dimensions() != std::vector<size_t>{B, qd[1], S})
+      throw std::runtime_error("Mask dimensions must match attention scores");   // :1123-1125
+    return attend_rows(impl, api::to_f32(q), api::to_f32(k), api::to_f32(v), B, qd[1], S, H, heads, mask);
+  }
+  // one query: attention_fast_incremental (:1254-1388), which takes the mask and ignores it
   DeviceBuffer dq = impl.upload(api::to_f32(q)), dk = impl.upload(api::to_f32(k)), dv = impl.upload(api::to_f32(v));
   DeviceBuffer dy(B * H * 4), scratch(B * heads * S * 4);
   check(ti_attention_f32((const float*)dq.ptr, (const float*)dk.ptr, (const float*)dv.ptr, (float*)dy.ptr,
