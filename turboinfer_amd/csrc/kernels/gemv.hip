@@ -1412,11 +1412,12 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
 // 32 v_mfma_f32_16x16x32_f16, then the fp32 group-scale FMA.  The workgroup grid is ordered so
 // that the row blocks sharing a column block run on one XCD (blockIdx % 8), where its L2
 // serves their common weight stream.
-constexpr int kTileBM = 128, kTileWR = 4;   // rows per workgroup (x 128 columns), weight ring
+constexpr int kTileBM = 128;   // rows per workgroup
 __host__ __device__ inline int tile_lds_bytes(int K, int tpw) { return 2 * kTileBM * 256 + align16(4 * tpw * (K >> 7) * 32); }
 
 // TPW: weight tiles per wave (2: 128 columns per workgroup; 1: 64 columns, twice the workgroups
-// for the narrow N = 4096 projections, which otherwise fill only 64 of 256 CUs at 256 rows).
+// for the narrow N = 4096 projections, which otherwise fill only 64 of 256 CUs at 256 rows;
+// 4: 256 columns, half the activation bytes per MFMA, when the rows give enough workgroups).
 template <int TPW>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1437,7 +1438,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
     ((u32x4*)sl)[i] = i < ntile_ok * KT * 2 ? ld_w(sg + i) : (u32x4){0u, 0u, 0u, 0u};
 
   const f16* xg = (const f16*)a.x;
-  auto issue_x = [&](int kg) {   // 32 DMA instructions per group, 4 per wave
+  auto issue_x = [&](int kg) __attribute__((always_inline)) {   // 32 DMA instructions per group, 4 per wave
     f16* dst = xb + (kg & 1) * kTileBM * 128;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1447,11 +1448,13 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
     }
   };
   const u32x4* tb = a.tiles + lane;
-  auto load_w = [&](u32x4 (&w)[TPW], int kg) {
+  auto load_w = [&](u32x4 (&w)[TPW], int kg) __attribute__((always_inline)) {
     kg = min(kg, KT - 1);
 #pragma unroll
     for (int t = 0; t < TPW; ++t) w[t] = ld_w(tb + ((size_t)min(t0 + wn * TPW + t, NT - 1) * KT + kg) * kWave);
   };
+  // weight ring: 4 groups deep (2 at TPW 4, whose 4-deep ring hipcc keeps in scratch)
+  constexpr int kTileWR = TPW == 4 ? 2 : 4;
   u32x4 W[kTileWR][TPW];
   issue_x(0);
 #pragma unroll
@@ -1463,7 +1466,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
     for (int b = 0; b < 4; ++b) acc[t][b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
   uint32_t magic;
   asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
-  auto compute = [&](const u32x4 (&w)[TPW], int kg) {
+  auto compute = [&](const u32x4 (&w)[TPW], int kg) __attribute__((always_inline)) {
     const f16* xr = xb + (kg & 1) * kTileBM * 128 + (wm * 64 + r) * 128;
     f16x8 xf[4][4];
 #pragma unroll
@@ -1510,16 +1513,24 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // epilogue straight from the accumulators (16 x 4 outputs per lane pattern of the MFMA)
-#pragma unroll
+  // epilogue straight from the accumulators (16 x 4 outputs per lane pattern of the MFMA); the
+  // tile loop stays rolled (64 inlined epilogues are too large to unroll), so its accumulators
+  // are picked by static selects and acc stays in registers
+#pragma unroll 1
   for (int t = 0; t < TPW; ++t) {
     const int tn = t0 + wn * TPW + t;
+    f32x4 av[4];
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt)
+      if (tt == t)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) av[b] = acc[tt][b];
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * 64 + b * 16 + 4 * (lane >> 4) + i;
-        epilogue_mb(a, tn < NT ? tn : NT - 1, m, r, acc[t][b][i], tn < NT && m < a.M);
+        epilogue_mb(a, tn < NT ? tn : NT - 1, m, r, av[b][i], tn < NT && m < a.M);
       }
   }
   if (a.epi.kind == TI_EPI_LOGITS_ARGMAX && a.epi.step_ctr && blockIdx.x == 0 && tid == 0)
@@ -1537,11 +1548,30 @@ __host__ inline bool tile_narrow_on() {
   return g_tile_narrow != 0;
 }
 
-// Weight tiles per wave of the tile kernel: 64-column blocks when 128-column ones would leave
-// CUs idle (TI_TILE_NARROW, on by default), else 128.  (A 256-column block, TPW 4, needs 64
-// VGPRs of weight ring; hipcc put the ring in scratch and it ran 10x slower.)
+// Weight tiles per wave of the tile kernel, by a per-CU byte model: a CU streams a bounded
+// number of bytes per microsecond, a workgroup moves 32 KiB of activations plus
+// 2 x 4 TPW KiB of weights per 128-k group (the two row-waves of a column read the same tiles),
+// and the launch takes ceil(workgroups / CUs) rounds: cost(TPW) = rounds x (32 + 8 TPW).  The
+// cheapest of TPW 2, 1 (TI_TILE_NARROW, default on), 4 (TI_TILE_WIDE, default on) wins.
 __host__ inline int tile_tpw(int N, int n_rb, int cus) {
-  return ((N >> 4) + 7) / 8 * n_rb < cus && tile_narrow_on() ? 1 : 2;
+  static int wide = -1;
+  if (wide < 0) {
+    const char* e = getenv("TI_TILE_WIDE");
+    wide = e ? atoi(e) != 0 : 1;
+  }
+  const int NT = N >> 4;
+  int best = 2;
+  long best_cost = -1;
+  for (int tpw : {2, 1, 4}) {
+    if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && !wide)) continue;
+    const long wgs = (long)(NT + 4 * tpw - 1) / (4 * tpw) * n_rb;
+    const long cost = (wgs + cus - 1) / cus * (32 + 8 * tpw);
+    if (best_cost < 0 || cost < best_cost) {
+      best = tpw;
+      best_cost = cost;
+    }
+  }
+  return best;
 }
 
 __host__ inline int gemv_xmode(int x_kind, int M, int K) {
@@ -1784,7 +1814,7 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<4, XM_F16F>, (const void*)gemv_wq_kernel<8, XM_F16F>,
       (const void*)gemv_wq_kernel<16, XM_F16F>, (const void*)gemv_wq_kernel<4, XM_ATTN>,
       (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS, TI_ROWS_FNS,
-      (const void*)gemm_tile_kernel<2>, (const void*)gemm_tile_kernel<1>};
+      (const void*)gemm_tile_kernel<4>, (const void*)gemm_tile_kernel<2>, (const void*)gemm_tile_kernel<1>};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
@@ -1982,6 +2012,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   hipStream_t s = (hipStream_t)stream;
   if (tile) {
     if (tpw == 1) hipLaunchKernelGGL(gemm_tile_kernel<1>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
+    else if (tpw == 4) hipLaunchKernelGGL(gemm_tile_kernel<4>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
     else hipLaunchKernelGGL(gemm_tile_kernel<2>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
     TI_LAUNCH_CHECK("gemm_tile_kernel");
     return TI_OK;
