@@ -89,59 +89,62 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
   for (int t = 0; t < DV; ++t) acc[t] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
   float m_run = -INFINITY, l_run = 0.0f;
   const int nkb = kmax / 16 + 1;
-  KRaw kn;
-  VRaw vn[4];
-  load(0, kn, vn);
-  for (int kb = 0; kb < nkb; ++kb) {
-    KRaw k;
-    VRaw v[4];
+  // K / V blocks in flight: a ring of kPfRing blocks, each slot refilled right after its block
+  // is consumed (one wave per SIMD: the ring, not other waves, hides the load latency)
+  constexpr int kPfRing = 4;
+  KRaw kr[kPfRing];
+  VRaw vr[kPfRing][4];
 #pragma unroll
-    for (int c = 0; c < KW; ++c) k[c] = kn[c];
+  for (int u = 0; u < kPfRing; ++u) load(u, kr[u], vr[u]);   // past nkb: clamped rows, zero V
+  for (int kb0 = 0; kb0 < nkb; kb0 += kPfRing) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = vn[j];
-    if (kb + 1 < nkb) load(kb + 1, kn, vn);
-    f32x4 s = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    for (int u = 0; u < kPfRing; ++u) {
+      const int kb = kb0 + u;
+      if (kb >= nkb) break;
+      f32x4 s = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int c = 0; c < DG; ++c) {
-      const uint32_t w = k[c >> 3][(c >> 1) & 3];
-      s = __builtin_amdgcn_mfma_f32_16x16x4f32(pf_h(w, c & 1), qv[c], s, 0, 0, 0);
-    }
-    float pv[4], bm = -INFINITY;
+      for (int c = 0; c < DG; ++c) {
+        const uint32_t w = kr[u][c >> 3][(c >> 1) & 3];
+        s = __builtin_amdgcn_mfma_f32_16x16x4f32(pf_h(w, c & 1), qv[c], s, 0, 0, 0);
+      }
+      float pv[4], bm = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bool ok = kb * 16 + 4 * g + i <= p;
-      pv[i] = ok ? s[i] : -INFINITY;
-      bm = fmaxf(bm, pv[i]);
-    }
-    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-    const float mn = fmaxf(m_run, bm);   // finite: key 0 is in every row's prefix
-    const float alpha = m_run == mn ? 1.0f : __expf(m_run - mn);
-    float ps = 0.0f;
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = kb * 16 + 4 * g + i <= p;
+        pv[i] = ok ? s[i] : -INFINITY;
+        bm = fmaxf(bm, pv[i]);
+      }
+      bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+      const float mn = fmaxf(m_run, bm);   // finite: key 0 is in every row's prefix
+      const float alpha = m_run == mn ? 1.0f : __expf(m_run - mn);
+      float ps = 0.0f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      pv[i] = pv[i] == -INFINITY ? 0.0f : __expf(pv[i] - mn);
-      ps += pv[i];
-    }
-    l_run = l_run * alpha + ps;
-    m_run = mn;
+      for (int i = 0; i < 4; ++i) {
+        pv[i] = pv[i] == -INFINITY ? 0.0f : __expf(pv[i] - mn);
+        ps += pv[i];
+      }
+      l_run = l_run * alpha + ps;
+      m_run = mn;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float ar = __shfl(alpha, 4 * g + i, 64);   // alpha of query 4g + i (row i of O)
+      for (int i = 0; i < 4; ++i) {
+        const float ar = __shfl(alpha, 4 * g + i, 64);   // alpha of query 4g + i (row i of O)
 #pragma unroll
-      for (int t = 0; t < DV; ++t) acc[t][i] *= ar;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint32_t vw[DV / 2];
-      if constexpr (HD == 128) {
-        vw[0] = v[j][0]; vw[1] = v[j][1]; vw[2] = v[j][2]; vw[3] = v[j][3];
-      } else {
-        vw[0] = v[j].x; vw[1] = v[j].y;
+        for (int t = 0; t < DV; ++t) acc[t][i] *= ar;
       }
 #pragma unroll
-      for (int t = 0; t < DV; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(pv[j], pf_h(vw[t >> 1], t & 1), acc[t], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        uint32_t vw[DV / 2];
+        if constexpr (HD == 128) {
+          vw[0] = vr[u][j][0]; vw[1] = vr[u][j][1]; vw[2] = vr[u][j][2]; vw[3] = vr[u][j][3];
+        } else {
+          vw[0] = vr[u][j].x; vw[1] = vr[u][j].y;
+        }
+#pragma unroll
+        for (int t = 0; t < DV; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(pv[j], pf_h(vw[t >> 1], t & 1), acc[t], 0, 0, 0);
+      }
+      if (kb + kPfRing < nkb) load(kb + kPfRing, kr[u], vr[u]);
     }
   }
   float lt = l_run + __shfl_xor(l_run, 16, 64);
