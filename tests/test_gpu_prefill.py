@@ -73,14 +73,15 @@ def test_prefill_start_pos_and_cache_contents(ti, oracle):
     e.close()
 
 
-@pytest.mark.parametrize("rows", [256, None])
-def test_prefill_tile_chunk_vs_oracle(ti, oracle, rows):
+@pytest.mark.parametrize("rows,n", [(256, 300), (None, 300), (None, 1000)])
+def test_prefill_tile_chunk_vs_oracle(ti, oracle, rows, n):
     """A 300-token prompt: with 256-row chunks, one through the LDS-tiled GEMM (ti_gemm_packed_rows
     says row-major there) and a 43-row chunk through the batched-rows kernel (packed); with the
-    default chunk (TI_GEMM_MAX_ROWS) the prompt runs as one 299-row tile chunk."""
-    cfg = dict(MID, max_seq=512)
+    default chunk (TI_GEMM_MAX_ROWS) the prompt runs as one 299-row tile chunk, and a 1000-token
+    prompt as one 999-row chunk (tile GEMM and MFMA attention at their largest row counts)."""
+    cfg = dict(MID, max_seq=1024)
     seed, jit = 21, 0.1
-    prompt = np.random.RandomState(9).randint(0, cfg["vocab"], size=300).tolist()
+    prompt = np.random.RandomState(9 if n == 300 else 10).randint(0, cfg["vocab"], size=n).tolist()   # wide margins
     ref, ref_logits = _oracle_tokens(oracle, cfg, seed, jit, prompt, 3)
     e = engine_for(ti, cfg)
     e.synth(seed, jit)
