@@ -98,7 +98,8 @@ int ti_wpack_host(const float* w, int K, int N_src, int N_total, int bits, int s
  * 16 bytes (int4; int8: 8 bytes per MFMA step in chunk s4 / 2) hold, for MFMA step s4, the
  * 8 weights k = 32*s4 + 8*(l >> 4) + e, so every 32-weight block is one MFMA's reduction.
  * Scales fp16 [N/16][K/128][4][16] (one per output row and 32-k block).  Runs on the fused
- * kernel only (M <= ti_gemm_max_rows, no packed rows). */
+ * kernel (more rows than its LDS image holds: in pieces) and, int4 with fp16 rows from 65 rows
+ * on, on the tile GEMM; no packed rows (ti_gemm_max_rows). */
 #define TI_BITS_G32 32
 /* Pack exact integer weights: q int8 [K][N_src] (int4: -8..7, int8: -127..127) with fp16 block
  * scales d [K/32][N_src]: weight(k, c) = d[k/32][c] * q[k][c] exactly, as ggml dequantizes a

@@ -88,14 +88,31 @@ def test_gemm_g32_rmsnorm_prologue(ti, oracle, bits, M):
     assert np.all(np.abs(y - xa.astype(np.float64) @ w.astype(np.float64)) <= bound)
 
 
-def test_g32_rejects_batched_rows(ti):
+@pytest.mark.parametrize("bits,M", [(4, 17), (4, 64), (4, 65), (4, 200), (4, 512), (8, 40)])
+def test_gemm_g32_many_rows(ti, bits, M):
+    """More rows than the fused kernel holds: int4 fp16 rows from 65 on run on the tile GEMM
+    (group-32 k order and per-block scales), fewer (and int8) in 16-row pieces of the fused
+    kernel."""
+    K, N = (4096, 256) if M <= 200 else (1024, 4096 + 64)
+    rng = np.random.RandomState(M + bits)
+    q, d, w = g32_weight(rng, K, N, bits)
+    td, sd = pack_g32(ti, q, d, bits)
+    x16 = rng.standard_normal((M, K)).astype(f16)
+    y = run_gemm(ti, td, sd, bits, x16, ti.X_F16, M, N, K)
+    assert_close_dot(y, x16.astype(f32), w)
+
+
+def test_g32_row_limits(ti):
     K, N = 4096, 64
     rng = np.random.RandomState(5)
     q, d, _ = g32_weight(rng, K, N, 4)
     td, sd = pack_g32(ti, q, d, 4)
-    assert ti.lib().ti_gemm_max_rows(4 | ti.BITS_G32, ti.X_F16, N, K) <= 16
-    with pytest.raises(ti.TiError):
-        run_gemm(ti, td, sd, 4, np.zeros((64, K), f16), ti.X_F16, 64, N, K)
+    L = ti.lib()
+    assert L.ti_gemm_max_rows(4 | ti.BITS_G32, ti.X_F16, N, K) == ti.GEMM_MAX_ROWS
+    assert L.ti_gemm_max_rows(8 | ti.BITS_G32, ti.X_F16, N, K) <= 16
+    assert L.ti_gemm_max_rows(4 | ti.BITS_G32, ti.X_F16_PACKED, N, K) == 0
+    with pytest.raises(ti.TiError):   # no packed-rows kernel for group-32 weights
+        run_gemm(ti, td, sd, 4, np.zeros((64, K), f16), ti.X_F16_PACKED, 64, N, K)
 
 
 G32_CFG = dict(vocab=1024, hidden=512, layers=2, heads=8, kv_heads=2, head_dim=64, inter=768, rope_theta=10000.0,
@@ -146,3 +163,58 @@ def test_engine_g32_decode_vs_oracle(ti, oracle, bits):
         tok = ref_t
     m.close()
     e.close()
+
+
+def test_engine_g32_prefill_vs_oracle(ti, oracle):
+    """A 100-token prompt through prefill (one 99-row chunk: rms_norm prep, the group-32 tile
+    GEMM, MFMA prefill attention) on group-32 int4 weights, then greedy decode, against the
+    oracle fed the same prompt token by token with the same weights."""
+    from pyoracle import OracleModel, _OrModel
+    cfg = G32_CFG
+    V, H, NL, I = cfg["vocab"], cfg["hidden"], cfg["layers"], cfg["inter"]
+    qd, kvd = cfg["heads"] * cfg["head_dim"], cfg["kv_heads"] * cfg["head_dim"]
+    m = OracleModel(oracle, cfg, 78, 0.1)
+    base = m.weights()
+    mm = C.cast(m.ptr, C.POINTER(_OrModel)).contents
+    rng = np.random.RandomState(300)
+    e = ti.Engine(V, H, NL, cfg["heads"], cfg["kv_heads"], cfg["head_dim"], I, bits=4 | ti.BITS_G32,
+                  max_seq=cfg["max_seq"], max_batch=1, rope_theta=cfg["rope_theta"], eps=cfg["eps"])
+    e.set_tensor(ti.E_EMBED, 0, base["token_embeddings.weight"])
+    e.set_tensor(ti.V_OUT_NORM, 0, base["norm.weight"])
+
+    def linear(slot, layer, ptr, K, N):
+        q, d, w = g32_weight(rng, K, N, 4)
+        e.set_tensor_q(slot, layer, q, d)
+        np.ctypeslib.as_array(ptr, shape=(K * N,))[:] = w.reshape(-1)
+
+    linear(ti.W_LM_HEAD, 0, mm.lm_head, H, V)
+    for l in range(NL):
+        p = f"layers.{l}."
+        e.set_tensor(ti.V_ATTN_NORM, l, base[p + "attention_norm.weight"])
+        e.set_tensor(ti.V_FFN_NORM, l, base[p + "ffn_norm.weight"])
+        linear(ti.W_Q, l, mm.wq[l], H, qd)
+        linear(ti.W_K, l, mm.wk[l], H, kvd)
+        linear(ti.W_V, l, mm.wv[l], H, kvd)
+        linear(ti.W_O, l, mm.wo[l], qd, H)
+        linear(ti.W_GATE, l, mm.wg[l], H, I)
+        linear(ti.W_UP, l, mm.wu[l], H, I)
+        linear(ti.W_DOWN, l, mm.wd[l], I, H)
+    prompt = np.random.RandomState(31).randint(0, V, size=100).tolist()
+    n_new = 3
+    ref, ref_lg = [], []
+    tok, lg = None, None
+    for t in prompt:
+        tok, lg = m.step(t)
+    for _ in range(n_new):
+        ref.append(tok)
+        ref_lg.append(lg)
+        tok, lg = m.step(tok)
+    got, glg = e.generate([prompt], n_new, want_logits=True)
+    m.close()
+    e.close()
+    for i, lgi in enumerate(ref_lg):
+        s = np.sort(lgi)
+        assert s[-1] - s[-2] > 3 * 2e-3 * float(np.max(np.abs(lgi))), f"step {i}: reference margin too small"
+    assert got[0].tolist() == ref
+    tol = 2e-3 * float(np.max(np.abs(ref_lg[-1])))
+    assert float(np.max(np.abs(glg[0].astype(np.float64) - ref_lg[-1]))) <= tol

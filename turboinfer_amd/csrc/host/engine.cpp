@@ -241,7 +241,7 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
     x_kind = TI_X_F16_PACKED;
     ldx = W.K;
     rows = ti_gemm_max_rows(c.bits, x_kind, W.N, W.K);
-  } else if (x_kind == TI_X_F32_RMSNORM && rows < M && c.bits == 4 && e->xn) {
+  } else if (x_kind == TI_X_F32_RMSNORM && rows < M && (c.bits & ~TI_BITS_G32) == 4 && e->xn) {
     TI_TRY(ti_rmsnorm_f16(static_cast<const float*>(x), ldx, nw, c.eps, e->xn, W.K, M, W.K, e->s));
     x = e->xn;
     x_kind = TI_X_F16;
@@ -801,7 +801,7 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     if ((rc = ti_memcpy_h2d(e->rope_cs, cs.data(), cs.size() * 4, e->s))) return fail(rc);
     if (const char* env = getenv("TI_ATTN_TARGET")) e->attn_target = std::max(1, atoi(env));
     e->splits_max = e->splits_for(1);
-    e->pf_rows = c.bits == 4 ? TI_GEMM_MAX_ROWS : 16;
+    e->pf_rows = (c.bits & ~TI_BITS_G32) == 4 ? TI_GEMM_MAX_ROWS : 16;   // int4 (also group-32): the tile GEMM
     e->rows_cap = std::max(B, e->pf_rows);
     const int R = e->rows_cap;
     const int Rp = (R + 15) / 16 * 16;   // packed operands hold whole 16-row blocks
@@ -1335,7 +1335,7 @@ int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32
   const ti_engine_config& c = e->c;
   if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_serve: compat engine");
   const int B = c.max_batch;
-  const int pf = e->pf_rows > 0 ? e->pf_rows : std::min(e->rows_cap, c.bits == 4 ? TI_GEMM_MAX_ROWS : 16);
+  const int pf = e->pf_rows > 0 ? e->pf_rows : std::min(e->rows_cap, (c.bits & ~TI_BITS_G32) == 4 ? TI_GEMM_MAX_ROWS : 16);
   int max_len = 1;
   for (int r = 0; r < n_req; ++r) {
     const int L = offsets[r + 1] - offsets[r];
@@ -1415,7 +1415,7 @@ int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32
 }
 
 int ti_engine_set_prefill(ti_engine* e, int rows) {
-  if (!e || e->c.compat || rows < 0 || rows > e->rows_cap || (rows > 0 && rows > (e->c.bits == 4 ? TI_GEMM_MAX_ROWS : 16)))
+  if (!e || e->c.compat || rows < 0 || rows > e->rows_cap || (rows > 0 && rows > ((e->c.bits & ~TI_BITS_G32) == 4 ? TI_GEMM_MAX_ROWS : 16)))
     return ti_set_error(TI_ERR_ARG, "ti_engine_set_prefill: rows %d", rows);
   e->pf_rows = rows;
   return TI_OK;

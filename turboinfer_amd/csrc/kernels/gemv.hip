@@ -1413,12 +1413,16 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
 // that the row blocks sharing a column block run on one XCD (blockIdx % 8), where its L2
 // serves their common weight stream.
 constexpr int kTileBM = 128;   // rows per workgroup
-__host__ __device__ inline int tile_lds_bytes(int K, int tpw) { return 2 * kTileBM * 256 + align16(4 * tpw * (K >> 7) * 32); }
+__host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false) {
+  return 2 * kTileBM * 256 + align16(4 * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
+}
 
 // TPW: weight tiles per wave (2: 128 columns per workgroup; 1: 64 columns, twice the workgroups
 // for the narrow N = 4096 projections, which otherwise fill only 64 of 256 CUs at 256 rows;
 // 4: 256 columns, half the activation bytes per MFMA, when the rows give enough workgroups).
-template <int TPW>
+// G32: group-32 int4 tiles (TI_BITS_G32): MFMA step s4 of a group reads k-chunk 4 s4 + kq and
+// carries its own scale (one per 32-k block), so each step's product is scaled separately.
+template <int TPW, bool G32 = false>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KT = a.K >> 7, NT = a.N >> 4;
@@ -1430,12 +1434,13 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   if (cb >= n_cb) return;
   const int m0 = rb * kTileBM, t0 = cb * 4 * TPW;
   f16* xb = (f16*)smem;                                       // [2][128 rows][128 k] swizzled
-  uint16_t* sl = (uint16_t*)(smem + 2 * kTileBM * 256);       // [4 TPW tiles][KT][16]
-  const int n_sc = 4 * TPW * KT * 2;                          // 16-byte pieces
-  const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16);
+  constexpr int SG = G32 ? 4 : 1;                             // scales per tile row and group
+  uint16_t* sl = (uint16_t*)(smem + 2 * kTileBM * 256);       // [4 TPW tiles][KT][SG][16]
+  const int n_sc = 4 * TPW * KT * 2 * SG;                     // 16-byte pieces
+  const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16 * SG);
   const int ntile_ok = min(4 * TPW, NT - t0);
   for (int i = tid; i < n_sc; i += kGemvThreads)
-    ((u32x4*)sl)[i] = i < ntile_ok * KT * 2 ? ld_w(sg + i) : (u32x4){0u, 0u, 0u, 0u};
+    ((u32x4*)sl)[i] = i < ntile_ok * KT * 2 * SG ? ld_w(sg + i) : (u32x4){0u, 0u, 0u, 0u};
 
   const f16* xg = (const f16*)a.x;
   auto issue_x = [&](int kg) __attribute__((always_inline)) {   // 32 DMA instructions per group, 4 per wave
@@ -1472,9 +1477,29 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) xf[b][s4] = *(const f16x8*)(xr + b * 16 * 128 + (((kq * 4 + s4) ^ r) * 8));
+      for (int s4 = 0; s4 < 4; ++s4)
+        xf[b][s4] = *(const f16x8*)(xr + b * 16 * 128 + (((G32 ? s4 * 4 + kq : kq * 4 + s4) ^ r) * 8));
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
+      if constexpr (G32) {
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const f16x8 bf = deq_int4_signed(w[t][s4], magic);
+          f32x4 tmp[4];
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            tmp[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[b][s4], bf, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+          const float sc = h2f(sl[(((wn * TPW + t) * KT + kg) * 4 + s4) * 16 + r]);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            acc[t][b][0] = fmaf(sc, tmp[b][0], acc[t][b][0]);
+            acc[t][b][1] = fmaf(sc, tmp[b][1], acc[t][b][1]);
+            acc[t][b][2] = fmaf(sc, tmp[b][2], acc[t][b][2]);
+            acc[t][b][3] = fmaf(sc, tmp[b][3], acc[t][b][3]);
+          }
+        }
+        continue;
+      }
       f32x4 tmp[4];
 #pragma unroll
       for (int b = 0; b < 4; ++b) tmp[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
@@ -1553,7 +1578,7 @@ __host__ inline bool tile_narrow_on() {
 // 2 x 4 TPW KiB of weights per 128-k group (the two row-waves of a column read the same tiles),
 // and the launch takes ceil(workgroups / CUs) rounds: cost(TPW) = rounds x (32 + 8 TPW).  The
 // cheapest of TPW 2, 1 (TI_TILE_NARROW, default on), 4 (TI_TILE_WIDE, default on) wins.
-__host__ inline int tile_tpw(int N, int n_rb, int cus) {
+__host__ inline int tile_tpw(int N, int K, bool g32, int n_rb, int cus) {
   static int wide = -1;
   if (wide < 0) {
     const char* e = getenv("TI_TILE_WIDE");
@@ -1563,7 +1588,7 @@ __host__ inline int tile_tpw(int N, int n_rb, int cus) {
   int best = 2;
   long best_cost = -1;
   for (int tpw : {2, 1, 4}) {
-    if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && !wide)) continue;
+    if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && !wide) || tile_lds_bytes(K, tpw, g32) > 160 * 1024) continue;
     const long wgs = (long)(NT + 4 * tpw - 1) / (4 * tpw) * n_rb;
     const long cost = (wgs + cus - 1) / cus * (32 + 8 * tpw);
     if (best_cost < 0 || cost < best_cost) {
@@ -1814,7 +1839,8 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<4, XM_F16F>, (const void*)gemv_wq_kernel<8, XM_F16F>,
       (const void*)gemv_wq_kernel<16, XM_F16F>, (const void*)gemv_wq_kernel<4, XM_ATTN>,
       (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS, TI_ROWS_FNS,
-      (const void*)gemm_tile_kernel<4>, (const void*)gemm_tile_kernel<2>, (const void*)gemm_tile_kernel<1>};
+      (const void*)gemm_tile_kernel<4>, (const void*)gemm_tile_kernel<2>, (const void*)gemm_tile_kernel<1>,
+      (const void*)gemm_tile_kernel<4, true>, (const void*)gemm_tile_kernel<2, true>, (const void*)gemm_tile_kernel<1, true>};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
@@ -1855,8 +1881,9 @@ extern "C" int ti_gemm_packed_rows(int bits, int M) { return bits == 4 && M > 16
 
 extern "C" int ti_gemm_max_rows(int bits, int x_kind, int N, int K) {
   if (N < 16 || K < 128) return 0;
-  if (bits & TI_BITS_G32) {   // group-32 weights: the fused kernel only
+  if (bits & TI_BITS_G32) {   // group-32 weights: the fused kernel; int4 fp16 rows also the tile kernel
     if (x_kind == TI_X_F16_PACKED) return 0;
+    if ((bits & ~TI_BITS_G32) == 4 && x_kind == TI_X_F16) return TI_GEMM_MAX_ROWS;   // 17..64: 16-row pieces
     int m = 16;
     while (m > 1 && !fused_fits(m, N, K, true)) --m;
     return fused_fits(m, N, K, true) ? m : 0;
@@ -1899,9 +1926,14 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   if (g32) bits &= ~TI_BITS_G32;
   if ((bits != 4 && bits != 8 && bits != 16) || (g32 && bits == 16))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: bits must be 4, 8 or 16 (+ TI_BITS_G32 for 4 / 8; got %d)", bits);
-  if (g32 && (chain || x_kind == TI_X_F16_PACKED || M > 16 || !fused_fits(M, N, K, true)))
-    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: group-32 weights run on the fused kernel: M <= "
-                        "ti_gemm_max_rows (M=%d N=%d K=%d), no chain, no packed rows", M, N, K);
+  // group-32: int4 fp16 rows from tile_rows() on run on the tile kernel, everything else on the
+  // fused kernel (more than 16 rows: in 16-row pieces, below)
+  const bool g32_tile = g32 && bits == 4 && x_kind == TI_X_F16 && M >= tile_rows() && !epi->out_packed;
+  int g32_rows = 16;   // rows per fused launch (its LDS image holds the x rows)
+  while (g32 && g32_rows > 1 && !fused_fits(g32_rows, N, K, true)) --g32_rows;
+  if (g32 && (chain || x_kind == TI_X_F16_PACKED || (!g32_tile && !fused_fits(std::min(M, g32_rows), N, K, true))))
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: group-32 weights: fused kernel rows (M=%d N=%d K=%d) "
+                        "or int4 fp16 rows >= %d; no chain, no packed rows", M, N, K, tile_rows());
   if (bits != 16 && !scales) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: scales required for bits %d", bits);
   if (M < 1 || M > TI_GEMM_MAX_ROWS)
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: M must be in [1,%d] (got %d)", TI_GEMM_MAX_ROWS, M);
@@ -1944,8 +1976,28 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     default:
       return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: unknown epilogue %d", epi->kind);
   }
+  if (g32 && !g32_tile && M > g32_rows) {   // pieces of g32_rows rows through the fused kernel
+    if (x_kind == TI_X_ATTN_SPLITS || x_kind == TI_X_F16_FOLDED || epi->out_packed)
+      return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: group-32 rows > 16 need plain x rows");
+    const size_t x_elem = x_kind == TI_X_F16 ? 2 : 4;
+    const size_t out_elem = epi->kind == TI_EPI_STORE_F16 || epi->kind == TI_EPI_SILU_MUL_F16 ? 2 : 4;
+    for (int m0 = 0; m0 < M; m0 += g32_rows) {
+      const int mm = std::min(g32_rows, M - m0);
+      ti_epilogue ep = *epi;
+      ep.out = static_cast<char*>(epi->out) + (size_t)m0 * epi->ldo * out_elem;
+      if (ep.pos) ep.pos += m0;
+      if (ep.k_cache) ep.k_cache += (size_t)m0 * ep.kv_stream_stride;
+      if (ep.v_cache) ep.v_cache += (size_t)m0 * ep.kv_stream_stride;
+      if (ep.argmax) ep.argmax += (size_t)m0 * TI_ARGMAX_SLOTS;
+      if (m0 + mm < M) ep.step_ctr = nullptr;
+      const int rc = gemm_impl(tiles, scales, bits | TI_BITS_G32, static_cast<const char*>(x) + (size_t)m0 * ldx * x_elem,
+                               x_kind, ldx, norm_w, eps, mm, N, K, &ep, nullptr, stream);
+      if (rc != TI_OK) return rc;
+    }
+    return TI_OK;
+  }
   const bool packed_x = x_kind == TI_X_F16_PACKED;
-  const bool batched = !g32 && (packed_x || use_batched(bits, x_kind, M, N, K));
+  const bool batched = g32 ? g32_tile : (packed_x || use_batched(bits, x_kind, M, N, K));
   if (epi->out_packed && (!batched || (epi->kind != TI_EPI_STORE_F16 && epi->kind != TI_EPI_SILU_MUL_F16) ||
                           (epi->ldo & 127)))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: out_packed needs the batched-rows kernel, a fp16 store / SiLU "
@@ -1963,10 +2015,10 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   if (tile) {
     n_rb = (M + kTileBM - 1) / kTileBM;
     // 64-column workgroups when 128-column ones would leave CUs idle (tile_tpw())
-    tpw = tile_tpw(N, n_rb, query_cus());
+    tpw = tile_tpw(N, K, g32, n_rb, query_cus());
     n_cb = ((N >> 4) + 4 * tpw - 1) / (4 * tpw);
     grid = (n_cb + 7) / 8 * 8 * n_rb;
-    lds = tile_lds_bytes(K, tpw);
+    lds = tile_lds_bytes(K, tpw, g32);
   } else if (rows) {
     rows_on();
     rows_shape(M, &rMB, &rRG);
@@ -2011,7 +2063,11 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   if (chain) chain->signaled = (uint32_t)grid;
   hipStream_t s = (hipStream_t)stream;
   if (tile) {
-    if (tpw == 1) hipLaunchKernelGGL(gemm_tile_kernel<1>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
+    if (g32) {
+      if (tpw == 1) hipLaunchKernelGGL((gemm_tile_kernel<1, true>), dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
+      else if (tpw == 4) hipLaunchKernelGGL((gemm_tile_kernel<4, true>), dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
+      else hipLaunchKernelGGL((gemm_tile_kernel<2, true>), dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
+    } else if (tpw == 1) hipLaunchKernelGGL(gemm_tile_kernel<1>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
     else if (tpw == 4) hipLaunchKernelGGL(gemm_tile_kernel<4>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
     else hipLaunchKernelGGL(gemm_tile_kernel<2>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
     TI_LAUNCH_CHECK("gemm_tile_kernel");
