@@ -17,16 +17,16 @@ T.check(L.ti_event_create(C.byref(a)))
 T.check(L.ti_event_create(C.byref(b)))
 heads, hd, max_seq = 32, 128, 2048
 rng = np.random.RandomState(0)
-kc = T.DeviceBuffer.from_array(rng.standard_normal((heads, max_seq, hd)).astype(np.float16))
-vc = T.DeviceBuffer.from_array(rng.standard_normal((heads, max_seq, hd)).astype(np.float16))
-for M in (256, 512, 1024):
+for kvh, M in [(32, 256), (32, 512), (32, 1024), (8, 512)]:   # 7B MHA; Llama-3-8B GQA 4
+    kc = T.DeviceBuffer.from_array(rng.standard_normal((kvh, max_seq, hd)).astype(np.float16))
+    vc = T.DeviceBuffer.from_array(rng.standard_normal((kvh, max_seq, hd)).astype(np.float16))
     q = T.DeviceBuffer.from_array(rng.standard_normal((M, heads * hd)).astype(np.float32))
     pos = T.DeviceBuffer.from_array(np.arange(M, dtype=np.int32))
     out = T.DeviceBuffer(M * heads * hd * 2)
     ws = T.DeviceBuffer(L.ti_attn_workspace_bytes(M, heads, hd, 4))
     ws.zero()
-    runs = {"prefill": lambda: L.ti_attn_prefill(q.ptr, kc.ptr, vc.ptr, max_seq, pos.ptr, M, heads, heads, hd, out.ptr, None),
-            "decode": lambda: L.ti_attn_decode(q.ptr, kc.ptr, vc.ptr, 0, max_seq, pos.ptr, M, heads, heads, hd, 4, ws.ptr,
+    runs = {"prefill": lambda: L.ti_attn_prefill(q.ptr, kc.ptr, vc.ptr, max_seq, pos.ptr, M, heads, kvh, hd, out.ptr, None),
+            "decode": lambda: L.ti_attn_decode(q.ptr, kc.ptr, vc.ptr, 0, max_seq, pos.ptr, M, heads, kvh, hd, 4, ws.ptr,
                                                out.ptr, None)}
     for name, f in runs.items():
         T.check(f())
@@ -36,4 +36,4 @@ for M in (256, 512, 1024):
         T.check(L.ti_event_record(b, None))
         ms = C.c_float()
         T.check(L.ti_event_elapsed_ms(a, b, C.byref(ms)))
-        print(f"M {M:5d} {name:8s}: {ms.value * 1e3 / 50:8.1f} us per launch", flush=True)
+        print(f"M {M:5d} kv_heads {kvh:2d} {name:8s}: {ms.value * 1e3 / 50:8.1f} us per launch", flush=True)

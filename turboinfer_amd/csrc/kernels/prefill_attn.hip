@@ -6,8 +6,9 @@
 // softmax, o = sum_j p_j v_j; q-head h reads kv-head h / (heads / kv_heads).
 //
 // The decode kernel (attention.hip) gives every row its own workgroups, so a chunk of R rows
-// reads the prefix R times.  Here one wave owns 16 query rows of one head and streams the keys
-// once for them in blocks of 16, with fp32 MFMA (v_mfma_f32_16x16x4_f32: the products and sums
+// reads the prefix R times.  Here one wave owns 16 (row, q-head) columns -- 16 rows of one head,
+// or 16 / G rows of all G heads of a GQA group -- and streams the kv-head's keys once for them in
+// blocks of 16, with fp32 MFMA (v_mfma_f32_16x16x4_f32: the products and sums
 // stay fp32, as in the reference; fp16 K / V convert exactly):
 //   S^T = K Q^T   A = K (lane: key l&15, dims (hd/4)(l>>4) + c), B = Q^T (query l&15, same
 //                 dims), hd/4 steps; D holds S^T[key 4(l>>4)+i][query l&15]
@@ -47,14 +48,17 @@ __device__ __forceinline__ float pf_h(uint32_t w, int hi) {
 template <int HD>
 __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc, int max_seq,
-                                                          const int32_t* __restrict__ pos, int M, int heads, int G,
+                                                          const int32_t* __restrict__ pos, int M, int heads, int gsh,
                                                           float scale, uint16_t* __restrict__ out) {
   constexpr int DG = HD / 4, DV = HD / 16, KW = DG / 8;
   using KRaw = typename PfRaw<HD>::K;
   using VRaw = typename PfRaw<HD>::V;
   const int lane = threadIdx.x, r = lane & 15, g = lane >> 4;
-  const int qb = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, kvh = h / G;
-  const int q0 = qb * 16, qi = min(q0 + r, M - 1);
+  // GQA: the 16 columns are (16 / G) rows x the G q-heads of kv-head blockIdx.y (column c: row
+  // c >> gsh, head c & (G - 1)), so each K / V block serves the whole group
+  const int G = 1 << gsh, qpw = 16 >> gsh;
+  const int qb = gridDim.x - 1 - blockIdx.x, kvh = blockIdx.y;
+  const int q0 = qb * qpw, qi = min(q0 + (r >> gsh), M - 1), h = kvh * G + (r & (G - 1));
   const int p = pos[qi];
   int kmax = p;
 #pragma unroll
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float inv = 1.0f / __shfl(lt, 4 * g + i, 64);
-    const int row = q0 + 4 * g + i;
+    const int col = 4 * g + i, row = q0 + (col >> gsh), hh = kvh * G + (col & (G - 1));
     uint32_t o[DV / 2];
 #pragma unroll
     for (int t = 0; t < DV / 2; ++t) {
@@ -161,7 +165,7 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
       o[t] = lo | ((uint32_t)hi << 16);
     }
     if (row < M) {
-      uint16_t* dst = out + ((size_t)row * heads + h) * HD + r * DV;
+      uint16_t* dst = out + ((size_t)row * heads + hh) * HD + r * DV;
       if constexpr (HD == 128) *(ti::u32x4*)dst = (ti::u32x4){o[0], o[1], o[2], o[3]};
       else *(uint2*)dst = make_uint2(o[0], o[1]);
     }
@@ -174,20 +178,23 @@ extern "C" int ti_attn_prefill(const float* q, const uint16_t* k_cache, const ui
                                const int32_t* pos, int M, int heads, int kv_heads, int head_dim, uint16_t* out,
                                ti_stream_t stream) {
   if (!q || !k_cache || !v_cache || !pos || !out) return ti_set_error(TI_ERR_ARG, "ti_attn_prefill: null pointer");
-  if (M < 1 || heads < 1 || kv_heads < 1 || heads % kv_heads || max_seq < 1 || (M + 15) / 16 > 65535 || heads > 65535)
+  if (M < 1 || heads < 1 || kv_heads < 1 || heads % kv_heads || max_seq < 1 || M > 65535 * 16 || heads > 65535)
     return ti_set_error(TI_ERR_ARG, "ti_attn_prefill: bad sizes M=%d heads=%d kv_heads=%d max_seq=%d", M, heads,
                         kv_heads, max_seq);
   if (head_dim != 64 && head_dim != 128)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_attn_prefill: head_dim %d not in {64,128}", head_dim);
-  const dim3 grid((M + 15) / 16, heads);
+  const int G = heads / kv_heads;
+  if (G & (G - 1) || G > 16) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_attn_prefill: heads / kv_heads %d not a power of 2 <= 16", G);
+  const int gsh = __builtin_ctz(G), qpw = 16 >> gsh;
+  const dim3 grid((M + qpw - 1) / qpw, kv_heads);
   const float scale = 1.0f / sqrtf((float)head_dim);   // tensor_engine.cpp:1288
   hipStream_t s = (hipStream_t)stream;
   if (head_dim == 128)
     hipLaunchKernelGGL(ti::attn_prefill_kernel<128>, grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq, pos, M, heads,
-                       heads / kv_heads, scale, out);
+                       gsh, scale, out);
   else
     hipLaunchKernelGGL(ti::attn_prefill_kernel<64>, grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq, pos, M, heads,
-                       heads / kv_heads, scale, out);
+                       gsh, scale, out);
   TI_LAUNCH_CHECK("attn_prefill_kernel");
   return TI_OK;
 }
