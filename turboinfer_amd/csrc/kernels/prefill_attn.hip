@@ -8,18 +8,19 @@
 // The decode kernel (attention.hip) gives every row its own workgroups, so a chunk of R rows
 // reads the prefix R times.  Here one wave owns 16 (row, q-head) columns -- 16 rows of one head,
 // or 16 / G rows of all G heads of a GQA group -- and streams the kv-head's keys once for them in
-// blocks of 16, with fp32 MFMA (v_mfma_f32_16x16x4_f32: the products and sums
-// stay fp32, as in the reference; fp16 K / V convert exactly):
-//   S^T = K Q^T   A = K (lane: key l&15, dims (hd/4)(l>>4) + c), B = Q^T (query l&15, same
-//                 dims), hd/4 steps; D holds S^T[key 4(l>>4)+i][query l&15]
-//   online softmax per query (column): 4 values per lane, two xor-shuffles across the lane
-//                 groups; masked keys (key > pos[query]) get p = 0
-//   O += P V      the key order inside a block is free, so step j takes keys 4(l>>4)+j: lane
-//                 l's own p[j] is the A operand, and B for output tile t is V[key][dim
-//                 (l&15) hd/16 + t], one 16-byte load per j for all tiles
-// Rows of O are rescaled by each block's alpha (read from the lane that owns that query).
-// Queries are dealt longest-prefix first.  Bounded by the MFMA rate: the longest wave runs
-// (R / 16) blocks x (hd/4 + hd/4) MFMAs.
+// blocks of 16, on fp16 MFMA with the fp32 operand (q, p) split into fp16 hi + lo: two MFMAs
+// give the products and sums to ~fp32 accuracy, as in the reference (K / V are fp16 exactly),
+// in an eighth of the MFMA cycles of v_mfma_f32_16x16x4_f32 (the first version):
+//   S^T = K Q^T   v_mfma_f32_16x16x32_f16, A = K (lane: key l&15, dims 32c + 8(l>>4) + e),
+//                 B = Q^T (column l&15, same dims), hd/32 steps x (hi, lo); D holds
+//                 S^T[key 4(l>>4)+i][column l&15]
+//   online softmax per column: 4 values per lane, two xor-shuffles across the lane groups;
+//                 masked keys (key > pos[row]) get p = 0
+//   O += P V      v_mfma_f32_16x16x16_f16: its A fragment (column l&15, keys 4(l>>4) + e) is
+//                 exactly the lane's own 4 p values (hi, lo); B for output tile t is V[key][dim
+//                 (l&15) hd/16 + t], half t of the lane's four 16-byte V loads (byte permutes)
+// Rows of O are rescaled by each block's alpha (read from the lane that owns that column).
+// Queries are dealt longest-prefix first; a 4-block K / V ring per wave hides the loads.
 #include <math.h>
 
 #include "common.hpp"
@@ -41,8 +42,12 @@ struct PfRaw<64> {
   using V = uint2;      // 4 dims
 };
 
-__device__ __forceinline__ float pf_h(uint32_t w, int hi) {
-  return (float)__builtin_bit_cast(_Float16, (uint16_t)(hi ? (w >> 16) : (w & 0xffffu)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+// fp32 x -> (hi, lo) fp16 with hi + lo = x to ~2^-22 relative
+__device__ __forceinline__ void pf_split(float x, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
 }
 
 template <int HD>
@@ -50,7 +55,7 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
                                                           const uint16_t* __restrict__ vc, int max_seq,
                                                           const int32_t* __restrict__ pos, int M, int heads, int gsh,
                                                           float scale, uint16_t* __restrict__ out) {
-  constexpr int DG = HD / 4, DV = HD / 16, KW = DG / 8;
+  constexpr int DV = HD / 16, KW = HD / 32;   // K: one 32-dim MFMA step per u32x4
   using KRaw = typename PfRaw<HD>::K;
   using VRaw = typename PfRaw<HD>::V;
   const int lane = threadIdx.x, r = lane & 15, g = lane >> 4;
@@ -63,24 +68,29 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
   int kmax = p;
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1) kmax = max(kmax, __shfl_xor(kmax, o, 64));
-  float qv[DG];
+  // B operand of step c: dims 32c + 8g + e of this lane's column, split into fp16 hi + lo
+  f16x8 qh[KW], ql[KW];
   {
-    const float* qr = q + ((size_t)qi * heads + h) * HD + g * DG;
+    const float* qr = q + ((size_t)qi * heads + h) * HD + 8 * g;
 #pragma unroll
-    for (int c = 0; c < DG / 4; ++c) {
-      const float4 t = *(const float4*)(qr + 4 * c);
-      qv[4 * c] = t.x * scale;
-      qv[4 * c + 1] = t.y * scale;
-      qv[4 * c + 2] = t.z * scale;
-      qv[4 * c + 3] = t.w * scale;
+    for (int c = 0; c < KW; ++c) {
+      const float4 t0 = *(const float4*)(qr + 32 * c), t1 = *(const float4*)(qr + 32 * c + 4);
+      const float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 hi, lo;
+        pf_split(v[e] * scale, hi, lo);
+        qh[c][e] = hi;
+        ql[c][e] = lo;
+      }
     }
   }
-  const uint16_t* kb0 = kc + (size_t)kvh * max_seq * HD + g * DG;
+  const uint16_t* kb0 = kc + (size_t)kvh * max_seq * HD + 8 * g;
   const uint16_t* vb0 = vc + (size_t)kvh * max_seq * HD + r * DV;
   auto load = [&](int kb, KRaw& k, VRaw (&v)[4]) {
     const int kk = min(kb * 16 + r, max_seq - 1);
 #pragma unroll
-    for (int c = 0; c < KW; ++c) k[c] = *(const u32x4*)(kb0 + (size_t)kk * HD + 8 * c);
+    for (int c = 0; c < KW; ++c) k[c] = *(const u32x4*)(kb0 + (size_t)kk * HD + 32 * c);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int kv = kb * 16 + 4 * g + j;
@@ -107,9 +117,10 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
       if (kb >= nkb) break;
       f32x4 s = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int c = 0; c < DG; ++c) {
-        const uint32_t w = kr[u][c >> 3][(c >> 1) & 3];
-        s = __builtin_amdgcn_mfma_f32_16x16x4f32(pf_h(w, c & 1), qv[c], s, 0, 0, 0);
+      for (int c = 0; c < KW; ++c) {
+        const f16x8 kf = __builtin_bit_cast(f16x8, kr[u][c]);
+        s = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[c], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[c], s, 0, 0, 0);
       }
       float pv[4], bm = -INFINITY;
 #pragma unroll
@@ -136,17 +147,31 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
 #pragma unroll
         for (int t = 0; t < DV; ++t) acc[t][i] *= ar;
       }
+      f16x4 ph, pl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        _Float16 hi, lo;
+        pf_split(pv[e], hi, lo);
+        ph[e] = hi;
+        pl[e] = lo;
+      }
+      uint32_t vw[4][DV / 2];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        uint32_t vw[DV / 2];
         if constexpr (HD == 128) {
-          vw[0] = vr[u][j][0]; vw[1] = vr[u][j][1]; vw[2] = vr[u][j][2]; vw[3] = vr[u][j][3];
+          vw[j][0] = vr[u][j][0]; vw[j][1] = vr[u][j][1]; vw[j][2] = vr[u][j][2]; vw[j][3] = vr[u][j][3];
         } else {
-          vw[0] = vr[u][j].x; vw[1] = vr[u][j].y;
+          vw[j][0] = vr[u][j].x; vw[j][1] = vr[u][j].y;
         }
+      }
 #pragma unroll
-        for (int t = 0; t < DV; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(pv[j], pf_h(vw[t >> 1], t & 1), acc[t], 0, 0, 0);
+      for (int t = 0; t < DV; ++t) {
+        const uint32_t sel = (t & 1) ? 0x07060302u : 0x05040100u;
+        const uint32_t b01 = __builtin_amdgcn_perm(vw[1][t >> 1], vw[0][t >> 1], sel);
+        const uint32_t b23 = __builtin_amdgcn_perm(vw[3][t >> 1], vw[2][t >> 1], sel);
+        const f16x4 bf = __builtin_bit_cast(f16x4, ((unsigned long long)b23 << 32) | b01);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(ph, bf, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(pl, bf, acc[t], 0, 0, 0);
       }
       if (kb + kPfRing < nkb) load(kb + kPfRing, kr[u], vr[u]);
     }
