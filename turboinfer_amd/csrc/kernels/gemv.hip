@@ -1412,9 +1412,10 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
 // 32 v_mfma_f32_16x16x32_f16, then the fp32 group-scale FMA.  The workgroup grid is ordered so
 // that the row blocks sharing a column block run on one XCD (blockIdx % 8), where its L2
 // serves their common weight stream.
-constexpr int kTileBM = 128;   // rows per workgroup
-__host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false) {
-  return 2 * kTileBM * 256 + align16(4 * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
+// WMR: row-waves per workgroup (2: 128 rows x 4 column-waves; 1: 64 rows x 8 column-waves, half
+// the activation block and no weight tile loaded twice)
+__host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, int wmr = 2) {
+  return 2 * 64 * wmr * 256 + align16((8 / wmr) * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
 }
 
 // TPW: weight tiles per wave (2: 128 columns per workgroup; 1: 64 columns, twice the workgroups
@@ -1422,32 +1423,33 @@ __host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false) 
 // 4: 256 columns, half the activation bytes per MFMA, when the rows give enough workgroups).
 // G32: group-32 int4 tiles (TI_BITS_G32): MFMA step s4 of a group reads k-chunk 4 s4 + kq and
 // carries its own scale (one per 32-k block), so each step's product is scaled separately.
-template <int TPW, bool G32 = false>
+template <int TPW, bool G32 = false, int WMR = 2>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb) {
+  constexpr int WCOL = kGemvWaves / WMR, BM = 64 * WMR;   // column-waves, rows per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KT = a.K >> 7, NT = a.N >> 4;
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, kq = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wave >> 2, wn = wave & 3;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wave / WCOL, wn = wave % WCOL;
   // blockIdx -> (row block, column block): the n_rb row blocks of a column block share an XCD
   const int b8 = blockIdx.x & 7, rest = blockIdx.x >> 3;
   const int rb = rest % n_rb, cb = (rest / n_rb) * 8 + b8;
   if (cb >= n_cb) return;
-  const int m0 = rb * kTileBM, t0 = cb * 4 * TPW;
-  f16* xb = (f16*)smem;                                       // [2][128 rows][128 k] swizzled
+  const int m0 = rb * BM, t0 = cb * WCOL * TPW;
+  f16* xb = (f16*)smem;                                       // [2][BM rows][128 k] swizzled
   constexpr int SG = G32 ? 4 : 1;                             // scales per tile row and group
-  uint16_t* sl = (uint16_t*)(smem + 2 * kTileBM * 256);       // [4 TPW tiles][KT][SG][16]
-  const int n_sc = 4 * TPW * KT * 2 * SG;                     // 16-byte pieces
+  uint16_t* sl = (uint16_t*)(smem + 2 * BM * 256);            // [WCOL TPW tiles][KT][SG][16]
+  const int n_sc = WCOL * TPW * KT * 2 * SG;                  // 16-byte pieces
   const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16 * SG);
-  const int ntile_ok = min(4 * TPW, NT - t0);
+  const int ntile_ok = min(WCOL * TPW, NT - t0);
   for (int i = tid; i < n_sc; i += kGemvThreads)
     ((u32x4*)sl)[i] = i < ntile_ok * KT * 2 * SG ? ld_w(sg + i) : (u32x4){0u, 0u, 0u, 0u};
 
   const f16* xg = (const f16*)a.x;
-  auto issue_x = [&](int kg) __attribute__((always_inline)) {   // 32 DMA instructions per group, 4 per wave
-    f16* dst = xb + (kg & 1) * kTileBM * 128;
+  auto issue_x = [&](int kg) __attribute__((always_inline)) {   // BM / 4 DMA instructions per group
+    f16* dst = xb + (kg & 1) * BM * 128;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = wave * 4 + q, row = 4 * j + (lane >> 4), p = lane & 15, c = p ^ (row & 15);
+    for (int q = 0; q < 2 * WMR; ++q) {
+      const int j = wave * 2 * WMR + q, row = 4 * j + (lane >> 4), p = lane & 15, c = p ^ (row & 15);
       const int m = min(m0 + row, a.M - 1);
       dma_1k(xg + (size_t)m * a.ldx + kg * 128 + c * 8, dst + j * 512);
     }
@@ -1472,7 +1474,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   uint32_t magic;
   asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
   auto compute = [&](const u32x4 (&w)[TPW], int kg) __attribute__((always_inline)) {
-    const f16* xr = xb + (kg & 1) * kTileBM * 128 + (wm * 64 + r) * 128;
+    const f16* xr = xb + (kg & 1) * BM * 128 + (wm * 64 + r) * 128;
     f16x8 xf[4][4];
 #pragma unroll
     for (int b = 0; b < 4; ++b)
@@ -1573,27 +1575,48 @@ __host__ inline bool tile_narrow_on() {
   return g_tile_narrow != 0;
 }
 
-// Weight tiles per wave of the tile kernel, by a per-CU byte model: a CU streams a bounded
-// number of bytes per microsecond, a workgroup moves 32 KiB of activations plus
-// 2 x 4 TPW KiB of weights per 128-k group (the two row-waves of a column read the same tiles),
-// and the launch takes ceil(workgroups / CUs) rounds: cost(TPW) = rounds x (32 + 8 TPW).  The
-// cheapest of TPW 2, 1 (TI_TILE_NARROW, default on), 4 (TI_TILE_WIDE, default on) wins.
-__host__ inline int tile_tpw(int N, int K, bool g32, int n_rb, int cus) {
-  static int wide = -1;
+// Tile kernel shape by a per-CU byte model: a CU streams a bounded number of bytes per
+// microsecond, a workgroup moves its activation block plus its weight tiles per
+// 128-k group, and the launch takes ceil(workgroups / CUs) rounds; the cheapest shape wins
+// (TI_TILE_NARROW / TI_TILE_WIDE / TI_TILE_WMR1 drop TPW 1 / TPW 4 / 64-row shapes, A/B knobs).
+#define TI_TILE_FNS                                                                                          \
+  (const void*)gemm_tile_kernel<1, false, 2>, (const void*)gemm_tile_kernel<2, false, 2>,                    \
+      (const void*)gemm_tile_kernel<4, false, 2>, (const void*)gemm_tile_kernel<1, true, 2>,                 \
+      (const void*)gemm_tile_kernel<2, true, 2>, (const void*)gemm_tile_kernel<4, true, 2>,                  \
+      (const void*)gemm_tile_kernel<1, false, 1>, (const void*)gemm_tile_kernel<2, false, 1>,                \
+      (const void*)gemm_tile_kernel<4, false, 1>, (const void*)gemm_tile_kernel<1, true, 1>,                 \
+      (const void*)gemm_tile_kernel<2, true, 1>, (const void*)gemm_tile_kernel<4, true, 1>
+__host__ inline const void* tile_fn(int tpw, bool g32, int wmr) {
+  static const void* const fns[] = {TI_TILE_FNS};
+  return fns[(wmr == 1 ? 6 : 0) + (g32 ? 3 : 0) + (tpw == 1 ? 0 : tpw == 2 ? 1 : 2)];
+}
+
+// Shapes considered: (row-waves WMR, tiles per wave TPW); a workgroup moves 16 WMR KiB of
+// activations and WMR x (8 / WMR) TPW KiB of weights per group.  TI_TILE_WMR1=0 keeps 128-row
+// workgroups (A/B knob).  Returns 8 * WMR + TPW.
+__host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
+  static int wide = -1, wmr1 = -1;
   if (wide < 0) {
     const char* e = getenv("TI_TILE_WIDE");
     wide = e ? atoi(e) != 0 : 1;
+    const char* f = getenv("TI_TILE_WMR1");
+    wmr1 = f ? atoi(f) != 0 : 1;
   }
   const int NT = N >> 4;
-  int best = 2;
+  int best = 8 * 2 + 2;
   long best_cost = -1;
-  for (int tpw : {2, 1, 4}) {
-    if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && !wide) || tile_lds_bytes(K, tpw, g32) > 160 * 1024) continue;
-    const long wgs = (long)(NT + 4 * tpw - 1) / (4 * tpw) * n_rb;
-    const long cost = (wgs + cus - 1) / cus * (32 + 8 * tpw);
-    if (best_cost < 0 || cost < best_cost) {
-      best = tpw;
-      best_cost = cost;
+  for (int wmr : {2, 1}) {
+    if (wmr == 1 && !wmr1) continue;
+    for (int tpw : {2, 1, 4}) {
+      if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && !wide) || tile_lds_bytes(K, tpw, g32, wmr) > 160 * 1024)
+        continue;
+      const int cols = (8 / wmr) * tpw;
+      const long wgs = (long)(NT + cols - 1) / cols * ((M + 64 * wmr - 1) / (64 * wmr));
+      const long cost = (wgs + cus - 1) / cus * (16 * wmr + 8 * tpw);
+      if (best_cost < 0 || cost < best_cost) {
+        best = 8 * wmr + tpw;
+        best_cost = cost;
+      }
     }
   }
   return best;
@@ -1839,8 +1862,7 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<4, XM_F16F>, (const void*)gemv_wq_kernel<8, XM_F16F>,
       (const void*)gemv_wq_kernel<16, XM_F16F>, (const void*)gemv_wq_kernel<4, XM_ATTN>,
       (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS, TI_ROWS_FNS,
-      (const void*)gemm_tile_kernel<4>, (const void*)gemm_tile_kernel<2>, (const void*)gemm_tile_kernel<1>,
-      (const void*)gemm_tile_kernel<4, true>, (const void*)gemm_tile_kernel<2, true>, (const void*)gemm_tile_kernel<1, true>};
+      TI_TILE_FNS};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
@@ -2011,14 +2033,15 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   int grid = 0, lds = 0, ntl = 0, rMB = 0, rRG = 0;
   const bool tile = batched && x_kind == TI_X_F16 && M >= tile_rows();
   const bool rows = !tile && batched && (packed_x || M > 32 || (M > 16 && rows_on()));
-  int n_cb = 0, n_rb = 0, tpw = 2;
+  int n_cb = 0, n_rb = 0, tpw = 2, wmr = 2;
   if (tile) {
-    n_rb = (M + kTileBM - 1) / kTileBM;
-    // 64-column workgroups when 128-column ones would leave CUs idle (tile_tpw())
-    tpw = tile_tpw(N, K, g32, n_rb, query_cus());
-    n_cb = ((N >> 4) + 4 * tpw - 1) / (4 * tpw);
+    const int shape = tile_shape(M, N, K, g32, query_cus());   // the byte model (tile_shape)
+    wmr = shape >> 3;
+    tpw = shape & 7;
+    n_rb = (M + 64 * wmr - 1) / (64 * wmr);
+    n_cb = ((N >> 4) + (8 / wmr) * tpw - 1) / ((8 / wmr) * tpw);
     grid = (n_cb + 7) / 8 * 8 * n_rb;
-    lds = tile_lds_bytes(K, tpw, g32);
+    lds = tile_lds_bytes(K, tpw, g32, wmr);
   } else if (rows) {
     rows_on();
     rows_shape(M, &rMB, &rRG);
@@ -2063,13 +2086,9 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   if (chain) chain->signaled = (uint32_t)grid;
   hipStream_t s = (hipStream_t)stream;
   if (tile) {
-    if (g32) {
-      if (tpw == 1) hipLaunchKernelGGL((gemm_tile_kernel<1, true>), dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
-      else if (tpw == 4) hipLaunchKernelGGL((gemm_tile_kernel<4, true>), dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
-      else hipLaunchKernelGGL((gemm_tile_kernel<2, true>), dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
-    } else if (tpw == 1) hipLaunchKernelGGL(gemm_tile_kernel<1>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
-    else if (tpw == 4) hipLaunchKernelGGL(gemm_tile_kernel<4>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
-    else hipLaunchKernelGGL(gemm_tile_kernel<2>, dim3(grid), dim3(kGemvThreads), lds, s, a, n_cb, n_rb);
+    const void* f = tile_fn(tpw, g32, wmr);
+    void* args[] = {&a, &n_cb, &n_rb};
+    TI_HIP_CHECK(hipLaunchKernel(f, dim3(grid), dim3(kGemvThreads), args, lds, s), "hipLaunchKernel(gemm_tile_kernel)");
     TI_LAUNCH_CHECK("gemm_tile_kernel");
     return TI_OK;
   }
