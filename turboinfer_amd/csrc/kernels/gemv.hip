@@ -1454,6 +1454,22 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
       dma_1k(xg + (size_t)m * a.ldx + kg * 128 + c * 8, dst + j * 512);
     }
   };
+#ifndef TI_TILE_XREG
+#define TI_TILE_XREG 0   // 1: the activation block through VGPRs + ds_write instead of LDS-DMA
+#endif
+  u32x4 xreg[2 * WMR];
+  auto load_xr = [&](int kg) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 2 * WMR; ++q) {
+      const int j = wave * 2 * WMR + q, row = 4 * j + (lane >> 4), c = (lane & 15) ^ (row & 15);
+      xreg[q] = *(const u32x4*)(xg + (size_t)min(m0 + row, a.M - 1) * a.ldx + kg * 128 + c * 8);
+    }
+  };
+  auto store_xr = [&](int kg) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 2 * WMR; ++q)
+      *(u32x4*)(xb + (kg & 1) * BM * 128 + (wave * 2 * WMR + q) * 512 + lane * 8) = xreg[q];
+  };
   const u32x4* tb = a.tiles + lane;
   auto load_w = [&](u32x4 (&w)[TPW], int kg) __attribute__((always_inline)) {
     kg = min(kg, KT - 1);
@@ -1463,7 +1479,8 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   // weight ring: 4 groups deep (2 at TPW 4, whose 4-deep ring hipcc keeps in scratch)
   constexpr int kTileWR = TPW == 4 ? 2 : 4;
   u32x4 W[kTileWR][TPW];
-  issue_x(0);
+  if constexpr (TI_TILE_XREG) load_xr(0);
+  else issue_x(0);
 #pragma unroll
   for (int u = 0; u < kTileWR - 1; ++u) load_w(W[u], u);
   f32x4 acc[TPW][4];
@@ -1530,10 +1547,16 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
       const int kg = k0 + u;
       // x(kg) landed (the loads younger than it: W(kg + WR - 2), TPW instructions) and every
       // wave is past compute(kg - 1), so buffer (kg + 1) & 1 is free
+      if constexpr (TI_TILE_XREG) {
+        if (kg < KT) store_xr(kg);
+      }
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TPW) : "memory");
       lds_barrier();
       if (kg < KT) {
-        if (kg + 1 < KT) issue_x(kg + 1);
+        if (kg + 1 < KT) {
+          if constexpr (TI_TILE_XREG) load_xr(kg + 1);
+          else issue_x(kg + 1);
+        }
         load_w(W[(u + kTileWR - 1) % kTileWR], kg + kTileWR - 1);
         compute(W[u], kg);
       }
