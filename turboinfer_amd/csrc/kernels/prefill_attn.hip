@@ -50,6 +50,10 @@ __device__ __forceinline__ void pf_split(float x, _Float16& hi, _Float16& lo) {
   lo = (_Float16)(x - (float)hi);
 }
 
+#ifndef TI_PF_RING
+#define TI_PF_RING 3   // K / V blocks in flight per wave (3: 248 VGPRs, two waves per SIMD)
+#endif
+
 template <int HD>
 __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc, int max_seq,
@@ -105,7 +109,7 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
   const int nkb = kmax / 16 + 1;
   // K / V blocks in flight: a ring of kPfRing blocks, each slot refilled right after its block
   // is consumed (one wave per SIMD: the ring, not other waves, hides the load latency)
-  constexpr int kPfRing = 4;
+  constexpr int kPfRing = TI_PF_RING;
   KRaw kr[kPfRing];
   VRaw vr[kPfRing][4];
 #pragma unroll
