@@ -108,7 +108,7 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
   float m_run = -INFINITY, l_run = 0.0f;
   const int nkb = kmax / 16 + 1;
   // K / V blocks in flight: a ring of kPfRing blocks, each slot refilled right after its block
-  // is consumed (one wave per SIMD: the ring, not other waves, hides the load latency)
+  // is consumed (one or two waves per SIMD: the ring, not other waves, hides the load latency)
   constexpr int kPfRing = TI_PF_RING;
   KRaw kr[kPfRing];
   VRaw vr[kPfRing][4];
