@@ -305,8 +305,9 @@ int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, const uint1
  * multi_head_attention, tensor_engine.cpp:1149-1252): the M rows are tokens of ONE stream whose
  * cache k_cache / v_cache [kv_heads][max_seq][head_dim] fp16 already holds their K / V; row m
  * attends to keys [0, pos[m]] (0 <= pos[m] < max_seq), q [M][heads*head_dim] fp32 ->
- * out [M][heads*head_dim] fp16.  One wave per 16 rows and head streams each key once for them
- * on fp32 MFMA (ti_attn_decode reads the prefix once per row).  head_dim 64 or 128;
+ * out [M][heads*head_dim] fp16.  One wave per 16 (row, q-head) columns streams each key once for
+ * them on fp16 MFMA with the fp32 operands split into fp16 hi + lo parts (fp32-accurate products;
+ * ti_attn_decode reads the prefix once per row).  head_dim 64 or 128;
  * heads % kv_heads == 0.  Replaces ti_attn_decode(kv_stream_stride = 0) for row-major chunks. */
 int ti_attn_prefill(const float* q, const uint16_t* k_cache, const uint16_t* v_cache, int max_seq,
                     const int32_t* pos, int M, int heads, int kv_heads, int head_dim, uint16_t* out,

@@ -11,7 +11,8 @@
 // throw std::runtime_error when no MI355X is visible; kCPU throws (the CPU path is the
 // reference itself -- there is no CPU fallback here).  Operations outside the decode hot
 // path (batch_matmul, gelu, layer_norm, concatenate, split, transpose, permute, add_bias,
-// scale, masked/prefill attention) throw std::runtime_error naming SURVEY.md 8(f).
+// scale) throw std::runtime_error naming SURVEY.md 8(f).  attention / multi_head_attention take
+// any query length and an optional float mask (the reference's sequence, on the device).
 #pragma once
 
 #include <cstddef>
@@ -51,7 +52,8 @@ class TensorEngine {
   Tensor silu(const Tensor& input);
   /// Row softmax over the last dimension with temperature.
   Tensor softmax(const Tensor& input, float temperature = 1.0f);
-  /// Single-query attention: query [B,1,D], key/value [B,S,D] (mask unsupported).
+  /// Attention: query [B,Sq,D], key/value [B,S,D], optional float mask added to the scores
+  /// (Sq == 1 without a mask is attention_fast_incremental).
   Tensor attention(const Tensor& query, const Tensor& key, const Tensor& value, const Tensor* mask = nullptr);
   Tensor attention_fast_incremental(const Tensor& query, const Tensor& key, const Tensor& value,
                                     const Tensor* mask = nullptr);

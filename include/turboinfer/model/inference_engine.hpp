@@ -13,7 +13,8 @@
 // fp16 KV cache in HBM, the whole decode step captured in a hipGraph.  Greedy requests
 // (top_k == 1) run their token loop on the device; other sampling settings and logprobs
 // take the logits to the host each step unless the device sampler runs them.  Prompts are
-// prefilled in chunks of up to 256 rows through the batched GEMM.
+// prefilled in chunks of up to 1024 rows through the tile GEMM and the MFMA causal attention
+// (DESIGN 4.6).
 //
 // Binary layout: InferenceConfig carries two trailing fields (weight_bits, gpu_index) that the
 // reference's struct does not have, so this header is a source drop-in, not a layout drop-in:

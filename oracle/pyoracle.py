@@ -95,6 +95,12 @@ class Oracle:
         L.or_beam_search.restype = C.c_int
         L.or_plumbing_forward_rows.argtypes = [SZ, SZ, SZ, SZ, _f32p]
         L.or_plumbing_forward_rows.restype = None
+        L.or_qmodel_synth.argtypes = [C.POINTER(ModelConfig), C.c_uint64, C.c_float]
+        L.or_qmodel_synth.restype = C.c_void_p
+        L.or_qmodel_free.argtypes = [C.c_void_p]
+        L.or_qmodel_fill_kv.argtypes = [C.c_void_p, C.c_int, C.c_uint64]
+        L.or_qmodel_step.argtypes = [C.c_void_p, C.c_int, _f32p]
+        L.or_qmodel_step.restype = C.c_int
         L.or_half_to_float.argtypes = [C.c_uint16]
         L.or_half_to_float.restype = C.c_float
         L.or_float_to_half.argtypes = [C.c_float]
@@ -316,6 +322,37 @@ class OracleModel:
     def close(self):
         if self.ptr:
             self.o.lib.or_model_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.close()
+
+
+class OracleDeepModel:
+    """The same synthetic model at full depth (ti_oracle_deep.c): weights kept as group-quantized
+    int8 + scales, steps bit-identical to OracleModel.step(kv_round_f16=True), multi-threaded."""
+
+    def __init__(self, oracle: Oracle, cfg: dict, seed: int, norm_jitter: float = 0.0):
+        self.o = oracle
+        self.cfg = cfg
+        c = ModelConfig(**cfg)
+        self.ptr = oracle.lib.or_qmodel_synth(C.byref(c), seed, norm_jitter)
+        if not self.ptr:
+            raise ValueError("or_qmodel_synth: bits must be 4 or 8")
+
+    def fill_kv(self, n, seed):
+        self.o.lib.or_qmodel_fill_kv(self.ptr, n, seed)
+
+    def step(self, token):
+        logits = np.empty(self.cfg["vocab"], np.float32)
+        t = self.o.lib.or_qmodel_step(self.ptr, int(token), logits)
+        if t < 0:
+            raise RuntimeError("or_qmodel_step: cache full")
+        return t, logits
+
+    def close(self):
+        if self.ptr:
+            self.o.lib.or_qmodel_free(self.ptr)
             self.ptr = None
 
     def __del__(self):

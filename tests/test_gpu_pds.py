@@ -69,3 +69,30 @@ def test_pds_long_context_replay(ti):
             assert e.pds_error() == 0
         e.close()
     assert np.array_equal(toks[True], toks[False])
+
+
+def test_pds_timeout_is_fatal(ti, monkeypatch):
+    """A hand-off wait that timed out (error word forced, TI_PDS_FORCE_ERR) must not hand back
+    tokens: generate / step raise, the engine turns persistent decode off and resets the
+    hand-off state, and the next call runs on the per-layer graph with correct results."""
+    v, h, l, nh, nkv, hd, inter = CFGS["l2_shape"]
+    ref = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=4, max_seq=256, max_batch=1, attn_splits=8)
+    ref.synth(0x7157, 0.1)
+    want = np.asarray(ref.generate([[1, 2, 3]], 6))
+    ref.close()
+    e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=4, max_seq=256, max_batch=1, attn_splits=8)
+    e.synth(0x7157, 0.1)
+    monkeypatch.setenv("TI_PDS_FORCE_ERR", "1")
+    assert e.set_pds(True) is True
+    monkeypatch.delenv("TI_PDS_FORCE_ERR")
+    with pytest.raises(ti.TiError, match="persistent decode"):
+        e.generate([[1, 2, 3]], 6)
+    assert e.set_pds(None) is False          # turned off by the failure
+    assert e.pds_error() == 0                # state reset
+    assert np.array_equal(np.asarray(e.generate([[1, 2, 3]], 6)), want)
+    monkeypatch.setenv("TI_PDS_FORCE_ERR", "1")
+    assert e.set_pds(True) is True
+    monkeypatch.delenv("TI_PDS_FORCE_ERR")
+    with pytest.raises(ti.TiError, match="persistent decode"):
+        e.step([5], [0])
+    e.close()

@@ -204,6 +204,25 @@ struct ti_engine {
 
 namespace {
 
+// Every ti_engine_* entry binds the engine's device for its duration and restores the caller's
+// current device on return (lazy allocations, graph (re)instantiation and launches all run on
+// e->c.device whatever device the calling thread has current): several engines on several
+// devices can be driven from one process, from any host thread (the reference
+// binds its device in TensorEngine::initialize, tensor_engine.cpp:425-487).
+struct DeviceScope {
+  int prev = -1;
+  bool changed = false;
+  explicit DeviceScope(int device) {
+    if (device >= 0 && hipGetDevice(&prev) == hipSuccess && prev != device) changed = hipSetDevice(device) == hipSuccess;
+  }
+  explicit DeviceScope(const ti_engine* e) : DeviceScope(e ? e->c.device : -1) {}
+  ~DeviceScope() {
+    if (changed) hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
 int validate(const ti_engine_config& c) {
   if (c.vocab < 1 || c.hidden < 1 || c.layers < 0 || c.inter < 1 || c.max_seq < 1 || c.max_batch < 1)
     return ti_set_error(TI_ERR_ARG, "ti_engine_create: non-positive size in config");
@@ -386,13 +405,35 @@ int enqueue_step_chained(ti_engine* e, int advance, bool first) {
 
 // After a synchronisation: fail (and re-arm) if any chained wait timed out.
 int chain_check(ti_engine* e) {
-  if (!e->chain_abort) return TI_OK;
-  uint32_t ab = 0;
-  TI_TRY(ti_memcpy_d2h(&ab, e->chain_abort, 4, e->s));
-  if (ab) {
-    TI_TRY(ti_memset(e->chain_abort, 0, 4, e->s));
-    TI_TRY(ti_stream_sync(e->s));
-    return ti_set_error(TI_ERR_HIP, "engine: a chained launch's in-kernel wait timed out (results invalid)");
+  if (e->chain_abort) {
+    uint32_t ab = 0;
+    TI_TRY(ti_memcpy_d2h(&ab, e->chain_abort, 4, e->s));
+    if (ab) {
+      TI_TRY(ti_memset(e->chain_abort, 0, 4, e->s));
+      TI_TRY(ti_stream_sync(e->s));
+      return ti_set_error(TI_ERR_HIP, "engine: a chained launch's in-kernel wait timed out (results invalid)");
+    }
+  }
+  // The persistent decode launch (pds.hip) bounds every hand-off wait: a wait that times out sets
+  // pds_err and the launch (and any later one) finishes without waiting, so its outputs are
+  // invalid.  Fatal here: the caller gets an error instead of tokens, the engine drops back to
+  // the per-layer graph (pds off, step graphs re-captured) and the hand-off state is reset.
+  if (e->pds_on && e->pds_err) {
+    uint32_t err = 0;
+    TI_TRY(ti_memcpy_d2h(&err, e->pds_err, 4, e->s));
+    if (err) {
+      e->pds_on = false;
+      for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
+      e->graphs.clear();
+      TI_TRY(ti_memset(e->pds_err, 0, 4, e->s));
+      TI_TRY(ti_memset(e->pds_ctr, 0, (size_t)e->c.layers * TI_PDS_CTR_WORDS_PER_LAYER * 4, e->s));
+      TI_TRY(ti_memset(e->pds_launches, 0, 256 * 4, e->s));
+      TI_TRY(ti_stream_sync(e->s));
+      return ti_set_error(TI_ERR_HIP,
+                          "engine: a persistent decode hand-off wait timed out (err 0x%x); results of this call are "
+                          "invalid, persistent decode is now off for this engine",
+                          err);
+    }
   }
   return TI_OK;
 }
@@ -621,6 +662,19 @@ int enqueue_step(ti_engine* e, int M, int advance) {
 // appends at its own position and attends to [0, base + t0 + j], causal).  No lm_head: the
 // decode loop takes over at the last prompt token.  Not graph-captured (host position upload).
 // TI_ATTN_PREFILL=0: prefill chunks through the decode attention kernel (A/B knob)
+static bool prefill_attn_on();
+
+// Decode-attention workspace: the largest need over the row counts that run the split kernel --
+// decode batches up to max_batch and prompt chunks of up to 64 rows (ti_gemm_packed_rows; longer
+// chunks run ti_attn_prefill, no workspace), all chunk sizes when TI_ATTN_PREFILL=0.
+size_t ws_bytes(const ti_engine* e) {
+  const ti_engine_config& c = e->c;
+  const int R = prefill_attn_on() ? std::min(e->rows_cap, std::max(c.max_batch, 64)) : e->rows_cap;
+  size_t b = 0;
+  for (int M = 1; M <= R; ++M) b = std::max(b, ti_attn_workspace_bytes(M, c.heads, c.head_dim, e->splits_for(M)));
+  return b;
+}
+
 static bool prefill_attn_on() {
   static const int on = [] {
     const char* v = getenv("TI_ATTN_PREFILL");
@@ -763,6 +817,7 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
   if (!cfg || !out) return ti_set_error(TI_ERR_ARG, "ti_engine_create: null");
   *out = nullptr;
   TI_TRY(validate(*cfg));
+  DeviceScope bind_(cfg->device);   // restores the caller's device after ti_init's hipSetDevice
   TI_TRY(ti_init(cfg->device));
   ti_engine* e = new ti_engine();
   e->c = *cfg;
@@ -807,7 +862,7 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     const int Rp = (R + 15) / 16 * 16;   // packed operands hold whole 16-row blocks
     if ((rc = e->alloc_t(&e->q, (size_t)R * qd)) || (rc = e->alloc_t(&e->attn, (size_t)Rp * qd)) ||
         (rc = e->alloc_t(&e->act, (size_t)Rp * I)) || (rc = e->alloc_t(&e->xn, (size_t)Rp * std::max(H, I))) ||
-        (rc = e->alloc(reinterpret_cast<void**>(&e->ws), ti_attn_workspace_bytes(R, c.heads, hd, e->splits_max))) ||
+        (rc = e->alloc(reinterpret_cast<void**>(&e->ws), ws_bytes(e))) ||
         (rc = e->alloc_t(&e->pf_ones, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->pf_zero, (size_t)1)) ||
         (rc = e->alloc_t(&e->pf_base, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->fx, (size_t)H)) ||
         (rc = e->alloc_t(&e->ss, (size_t)256)) ||
@@ -869,6 +924,7 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
 
 int ti_engine_destroy(ti_engine* e) {
   if (e) {
+    DeviceScope bind_(e);
     hipStreamSynchronize(e->s);
     delete e;
   }
@@ -877,12 +933,14 @@ int ti_engine_destroy(ti_engine* e) {
 
 int ti_engine_get_stream(ti_engine* e, void** stream) {
   if (!e || !stream) return ti_set_error(TI_ERR_ARG, "ti_engine_get_stream: null");
+  DeviceScope bind_(e);
   *stream = (void*)e->s;
   return TI_OK;
 }
 
 int ti_engine_memory(ti_engine* e, size_t* wb, size_t* kb) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_memory: null");
+  DeviceScope bind_(e);
   if (wb) *wb = e->weight_bytes;
   if (kb) *kb = e->kv_bytes;
   return TI_OK;
@@ -890,6 +948,7 @@ int ti_engine_memory(ti_engine* e, size_t* wb, size_t* kb) {
 
 int ti_engine_set_tensor(ti_engine* e, int slot, int layer, const float* data, int scale_mode) {
   if (!e || !data) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor: null");
+  DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
   const int H = c.hidden, I = c.inter, V = c.vocab;
   const bool per_layer = slot <= TI_W_DOWN || slot == TI_V_ATTN_NORM || slot == TI_V_FFN_NORM;
@@ -949,6 +1008,7 @@ int ti_engine_set_tensor(ti_engine* e, int slot, int layer, const float* data, i
 // d [K/32][N_src], packed without re-quantization (ti_wpack_q_host).
 int ti_engine_set_tensor_q(ti_engine* e, int slot, int layer, const int8_t* q, const uint16_t* d) {
   if (!e || !q || !d) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q: null");
+  DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
   if (!(c.bits & TI_BITS_G32)) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q: engine bits %d lack TI_BITS_G32", c.bits);
   if (layer < 0 || (slot <= TI_W_DOWN && layer >= c.layers)) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q: layer %d", layer);
@@ -979,6 +1039,7 @@ int ti_engine_set_tensor_q(ti_engine* e, int slot, int layer, const int8_t* q, c
 
 int ti_engine_synth(ti_engine* e, uint64_t seed, float norm_jitter) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_synth: null");
+  DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
   if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_synth: compat engines take the reference model");
   if (c.bits & TI_BITS_G32)
@@ -1005,6 +1066,7 @@ int ti_engine_synth(ti_engine* e, uint64_t seed, float norm_jitter) {
 
 int ti_engine_fill_kv(ti_engine* e, int stream, int n, uint64_t seed) {
   if (!e || e->c.compat) return ti_set_error(TI_ERR_ARG, "ti_engine_fill_kv: no KV cache");
+  DeviceScope bind_(e);
   if (stream < 0 || stream >= e->c.max_batch || n < 0 || n > e->c.max_seq)
     return ti_set_error(TI_ERR_ARG, "ti_engine_fill_kv: stream %d n %d", stream, n);
   for (int l = 0; l < e->c.layers; ++l) {
@@ -1020,6 +1082,7 @@ int ti_engine_fill_kv(ti_engine* e, int stream, int n, uint64_t seed) {
 int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_t* lens, int stride,
                        const int32_t* start_pos, int max_new, int32_t* out_tokens, float* last_logits) {
   if (!e || !prompts || !lens || !out_tokens) return ti_set_error(TI_ERR_ARG, "ti_engine_generate: null");
+  DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
   if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_generate: use ti_engine_compat_step for compat engines");
   if (n < 1 || n > c.max_batch || max_new < 1) return ti_set_error(TI_ERR_ARG, "ti_engine_generate: n=%d max_new=%d", n, max_new);
@@ -1076,6 +1139,7 @@ int ti_engine_generate_sampled(ti_engine* e, int n, const int32_t* prompts, cons
                                const int32_t* start_pos, int max_new, float temperature, int top_k, float top_p,
                                const float* draws, int32_t* out_tokens, float* out_logprobs) {
   if (!e || !draws) return ti_set_error(TI_ERR_ARG, "ti_engine_generate_sampled: null");
+  DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
   if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_generate_sampled: compat engine");
   if (n < 1 || n > c.max_batch || max_new < 1) return ti_set_error(TI_ERR_ARG, "ti_engine_generate_sampled: n=%d max_new=%d", n, max_new);
@@ -1205,16 +1269,18 @@ int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int len, int max_
                           float* out_log_prob, float* out_score, int32_t* out_finished, int* out_count) {
   if (!e || !prompt || !out_count || len < 1 || max_new < 0 || (max_new > 0 && !out_tokens))
     return ti_set_error(TI_ERR_ARG, "ti_engine_beam_search: bad arguments");
+  DeviceScope bind_(e);
   if (beam_size < 1) return ti_set_error(TI_ERR_ARG, "ti_engine_beam_search: Beam size must be greater than 0");
   const ti_engine_config& c = e->c;
   if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_beam_search: compat engine");
   if (len + max_new - 1 > c.max_seq)
     return ti_set_error(TI_ERR_ARG, "ti_engine_beam_search: %d + %d tokens exceed max_seq %d", len, max_new, c.max_seq);
-  if (max_new > 0 && beam_size > c.max_batch)
-    return ti_set_error(TI_ERR_ARG, "ti_engine_beam_search: beam_size %d exceeds the engine's %d stream slots",
-                        beam_size, c.max_batch);
+  // More beams than stream slots: every candidate's next-token logits come from a full pass over
+  // its sequence in slot 0 (prefill + one step), as the reference recomputes each candidate
+  // (:1961) -- slower, same decisions.
+  const bool recompute = beam_size > c.max_batch;
   const size_t V = (size_t)c.vocab;
-  std::vector<float> logits((size_t)c.max_batch * V);
+  std::vector<float> logits((size_t)std::max(c.max_batch, beam_size) * V);
   auto cmp = [](const Beam& a, const Beam& b) { return a.log_prob < b.log_prob; };
   std::priority_queue<Beam, std::vector<Beam>, decltype(cmp)> beam(cmp);
   Beam init;
@@ -1234,7 +1300,14 @@ int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int len, int max_
     // next-token logits of every live beam: the prompt's prefill + first step into slot 0, then
     // one batched decode step over the slots (each feeds its last token at its own position;
     // slots no beam owns decode a dummy token into their own, unused cache)
-    if (step == 0) {
+    if (recompute) {
+      for (size_t i = 0; i < cur.size(); ++i) {
+        cur[i].slot = (int)i;   // row of `logits`
+        const int n = (int)cur[i].tokens.size();
+        int32_t tok = 0;
+        TI_TRY(ti_engine_generate(e, 1, cur[i].tokens.data(), &n, n, nullptr, 1, &tok, logits.data() + i * V));
+      }
+    } else if (step == 0) {
       int32_t tok = 0;
       TI_TRY(ti_engine_generate(e, 1, prompt, &len, len, nullptr, 1, &tok, logits.data()));
     } else {
@@ -1281,7 +1354,7 @@ int ti_engine_beam_search(ti_engine* e, const int32_t* prompt, int len, int max_
     // the others fork the parent's cache (positions 0 .. parent length - 1) into a free slot
     std::vector<char> owned(c.max_batch, 0);
     std::vector<size_t> forks;
-    for (size_t i = 0; i < keep; ++i) {
+    for (size_t i = 0; i < (recompute ? 0 : keep); ++i) {
       if (next[i].finished) continue;
       if (!owned[next[i].slot]) owned[next[i].slot] = 1;
       else forks.push_back(i);
@@ -1332,6 +1405,7 @@ int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32
                     int chunk, int32_t* out_tokens, int32_t* out_len) {
   if (!e || !prompts || !offsets || !out_tokens || !out_len || n_req < 1 || max_new < 1 || chunk < 1)
     return ti_set_error(TI_ERR_ARG, "ti_engine_serve: bad arguments");
+  DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
   if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_serve: compat engine");
   const int B = c.max_batch;
@@ -1392,6 +1466,7 @@ int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32
     TI_TRY(run_steps(e, B, 1, S));
     TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
     TI_TRY(read_argmax(e, B, am));   // synchronises the stream
+    TI_TRY(chain_check(e));          // before any token of the chunk is handed out
     for (int m = 0; m < B; ++m) {
       const int r = slot_req[m];
       if (r < 0) continue;
@@ -1409,7 +1484,6 @@ int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32
       }
       if (slot_req[m] >= 0) slot_pos[m] += S;
     }
-    TI_TRY(chain_check(e));
   }
   return TI_OK;
 }
@@ -1417,12 +1491,14 @@ int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32
 int ti_engine_set_prefill(ti_engine* e, int rows) {
   if (!e || e->c.compat || rows < 0 || rows > e->rows_cap || (rows > 0 && rows > ((e->c.bits & ~TI_BITS_G32) == 4 ? TI_GEMM_MAX_ROWS : 16)))
     return ti_set_error(TI_ERR_ARG, "ti_engine_set_prefill: rows %d", rows);
+  DeviceScope bind_(e);
   e->pf_rows = rows;
   return TI_OK;
 }
 
 int ti_engine_step(ti_engine* e, int n, const int32_t* tokens, const int32_t* pos, float* logits) {
   if (!e || !tokens || !pos) return ti_set_error(TI_ERR_ARG, "ti_engine_step: null");
+  DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
   if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_step: compat engine");
   if (n < 1 || n > c.max_batch) return ti_set_error(TI_ERR_ARG, "ti_engine_step: n=%d", n);
@@ -1444,6 +1520,7 @@ int ti_engine_step(ti_engine* e, int n, const int32_t* tokens, const int32_t* po
 
 int ti_engine_compat_step(ti_engine* e, int placeholder_offset, float* logits) {
   if (!e || !e->c.compat) return ti_set_error(TI_ERR_ARG, "ti_engine_compat_step: not a compat engine");
+  DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
   const int H = c.hidden, I = c.inter, V = c.vocab;
   std::vector<int32_t> zero(1, 0);
@@ -1475,6 +1552,7 @@ int ti_engine_compat_step(ti_engine* e, int placeholder_offset, float* logits) {
 
 int ti_engine_replay_prepare(ti_engine* e, int n, int kv_len, int start_token) {
   if (!e || e->c.compat) return ti_set_error(TI_ERR_ARG, "ti_engine_replay_prepare: bad engine");
+  DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
   if (n < 1 || n > c.max_batch || kv_len < 1 || kv_len > c.max_seq || start_token < 0 || start_token >= c.vocab)
     return ti_set_error(TI_ERR_ARG, "ti_engine_replay_prepare: n=%d kv_len=%d", n, kv_len);
@@ -1494,17 +1572,20 @@ int ti_engine_replay_prepare(ti_engine* e, int n, int kv_len, int start_token) {
 
 int ti_engine_replay_run(ti_engine* e, int steps) {
   if (!e || e->replay_M < 1) return ti_set_error(TI_ERR_ARG, "ti_engine_replay_run: call ti_engine_replay_prepare first");
+  DeviceScope bind_(e);
   return run_steps(e, e->replay_M, 0, steps);
 }
 
 int ti_engine_sync(ti_engine* e) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_sync: null");
+  DeviceScope bind_(e);
   TI_TRY(ti_stream_sync(e->s));
   return chain_check(e);
 }
 
 int ti_engine_set_chain(ti_engine* e, int on, int* active) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_chain: null");
+  DeviceScope bind_(e);
   if (on >= 0) e->chain_on = on != 0;
   if (active) *active = chain_usable(e, 1) ? 1 : 0;
   return TI_OK;
@@ -1512,6 +1593,7 @@ int ti_engine_set_chain(ti_engine* e, int on, int* active) {
 
 int ti_engine_set_fold(ti_engine* e, int on, int* active) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_fold: null");
+  DeviceScope bind_(e);
   if (on >= 0 && ((on != 0) != e->fold_on || (on != 0) != e->part_on)) {
     TI_TRY(ti_stream_sync(e->s));   // captured step graphs bake the setting in
     for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
@@ -1524,6 +1606,7 @@ int ti_engine_set_fold(ti_engine* e, int on, int* active) {
 
 int ti_engine_set_qkv_attn(ti_engine* e, int on, int* active) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_qkv_attn: null");
+  DeviceScope bind_(e);
   if (on >= 0 && (on != 0) != e->qa_on) {
     TI_TRY(ti_stream_sync(e->s));   // captured step graphs bake the setting in
     for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
@@ -1536,18 +1619,25 @@ int ti_engine_set_qkv_attn(ti_engine* e, int on, int* active) {
 
 int ti_engine_set_pds(ti_engine* e, int on, int* active) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_pds: null");
+  DeviceScope bind_(e);
   if (on >= 0 && (on != 0) != e->pds_on) {
     TI_TRY(ti_stream_sync(e->s));   // captured step graphs bake the setting in
     for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
     e->graphs.clear();
     e->pds_on = on != 0;
   }
+  // diagnostic (tests/test_gpu_pds.py): TI_PDS_FORCE_ERR=1 pre-sets the hand-off error word, so
+  // the next persistent launch runs without waits and the engine must report it as fatal
+  if (on > 0 && e->pds_err)
+    if (const char* env = getenv("TI_PDS_FORCE_ERR"))
+      if (atoi(env) != 0) TI_TRY(ti_memset(e->pds_err, 0xff, 4, e->s));
   if (active) *active = pds_usable(e, 1) ? 1 : 0;
   return TI_OK;
 }
 
 int ti_engine_pds_timestamps(ti_engine* e, unsigned long long* out, size_t n) {
   if (!e || !out) return ti_set_error(TI_ERR_ARG, "ti_engine_pds_timestamps: null");
+  DeviceScope bind_(e);
   if (!e->pds_ts) return ti_set_error(TI_ERR_ARG, "ti_engine_pds_timestamps: engine built without TI_PDS_TS=1");
   const size_t have = (size_t)256 * e->c.layers * 5 * 8;
   TI_TRY(ti_stream_sync(e->s));
@@ -1557,6 +1647,7 @@ int ti_engine_pds_timestamps(ti_engine* e, unsigned long long* out, size_t n) {
 
 int ti_engine_pds_error(ti_engine* e, uint32_t* err) {
   if (!e || !err) return ti_set_error(TI_ERR_ARG, "ti_engine_pds_error: null");
+  DeviceScope bind_(e);
   *err = 0;
   if (!e->pds_err) return TI_OK;
   TI_TRY(ti_stream_sync(e->s));
@@ -1566,6 +1657,7 @@ int ti_engine_pds_error(ti_engine* e, uint32_t* err) {
 
 int ti_engine_last_tokens(ti_engine* e, int n, int32_t* tokens) {
   if (!e || !tokens || n < 1 || n > e->c.max_batch) return ti_set_error(TI_ERR_ARG, "ti_engine_last_tokens");
+  DeviceScope bind_(e);
   std::vector<unsigned long long> am;
   TI_TRY(read_argmax(e, n, am));
   for (int m = 0; m < n; ++m) tokens[m] = (int32_t)(0xFFFFFFFFu - (uint32_t)(am[m] & 0xFFFFFFFFull));
@@ -1575,6 +1667,7 @@ int ti_engine_last_tokens(ti_engine* e, int n, int32_t* tokens) {
 int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, double* avg_us, double* bytes) {
   if (!e || e->c.compat || !avg_us || !bytes || reps < 1 || n < 1 || n > e->c.max_batch || e->c.layers < 1)
     return ti_set_error(TI_ERR_ARG, "ti_engine_time_kernel: bad arguments");
+  DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
   const int H = c.hidden, I = c.inter, qd = e->qd(), kvd = e->kvd();
   const bool fold = fold_usable(e, n), part = part_usable(e, n);
@@ -1670,19 +1763,19 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
   hipGraphDestroy(graph);
   E_CHECK(ei, "hipGraphInstantiate");
   const int rounds = std::max(4, 4096 / reps);
-  hipEvent_t a, b;
-  E_CHECK(hipEventCreate(&a), "hipEventCreate");
-  E_CHECK(hipEventCreate(&b), "hipEventCreate");
-  hipError_t el = hipGraphLaunch(gx, e->s);   // warm (code objects, caches, clocks)
+  hipEvent_t a = nullptr, b = nullptr;
+  hipError_t el = hipEventCreate(&a);
+  if (el == hipSuccess) el = hipEventCreate(&b);
+  if (el == hipSuccess) el = hipGraphLaunch(gx, e->s);   // warm (code objects, caches, clocks)
   if (el == hipSuccess) el = hipEventRecord(a, e->s);
   for (int r = 0; r < rounds && el == hipSuccess; ++r) el = hipGraphLaunch(gx, e->s);
   if (el == hipSuccess) el = hipEventRecord(b, e->s);
   if (el == hipSuccess) el = hipEventSynchronize(b);
   float ms = 0.0f;
   if (el == hipSuccess) el = hipEventElapsedTime(&ms, a, b);
-  hipEventDestroy(a);
-  hipEventDestroy(b);
-  hipGraphExecDestroy(gx);
+  if (a) hipEventDestroy(a);
+  if (b) hipEventDestroy(b);
+  hipGraphExecDestroy(gx);   // on every path after instantiation
   E_CHECK(el, "ti_engine_time_kernel: graph replay");
   // per projection (all row chunks of it, and the rms_norm prep of the batched path)
   *avg_us = (double)ms * 1000.0 / ((double)reps * rounds);

@@ -1851,7 +1851,7 @@ static int launch_rows(const GemvArgs& a, int MB, int RG, int ntl, int grid, int
       (const void*)gemv_mb_kernel<2, 2>, (const void*)gemv_mb_kernel<2, 3>, (const void*)gemv_mb_kernel<2, 4>, \
       (const void*)gemv_mb_kernel<2, 5>, (const void*)gemv_mb_kernel<2, 6>
 
-static bool g_prepared = false;
+static unsigned long long g_prepared = 0;   // devices (bit per ordinal) whose attributes are set
 
 }  // namespace ti
 
@@ -1871,7 +1871,10 @@ static int query_cus() {
 extern "C" int ti_gemm_prepare(void) {
   using namespace ti;
   query_cus();
-  if (g_prepared) return TI_OK;
+  int dev = 0;
+  TI_HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
+  const unsigned long long bit = 1ull << (dev & 63);
+  if (g_prepared & bit) return TI_OK;
   const void* fns[] = {
       (const void*)gemv_wq_kernel<4, XM_F16>,  (const void*)gemv_wq_kernel<4, XM_F32>,
       (const void*)gemv_wq_kernel<4, XM_NORM1>, (const void*)gemv_wq_kernel<4, XM_NORM>,
@@ -1889,7 +1892,7 @@ extern "C" int ti_gemm_prepare(void) {
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
-  g_prepared = true;
+  g_prepared |= bit;
   return TI_OK;
 }
 
@@ -2089,7 +2092,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     if (!chain->abort_flag || ((uintptr_t)epi->out & 3) || ((uintptr_t)epi->k_cache & 3) || ((uintptr_t)epi->v_cache & 3))
       return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16_chained: abort_flag required, outputs 4-byte aligned");
   }
-  if ((lds > 64 * 1024 || chain) && !g_prepared) {
+  if (lds > 64 * 1024 || chain) {   // no-op once this device is prepared
     const int rc = ti_gemm_prepare();
     if (rc != TI_OK) return rc;
   }

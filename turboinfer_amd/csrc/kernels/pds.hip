@@ -13,15 +13,16 @@
 // and refills it past phase and layer boundaries, so while a workgroup waits for the previous
 // phase's output vector its next phase's first bytes are already landing.
 //
-// Shape: one 9-wave workgroup per CU (grid = kv_heads * 8 = 256).
+// Shape: one 8-wave workgroup per CU (grid = kv_heads * 8 = 256).
 //   * waves 0-7 ("C"): the weight / K/V stream and the MFMA / softmax math, item for item
 //     the arithmetic of gemv_wq_kernel (fold, partials modes) and attn_split_body (non-HP,
 //     G = 1): wave w owns k-tiles w, w+8, ... of every tile, key slots w, w+8, ... of its
 //     split; they issue only ring loads (plus the staging loads right after a hand-off).
-//   * wave 8 ("X"): polls the hand-off counters, reduces the C waves' partials and runs the
-//     epilogues (RoPE + KV append, residual + folded rms_norm, SiLU*up, split partials), then
-//     publishes them write-through (sc1) and signals.  It has no ring loads in flight, so its
-//     s_waitcnt vmcnt(0) before the signal drains only its own stores.
+//   * wave 7 is also the control wave ("X"): it polls the hand-off counters, reduces the C waves'
+//     partials and runs the epilogues (RoPE + KV append, residual + folded rms_norm, SiLU*up,
+//     split partials), then publishes them write-through (sc1) and signals.  The next phase's
+//     ring units are issued only after that signal, so its s_waitcnt vmcnt(0) drains only its
+//     own stores.  (A 9th, stream-free control wave was measured slower: DESIGN 4.15.)
 // Per phase: X polls -> barrier -> C waves stage x / scales with sc1 loads (+ int4 offset
 // correction) -> barrier -> C waves consume their units -> barrier -> X epilogue + signal.
 // Hand-off form: MI355X_MICROARCH.md "Hand-offs measured with sc1 loads", first row (one lane
@@ -777,12 +778,28 @@ int ti_pds_decode(const ti_pds_args* h, ti_stream_t s) {
   a.err = h->err;
   a.zero = (const u32x4*)h->zero;
   a.ts = h->ts;
-  static bool attr = false;
-  if (!attr) {
+  // per device: the LDS attribute, and co-residency -- every wait in the kernel needs all `grid`
+  // workgroups resident at once (one per CU): the occupancy query times the CU count must cover
+  // the grid, or nothing is launched.  (Residency taken by other work at run time is caught by
+  // the bounded waits: pds_err, fatal in the engine's hand-off check.)
+  static unsigned long long attr = 0;
+  static int resident[64] = {0};
+  int dev = 0;
+  TI_HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
+  dev &= 63;
+  if (!(attr >> dev & 1ull)) {
     TI_HIP_CHECK(hipFuncSetAttribute((const void*)pds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes),
                  "hipFuncSetAttribute(pds_kernel)");
-    attr = true;
+    int per_cu = 0, cus = 0;
+    TI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pds_kernel, kPdsThreads, kLdsBytes),
+                 "hipOccupancyMaxActiveBlocksPerMultiprocessor(pds_kernel)");
+    TI_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute(CUs)");
+    resident[dev] = per_cu * cus;
+    attr |= 1ull << dev;
   }
+  if (resident[dev] < h->grid)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_pds_decode: %d workgroups cannot all be resident (%d)", h->grid,
+                        resident[dev]);
   hipLaunchKernelGGL(pds_kernel, dim3(h->grid), dim3(kPdsThreads), kLdsBytes, (hipStream_t)s, a);
   TI_LAUNCH_CHECK("pds_kernel");
   return TI_OK;
