@@ -185,8 +185,16 @@ struct ti_engine {
     return TI_OK;
   }
   int attn_target = 256;   // attention workgroups aimed at (env TI_ATTN_TARGET, A/B knob)
+  int gqa_part_splits = 8;   // env TI_ATTN_GQA_PART (0: off), see splits_for
   int splits_for(int M) const {
     if (c.attn_splits > 0) return c.attn_splits;
+    // one stream of a GQA model (>= 4 q-heads per kv-head) with a small cache per kv-head
+    // (<= 1 MiB of K + V: TinyLlama at 2048): few long splits whose partials the O projection
+    // merges (part_usable), instead of 64+ short splits merged by a last arriver
+    // (attention run head by head: ti_attn_decode_partials' GQA expansion, heads x splits workgroups)
+    if (M == 1 && gqa_part_splits >= 2 && part_on && c.heads >= 4 * c.kv_heads &&
+        (size_t)c.max_seq * c.head_dim * 4 <= ((size_t)1 << 20))
+      return std::min(gqa_part_splits, std::max(2, std::min(c.max_seq / 64, (attn_target + c.heads - 1) / c.heads)));
     // one 8-wave attention workgroup per CU: a second round of workgroups costs a whole
     // workgroup latency (load, merge hand-off) for little bandwidth (tools/probe_attn.hip)
     const int target = attn_target;
@@ -855,6 +863,8 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     if ((rc = ti_rope_table(pv.data(), c.max_seq, hd, c.rope_theta, cs.data()))) return fail(rc);
     if ((rc = ti_memcpy_h2d(e->rope_cs, cs.data(), cs.size() * 4, e->s))) return fail(rc);
     if (const char* env = getenv("TI_ATTN_TARGET")) e->attn_target = std::max(1, atoi(env));
+    if (const char* env = getenv("TI_ATTN_GQA_PART")) e->gqa_part_splits = std::min(TI_ATTN_MAX_PART_SPLITS, atoi(env));
+    if (const char* env = getenv("TI_ATTN_PART")) e->part_on = atoi(env) != 0;
     e->splits_max = e->splits_for(1);
     e->pf_rows = (c.bits & ~TI_BITS_G32) == 4 ? TI_GEMM_MAX_ROWS : 16;   // int4 (also group-32): the tile GEMM
     e->rows_cap = std::max(B, e->pf_rows);

@@ -102,7 +102,17 @@ static int attn_impl(const float* q, const uint16_t* k_cache, const uint16_t* v_
   // prefix [0, pos[m]] of the shared cache
   if (kv_stream_stride != 0 && kv_stream_stride < (int64_t)kv_heads * max_seq * head_dim)
     return ti_set_error(TI_ERR_ARG, "ti_attn_decode: kv_stream_stride too small");
-  const int G = heads / kv_heads;
+  // one stream, partials mode, GQA: run head by head (AttnArgs::kv_shift), so a short cache per
+  // kv-head is streamed by G times as many workgroups (from the L2 / MALL after the first)
+  const bool expand = part_o && M == 1 && heads > kv_heads;
+  const int G = expand ? 1 : heads / kv_heads;
+  int kv_shift = 0;
+  if (expand) {
+    while ((kv_heads << kv_shift) < heads) ++kv_shift;
+    if ((kv_heads << kv_shift) != heads)
+      return ti_set_error(TI_ERR_UNSUPPORTED, "ti_attn_decode_partials: heads/kv_heads %d not a power of two",
+                          heads / kv_heads);
+  }
   // splits only shape the work (results agree to rounding); the merge stages all partials
   // of a kv-head group in LDS, which bounds them.
   if (!part_o) splits = std::min(splits, std::max(1, ti::attn_max_splits(G, head_dim)));
@@ -124,7 +134,8 @@ static int attn_impl(const float* q, const uint16_t* k_cache, const uint16_t* v_
   a.max_seq = max_seq;
   a.M = M;
   a.heads = heads;
-  a.kv_heads = kv_heads;
+  a.kv_heads = expand ? heads : kv_heads;
+  a.kv_shift = kv_shift;
   a.splits = splits;
   a.scale = 1.0f / sqrtf((float)head_dim);   // tensor_engine.cpp:1288 (hidden = head_dim per head)
   a.chain = chain_dev(chain);
@@ -133,7 +144,7 @@ static int attn_impl(const float* q, const uint16_t* k_cache, const uint16_t* v_
       return ti_set_error(TI_ERR_ARG, "ti_attn_decode_chained: abort_flag required, out 4-byte aligned");
     if ((int64_t)max_seq * head_dim * 2 >= 0x7fffffffLL)
       return ti_set_error(TI_ERR_UNSUPPORTED, "ti_attn_decode_chained: a (stream, kv-head) cache exceeds 2 GiB");
-    chain->signaled = (uint32_t)(splits * kv_heads * M);
+    chain->signaled = (uint32_t)(splits * a.kv_heads * M);
   }
   hipStream_t s = (hipStream_t)stream;
   return head_dim == 128 ? dispatch_group<128>(a, G, s, chain) : dispatch_group<64>(a, G, s, chain);

@@ -26,6 +26,10 @@ struct AttnArgs {
   uint16_t* part_o;   // [M][heads][splits][HD] fp16, nullptr = merge in this launch
   float* part_ml;     // [M][heads][splits][2]
   int32_t out_kt;     // > 0: out in TI_X_F16_PACKED order with K / 128 = out_kt (ti_attn_decode_packed)
+  // GQA run head by head (kv_heads here = heads, G = 1): workgroup head h reads the cache of kv-head
+  // h >> kv_shift.  The G q-heads of a kv-head then stream its K/V from the L2 / MALL in parallel
+  // instead of one workgroup serving all of them (one stream, partials mode: DESIGN 4.16).
+  int32_t kv_shift;
 };
 
 #ifndef TI_ATTN_RING
@@ -136,7 +140,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
   if constexpr (CH && !EARLY) chain_wait(a.chain);
   const int L = (CH && !EARLY ? (int)__builtin_amdgcn_readfirstlane(ld_sc1_u32(a.pos + m)) : a.pos[m]) + 1;
   // K/V of this workgroup's (stream, kv-head): [max_seq][HD] fp16 from wg_off
-  const int64_t wg_off = (int64_t)m * a.stride + (int64_t)kvh * a.max_seq * HD;
+  const int64_t wg_off = (int64_t)m * a.stride + (int64_t)(kvh >> a.kv_shift) * a.max_seq * HD;
   const __amdgpu_buffer_rsrc_t rk = sc1_rsrc(a.kc + wg_off), rv = sc1_rsrc(a.vc + wg_off), rq = sc1_rsrc(a.q);
   // Chained: only the row at L - 1 was written by the previous launch (the QKV epilogue of
   // this step); rows before it were written by earlier steps and never change afterwards, so
