@@ -79,7 +79,7 @@ int ti_engine_generate(ti_engine* e, int n_streams, const int32_t* prompts, cons
  * temperature, top-k, softmax, top-p, the draw) and feeds the token back, so the loop never
  * returns to the host.  draws [n][max_new]: the uniform draw of each stream's t-th new token
  * (the reference takes them from its engine's mt19937, uniform_real_distribution<float>);
- * 1 <= top_k <= min(vocab, TI_SAMPLE_MAX_K).  out_logprobs (nullable) [n][max_new] = log p of
+ * 1 <= top_k <= vocab (above TI_SAMPLE_MAX_K the engine keeps a sampler workspace).  out_logprobs (nullable) [n][max_new] = log p of
  * each sampled token. */
 int ti_engine_generate_sampled(ti_engine* e, int n_streams, const int32_t* prompts, const int32_t* prompt_lens,
                                int prompt_stride, const int32_t* start_pos, int max_new, float temperature,

@@ -362,7 +362,11 @@ typedef struct ti_pds_args {
   uint32_t* err;
   const void* zero;                  /* >= 2 KiB of readable memory, never written */
   unsigned long long* ts;            /* diagnostic phase timestamps [grid][n_layers][5][8], or NULL */
+  /* data-tagged hand-offs: 8-byte {payload, tag} granules, ti_pds_granule_words(...) of them,
+   * zero before the first launch */
+  unsigned long long* gran;
 } ti_pds_args;
+size_t ti_pds_granule_words(int H, int I, int qd, int heads, int grid);
 #define TI_PDS_CTR_WORDS_PER_LAYER (5 * 8 * 32)
 int ti_pds_decode(const ti_pds_args* a, ti_stream_t s);
 /* One launch of a chain (ti_chain): the same attention; K/V, q and pos read with sc1 loads
@@ -404,7 +408,7 @@ int ti_step_begin_chained(const ti_step_args* a, ti_chain* chain, ti_stream_t s)
 /* ------------------------------------------------------- on-device sampling
  * InferenceEngine::sample_next_token (inference_engine.cpp:1554-1673) per stream, the uniform
  * draw supplied (the reference draws it from the engine's mt19937): temperature, top-k
- * (1 <= top_k <= min(V, TI_SAMPLE_MAX_K)), softmax, top-p, the draw.  Sums run over the
+ * (1 <= top_k <= V; above TI_SAMPLE_MAX_K with a workspace, below), softmax, top-p, the draw.  Sums run over the
  * survivors in index order (the reference's loops over V add exact zeros elsewhere); exp/log
  * are the device's, equal logits at the k-th place and equal probabilities at the top-p cut
  * go lowest index first.  One 1024-thread workgroup per stream. */
@@ -420,6 +424,16 @@ int ti_sample_device(const float* logits, int ldl, int M, int V, float temperatu
 int ti_sample_step(const float* logits, int ldl, int M, int V, float temperature, int top_k, float top_p,
                    const float* draws, int draw_stride, const int32_t* step_ctr, int advance, const int32_t* n_in,
                    unsigned long long* argmax, float* logprobs, ti_stream_t s);
+/* Any top_k up to V (the reference accepts any k, inference_engine.cpp:1585-1598): above
+ * TI_SAMPLE_MAX_K the survivors' arrays live in a caller-provided device workspace of
+ * M * ti_sample_workspace_bytes(V, top_k) bytes (0 for top_k <= TI_SAMPLE_MAX_K, where ws may be
+ * null); the _ws forms take it, the plain forms are the _ws forms with ws = null. */
+size_t ti_sample_workspace_bytes(int V, int top_k);
+int ti_sample_device_ws(const float* logits, int ldl, int M, int V, float temperature, int top_k, float top_p,
+                        const float* draws, int32_t* tokens, float* logprobs, void* ws, ti_stream_t s);
+int ti_sample_step_ws(const float* logits, int ldl, int M, int V, float temperature, int top_k, float top_p,
+                      const float* draws, int draw_stride, const int32_t* step_ctr, int advance, const int32_t* n_in,
+                      unsigned long long* argmax, float* logprobs, void* ws, ti_stream_t s);
 
 /* -------------------------------------------------------------- fp32 op level */
 /* y[r][n] (+)= sum_k a[r][k]*b[k][n], b the reference [K][N] fp32 layout, one fmaf per k

@@ -82,7 +82,8 @@ EXPORTED = [
     "ti_attn_decode_partials", "ti_sample_device", "ti_sample_step", "ti_engine_generate_sampled",
     "ti_engine_beam_search", "ti_engine_serve", "ti_qkv_attn_fused", "ti_engine_set_qkv_attn",
     "ti_pds_decode", "ti_engine_set_pds", "ti_engine_pds_error", "ti_engine_pds_timestamps",
-    "ti_wpack_q_host", "ti_engine_set_tensor_q",
+    "ti_wpack_q_host", "ti_engine_set_tensor_q", "ti_sample_workspace_bytes", "ti_sample_device_ws",
+    "ti_sample_step_ws", "ti_pds_granule_words",
 ]
 
 _lib = None
@@ -133,6 +134,10 @@ def lib() -> C.CDLL:
         L.ti_attn_prefill.argtypes = [vp, vp, vp, i32, vp, i32, i32, i32, i32, vp, vp]
         if hasattr(L, "ti_sample_device"):
             L.ti_sample_device.argtypes = [vp, i32, i32, i32, f32, i32, f32, vp, vp, vp, vp]
+        if hasattr(L, "ti_sample_device_ws"):
+            L.ti_sample_device_ws.argtypes = [vp, i32, i32, i32, f32, i32, f32, vp, vp, vp, vp, vp]
+            L.ti_sample_workspace_bytes.argtypes = [i32, i32]
+            L.ti_sample_workspace_bytes.restype = sz
             L.ti_engine_generate_sampled.argtypes = [vp, i32, vp, vp, i32, vp, i32, f32, i32, f32, vp, vp, vp]
         if hasattr(L, "ti_engine_serve"):
             L.ti_engine_serve.argtypes = [vp, i32, vp, vp, i32, i32, i32, vp, vp]

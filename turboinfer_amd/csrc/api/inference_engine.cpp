@@ -511,8 +511,8 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
         const size_t b = budget(batches[c0 + m].size());
         for (size_t t = 0; t < std::min(b, steps_new); ++t) fresh[m].push_back(out[(size_t)m * steps_new + t]);
       }
-    } else if (n == 1 && config_.top_k >= 1 && config_.top_k <= (size_t)std::min(V, TI_SAMPLE_MAX_K)) {
-      // one request, top-k in the device sampler's range: the whole loop on the device
+    } else if (n == 1 && config_.top_k >= 1 && config_.top_k <= (size_t)V) {
+      // one request with top-k sampling (any k up to the vocabulary): the whole loop on the device
       // (ti_engine_generate_sampled), fed the engine's mt19937 draws in the reference's order;
       // the generator then advances by the draws the request actually used (one per token)
       const auto& p = batches[c0];

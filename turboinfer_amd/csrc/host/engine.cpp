@@ -111,6 +111,8 @@ struct ti_engine {
   float* draws = nullptr;      // [max_batch][draw_cap] uniform draws, per new token
   float* lps = nullptr;        // [max_batch][draw_cap] log p of the sampled tokens
   int draw_cap = 0;
+  void* samp_ws = nullptr;     // ti_sample_step_ws workspace (top_k > TI_SAMPLE_MAX_K)
+  size_t samp_ws_bytes = 0;
   // prefill (forward_pass over prompt tokens): up to pf_rows prompt tokens of one stream run
   // as rows of the batched path, sharing that stream's KV cache (stride 0)
   int pf_rows = 0;             // 0 = off (prompts consumed one token per decode step)
@@ -148,6 +150,7 @@ struct ti_engine {
   uint32_t* pds_launches = nullptr;     // [256]
   uint32_t* pds_err = nullptr;
   void* pds_zero = nullptr;             // 4 KiB of zeros, never written
+  unsigned long long* pds_gran = nullptr;   // granule hand-offs (ti_pds_granule_words)
   unsigned long long* pds_ts = nullptr; // TI_PDS_TS=1: phase timestamps of the last launch
 
   int qd() const { return c.heads * c.head_dim; }
@@ -436,6 +439,9 @@ int chain_check(ti_engine* e) {
       TI_TRY(ti_memset(e->pds_err, 0, 4, e->s));
       TI_TRY(ti_memset(e->pds_ctr, 0, (size_t)e->c.layers * TI_PDS_CTR_WORDS_PER_LAYER * 4, e->s));
       TI_TRY(ti_memset(e->pds_launches, 0, 256 * 4, e->s));
+      // launch epochs restart: stale granules would carry the new epochs' tags
+      TI_TRY(ti_memset(e->pds_gran, 0,
+                       ti_pds_granule_words(e->c.hidden, e->c.inter, e->qd(), e->c.heads, e->c.kv_heads * 8) * 8, e->s));
       TI_TRY(ti_stream_sync(e->s));
       return ti_set_error(TI_ERR_HIP,
                           "engine: a persistent decode hand-off wait timed out (err 0x%x); results of this call are "
@@ -587,6 +593,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     pa.launches = e->pds_launches;
     pa.err = e->pds_err;
     pa.zero = e->pds_zero;
+    pa.gran = e->pds_gran;
     pa.ts = e->pds_ts;
     TI_TRY(ti_pds_decode(&pa, e->s));
     n_ss = pa.grid;
@@ -659,8 +666,8 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   el.advance = advance;
   TI_TRY(gemm(e->lm, e->h, TI_X_F32_RMSNORM, H, 4, e->out_norm, el, 4, true));
   if (e->samp_on)   // sample_next_token on the device; its key feeds the token back (ti_hip.h)
-    TI_TRY(ti_sample_step(e->logits, V, M, V, e->samp_t, e->samp_k, e->samp_p, e->draws, e->draw_cap, e->step_ctr,
-                          advance, e->n_in, e->argmax, e->lps, e->s));
+    TI_TRY(ti_sample_step_ws(e->logits, V, M, V, e->samp_t, e->samp_k, e->samp_p, e->draws, e->draw_cap, e->step_ctr,
+                             advance, e->n_in, e->argmax, e->lps, e->samp_ws, e->s));
   return TI_OK;
 }
 
@@ -914,7 +921,8 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
           (rc = ti_memcpy_h2d(e->pds_layers, pl.data(), pl.size() * sizeof(ti_pds_layer), e->s)) ||
           (rc = e->alloc_t(&e->pds_ctr, (size_t)c.layers * TI_PDS_CTR_WORDS_PER_LAYER)) ||
           (rc = e->alloc_t(&e->pds_launches, (size_t)256)) || (rc = e->alloc_t(&e->pds_err, (size_t)1)) ||
-          (rc = e->alloc(&e->pds_zero, 4096)))
+          (rc = e->alloc(&e->pds_zero, 4096)) ||
+          (rc = e->alloc_t(&e->pds_gran, ti_pds_granule_words(H, I, e->qd(), c.heads, c.kv_heads * 8))))
         return fail(rc);
       if (const char* env = getenv("TI_PDS")) e->pds_on = atoi(env) != 0;
       if (const char* env = getenv("TI_PDS_TS"))
@@ -1153,9 +1161,8 @@ int ti_engine_generate_sampled(ti_engine* e, int n, const int32_t* prompts, cons
   const ti_engine_config& c = e->c;
   if (c.compat) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_generate_sampled: compat engine");
   if (n < 1 || n > c.max_batch || max_new < 1) return ti_set_error(TI_ERR_ARG, "ti_engine_generate_sampled: n=%d max_new=%d", n, max_new);
-  if (top_k < 1 || top_k > TI_SAMPLE_MAX_K || top_k > c.vocab)
-    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_generate_sampled: top_k %d not in [1, %d]", top_k,
-                        std::min(c.vocab, TI_SAMPLE_MAX_K));
+  if (top_k < 1 || top_k > c.vocab)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_generate_sampled: top_k %d not in [1, vocab %d]", top_k, c.vocab);
   auto drop_graphs = [&]() -> int {
     TI_TRY(ti_stream_sync(e->s));
     for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
@@ -1168,6 +1175,15 @@ int ti_engine_generate_sampled(ti_engine* e, int n, const int32_t* prompts, cons
     TI_TRY(e->alloc_t(&e->draws, (size_t)c.max_batch * cap));
     TI_TRY(e->alloc_t(&e->lps, (size_t)c.max_batch * cap));
     e->draw_cap = cap;
+  }
+  // top_k above TI_SAMPLE_MAX_K: the sampler's survivors live in an HBM workspace (per stream)
+  const size_t wsb = ti_sample_workspace_bytes(c.vocab, top_k) * (size_t)c.max_batch;
+  if (wsb > e->samp_ws_bytes) {
+    TI_TRY(drop_graphs());
+    void* p = nullptr;
+    TI_TRY(e->alloc(&p, wsb));
+    e->samp_ws = p;
+    e->samp_ws_bytes = wsb;
   }
   if (e->samp_t != temperature || e->samp_k != top_k || e->samp_p != top_p) {   // kernel arguments of the graph
     TI_TRY(drop_graphs());

@@ -1414,8 +1414,9 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
 // serves their common weight stream.
 // WMR: row-waves per workgroup (2: 128 rows x 4 column-waves; 1: 64 rows x 8 column-waves, half
 // the activation block and no weight tile loaded twice)
-__host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, int wmr = 2) {
-  return 2 * 64 * wmr * 256 + align16((8 / wmr) * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
+// XB: activation-block buffers (2: double buffer; 4: issued three groups ahead, when the LDS holds them)
+__host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, int wmr = 2, int xb = 2) {
+  return xb * 64 * wmr * 256 + align16((8 / wmr) * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
 }
 
 // TPW: weight tiles per wave (2: 128 columns per workgroup; 1: 64 columns, twice the workgroups
@@ -1423,9 +1424,44 @@ __host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, 
 // 4: 256 columns, half the activation bytes per MFMA, when the rows give enough workgroups).
 // G32: group-32 int4 tiles (TI_BITS_G32): MFMA step s4 of a group reads k-chunk 4 s4 + kq and
 // carries its own scale (one per 32-k block), so each step's product is scaled separately.
-template <int TPW, bool G32 = false, int WMR = 2>
+#ifndef TI_TILE_ASM
+// 1: both operand streams of the k-loop issued from inline asm (the activation block's LDS-DMA,
+// the weight tiles' VGPR loads) with hand-counted waits.  Beside a builtin LDS-DMA hipcc's waitcnt
+// pass cannot count the VGPR weight loads and drains vmcnt(0) before every group
+// (cdna_hip_programming.md section 5, "Three .s-level traps" (b)); with only the DMA hidden its
+// weight waits count the DMAs as older loads and cut the lookahead; with both hidden every group's
+// loads stay in flight across the barrier as deep as the rings allow.
+#define TI_TILE_ASM 1
+#endif
+#ifndef TI_TILE_WNT
+#define TI_TILE_WNT 0   // weight tiles are re-read by the row blocks of a column block (L2): default policy
+#endif
+// 64 lanes x 16 B -> LDS at the wave-uniform byte address lds (M0 set and restored in the statement)
+__device__ __forceinline__ void dma_1k_asm(const void* src_lane, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src_lane), "s"(lds)
+               : "memory");
+}
+// A 16-byte VGPR load hipcc does not count (beside the asm DMA it could not count its own loads
+// exactly either): the caller waits with a counted s_waitcnt and ties the destination ("+v")
+// before any use (cdna_hip_programming.md 5.7, item 1, form ii).
+__device__ __forceinline__ u32x4 ld_w_asm(const u32x4* p) {
+  u32x4 v;
+#if TI_TILE_WNT
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+#else
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+#endif
+  return v;
+}
+
+template <int TPW, bool G32 = false, int WMR = 2, int XB = 2>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb) {
   constexpr int WCOL = kGemvWaves / WMR, BM = 64 * WMR;   // column-waves, rows per workgroup
+  static_assert(XB == 2 || (XB == 4 && TI_TILE_ASM), "deep activation ring: asm-issued DMA only");
+  constexpr int XL = XB - 1;                               // groups of activations issued ahead
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KT = a.K >> 7, NT = a.N >> 4;
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, kq = lane >> 4;
@@ -1437,7 +1473,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   const int m0 = rb * BM, t0 = cb * WCOL * TPW;
   f16* xb = (f16*)smem;                                       // [2][BM rows][128 k] swizzled
   constexpr int SG = G32 ? 4 : 1;                             // scales per tile row and group
-  uint16_t* sl = (uint16_t*)(smem + 2 * BM * 256);            // [WCOL TPW tiles][KT][SG][16]
+  uint16_t* sl = (uint16_t*)(smem + XB * BM * 256);           // [WCOL TPW tiles][KT][SG][16]
   const int n_sc = WCOL * TPW * KT * 2 * SG;                  // 16-byte pieces
   const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16 * SG);
   const int ntile_ok = min(WCOL * TPW, NT - t0);
@@ -1445,13 +1481,18 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
     ((u32x4*)sl)[i] = i < ntile_ok * KT * 2 * SG ? ld_w(sg + i) : (u32x4){0u, 0u, 0u, 0u};
 
   const f16* xg = (const f16*)a.x;
+  const uint32_t xb_lds = (uint32_t)(uintptr_t)xb;   // LDS byte address of the staging buffers
   auto issue_x = [&](int kg) __attribute__((always_inline)) {   // BM / 4 DMA instructions per group
-    f16* dst = xb + (kg & 1) * BM * 128;
+    f16* dst = xb + (kg & (XB - 1)) * BM * 128;
 #pragma unroll
     for (int q = 0; q < 2 * WMR; ++q) {
       const int j = wave * 2 * WMR + q, row = 4 * j + (lane >> 4), p = lane & 15, c = p ^ (row & 15);
       const int m = min(m0 + row, a.M - 1);
-      dma_1k(xg + (size_t)m * a.ldx + kg * 128 + c * 8, dst + j * 512);
+      if constexpr (TI_TILE_ASM)
+        dma_1k_asm(xg + (size_t)m * a.ldx + kg * 128 + c * 8,
+                   __builtin_amdgcn_readfirstlane(xb_lds + (uint32_t)(((kg & (XB - 1)) * BM * 128 + j * 512) * 2)));
+      else
+        dma_1k(xg + (size_t)m * a.ldx + kg * 128 + c * 8, dst + j * 512);
     }
   };
 #ifndef TI_TILE_XREG
@@ -1474,15 +1515,22 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   auto load_w = [&](u32x4 (&w)[TPW], int kg) __attribute__((always_inline)) {
     kg = min(kg, KT - 1);
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) w[t] = ld_w(tb + ((size_t)min(t0 + wn * TPW + t, NT - 1) * KT + kg) * kWave);
+    for (int t = 0; t < TPW; ++t) {
+      const u32x4* src = tb + ((size_t)min(t0 + wn * TPW + t, NT - 1) * KT + kg) * kWave;
+      if constexpr (TI_TILE_ASM) w[t] = ld_w_asm(src);
+      else w[t] = ld_w(src);
+    }
   };
-  // weight ring: 4 groups deep (2 at TPW 4, whose 4-deep ring hipcc keeps in scratch)
-  constexpr int kTileWR = TPW == 4 ? 2 : 4;
+  // weight ring: 4 groups deep (2 at TPW 4, whose 4-deep ring hipcc keeps in scratch); the asm
+  // pipeline keeps 3 (the covering wait then retires W(kg) together with x(kg), see below)
+  constexpr int kTileWR = TI_TILE_ASM ? 3 : (TPW == 4 ? 2 : 4);
   u32x4 W[kTileWR][TPW];
-  if constexpr (TI_TILE_XREG) load_xr(0);
-  else issue_x(0);
+  if constexpr (!TI_TILE_ASM) {   // (the asm pipeline issues its first loads inside its loop)
+    if constexpr (TI_TILE_XREG) load_xr(0);
+    else issue_x(0);
 #pragma unroll
-  for (int u = 0; u < kTileWR - 1; ++u) load_w(W[u], u);
+    for (int u = 0; u < kTileWR - 1; ++u) load_w(W[u], u);
+  }
   f32x4 acc[TPW][4];
 #pragma unroll
   for (int t = 0; t < TPW; ++t)
@@ -1491,7 +1539,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   uint32_t magic;
   asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
   auto compute = [&](const u32x4 (&w)[TPW], int kg) __attribute__((always_inline)) {
-    const f16* xr = xb + (kg & 1) * BM * 128 + (wm * 64 + r) * 128;
+    const f16* xr = xb + (kg & (XB - 1)) * BM * 128 + (wm * 64 + r) * 128;
     f16x8 xf[4][4];
 #pragma unroll
     for (int b = 0; b < 4; ++b)
@@ -1541,6 +1589,39 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   // Per group kg: x(kg) and W(kg) were issued earlier; issue x(kg + 1) and W(kg + WR - 1),
   // wait until only those weight loads are younger than x(kg + 1)... (see below), compute kg.
   const int KTP = (KT + kTileWR - 1) / kTileWR * kTileWR;
+  if constexpr (TI_TILE_ASM) {
+    // Every group issues, in order, x(kg + XL) (2 WMR DMA instructions into buffer
+    // (kg + XL) % XB, read last in group kg - 1) and W(kg + 2) (TPW loads into ring slot
+    // (kg + 2) % 3), both clamped into [0, KT): the same count in every group, so the waits are
+    // constants.  The loop starts at group -3 with the compute off, which also makes the first
+    // loads the loop's own code (no prologue whose registers hipcc could shuffle in flight).
+    //   x(kg): younger loads at the top of group kg are W(kg + 3 - XL) and XL - 1 whole groups
+    //          -> vmcnt(NX), then the barrier makes every wave's part visible;
+    //   W(kg): after group kg's own issue, two whole groups are younger -> vmcnt(NWT), then the
+    //          slot's registers are tied ("+v") so nothing reads them earlier.
+    constexpr int NX = (XL - 1) * (2 * WMR + TPW) + TPW, NWT = 2 * (2 * WMR + TPW);
+    for (int k0 = -kTileWR; k0 < KT; k0 += kTileWR) {
+#pragma unroll
+      for (int u = 0; u < kTileWR; ++u) {
+        const int kg = k0 + u;
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NX) : "memory");   // x(kg): this wave's DMA
+        lds_barrier();
+        issue_x(max(0, min(kg + XL, KT - 1)));
+        load_w(W[(u + 2) % kTileWR], max(0, kg + 2));
+        // (also in the groups without compute: a slot's load is always consumed by its tie, so
+        // hipcc never hands its registers to anything else while the load is in flight)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NWT) : "memory");   // W(kg)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) asm volatile("" : "+v"(W[u][t]));
+        if (kg >= 0 && kg < KT) compute(W[u], kg);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped loads past the end
+#pragma unroll
+    for (int u = 0; u < kTileWR; ++u)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) asm volatile("" : "+v"(W[u][t]));
+  } else {
   for (int k0 = 0; k0 < KTP; k0 += kTileWR) {
 #pragma unroll
     for (int u = 0; u < kTileWR; ++u) {
@@ -1561,6 +1642,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
         compute(W[u], kg);
       }
     }
+  }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // epilogue straight from the accumulators (16 x 4 outputs per lane pattern of the MFMA); the
@@ -1602,16 +1684,32 @@ __host__ inline bool tile_narrow_on() {
 // microsecond, a workgroup moves its activation block plus its weight tiles per
 // 128-k group, and the launch takes ceil(workgroups / CUs) rounds; the cheapest shape wins
 // (TI_TILE_NARROW / TI_TILE_WIDE / TI_TILE_WMR1 drop TPW 1 / TPW 4 / 64-row shapes, A/B knobs).
-#define TI_TILE_FNS                                                                                          \
-  (const void*)gemm_tile_kernel<1, false, 2>, (const void*)gemm_tile_kernel<2, false, 2>,                    \
-      (const void*)gemm_tile_kernel<4, false, 2>, (const void*)gemm_tile_kernel<1, true, 2>,                 \
-      (const void*)gemm_tile_kernel<2, true, 2>, (const void*)gemm_tile_kernel<4, true, 2>,                  \
-      (const void*)gemm_tile_kernel<1, false, 1>, (const void*)gemm_tile_kernel<2, false, 1>,                \
-      (const void*)gemm_tile_kernel<4, false, 1>, (const void*)gemm_tile_kernel<1, true, 1>,                 \
-      (const void*)gemm_tile_kernel<2, true, 1>, (const void*)gemm_tile_kernel<4, true, 1>
-__host__ inline const void* tile_fn(int tpw, bool g32, int wmr) {
+#if TI_TILE_ASM
+#define TI_TILE_XB4 4
+#else
+#define TI_TILE_XB4 2
+#endif
+#define TI_TILE_FNS_XB(XB)                                                                                     \
+  (const void*)gemm_tile_kernel<1, false, 2, XB>, (const void*)gemm_tile_kernel<2, false, 2, XB>,              \
+      (const void*)gemm_tile_kernel<4, false, 2, XB>, (const void*)gemm_tile_kernel<1, true, 2, XB>,           \
+      (const void*)gemm_tile_kernel<2, true, 2, XB>, (const void*)gemm_tile_kernel<4, true, 2, XB>,            \
+      (const void*)gemm_tile_kernel<1, false, 1, XB>, (const void*)gemm_tile_kernel<2, false, 1, XB>,          \
+      (const void*)gemm_tile_kernel<4, false, 1, XB>, (const void*)gemm_tile_kernel<1, true, 1, XB>,           \
+      (const void*)gemm_tile_kernel<2, true, 1, XB>, (const void*)gemm_tile_kernel<4, true, 1, XB>
+#define TI_TILE_FNS TI_TILE_FNS_XB(2), TI_TILE_FNS_XB(TI_TILE_XB4)
+__host__ inline const void* tile_fn(int tpw, bool g32, int wmr, int xb) {
   static const void* const fns[] = {TI_TILE_FNS};
-  return fns[(wmr == 1 ? 6 : 0) + (g32 ? 3 : 0) + (tpw == 1 ? 0 : tpw == 2 ? 1 : 2)];
+  return fns[(xb == 4 ? 12 : 0) + (wmr == 1 ? 6 : 0) + (g32 ? 3 : 0) + (tpw == 1 ? 0 : tpw == 2 ? 1 : 2)];
+}
+// the deep activation ring when it fits the LDS (TI_TILE_XB=2 forces the double buffer: A/B knob)
+__host__ inline int tile_xb(int K, int tpw, bool g32, int wmr) {
+  static int force = -1;
+  if (force < 0) {
+    const char* e = getenv("TI_TILE_XB");
+    force = e ? atoi(e) : 0;
+  }
+  if (TI_TILE_XB4 != 4 || force == 2) return 2;
+  return tile_lds_bytes(K, tpw, g32, wmr, 4) <= 160 * 1024 ? 4 : 2;
 }
 
 // Shapes considered: (row-waves WMR, tiles per wave TPW); a workgroup moves 16 WMR KiB of
@@ -1631,7 +1729,9 @@ __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
   for (int wmr : {2, 1}) {
     if (wmr == 1 && !wmr1) continue;
     for (int tpw : {2, 1, 4}) {
-      if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && !wide) || tile_lds_bytes(K, tpw, g32, wmr) > 160 * 1024)
+      // (group-32 at TPW 4 spills to scratch: kept out, its asm-loaded weight ring must stay in VGPRs)
+      if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && (!wide || (g32 && TI_TILE_ASM))) ||
+          tile_lds_bytes(K, tpw, g32, wmr) > 160 * 1024)
         continue;
       const int cols = (8 / wmr) * tpw;
       const long wgs = (long)(NT + cols - 1) / cols * ((M + 64 * wmr - 1) / (64 * wmr));
@@ -2059,7 +2159,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   int grid = 0, lds = 0, ntl = 0, rMB = 0, rRG = 0;
   const bool tile = batched && x_kind == TI_X_F16 && M >= tile_rows();
   const bool rows = !tile && batched && (packed_x || M > 32 || (M > 16 && rows_on()));
-  int n_cb = 0, n_rb = 0, tpw = 2, wmr = 2;
+  int n_cb = 0, n_rb = 0, tpw = 2, wmr = 2, xbuf = 2;
   if (tile) {
     const int shape = tile_shape(M, N, K, g32, query_cus());   // the byte model (tile_shape)
     wmr = shape >> 3;
@@ -2067,7 +2167,8 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     n_rb = (M + 64 * wmr - 1) / (64 * wmr);
     n_cb = ((N >> 4) + (8 / wmr) * tpw - 1) / ((8 / wmr) * tpw);
     grid = (n_cb + 7) / 8 * 8 * n_rb;
-    lds = tile_lds_bytes(K, tpw, g32, wmr);
+    xbuf = tile_xb(K, tpw, g32, wmr);
+    lds = tile_lds_bytes(K, tpw, g32, wmr, xbuf);
   } else if (rows) {
     rows_on();
     rows_shape(M, &rMB, &rRG);
@@ -2112,7 +2213,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   if (chain) chain->signaled = (uint32_t)grid;
   hipStream_t s = (hipStream_t)stream;
   if (tile) {
-    const void* f = tile_fn(tpw, g32, wmr);
+    const void* f = tile_fn(tpw, g32, wmr, xbuf);
     void* args[] = {&a, &n_cb, &n_rb};
     TI_HIP_CHECK(hipLaunchKernel(f, dim3(grid), dim3(kGemvThreads), args, lds, s), "hipLaunchKernel(gemm_tile_kernel)");
     TI_LAUNCH_CHECK("gemm_tile_kernel");

@@ -76,7 +76,18 @@ struct PdsArgs {
   uint32_t* err;            // poll timeouts
   const u32x4* zero;        // >= 2 KiB readable, never written: dummy ring loads
   unsigned long long* ts;   // diagnostic phase timestamps [grid][layers][5][8] or null
+  // granule hand-offs (8-byte {payload, tag}, one sc1 store / one sc1 load each)
+  unsigned long long* fxg;  // [H / 2]: fp16 pairs of the fold (O -> gate/up, down -> next QKV)
+  unsigned long long* ssg;  // [grid]: the fold's sums of h^2
+  unsigned long long* qg;   // [qd]: RoPE'd q (QKV -> attention)
+  unsigned long long* kvg;  // [heads][2][head_dim / 2]: the fresh K, V rows (fp16 pairs)
+  unsigned long long* actg; // [I / 2]: SiLU * up (gate/up -> down)
 };
+
+// Granule layout of PdsArgs (ti_pds_granule_words)
+__host__ __device__ inline size_t pds_gran_words(int H, int I, int qd, int heads, int grid) {
+  return (size_t)H / 2 + (size_t)grid + (size_t)qd + (size_t)heads * kPdsHd + (size_t)I / 2;
+}
 
 // Static partition of a GEMV phase for workgroup bid (the same as gemv_wq_kernel's grid).
 struct PdsLin {
@@ -109,7 +120,8 @@ constexpr int kLdsQ = kLdsML + 64;                    // q of the head [128] f32
 constexpr int kLdsKV = kLdsQ + kPdsHd * 4;            // fresh K row [128], V row [128] fp16
 constexpr int kLdsH = kLdsKV + 2 * kPdsHd * 2;        // residual rows [16] f32
 constexpr int kLdsCs = kLdsH + 64;                    // RoPE (cos, sin) [128] f32
-constexpr int kLdsBytes = kLdsCs + kPdsHd * 4;
+constexpr int kLdsMisc = kLdsCs + kPdsHd * 4;          // launch epoch, dead flag (u32)
+constexpr int kLdsBytes = kLdsMisc + 16;
 
 __device__ __forceinline__ void pds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -143,6 +155,50 @@ __device__ __forceinline__ void pds_signal(uint32_t* c, int bid, int lane) {
   if (lane == 0)
     __hip_atomic_fetch_add(c + (bid & (kPdsShards - 1)) * kPdsShardWords, 1u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- data-tagged hand-offs (MI355X_MICROARCH.md price list: granule, handoff-1to1, allgather):
+// a producer stores {payload, tag} as ONE 8-byte sc1 store -- no drain, no counter -- and the
+// consumer polls the data itself with 8-byte sc1 loads until every tag is this launch's.  The
+// tag names (launch epoch, layer, producing phase) and is never 0, the zeroed buffer's value.
+// A buffer is rewritten only after a full all-to-all dependency on its readers (fx: O(l) then
+// down(l); ss likewise; q, kv, act once per layer), so no reader can see a granule overwritten.
+__device__ __forceinline__ uint32_t pds_tag(uint32_t epoch, int l, int ph) {
+  return ((epoch * 64u + (uint32_t)l) * 8u + (uint32_t)ph) + 1u;
+}
+__device__ __forceinline__ void st_gran(unsigned long long* p, uint32_t payload, uint32_t tag) {
+  st_sc1_u64(p, ((unsigned long long)tag << 32) | payload);
+}
+// NG granules at g[0], g[stride], ...: wait (bounded, like pds_poll) until all carry `tag`.
+template <int NG>
+__device__ __forceinline__ void gather_gran(const unsigned long long* g, int stride, uint32_t tag, uint32_t (&out)[NG],
+                                            uint32_t* err, bool& dead) {
+  unsigned long long v[NG];
+#pragma unroll
+  for (int i = 0; i < NG; ++i) v[i] = ld_sc1_u64(g + i * stride);
+  auto ready = [&]() {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) ok = ok && (uint32_t)(v[i] >> 32) == tag;
+    return ok;
+  };
+  if (!ready() && !dead) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int i = 0; i < NG; ++i)
+        if ((uint32_t)(v[i] >> 32) != tag) v[i] = ld_sc1_u64(g + i * stride);
+      if (ready()) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+        atomicOr(err, 2u);
+        dead = true;
+        break;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NG; ++i) out[i] = (uint32_t)v[i];
 }
 
 // Pointers reach the kernel through the layer table (generic): cast them to the global address
@@ -292,7 +348,8 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
 
   // ---------------------------------------------------------------- X wave: setup
   uint32_t epoch = 0;
-  bool dead = false;   // X: a hand-off wait timed out (this or an earlier launch)
+  bool dead = false;   // a hand-off wait timed out (this or an earlier launch): no wait blocks again
+  uint32_t* misc_l = (uint32_t*)(smem + kLdsMisc);
   const int t0o = (int)((unsigned)bid * (unsigned)(H >> 4) / (unsigned)grid);   // O / down tile of this workgroup (N = H: the same partition)
   if (is_x) {
     if (lane == 0) {
@@ -303,8 +360,15 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
     dead = __builtin_amdgcn_readfirstlane(ld_sc1_u32(a.err)) != 0u;
     if (lane < 16) h_l[lane] = gptr(a.h)[t0o * 16 + lane];
     for (int j = lane; j < HD; j += kWave) cs_l[j] = gptr(a.rope_cs)[(size_t)pos * HD + j];
+    if (lane == 0) {
+      misc_l[0] = epoch;
+      misc_l[1] = dead ? 1u : 0u;
+    }
   }
-  const uint32_t target = (uint32_t)grid * (epoch + 1);   // X only: arrivals of this launch
+  pds_barrier();
+  epoch = __builtin_amdgcn_readfirstlane(misc_l[0]);   // every wave: the granule tags
+  dead = misc_l[1] != 0u;
+  const uint32_t target = (uint32_t)grid * (epoch + 1);   // X only: arrivals of this launch (ATT -> O)
   // diagnostic: s_memrealtime (100 MHz) at phase events k of (layer l, phase ph), lane 0 of the
   // X wave (k = 0 poll start, 1 poll done, 2 staged, 4 consumed, 5 signalled) or C wave 0 (3)
   auto ts = [&](int l, int ph, int k) {
@@ -325,6 +389,27 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       float part = 0.0f;
       if (idx < K8) {
         f16x8 hx = __builtin_bit_cast(f16x8, ld_sc1_b128(src, (uint32_t)idx * 16u));
+        const f16 s16 = (f16)0.0625f;
+        hx[2] *= s16; hx[3] *= s16; hx[6] *= s16; hx[7] *= s16;
+        *(f16x8*)(xl + 8 * idx) = hx;
+        const float lo = ((float)hx[0] + (float)hx[1]) + ((float)hx[4] + (float)hx[5]);
+        const float hi = ((float)hx[2] + (float)hx[3]) + ((float)hx[6] + (float)hx[7]);
+        part = 1032.0f * lo + 1152.0f * hi;
+      }
+      part = group_sum<16>(part);
+      if (idx < K8 && (lane & 15) == 0) corr[idx >> 4] = part;
+    }
+  };
+  // the same from granules: thread idx's 8 fp16 are 4 granules {fp16 pair, tag}
+  auto stage_f16_g = [&](const unsigned long long* g, int K, uint32_t tag) {
+    const int K8 = K >> 3;
+    for (int i0 = 0; i0 < K8; i0 += kPdsCThreads) {
+      const int idx = i0 + tid;
+      float part = 0.0f;
+      if (idx < K8) {
+        uint32_t w[4];
+        gather_gran<4>(g + 4 * idx, 1, tag, w, a.err, dead);
+        f16x8 hx = __builtin_bit_cast(f16x8, (u32x4){w[0], w[1], w[2], w[3]});
         const f16 s16 = (f16)0.0625f;
         hx[2] *= s16; hx[3] *= s16; hx[6] *= s16; hx[7] *= s16;
         *(f16x8*)(xl + 8 * idx) = hx;
@@ -403,9 +488,20 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
     t = group_sum<kWave>(t);
     return sqrtf(t / (float)K + a.eps);
   };
+  auto fold_rms_g = [&](int n_ss, int K, uint32_t tag) {
+    float t = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t w[1];
+      gather_gran<1>(a.ssg + (lane + 64 * j < n_ss ? lane + 64 * j : 0), 1, tag, w, a.err, dead);
+      t += lane + 64 * j < n_ss ? __builtin_bit_cast(float, w[0]) : 0.0f;
+    }
+    t = group_sum<kWave>(t);
+    return sqrtf(t / (float)K + a.eps);
+  };
   // X wave: residual epilogue of the workgroup's single tile (O, down) with the fold into the
   // next projection's input (epilogue TI_EPI_RESID_F32 with fold_x, M = 1)
-  auto resid_fold = [&](const float* nw) {
+  auto resid_fold = [&](const float* nw, uint32_t gtag) {   // gtag 0: plain stores (the lm_head's input)
     const int n = lane & 15;
     const float v = tile_sum(0, n);
     const float fw = gptr(nw)[t0o * 16 + n];
@@ -417,9 +513,14 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       ssacc = fmaf(rr, rr, ssacc);
     }
     const uint32_t hv = f2h(rr * fw), hp = lane_xor_u32<1>(hv);
-    if (lane < 16 && !(n & 1)) st_sc1_u32(a.fx + t0o * 16 + n, hv | (hp << 16));
     const float sw = group_sum<kWave>(ssacc);
-    if (lane == 0) st_sc1_f32(a.ss + bid, sw);
+    if (gtag) {
+      if (lane < 16 && !(n & 1)) st_gran(a.fxg + (t0o * 16 + n) / 2, hv | (hp << 16), gtag);
+      if (lane == 0) st_gran(a.ssg + bid, __builtin_bit_cast(uint32_t, sw), gtag);
+    } else {
+      if (lane < 16 && !(n & 1)) st_sc1_u32(a.fx + t0o * 16 + n, hv | (hp << 16));
+      if (lane == 0) st_sc1_f32(a.ss + bid, sw);
+    }
   };
 
   for (int l = 0; l < a.n_layers; ++l) {
@@ -431,13 +532,14 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
     {
       const PdsLin p = lin_params(PH_QKV);
       if (is_x) ts(l, PH_QKV, 0);
-      if (is_x && l > 0) pds_poll(ctr_of(l - 1, PH_DN), target, a.err, lane, dead);
       if (is_x) ts(l, PH_QKV, 1);
       stage_scales(p, ly.scales[0]);   // constant: before the hand-off
       pds_barrier();
       float rms = 1.0f;
-      stage_f16(a.fx, H);
-      if (is_x) rms = fold_rms(l == 0 ? a.n_ss0 : grid, H);
+      // layer 0: the fold step_begin wrote before this launch; then the previous down's granules
+      if (l == 0) stage_f16(a.fx, H);
+      else stage_f16_g(a.fxg, H, pds_tag(epoch, l - 1, PH_DN));
+      if (is_x) rms = l == 0 ? fold_rms(a.n_ss0, H) : fold_rms_g(grid, H, pds_tag(epoch, l - 1, PH_DN));
       pds_barrier();
       if (is_x) ts(l, PH_QKV, 2);
       ac = acur(l);   // the attention's first block: issued after the closing barrier
@@ -463,19 +565,19 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
           rv = (d & 1) == 0 ? fmaf(-partner, cs.y, v * cs.x) : fmaf(v, cs.x, partner * cs.y);
         }
         const uint32_t hv = f2h(rv), hp = lane_xor_u32<1>(hv);
+        const uint32_t tq = pds_tag(epoch, l, PH_QKV);
         if (ok) {
           if (ng < qd) {
-            st_sc1_f32(a.q + ng, rv);
+            st_gran(a.qg + ng, __builtin_bit_cast(uint32_t, rv), tq);
           } else if (!(n & 1)) {
             const bool is_k = qk;
             const int c = ng - qd - (is_k ? 0 : qd);
             const int kh = c / HD, d = c - kh * HD;
-            uint16_t* cache = is_k ? ly.k_cache : ly.v_cache;
-            __hip_atomic_store(gptr_w((uint32_t*)(cache + ((size_t)kh * a.max_seq + pos) * HD + d)), hv | (hp << 16),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint16_t* cache = is_k ? ly.k_cache : ly.v_cache;   // for later launches
+            gptr_w((uint32_t*)(cache + ((size_t)kh * a.max_seq + pos) * HD + d))[0] = hv | (hp << 16);
+            st_gran(a.kvg + ((size_t)kh * 2 + (is_k ? 0 : 1)) * (HD / 2) + d / 2, hv | (hp << 16), tq);
           }
         }
-        pds_signal(cl + PH_QKV * kPdsShards * kPdsShardWords, bid, lane);
         ts(l, PH_QKV, 5);
       }
       // the next phase's first units: issued once the epilogue's stores have drained (they
@@ -489,15 +591,20 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
     {
       if (is_x) {
         ts(l, PH_ATT, 0);
-        pds_poll(ctr_of(l, PH_QKV), target, a.err, lane, dead);
         ts(l, PH_ATT, 1);
-        // q of the head and, if this split holds it, the fresh K/V row at pos (sc1)
-        for (int j = lane; j < HD; j += kWave) q_l[j] = ld_sc1_f32(a.q + kvh * HD + j);
-        if (pos >= s0 && pos < s1 && lane < 32) {
-          const size_t e = (size_t)kv_off + (size_t)pos * HD;
-          const uint16_t* src = lane < 16 ? ly.k_cache : ly.v_cache;
-          const u32x4 v = ld_sc1_b128(src, (uint32_t)((e + (lane & 15) * 8) * 2));
-          *(u32x4*)((lane < 16 ? kf_l : vf_l) + (lane & 15) * 8) = v;
+        // q of the head and, if this split holds it, the fresh K/V row at pos: QKV's granules
+        const uint32_t tq = pds_tag(epoch, l, PH_QKV);
+        {
+          uint32_t w[2];
+          gather_gran<2>(a.qg + kvh * HD + lane, kWave, tq, w, a.err, dead);
+          q_l[lane] = __builtin_bit_cast(float, w[0]);
+          q_l[lane + kWave] = __builtin_bit_cast(float, w[1]);
+        }
+        if (pos >= s0 && pos < s1) {
+          uint32_t w[2];
+          gather_gran<2>(a.kvg + (size_t)kvh * 2 * (HD / 2) + lane, HD / 2, tq, w, a.err, dead);
+          ((uint32_t*)kf_l)[lane] = w[0];
+          ((uint32_t*)vf_l)[lane] = w[1];
         }
       }
       pds_barrier();
@@ -645,8 +752,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       pds_barrier();
       if (is_x) ts(l, PH_O, 4);
       if (is_x) {
-        resid_fold(ly.ffn_norm);
-        pds_signal(cl + PH_O * kPdsShards * kPdsShardWords, bid, lane);
+        resid_fold(ly.ffn_norm, pds_tag(epoch, l, PH_O));
         ts(l, PH_O, 5);
       }
       // the next phase's first units: issued once the epilogue's stores have drained (they
@@ -661,13 +767,12 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
     {
       const PdsLin p = lin_params(PH_GU);
       if (is_x) ts(l, PH_GU, 0);
-      if (is_x) pds_poll(ctr_of(l, PH_O), target, a.err, lane, dead);
       if (is_x) ts(l, PH_GU, 1);
       stage_scales(p, ly.scales[2]);
       pds_barrier();
       float rms = 1.0f;
-      stage_f16(a.fx, H);
-      if (is_x) rms = fold_rms(grid, H);
+      stage_f16_g(a.fxg, H, pds_tag(epoch, l, PH_O));
+      if (is_x) rms = fold_rms_g(grid, H, pds_tag(epoch, l, PH_O));
       pds_barrier();
       if (is_x) ts(l, PH_GU, 2);
       GCur gnx = gcur(l, PH_DN);
@@ -683,9 +788,8 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
           const float up = lane_xor<8>(v);
           const float s = v / (1.0f + expf(-v));
           const uint32_t hv = f2h(up * s), hp = lane_xor_u32<1>(hv);
-          if (ok && n < 8 && !(n & 1)) st_sc1_u32(a.act + (p.t0 + tl) * 8 + n, hv | (hp << 16));
+          if (ok && n < 8 && !(n & 1)) st_gran(a.actg + ((p.t0 + tl) * 8 + n) / 2, hv | (hp << 16), pds_tag(epoch, l, PH_GU));
         }
-        pds_signal(cl + PH_GU * kPdsShards * kPdsShardWords, bid, lane);
         ts(l, PH_GU, 5);
       }
       // the next phase's first units: issued once the epilogue's stores have drained (they
@@ -700,11 +804,10 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
     {
       const PdsLin p = lin_params(PH_DN);
       if (is_x) ts(l, PH_DN, 0);
-      if (is_x) pds_poll(ctr_of(l, PH_GU), target, a.err, lane, dead);
       if (is_x) ts(l, PH_DN, 1);
       stage_scales(p, ly.scales[3]);
       pds_barrier();
-      stage_f16(a.act, I);
+      stage_f16_g(a.actg, I, pds_tag(epoch, l, PH_GU));
       pds_barrier();
       if (is_x) ts(l, PH_DN, 2);
       GCur gnx = gcur(l + 1, PH_QKV);
@@ -713,8 +816,9 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       pds_barrier();
       if (is_x) ts(l, PH_DN, 4);
       if (is_x) {
-        resid_fold(l + 1 < a.n_layers ? a.layers[l + 1].attn_norm : a.out_norm);
-        pds_signal(cl + PH_DN * kPdsShards * kPdsShardWords, bid, lane);
+        // the last layer's fold goes to the lm_head launch: plain write-through stores
+        resid_fold(l + 1 < a.n_layers ? a.layers[l + 1].attn_norm : a.out_norm,
+                   l + 1 < a.n_layers ? pds_tag(epoch, l, PH_DN) : 0u);
         ts(l, PH_DN, 5);
       }
       // the next phase's first units: issued once the epilogue's stores have drained (they
@@ -734,10 +838,14 @@ using namespace ti;
 
 extern "C" {
 
+size_t ti_pds_granule_words(int H, int I, int qd, int heads, int grid) { return pds_gran_words(H, I, qd, heads, grid); }
+
 int ti_pds_decode(const ti_pds_args* h, ti_stream_t s) {
   if (!h || !h->layers || !h->pos || !h->h || !h->fx || !h->ss || !h->q || !h->act || !h->part_o || !h->part_ml ||
-      !h->ctr || !h->launches || !h->err || !h->zero || !h->rope_cs || !h->out_norm)
+      !h->ctr || !h->launches || !h->err || !h->zero || !h->rope_cs || !h->out_norm || !h->gran)
     return ti_set_error(TI_ERR_ARG, "ti_pds_decode: null pointer");
+  if (h->n_layers < 1 || h->n_layers > 64)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_pds_decode: %d layers (granule tags hold 64)", h->n_layers);
   if (h->head_dim != kPdsHd || h->heads != h->kv_heads || h->heads * kPdsSplits != h->grid || h->grid > 256 ||
       h->qd != h->heads * h->head_dim || h->H % 128 || h->I % 128 || h->qd % 128 || h->H / 16 != h->grid ||
       h->qd > 4096 || h->I + 8 > kLdsXBytes / 2 || h->H + 8 > kLdsXBytes / 2)
@@ -778,6 +886,11 @@ int ti_pds_decode(const ti_pds_args* h, ti_stream_t s) {
   a.err = h->err;
   a.zero = (const u32x4*)h->zero;
   a.ts = h->ts;
+  a.fxg = h->gran;
+  a.ssg = a.fxg + h->H / 2;
+  a.qg = a.ssg + h->grid;
+  a.kvg = a.qg + h->qd;
+  a.actg = a.kvg + (size_t)h->heads * kPdsHd;
   // per device: the LDS attribute, and co-residency -- every wait in the kernel needs all `grid`
   // workgroups resident at once (one per CU): the occupancy query times the CU count must cover
   // the grid, or nothing is launched.  (Residency taken by other work at run time is caught by

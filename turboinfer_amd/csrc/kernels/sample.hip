@@ -17,8 +17,9 @@
 // select over the whole row, LDS histograms, when there are more than 2048 of them); the
 // survivors (ties lowest index first) are compacted in index order with block scans.  (A
 // radix pass over the row costs ~14 us: one bin takes most keys, so the LDS atomics
-// serialise.)  k above 1024 (up to TI_SAMPLE_MAX_K) goes to the radix select directly, and
-// the per-survivor steps stride over the survivors.  Differences to the reference: exp / log are the device's (<= 1 ulp from
+// serialise.)  k above 1024 goes to the radix select directly, and the per-survivor steps
+// stride over the survivors; above TI_SAMPLE_MAX_K (any k up to V) the survivor arrays live in a
+// per-row HBM workspace instead of LDS (sample_kernel<true>).  Differences to the reference: exp / log are the device's (<= 1 ulp from
 // glibc), and equal logits at the k-th place / equal probabilities at the top-p cut are taken
 // lowest index first (libstdc++'s std::sort leaves their order unspecified).
 #include <math.h>
@@ -43,7 +44,22 @@ struct SampArgs {
   int32_t* tokens;             // [M], nullable
   float* logprobs;             // [M][lp_stride], nullable
   int32_t lp_stride;
+  char* ws;                    // top_k > TI_SAMPLE_MAX_K: per-row survivor arrays in HBM (ws_bytes each)
+  size_t ws_bytes;
 };
+
+// Survivor arrays of one row when they do not fit in LDS (top_k > TI_SAMPLE_MAX_K, up to V):
+// val f32[V], idx i32[V], p f32[V], sorted f32[V], rank i32[V] (each 16-byte aligned: the
+// sequential sums read float4s), then the top-p sort keys u64[P]
+// (P = the power of two >= V, at least 64).  Read and written by the row's one workgroup only
+// (its barriers order them).
+__host__ __device__ inline int samp_pow2(int n) {
+  int P = 64;
+  while (P < n) P <<= 1;
+  return P;
+}
+__host__ __device__ inline size_t samp_ws_array(int V) { return ((size_t)V * 4 + 15) & ~(size_t)15; }   // 16-B aligned
+__host__ __device__ inline size_t samp_ws_row_bytes(int V) { return 5 * samp_ws_array(V) + (size_t)samp_pow2(V) * 8; }
 
 __device__ __forceinline__ uint32_t samp_key(float v) {
   const uint32_t u = __builtin_bit_cast(uint32_t, v);
@@ -79,24 +95,42 @@ __device__ int block_excl_scan(int v, int* total, int* s_w) {
   return r;
 }
 
+// BIG: top_k above TI_SAMPLE_MAX_K -- the survivor arrays live in the row's HBM workspace
+// (the same steps on them; the sequential sums read them from global memory).
+template <bool BIG>
 __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) {
+  constexpr int LK = BIG ? 1 : TI_SAMPLE_MAX_K;   // LDS survivor capacity
   __shared__ uint32_t hist[256];
   __shared__ int s_w[kSampWaves + 1];
   __shared__ uint32_t s_prefix;
   __shared__ int s_left, s_tok;
   __shared__ float s_lp;
-  __shared__ float s_val[TI_SAMPLE_MAX_K];
-  __shared__ __attribute__((aligned(16))) float s_p[TI_SAMPLE_MAX_K], s_sorted[TI_SAMPLE_MAX_K];
+  __shared__ float l_val[LK];
+  __shared__ __attribute__((aligned(16))) float l_p[LK], l_sorted[LK];
   __shared__ int s_cut;
-  __shared__ int s_idx[TI_SAMPLE_MAX_K];
-  __shared__ int s_rank[TI_SAMPLE_MAX_K];
-  __shared__ unsigned long long s_key[TI_SAMPLE_MAX_K];   // top-p sort keys
+  __shared__ int l_idx[LK];
+  __shared__ int l_rank[LK];
+  __shared__ unsigned long long l_key[LK];   // top-p sort keys
   __shared__ float s_mx[kSampWaves];
-  constexpr int kCand = 2048;
+  constexpr int kCand = BIG ? 1 : 2048;
   __shared__ uint32_t s_ck[kCand];
   __shared__ int s_ci[kCand];
   __shared__ uint8_t s_cf[kCand];
   const int m = blockIdx.x, tid = threadIdx.x, V = a.V, k = a.top_k;
+  const int CAP = BIG ? V : TI_SAMPLE_MAX_K;
+  float *s_val = l_val, *s_p = l_p, *s_sorted = l_sorted;
+  int *s_idx = l_idx, *s_rank = l_rank;
+  unsigned long long* s_key = l_key;
+  if constexpr (BIG) {
+    char* w = a.ws + (size_t)m * a.ws_bytes;
+    const size_t A = samp_ws_array(V);
+    s_val = (float*)w;
+    s_idx = (int*)(w + A);
+    s_p = (float*)(w + 2 * A);
+    s_sorted = (float*)(w + 3 * A);
+    s_rank = (int*)(w + 4 * A);
+    s_key = (unsigned long long*)(w + 5 * A);
+  }
   const float* row = a.logits + (size_t)m * a.ldl;
   const bool temp = a.temperature != 1.0f && a.temperature > 0.0f;
   auto lg = [&](int i) { return temp ? row[i] / a.temperature : row[i]; };
@@ -200,7 +234,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
   // (k above the thread count: no k-th maximum to bound with, straight to the radix select)
   int tot = kCand + 1, cbase = 0;
   uint32_t tau0 = 0u;
-  if (k <= kSampThreads) {
+  if (!BIG && k <= kSampThreads) {
     uint32_t tmax = 0u;   // below every finite key
     own([&](int, uint32_t key, bool ok) { tmax = ok && key > tmax ? key : tmax; });
     int unused;
@@ -211,7 +245,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
   }
   const int C_tot = tot;
   int n;
-  if (C_tot <= kCand) {
+  if (!BIG && C_tot <= kCand) {
     int run = cbase;
     own([&](int i, uint32_t key, bool ok) {
       const bool c = ok && key >= tau0;
@@ -279,7 +313,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
       const unsigned long long me = __ballot(eq);
       const bool keep = (ok && key > kth) || (eq && eq_run + below(me) < need_eq);
       const unsigned long long mk = __ballot(keep);
-      if (keep && run + below(mk) < TI_SAMPLE_MAX_K) {
+      if (keep && run + below(mk) < CAP) {
         s_val[run + below(mk)] = temp ? row[i] / a.temperature : row[i];
         s_idx[run + below(mk)] = i;
       }
@@ -287,7 +321,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
       eq_run += __popcll(me);
     });
     __syncthreads();
-    n = min(tot, TI_SAMPLE_MAX_K);   // == k
+    n = min(tot, CAP);   // == k
   }
 
   // ---- softmax over the survivors (the others are exp(-inf) = 0 in the reference's loops)
@@ -425,19 +459,33 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(const SampArgs a) 
 
 }  // namespace ti
 
-static int sample_launch(const ti::SampArgs& a, int M, ti_stream_t stream) {
+extern "C" size_t ti_sample_workspace_bytes(int V, int top_k) {
+  return V >= 1 && top_k > TI_SAMPLE_MAX_K ? ti::samp_ws_row_bytes(V) : 0;
+}
+
+static int sample_launch(ti::SampArgs a, int M, ti_stream_t stream) {
   if (!a.logits || !a.draws || M < 1 || a.V < 1 || a.ldl < a.V || a.draw_stride < 1)
     return ti_set_error(TI_ERR_ARG, "ti_sample: bad arguments");
-  if (a.top_k < 1 || a.top_k > TI_SAMPLE_MAX_K || a.top_k > a.V)
-    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_sample: top_k %d not in [1, min(V, %d)]", a.top_k, TI_SAMPLE_MAX_K);
-  hipLaunchKernelGGL(ti::sample_kernel, dim3(M), dim3(ti::kSampThreads), 0, (hipStream_t)stream, a);
+  if (a.top_k < 1 || a.top_k > a.V)
+    return ti_set_error(TI_ERR_ARG, "ti_sample: top_k %d not in [1, V = %d]", a.top_k, a.V);
+  if (a.top_k > TI_SAMPLE_MAX_K) {
+    if (!a.ws)
+      return ti_set_error(TI_ERR_ARG, "ti_sample: top_k %d > %d needs a workspace (ti_sample_workspace_bytes)", a.top_k,
+                          TI_SAMPLE_MAX_K);
+    a.ws_bytes = ti::samp_ws_row_bytes(a.V);
+    hipLaunchKernelGGL(ti::sample_kernel<true>, dim3(M), dim3(ti::kSampThreads), 0, (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL(ti::sample_kernel<false>, dim3(M), dim3(ti::kSampThreads), 0, (hipStream_t)stream, a);
+  }
   TI_LAUNCH_CHECK("sample_kernel");
   return TI_OK;
 }
 
-extern "C" int ti_sample_device(const float* logits, int ldl, int M, int V, float temperature, int top_k, float top_p,
-                                const float* draws, int32_t* tokens, float* logprobs, ti_stream_t stream) {
+extern "C" int ti_sample_device_ws(const float* logits, int ldl, int M, int V, float temperature, int top_k,
+                                   float top_p, const float* draws, int32_t* tokens, float* logprobs, void* ws,
+                                   ti_stream_t stream) {
   ti::SampArgs a{};
+  a.ws = (char*)ws;
   a.logits = logits;
   a.ldl = ldl;
   a.V = V;
@@ -453,10 +501,17 @@ extern "C" int ti_sample_device(const float* logits, int ldl, int M, int V, floa
   return sample_launch(a, M, stream);
 }
 
-extern "C" int ti_sample_step(const float* logits, int ldl, int M, int V, float temperature, int top_k, float top_p,
-                              const float* draws, int draw_stride, const int32_t* step_ctr, int advance,
-                              const int32_t* n_in, unsigned long long* argmax, float* logprobs, ti_stream_t stream) {
+extern "C" int ti_sample_device(const float* logits, int ldl, int M, int V, float temperature, int top_k, float top_p,
+                                const float* draws, int32_t* tokens, float* logprobs, ti_stream_t stream) {
+  return ti_sample_device_ws(logits, ldl, M, V, temperature, top_k, top_p, draws, tokens, logprobs, nullptr, stream);
+}
+
+extern "C" int ti_sample_step_ws(const float* logits, int ldl, int M, int V, float temperature, int top_k,
+                                 float top_p, const float* draws, int draw_stride, const int32_t* step_ctr, int advance,
+                                 const int32_t* n_in, unsigned long long* argmax, float* logprobs, void* ws,
+                                 ti_stream_t stream) {
   ti::SampArgs a{};
+  a.ws = (char*)ws;
   a.logits = logits;
   a.ldl = ldl;
   a.V = V;
@@ -473,4 +528,11 @@ extern "C" int ti_sample_step(const float* logits, int ldl, int M, int V, float 
   a.lp_stride = draw_stride;
   if (!step_ctr || !argmax) return ti_set_error(TI_ERR_ARG, "ti_sample_step: step_ctr and argmax required");
   return sample_launch(a, M, stream);
+}
+
+extern "C" int ti_sample_step(const float* logits, int ldl, int M, int V, float temperature, int top_k, float top_p,
+                              const float* draws, int draw_stride, const int32_t* step_ctr, int advance,
+                              const int32_t* n_in, unsigned long long* argmax, float* logprobs, ti_stream_t stream) {
+  return ti_sample_step_ws(logits, ldl, M, V, temperature, top_k, top_p, draws, draw_stride, step_ctr, advance, n_in,
+                           argmax, logprobs, nullptr, stream);
 }
