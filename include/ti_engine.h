@@ -59,6 +59,10 @@ int ti_engine_set_tensor(ti_engine* e, int slot, int layer, const float* data, i
  * scales d [K/32][N], weight = d * q -- no re-quantization.  ti_engine_set_tensor on such an
  * engine quantizes fp32 weights per 32-block (absmax / 7 or / 127). */
 int ti_engine_set_tensor_q(ti_engine* e, int slot, int layer, const int8_t* q, const uint16_t* d);
+/* GGUF Q4_1 blocks (model_loader.cpp:165-182, ggml's format) kept exact on an engine with bits
+ * 4 | TI_BITS_G32 | TI_BITS_AFF: q uint8 [K][N_src] (0..15), d and m fp16 [K/32][N_src],
+ * weight = d * q + m (ti_wpack_q1_host). */
+int ti_engine_set_tensor_q1(ti_engine* e, int slot, int layer, const uint8_t* q, const uint16_t* d, const uint16_t* m);
 /* Synthetic model of SURVEY 8(d) generated on the device (bit-identical to the oracle's
  * or_model_synth for the same seed / jitter). */
 int ti_engine_synth(ti_engine* e, uint64_t seed, float norm_jitter);

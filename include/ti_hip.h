@@ -89,7 +89,9 @@ size_t ti_wpack_scale_bytes(int bits, int K, int N);
  *   TI_ROWS_CONCAT      : row_offset + c
  *   TI_ROWS_INTERLEAVE8 : 16*(c/8) + (c%8) + row_offset   (row_offset 0 = gate, 8 = up)
  * scale_mode: per group of 128 (absmax/7 or /127, reference quantize_to_int* formula per
- * group), one per-tensor scale (reference Quantizer), or unit (reference raw cast). */
+ * group), one per-tensor scale (reference Quantizer), or unit (reference raw cast).
+ * bits | TI_BITS_G32: per 32-block absmax scales.  bits 4 | TI_BITS_G32 | TI_BITS_AFF: ggml's
+ * Q4_1 rounding per 32-block (d = (max - min) / 15, m = min; scale_mode ignored). */
 int ti_wpack_host(const float* w, int K, int N_src, int N_total, int bits, int scale_mode,
                   int row_map, int row_offset, void* tiles, uint16_t* scales);
 
@@ -106,6 +108,15 @@ int ti_wpack_host(const float* w, int K, int N_src, int N_total, int bits, int s
  * Q4_0 / Q8_0 block (bits = 4 or 8, TI_BITS_G32 implied; rows mapped as in ti_wpack_host). */
 int ti_wpack_q_host(const int8_t* q, const uint16_t* d, int K, int N_src, int N_total, int bits, int row_map,
                     int row_offset, void* tiles, uint16_t* scales);
+/* Affine group-32 int4 (GGUF Q4_1 blocks, ggml's format: weight = d * q + m, q in 0..15, d and m
+ * fp16 per 32-weight block): bits = 4 | TI_BITS_G32 | TI_BITS_AFF.  Tiles hold q - 8 like Q4_0
+ * blocks; the scale buffer holds d [N/16][K/128][4][16] followed by m in the same layout
+ * (ti_wpack_scale_bytes counts both).  The kernels add (8 d + m) * (the block's sum of x) per
+ * block.  Fused kernel only (more rows run in pieces); no tile GEMM, no packed rows. */
+#define TI_BITS_AFF 64
+/* q uint8 [K][N_src] (0..15), d and m fp16 [K/32][N_src]: weight(k, c) = d * q + m. */
+int ti_wpack_q1_host(const uint8_t* q, const uint16_t* d, const uint16_t* m, int K, int N_src, int N_total, int row_map,
+                     int row_offset, void* tiles, uint16_t* scales);
 
 /* The synthetic model of SURVEY 8(d) generated straight into device tiles:
  * element (k, c) of tensor `tensor_id` = u(seed, tensor_id, k*N_src + c) * amp,

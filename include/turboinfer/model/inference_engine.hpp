@@ -27,7 +27,9 @@
 //     reference_compat path -- placeholder embeddings, attention bypass, ReLU FFN, fp32.
 // Weight formats: fp32 tensors are packed as `weight_bits` (4/8: symmetric group-128
 // quantization, 16: fp16); int8 / int32 tensors from Quantizer::quantize_model keep their
-// integer values with unit scale (the reference's raw-cast semantics).
+// integer values with unit scale (the reference's raw-cast semantics).  GGUF Q4_0 / Q4_1 / Q8_0
+// checkpoints keep their 32-weight blocks exactly (weight_bits 0 picks 4 | 32, 4 | 32 | 64 or
+// 8 | 32: TI_BITS_G32, TI_BITS_AFF of ti_hip.h).
 #pragma once
 
 #include <cstddef>
@@ -53,7 +55,7 @@ struct InferenceConfig {
   bool use_cache = true;
   core::ComputeDevice device = core::ComputeDevice::kAuto;
   // ---- MI355X additions (trailing, defaulted)
-  int weight_bits = 0;          ///< 4 / 8 / 16 for fp32 weights; 0 = auto (fp32 -> 16, ints -> their width)
+  int weight_bits = 0;          ///< 4 / 8 / 16 (| 32 group-32, | 32 | 64 Q4_1); 0 = auto (fp32 -> 16, ints -> their width, GGUF blocks kept)
   int gpu_index = 0;            ///< HIP device this engine binds
 };
 

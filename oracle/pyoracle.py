@@ -314,6 +314,23 @@ class OracleModel:
             out[p + "ffn_norm.weight"] = arr(m.ffn_norm[l], H)
         return out
 
+    def set_weights(self, w):
+        """Overwrite the oracle's tensors in place from a dict shaped like weights() (e.g. the
+        same tensors after a GGUF quantize -> dequantize round trip)."""
+        m = C.cast(self.ptr, C.POINTER(_OrModel)).contents
+        c = self.cfg
+        ptrs = {"token_embeddings.weight": m.emb, "norm.weight": m.out_norm, "lm_head.weight": m.lm_head}
+        for l in range(c["layers"]):
+            p = f"layers.{l}."
+            ptrs.update({p + "attention.q_proj.weight": m.wq[l], p + "attention.k_proj.weight": m.wk[l],
+                         p + "attention.v_proj.weight": m.wv[l], p + "attention.o_proj.weight": m.wo[l],
+                         p + "feed_forward.w3.weight": m.wg[l], p + "feed_forward.w1.weight": m.wu[l],
+                         p + "feed_forward.w2.weight": m.wd[l], p + "attention_norm.weight": m.attn_norm[l],
+                         p + "ffn_norm.weight": m.ffn_norm[l]})
+        for k, v in w.items():
+            a = np.ascontiguousarray(v, np.float32).reshape(-1)
+            np.ctypeslib.as_array(ptrs[k], shape=(a.size,))[:] = a
+
     def step(self, token, kv_round_f16=True):
         logits = np.empty(self.cfg["vocab"], np.float32)
         t = self.o.lib.or_decode_step(self.ptr, int(token), logits, int(kv_round_f16))

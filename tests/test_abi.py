@@ -138,3 +138,28 @@ def test_int4_range_is_reference_symmetric(oracle):
     tiles, scales = T.wpack_host(w, 4)
     q, _ = unpack_tiles(tiles, scales, 4, 128, 16)
     assert q.min() >= -7 and q.max() <= 7 and q.min() == -7 or q.max() == 7
+
+
+def test_wpack_q41_rounding_matches_ggml(L):
+    """fp32 weights packed for an affine group-32 engine (ti_wpack_host, bits 4 | G32 | AFF)
+    equal the packing of ggml's Q4_1 blocks of the same weights (gguf_oracle.quant_q4_1, the
+    reference quantizer) through ti_wpack_q1_host: same rounding, same fp16 d and m."""
+    import gguf_oracle as G
+    K, N = 256, 48
+    rng = np.random.RandomState(11)
+    w = (rng.standard_normal((K, N)) * 0.05 + rng.uniform(-0.02, 0.02, (1, N))).astype(np.float32)
+    w[32:64, 5] = 0.125                           # a constant block: d = 0
+    bits = 4 | T.BITS_G32 | T.BITS_AFF
+    tb, sb = L.ti_wpack_tile_bytes(bits, K, N), L.ti_wpack_scale_bytes(bits, K, N)
+    assert sb == 2 * L.ti_wpack_scale_bytes(4 | T.BITS_G32, K, N)
+    t1, s1 = np.zeros(tb, np.uint8), np.zeros(sb // 2, np.uint16)
+    assert L.ti_wpack_host(w.ctypes.data, K, N, N, bits, T.SCALE_GROUP, 0, 0, t1.ctypes.data, s1.ctypes.data) == 0
+    raw = np.frombuffer(G.quant_q4_1(np.ascontiguousarray(w.T)), np.uint8).reshape(N, K // 32, 20)
+    d = raw[:, :, 0:2].copy().view(np.uint16)[..., 0].T.copy()
+    m = raw[:, :, 2:4].copy().view(np.uint16)[..., 0].T.copy()
+    qs = raw[:, :, 4:]
+    q = np.concatenate([qs & 15, qs >> 4], axis=2).reshape(N, K).T.copy()   # [K][N], 0..15
+    t2, s2 = np.zeros(tb, np.uint8), np.zeros(sb // 2, np.uint16)
+    assert L.ti_wpack_q1_host(q.ctypes.data, d.ctypes.data, m.ctypes.data, K, N, N, 0, 0, t2.ctypes.data,
+                              s2.ctypes.data) == 0
+    assert np.array_equal(t1, t2) and np.array_equal(s1, s2)

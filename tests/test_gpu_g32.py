@@ -218,3 +218,179 @@ def test_engine_g32_prefill_vs_oracle(ti, oracle):
     assert got[0].tolist() == ref
     tol = 2e-3 * float(np.max(np.abs(ref_lg[-1])))
     assert float(np.max(np.abs(glg[0].astype(np.float64) - ref_lg[-1]))) <= tol
+
+
+# ------------------------------------------------------------------ affine blocks (GGUF Q4_1)
+def q1_weight(rng, K, N):
+    """Q4_1 blocks as ggml stores them: q in 0..15, fp16 d and m per 32 weights (m near -8 d, as
+    the quantizer's block minimum of centred weights); w = q * d + m in fp32 (gguf.cpp
+    dequant_q4_1's expression)."""
+    q = rng.randint(0, 16, size=(K, N)).astype(np.uint8)
+    amp = 0.3 / np.sqrt(K) / 4.0
+    d = (rng.uniform(0.5, 1.5, size=(K // 32, N)) * amp).astype(f16)
+    m = (-d.astype(f32) * rng.uniform(5.0, 11.0, size=d.shape)).astype(f16)
+    D, Mn = np.repeat(d.astype(f32), 32, axis=0), np.repeat(m.astype(f32), 32, axis=0)
+    w = (q.astype(f32) * D + Mn).astype(f32)
+    parts = np.abs((q.astype(f32) - 8) * D) + np.abs(8 * D + Mn)   # the kernel's two terms
+    return q, d, m, w, parts
+
+
+def pack_q1(ti, q, d, m):
+    L = ti.lib()
+    K, N = q.shape
+    bits = 4 | ti.BITS_G32 | ti.BITS_AFF
+    tiles = np.zeros(L.ti_wpack_tile_bytes(bits, K, N), np.uint8)
+    scales = np.zeros(L.ti_wpack_scale_bytes(bits, K, N) // 2, np.uint16)
+    qa = np.ascontiguousarray(q)
+    da, ma = np.ascontiguousarray(d).view(np.uint16), np.ascontiguousarray(m).view(np.uint16)
+    ti.check(L.ti_wpack_q1_host(qa.ctypes.data, da.ctypes.data, ma.ctypes.data, K, N, N, 0, 0, tiles.ctypes.data,
+                                scales.ctypes.data))
+    return ti.DeviceBuffer.from_array(tiles), ti.DeviceBuffer.from_array(scales)
+
+
+def run_gemm_q1(ti, td, sd, x, x_kind, M, N, K, norm=None):
+    return run_gemm(ti, td, sd, 4 | ti.BITS_AFF, x, x_kind, M, N, K, norm)
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 128, 16), (1, 4096, 256), (3, 384, 80), (16, 1024, 64), (2, 11008, 32),
+                                   (40, 4096, 128)])
+def test_gemm_q41_matches_exact_blocks(ti, M, K, N):
+    """Affine blocks: y = x . (d q + m) with the block term (8 d + m) * sum(x over the block)
+    added to the offset-8 int4 product; held to the fp32-summation bound of both terms."""
+    rng = np.random.RandomState(7 * K + N + M)
+    q, d, m, w, parts = q1_weight(rng, K, N)
+    td, sd = pack_q1(ti, q, d, m)
+    for x_kind, xd in ((ti.X_F32, f32), (ti.X_F16, f16)):
+        x = rng.standard_normal((M, K)).astype(xd)
+        y = run_gemm_q1(ti, td, sd, x, x_kind, M, N, K)
+        xa = x.astype(f16).astype(f32)
+        ref = xa.astype(np.float64) @ w.astype(np.float64)
+        bound = 2e-5 * (np.abs(xa).astype(np.float64) @ parts.astype(np.float64)) + 1e-6
+        err = np.abs(y.astype(np.float64) - ref)
+        assert np.all(err <= bound), f"{x_kind}: max err {err.max()} vs bound {bound.min()}"
+
+
+@pytest.mark.parametrize("M", [1, 4])
+def test_gemm_q41_rmsnorm_prologue(ti, oracle, M):
+    K, N = 2048, 64
+    rng = np.random.RandomState(41 + M)
+    q, d, m, w, parts = q1_weight(rng, K, N)
+    td, sd = pack_q1(ti, q, d, m)
+    x = (rng.standard_normal((M, K)) * 3).astype(f32)
+    nw = (1 + 0.1 * rng.standard_normal(K)).astype(f32)
+    y = run_gemm_q1(ti, td, sd, x, ti.X_F32_RMSNORM, M, N, K, norm=nw)
+    xa = oracle.rms_norm(x, nw).astype(f16).astype(f32)
+    bound = (2e-5 + 1e-3) * (np.abs(xa) @ parts) + 1e-6   # one fp16 ulp of the normalised row
+    assert np.all(np.abs(y - xa.astype(np.float64) @ w.astype(np.float64)) <= bound)
+
+
+def test_q41_limits(ti):
+    L = ti.lib()
+    bits = 4 | ti.BITS_G32 | ti.BITS_AFF
+    assert L.ti_gemm_max_rows(bits, ti.X_F16, 64, 4096) == ti.GEMM_MAX_ROWS   # fused 16-row pieces
+    assert L.ti_gemm_max_rows(bits, ti.X_F16_PACKED, 64, 4096) == 0
+    q = np.full((128, 16), 16, np.uint8)   # outside 0..15
+    d = np.zeros((4, 16), f16)
+    with pytest.raises(ti.TiError):
+        pack_q1(ti, q, d, d)
+
+
+@pytest.mark.parametrize("prompt_len", [1, 100])
+def test_engine_q41_vs_oracle(ti, oracle, prompt_len):
+    """A GQA model whose every linear weight is exact Q4_1 blocks (engine bits 4 | G32 | AFF,
+    weights through ti_engine_set_tensor_q1) against the oracle with the dequantized weights:
+    a prompt (100 tokens: prefill in fused 16-row pieces) then greedy decode, logits within the
+    engine tests' bar."""
+    from pyoracle import OracleModel, _OrModel
+    cfg = G32_CFG
+    V, H, NL, I = cfg["vocab"], cfg["hidden"], cfg["layers"], cfg["inter"]
+    qd, kvd = cfg["heads"] * cfg["head_dim"], cfg["kv_heads"] * cfg["head_dim"]
+    m = OracleModel(oracle, cfg, 79, 0.1)
+    base = m.weights()
+    mm = C.cast(m.ptr, C.POINTER(_OrModel)).contents
+    rng = np.random.RandomState(500 + prompt_len)
+    e = ti.Engine(V, H, NL, cfg["heads"], cfg["kv_heads"], cfg["head_dim"], I, bits=4 | ti.BITS_G32 | ti.BITS_AFF,
+                  max_seq=cfg["max_seq"], max_batch=1, rope_theta=cfg["rope_theta"], eps=cfg["eps"])
+    e.set_tensor(ti.E_EMBED, 0, base["token_embeddings.weight"])
+    e.set_tensor(ti.V_OUT_NORM, 0, base["norm.weight"])
+
+    def linear(slot, layer, ptr, K, N):
+        q, d, mn, w, _ = q1_weight(rng, K, N)
+        e.set_tensor_q1(slot, layer, q, d, mn)
+        np.ctypeslib.as_array(ptr, shape=(K * N,))[:] = w.reshape(-1)
+
+    linear(ti.W_LM_HEAD, 0, mm.lm_head, H, V)
+    for l in range(NL):
+        p = f"layers.{l}."
+        e.set_tensor(ti.V_ATTN_NORM, l, base[p + "attention_norm.weight"])
+        e.set_tensor(ti.V_FFN_NORM, l, base[p + "ffn_norm.weight"])
+        linear(ti.W_Q, l, mm.wq[l], H, qd)
+        linear(ti.W_K, l, mm.wk[l], H, kvd)
+        linear(ti.W_V, l, mm.wv[l], H, kvd)
+        linear(ti.W_O, l, mm.wo[l], qd, H)
+        linear(ti.W_GATE, l, mm.wg[l], H, I)
+        linear(ti.W_UP, l, mm.wu[l], H, I)
+        linear(ti.W_DOWN, l, mm.wd[l], I, H)
+    prompt = np.random.RandomState(33).randint(0, V, size=prompt_len).tolist()
+    n_new = 4
+    ref, ref_lg = [], []
+    tok, lg = None, None
+    for t in prompt:
+        tok, lg = m.step(t)
+    for _ in range(n_new):
+        ref.append(tok)
+        ref_lg.append(lg)
+        tok, lg = m.step(tok)
+    got, glg = e.generate([prompt], n_new, want_logits=True)
+    m.close()
+    e.close()
+    tol = 2e-3 * float(np.max(np.abs(ref_lg[-1])))
+    for i, lgi in enumerate(ref_lg):
+        s = np.sort(lgi)
+        if s[-1] - s[-2] <= 3 * 2e-3 * float(np.max(np.abs(lgi))):
+            pytest.fail(f"step {i}: reference margin too small")
+    assert got[0].tolist() == ref
+    assert float(np.max(np.abs(glg[0].astype(np.float64) - ref_lg[-1]))) <= tol
+
+
+def test_engine_q41_fp32_upload_matches_ggml_rounding(ti, oracle):
+    """ti_engine_set_tensor (fp32) on an affine engine rounds each 32-block as ggml's Q4_1
+    quantizer does (gguf_oracle.quant_q4_1): the same weights through set_tensor and through the
+    oracle's quantize -> dequantize give the same greedy tokens and close logits."""
+    import gguf_oracle as G
+    from pyoracle import OracleModel
+    cfg = G32_CFG
+    V, H, NL, I = cfg["vocab"], cfg["hidden"], cfg["layers"], cfg["inter"]
+    m = OracleModel(oracle, cfg, 80, 0.1)
+    w = m.weights()
+    e = ti.Engine(V, H, NL, cfg["heads"], cfg["kv_heads"], cfg["head_dim"], I, bits=4 | ti.BITS_G32 | ti.BITS_AFF,
+                  max_seq=cfg["max_seq"], max_batch=1, rope_theta=cfg["rope_theta"], eps=cfg["eps"])
+    slots = {"attention.q_proj.weight": ti.W_Q, "attention.k_proj.weight": ti.W_K, "attention.v_proj.weight": ti.W_V,
+             "attention.o_proj.weight": ti.W_O, "feed_forward.w3.weight": ti.W_GATE, "feed_forward.w1.weight": ti.W_UP,
+             "feed_forward.w2.weight": ti.W_DOWN, "attention_norm.weight": ti.V_ATTN_NORM,
+             "ffn_norm.weight": ti.V_FFN_NORM}
+    deq = dict(w)
+
+    def q41(v):   # ggml blocks run along K of each output column: the [N][K] tensor's rows
+        a = np.ascontiguousarray(v.T, f32)
+        return np.ascontiguousarray(G.dequant(G.quant_q4_1(a), G.T_Q4_1, a.size).reshape(a.shape).T)
+
+    e.set_tensor(ti.E_EMBED, 0, w["token_embeddings.weight"])
+    e.set_tensor(ti.V_OUT_NORM, 0, w["norm.weight"])
+    e.set_tensor(ti.W_LM_HEAD, 0, w["lm_head.weight"])
+    deq["lm_head.weight"] = q41(w["lm_head.weight"])
+    for l in range(NL):
+        for k, slot in slots.items():
+            v = w[f"layers.{l}.{k}"]
+            e.set_tensor(slot, l, v)
+            if v.ndim == 2:
+                deq[f"layers.{l}.{k}"] = q41(v)
+    m.set_weights(deq)
+    tok = 7
+    for pos in range(10):
+        ref_t, ref_lg = m.step(tok)
+        lg = e.step([tok], [pos])[0]
+        assert float(np.max(np.abs(lg.astype(np.float64) - ref_lg))) <= 2e-3 * float(np.max(np.abs(ref_lg))), pos
+        tok = ref_t
+    m.close()
+    e.close()

@@ -28,7 +28,8 @@ ATTN_MAX_PART_SPLITS = 8           # TI_ATTN_MAX_PART_SPLITS (include/ti_hip.h)
 EPI_STORE_F32, EPI_STORE_F16, EPI_RESID_F32, EPI_SILU_MUL_F16, EPI_QKV_ROPE_KV, EPI_LOGITS_ARGMAX = range(6)
 ARGMAX_SLOTS = 32
 GEMM_MAX_ROWS = 1024                # TI_GEMM_MAX_ROWS (include/ti_hip.h)
-BITS_G32 = 32                       # TI_BITS_G32 (include/ti_hip.h): group-32 weights (GGUF Q4_0 / Q8_0)   # TI_ARGMAX_SLOTS (include/ti_hip.h)
+BITS_G32 = 32                       # TI_BITS_G32 (include/ti_hip.h): group-32 weights (GGUF Q4_0 / Q8_0)
+BITS_AFF = 64                       # TI_BITS_AFF: affine group-32 int4 (GGUF Q4_1), with BITS_G32 | 4   # TI_ARGMAX_SLOTS (include/ti_hip.h)
 SCALE_GROUP, SCALE_TENSOR, SCALE_UNIT = 0, 1, 2
 ROWS_CONCAT, ROWS_INTERLEAVE8 = 0, 1
 (W_Q, W_K, W_V, W_O, W_GATE, W_UP, W_DOWN, W_LM_HEAD, V_ATTN_NORM, V_FFN_NORM, V_OUT_NORM, E_EMBED) = range(12)
@@ -83,6 +84,7 @@ EXPORTED = [
     "ti_engine_beam_search", "ti_engine_serve", "ti_qkv_attn_fused", "ti_engine_set_qkv_attn",
     "ti_pds_decode", "ti_engine_set_pds", "ti_engine_pds_error", "ti_engine_pds_timestamps",
     "ti_wpack_q_host", "ti_engine_set_tensor_q", "ti_sample_workspace_bytes", "ti_sample_device_ws",
+    "ti_wpack_q1_host", "ti_engine_set_tensor_q1",
     "ti_sample_step_ws", "ti_pds_granule_words",
 ]
 
@@ -172,6 +174,9 @@ def lib() -> C.CDLL:
         if hasattr(L, "ti_engine_set_tensor_q"):
             L.ti_engine_set_tensor_q.argtypes = [vp, i32, i32, vp, vp]
             L.ti_wpack_q_host.argtypes = [vp, vp, i32, i32, i32, i32, i32, i32, vp, vp]
+        if hasattr(L, "ti_engine_set_tensor_q1"):
+            L.ti_engine_set_tensor_q1.argtypes = [vp, i32, i32, vp, vp, vp]
+            L.ti_wpack_q1_host.argtypes = [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]
         L.ti_engine_synth.argtypes = [vp, u64, f32]
         L.ti_engine_fill_kv.argtypes = [vp, i32, i32, u64]
         L.ti_engine_generate.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp]
@@ -342,6 +347,14 @@ class Engine:
         da = np.ascontiguousarray(d, np.float16).view(np.uint16)
         check(lib().ti_engine_set_tensor_q(self.h, slot, layer, qa.ctypes.data, da.ctypes.data))
 
+
+    def set_tensor_q1(self, slot, layer, q, d, m):
+        """Exact GGUF Q4_1 blocks (engine bits 4 | BITS_G32 | BITS_AFF): q uint8 [K][N] (0..15),
+        d, m fp16 [K/32][N]; weight = d * q + m."""
+        qa = np.ascontiguousarray(q, np.uint8)
+        da = np.ascontiguousarray(d, np.float16).view(np.uint16)
+        ma = np.ascontiguousarray(m, np.float16).view(np.uint16)
+        check(lib().ti_engine_set_tensor_q1(self.h, slot, layer, qa.ctypes.data, da.ctypes.data, ma.ctypes.data))
     def set_tensor(self, slot, layer, data, scale_mode=SCALE_GROUP):
         a = np.ascontiguousarray(data, np.float32)
         check(lib().ti_engine_set_tensor(self.h, slot, layer, _ptr(a), scale_mode))

@@ -153,6 +153,60 @@ bool recover_g32(const std::vector<float>& w, size_t K, size_t N, int bits, std:
   return true;
 }
 
+// GGUF Q4_1 checkpoints likewise: every block is fl(q * d + m) with q in [0, 15] and d, m fp16
+// (gguf.cpp dequant_q4_1).  ggml's Q4_1 quantizer maps the block minimum to q = 0 (so m is the
+// smallest value, exactly) and the maximum to q = 15; d is the fp16 nearest (max - m) / 15 or
+// one of its neighbours.  Every candidate is verified weight by weight.
+bool recover_q41(const std::vector<float>& w, size_t K, size_t N, std::vector<int8_t>& q, std::vector<uint16_t>& d,
+                 std::vector<uint16_t>& m) {
+  if (K % 32 || w.size() != K * N) return false;
+  q.assign(K * N, 0);
+  d.assign(K / 32 * N, 0);
+  m.assign(K / 32 * N, 0);
+  auto half_bits = [](float f) {
+    const _Float16 h = (_Float16)f;
+    uint16_t u;
+    std::memcpy(&u, &h, 2);
+    return u;
+  };
+  auto half_val = [](uint16_t u) {
+    _Float16 h;
+    std::memcpy(&h, &u, 2);
+    return (float)h;
+  };
+  for (size_t n = 0; n < N; ++n)
+    for (size_t b = 0; b < K / 32; ++b) {
+      float lo = INFINITY, hi = -INFINITY;
+      for (size_t k = 32 * b; k < 32 * b + 32; ++k) {
+        lo = std::min(lo, w[k * N + n]);
+        hi = std::max(hi, w[k * N + n]);
+      }
+      const uint16_t mh = half_bits(lo);
+      if (half_val(mh) != lo) return false;
+      m[b * N + n] = mh;
+      if (hi == lo) continue;   // constant block: q = 0, d = 0
+      const uint16_t d0 = half_bits((hi - lo) / 15.0f);
+      bool found = false;
+      for (int dj : {0, 1, -1, 2, -2}) {
+        const uint16_t dh = (uint16_t)(d0 + dj);
+        const float dd = half_val(dh);
+        if (!(dd > 0.0f) || !std::isfinite(dd)) continue;
+        bool ok = true;
+        for (size_t k = 32 * b; k < 32 * b + 32 && ok; ++k) {
+          const float x = w[k * N + n], r = std::rint((x - lo) / dd);
+          ok = r >= 0.0f && r <= 15.0f && r * dd + lo == x;
+        }
+        if (!ok) continue;
+        for (size_t k = 32 * b; k < 32 * b + 32; ++k) q[k * N + n] = (int8_t)std::rint((w[k * N + n] - lo) / dd);
+        d[b * N + n] = dh;
+        found = true;
+        break;
+      }
+      if (!found) return false;
+    }
+  return true;
+}
+
 bool is_int(const core::Tensor& t) {
   return t.dtype() == core::DataType::kInt8 || t.dtype() == core::DataType::kInt32 ||
          t.dtype() == core::DataType::kInt16 || t.dtype() == core::DataType::kUInt8;
@@ -171,18 +225,27 @@ class InferenceEngineImpl {
   float total_time_ms = 0.0f, peak_tps = 0.0f;
 
   bool gguf_src = false;  // built from a GGUF-read ModelData (llama.cpp names)
-  // group-32 blocks recovered per linear weight (recover_g32), reused by upload()
-  std::map<const core::Tensor*, std::pair<std::vector<int8_t>, std::vector<uint16_t>>> g32;
+  // group-32 blocks recovered per linear weight (recover_g32 / recover_q41), reused by upload()
+  struct Blocks {
+    std::vector<int8_t> q;
+    std::vector<uint16_t> d, m;   // m: Q4_1 block minimums
+  };
+  std::map<const core::Tensor*, Blocks> g32;
+
+  static bool recover(const std::vector<float>& w, size_t K, size_t N, int bits, Blocks& b) {
+    return (bits & TI_BITS_AFF) ? recover_q41(w, K, N, b.q, b.d, b.m)
+                                : recover_g32(w, K, N, bits & ~TI_BITS_G32, b.q, b.d);
+  }
 
   InferenceEngineImpl() { rng.seed((unsigned)std::chrono::steady_clock::now().time_since_epoch().count()); }
 
-  // every linear weight of the model is exact group-32 blocks of `bits` (cached on success)
+  // every linear weight of the model is exact group-32 blocks of `bits` (4 | G32, 8 | G32 or
+  // 4 | G32 | AFF; cached on success)
   bool all_g32(const ModelData& m, size_t L, size_t H, size_t qd, size_t kvd, size_t I, size_t V, int bits) {
     g32.clear();
     auto one = [&](const core::Tensor* t, size_t K, size_t N) {
       if (!t || t->shape().total_size() != K * N) return false;
-      auto& e = g32[t];
-      return recover_g32(api::to_f32(*t), K, N, bits, e.first, e.second);
+      return recover(api::to_f32(*t), K, N, bits, g32[t]);
     };
     bool ok = one(find(m, {"lm_head.weight", "output.weight"}), H, V);
     for (size_t l = 0; l < L && ok; ++l)
@@ -203,18 +266,21 @@ class InferenceEngineImpl {
   void upload(int slot, int layer, const core::Tensor& t, size_t K, size_t N, int bits) {
     if ((bits & TI_BITS_G32) && t.shape().total_size() == K * N) {   // exact blocks when the weight has them
       auto it = g32.find(&t);
-      std::vector<int8_t> q;
-      std::vector<uint16_t> d;
+      Blocks b;
       if (it != g32.end()) {
-        q.swap(it->second.first);
-        d.swap(it->second.second);
+        b = std::move(it->second);
         g32.erase(it);
       }
-      if (!q.empty() || recover_g32(api::to_f32(t), K, N, bits & ~TI_BITS_G32, q, d)) {
-        check(ti_engine_set_tensor_q(eng, slot, layer, q.data(), d.data()), "ti_engine_set_tensor_q");
+      if (!b.q.empty() || recover(api::to_f32(t), K, N, bits, b)) {
+        if (bits & TI_BITS_AFF)
+          check(ti_engine_set_tensor_q1(eng, slot, layer, reinterpret_cast<const uint8_t*>(b.q.data()), b.d.data(),
+                                        b.m.data()),
+                "ti_engine_set_tensor_q1");
+        else
+          check(ti_engine_set_tensor_q(eng, slot, layer, b.q.data(), b.d.data()), "ti_engine_set_tensor_q");
         return;
       }
-    }
+    }   // otherwise quantized below (ggml's Q4_1 rounding on affine engines, ti_wpack_host)
     if (t.shape().total_size() != K * N)
       throw std::runtime_error("InferenceEngine: weight for slot " + std::to_string(slot) + " layer " +
                                std::to_string(layer) + " has " + std::to_string(t.shape().total_size()) +
@@ -268,14 +334,17 @@ class InferenceEngineImpl {
         const std::vector<float> v = api::to_f32(*up0);
         for (float x : v)
           if (x < -8.0f || x > 7.0f) bits = 8;
-      } else if (gguf_src && q0) {   // Q4_0 / Q8_0 checkpoint: keep its blocks
+      } else if (gguf_src && q0) {   // Q4_0 / Q4_1 / Q8_0 checkpoint: keep its blocks
         const size_t kvd = k0 ? k0->shape().total_size() / H : H;
-        if (all_g32(m, L, H, H, kvd, I, V, 4)) bits = 4 | TI_BITS_G32;
-        else if (all_g32(m, L, H, H, kvd, I, V, 8)) bits = 8 | TI_BITS_G32;
+        if (all_g32(m, L, H, H, kvd, I, V, 4 | TI_BITS_G32)) bits = 4 | TI_BITS_G32;
+        else if (all_g32(m, L, H, H, kvd, I, V, 4 | TI_BITS_G32 | TI_BITS_AFF)) bits = 4 | TI_BITS_G32 | TI_BITS_AFF;
+        else if (all_g32(m, L, H, H, kvd, I, V, 8 | TI_BITS_G32)) bits = 8 | TI_BITS_G32;
       }
     }
-    if (bits != 4 && bits != 8 && bits != 16 && bits != (4 | TI_BITS_G32) && bits != (8 | TI_BITS_G32))
-      throw std::runtime_error("InferenceEngine: weight_bits must be 4, 8, 16 or 4 / 8 | 32 (group-32 blocks)");
+    if (bits != 4 && bits != 8 && bits != 16 && bits != (4 | TI_BITS_G32) && bits != (8 | TI_BITS_G32) &&
+        bits != (4 | TI_BITS_G32 | TI_BITS_AFF))
+      throw std::runtime_error(
+          "InferenceEngine: weight_bits must be 4, 8, 16, 4 / 8 | 32 (group-32 blocks) or 4 | 32 | 64 (Q4_1 blocks)");
     cfg.vocab = (int)V;
     cfg.hidden = (int)H;
     cfg.layers = (int)L;
@@ -639,8 +708,8 @@ std::string InferenceEngine::performance_stats() const {
   if (im.total_time_ms > 0.0f)
     os << "  Average Tokens/Second: " << (im.total_tokens / (im.total_time_ms / 1000.0f)) << "\n";
   os << "  Peak Tokens/Second: " << im.peak_tps << "\n";
-  os << "  Device Memory: " << (memory_usage() / (1024.0 * 1024.0)) << " MB (weights " << (im.cfg.bits & ~TI_BITS_G32)
-     << "-bit" << ((im.cfg.bits & TI_BITS_G32) ? " group-32 blocks" : "") << ", fp16 KV, " << im.capacity
+  os << "  Device Memory: " << (memory_usage() / (1024.0 * 1024.0)) << " MB (weights " << (im.cfg.bits & ~(TI_BITS_G32 | TI_BITS_AFF))
+     << "-bit" << ((im.cfg.bits & TI_BITS_AFF) ? " affine group-32 blocks" : (im.cfg.bits & TI_BITS_G32) ? " group-32 blocks" : "") << ", fp16 KV, " << im.capacity
      << " stream(s) x " << im.cfg.max_seq << " slots)\n";
   os << "  Mode: " << (im.compat ? "reference_compat (plumbing model)" : "llama decode") << "\n";
   return os.str();

@@ -243,8 +243,10 @@ int validate(const ti_engine_config& c) {
   const int G = c.heads / c.kv_heads;
   if (G != 1 && G != 2 && G != 4 && G != 8) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_create: GQA group %d", G);
   if (c.head_dim != 64 && c.head_dim != 128) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_create: head_dim %d", c.head_dim);
-  if (c.bits != 4 && c.bits != 8 && c.bits != 16 && c.bits != (4 | TI_BITS_G32) && c.bits != (8 | TI_BITS_G32))
-    return ti_set_error(TI_ERR_ARG, "ti_engine_create: bits %d (4, 8, 16; 4 or 8 | TI_BITS_G32)", c.bits);
+  if (c.bits != 4 && c.bits != 8 && c.bits != 16 && c.bits != (4 | TI_BITS_G32) && c.bits != (8 | TI_BITS_G32) &&
+      c.bits != (4 | TI_BITS_G32 | TI_BITS_AFF))
+    return ti_set_error(TI_ERR_ARG, "ti_engine_create: bits %d (4, 8, 16; 4 or 8 | TI_BITS_G32; 4 | TI_BITS_G32 | "
+                        "TI_BITS_AFF)", c.bits);
   const int qd = c.heads * c.head_dim, kvd = c.kv_heads * c.head_dim;
   if (c.hidden % 128 || qd % 128 || c.inter % 128)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_create: hidden, heads*head_dim and inter must be multiples of 128");
@@ -874,6 +876,7 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     if (const char* env = getenv("TI_ATTN_PART")) e->part_on = atoi(env) != 0;
     e->splits_max = e->splits_for(1);
     e->pf_rows = (c.bits & ~TI_BITS_G32) == 4 ? TI_GEMM_MAX_ROWS : 16;   // int4 (also group-32): the tile GEMM
+    // (affine group-32 runs the fused kernel only: prompt chunks of its 16 rows)
     e->rows_cap = std::max(B, e->pf_rows);
     const int R = e->rows_cap;
     const int Rp = (R + 15) / 16 * 16;   // packed operands hold whole 16-row blocks
@@ -1022,14 +1025,18 @@ int ti_engine_set_tensor(ti_engine* e, int slot, int layer, const float* data, i
   return TI_OK;
 }
 
-// Exact group-32 weights (GGUF Q4_0 / Q8_0 blocks): q [K][N_src] int8 and fp16 block scales
-// d [K/32][N_src], packed without re-quantization (ti_wpack_q_host).
-int ti_engine_set_tensor_q(ti_engine* e, int slot, int layer, const int8_t* q, const uint16_t* d) {
-  if (!e || !q || !d) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q: null");
+// Exact group-32 weights: Q4_0 / Q8_0 blocks (q int8, d) or, with m, Q4_1 blocks (q 0..15, d, m;
+// TI_BITS_AFF engines), packed without re-quantization (ti_wpack_q_host / ti_wpack_q1_host).
+static int set_tensor_blocks(ti_engine* e, int slot, int layer, const void* q, const uint16_t* d, const uint16_t* m) {
+  const char* fn = m ? "ti_engine_set_tensor_q1" : "ti_engine_set_tensor_q";
+  if (!e || !q || !d) return ti_set_error(TI_ERR_ARG, "%s: null", fn);
   DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
-  if (!(c.bits & TI_BITS_G32)) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q: engine bits %d lack TI_BITS_G32", c.bits);
-  if (layer < 0 || (slot <= TI_W_DOWN && layer >= c.layers)) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q: layer %d", layer);
+  if (!(c.bits & TI_BITS_G32)) return ti_set_error(TI_ERR_ARG, "%s: engine bits %d lack TI_BITS_G32", fn, c.bits);
+  if (((c.bits & TI_BITS_AFF) != 0) != (m != nullptr))
+    return ti_set_error(TI_ERR_ARG, "%s: engine bits %d (%s blocks expected)", fn, c.bits,
+                        (c.bits & TI_BITS_AFF) ? "affine Q4_1" : "Q4_0 / Q8_0");
+  if (layer < 0 || (slot <= TI_W_DOWN && layer >= c.layers)) return ti_set_error(TI_ERR_ARG, "%s: layer %d", fn, layer);
   const int H = c.hidden, I = c.inter, V = c.vocab, qd = e->qd(), kvd = e->kvd();
   DevLinear* L = nullptr;
   int K = 0, Nsrc = 0, map = TI_ROWS_CONCAT, off = 0;
@@ -1042,17 +1049,29 @@ int ti_engine_set_tensor_q(ti_engine* e, int slot, int layer, const int8_t* q, c
     case TI_W_UP: L = &e->layer[layer].gu; K = H; Nsrc = I; map = TI_ROWS_INTERLEAVE8; off = 8; break;
     case TI_W_DOWN: L = &e->layer[layer].down; K = I; Nsrc = H; break;
     case TI_W_LM_HEAD: L = &e->lm; K = H; Nsrc = V; break;
-    default: return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q: slot %d is not a linear weight", slot);
+    default: return ti_set_error(TI_ERR_ARG, "%s: slot %d is not a linear weight", fn, slot);
   }
   const size_t tb = ti_wpack_tile_bytes(c.bits, L->K, L->N), sb = ti_wpack_scale_bytes(c.bits, L->K, L->N);
   std::vector<uint8_t> th(tb);
   std::vector<uint16_t> sh(sb / 2 + 1);
   TI_TRY(ti_memcpy_d2h(th.data(), L->tiles, tb, e->s));
   TI_TRY(ti_memcpy_d2h(sh.data(), L->scales, sb, e->s));
-  TI_TRY(ti_wpack_q_host(q, d, K, Nsrc, L->N, c.bits, map, off, th.data(), sh.data()));
+  if (m)
+    TI_TRY(ti_wpack_q1_host(static_cast<const uint8_t*>(q), d, m, K, Nsrc, L->N, map, off, th.data(), sh.data()));
+  else
+    TI_TRY(ti_wpack_q_host(static_cast<const int8_t*>(q), d, K, Nsrc, L->N, c.bits, map, off, th.data(), sh.data()));
   TI_TRY(ti_memcpy_h2d(L->tiles, th.data(), tb, e->s));
   TI_TRY(ti_memcpy_h2d(L->scales, sh.data(), sb, e->s));
   return ti_stream_sync(e->s);
+}
+
+int ti_engine_set_tensor_q(ti_engine* e, int slot, int layer, const int8_t* q, const uint16_t* d) {
+  return set_tensor_blocks(e, slot, layer, q, d, nullptr);
+}
+
+int ti_engine_set_tensor_q1(ti_engine* e, int slot, int layer, const uint8_t* q, const uint16_t* d, const uint16_t* m) {
+  if (!m) return ti_set_error(TI_ERR_ARG, "ti_engine_set_tensor_q1: null");
+  return set_tensor_blocks(e, slot, layer, q, d, m);
 }
 
 int ti_engine_synth(ti_engine* e, uint64_t seed, float norm_jitter) {

@@ -39,12 +39,13 @@ inline uint16_t to_half(float f) {
 
 extern "C" size_t ti_wpack_tile_bytes(int bits, int K, int N) {
   if (K <= 0 || N <= 0) return 0;
-  return (size_t)(N / 16) * (size_t)(K / 128) * 256u * (size_t)(bits & ~TI_BITS_G32);
+  return (size_t)(N / 16) * (size_t)(K / 128) * 256u * (size_t)(bits & ~(TI_BITS_G32 | TI_BITS_AFF));
 }
 
 extern "C" size_t ti_wpack_scale_bytes(int bits, int K, int N) {
   if (bits == 16 || K <= 0 || N <= 0) return 0;
-  return (size_t)(N / 16) * (size_t)(K / 128) * 16u * sizeof(uint16_t) * ((bits & TI_BITS_G32) ? 4u : 1u);
+  return (size_t)(N / 16) * (size_t)(K / 128) * 16u * sizeof(uint16_t) * ((bits & TI_BITS_G32) ? 4u : 1u) *
+         ((bits & TI_BITS_AFF) ? 2u : 1u);   // affine group-32: the block minimums follow the scales
 }
 
 namespace {
@@ -113,6 +114,30 @@ extern "C" int ti_wpack_q_host(const int8_t* q, const uint16_t* d, int K, int N_
 extern "C" int ti_wpack_host(const float* w, int K, int N_src, int N_total, int bits, int scale_mode, int row_map,
                              int row_offset, void* tiles, uint16_t* scales) {
   if (!w || !tiles) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: null pointer");
+  if (bits == (4 | TI_BITS_G32 | TI_BITS_AFF)) {
+    // fp32 weights onto an affine group-32 engine: ggml's Q4_1 rounding per 32-block
+    // (d = (max - min) / 15, m = min, q = round-half-up((w - min) / d) clamped to 15), then packed exactly
+    if (K <= 0 || (K & 127) || N_src <= 0) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: K %% 128 (K=%d)", K);
+    std::vector<uint8_t> q((size_t)K * N_src);
+    std::vector<uint16_t> d((size_t)(K / 32) * N_src), m(d.size());
+    for (int c = 0; c < N_src; ++c)
+      for (int b = 0; b < K / 32; ++b) {
+        float lo = INFINITY, hi = -INFINITY;
+        for (int i = 0; i < 32; ++i) {
+          const float v = w[(size_t)(b * 32 + i) * N_src + c];
+          lo = std::min(lo, v);
+          hi = std::max(hi, v);
+        }
+        const float dd = (hi - lo) / 15.0f, id = dd != 0.0f ? 1.0f / dd : 0.0f;
+        d[(size_t)b * N_src + c] = to_half(dd);
+        m[(size_t)b * N_src + c] = to_half(lo);
+        for (int i = 0; i < 32; ++i) {
+          const size_t at = (size_t)(b * 32 + i) * N_src + c;
+          q[at] = (uint8_t)std::min(15, (int)((w[at] - lo) * id + 0.5f));
+        }
+      }
+    return ti_wpack_q1_host(q.data(), d.data(), m.data(), K, N_src, N_total, row_map, row_offset, tiles, scales);
+  }
   const bool g32 = (bits & TI_BITS_G32) != 0;
   bits &= ~TI_BITS_G32;
   if ((bits != 4 && bits != 8 && bits != 16) || (g32 && bits == 16)) return ti_set_error(TI_ERR_ARG, "ti_wpack_host: bits %d", bits);
@@ -169,4 +194,25 @@ extern "C" int ti_wpack_host(const float* w, int K, int N_src, int N_total, int 
     }
   }
   return TI_OK;
+}
+
+// GGUF Q4_1 blocks (ggml: weight = d * q + m, q in 0..15): the tiles and scales of the Q4_0 form
+// with q - 8 (the kernels' offset-8 nibbles hold q itself), then the block minimums m packed in
+// the scales' layout right after them.
+extern "C" int ti_wpack_q1_host(const uint8_t* q, const uint16_t* d, const uint16_t* m, int K, int N_src, int N_total,
+                                int row_map, int row_offset, void* tiles, uint16_t* scales) {
+  if (!q || !d || !m || !tiles || !scales) return ti_set_error(TI_ERR_ARG, "ti_wpack_q1_host: null pointer");
+  if (K <= 0 || (K & 127) || N_total <= 0 || (N_total & 15) || N_src <= 0)
+    return ti_set_error(TI_ERR_ARG, "ti_wpack_q1_host: K %% 128 / N %% 16 (K=%d N_total=%d)", K, N_total);
+  std::vector<int8_t> v((size_t)K * N_src);
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (q[i] > 15) return ti_set_error(TI_ERR_ARG, "ti_wpack_q1_host: weight %d outside [0, 15]", (int)q[i]);
+    v[i] = (int8_t)((int)q[i] - 8);
+  }
+  int rc = ti_wpack_q_host(v.data(), d, K, N_src, N_total, 4, row_map, row_offset, tiles, scales);
+  if (rc != TI_OK) return rc;
+  // the minimums through the same scale packing (into a scratch tile image)
+  std::vector<uint8_t> scratch(ti_wpack_tile_bytes(4, K, N_total));
+  uint16_t* mins = scales + ti_wpack_scale_bytes(4 | TI_BITS_G32, K, N_total) / sizeof(uint16_t);
+  return ti_wpack_q_host(v.data(), m, K, N_src, N_total, 4, row_map, row_offset, scratch.data(), mins);
 }

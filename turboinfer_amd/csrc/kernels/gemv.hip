@@ -88,11 +88,11 @@ __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
 // weights in flight), never more than there are 16-row tiles.
 static int g_wg_per_cu = 0;   // TI_GEMV_WG_PER_CU (tuning knob), default 1
 
-__host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_wg, bool g32 = false);
+__host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_wg, bool g32 = false, bool aff = false);
 
 // Tiles per workgroup are bounded by the LDS image (partial slabs and scales grow with
 // them): very wide outputs (a 128k vocabulary) get more workgroups than CUs.
-__host__ inline int gemv_grid(int M, int N, int K, int num_cus, bool g32 = false) {
+__host__ inline int gemv_grid(int M, int N, int K, int num_cus, bool g32 = false, bool aff = false) {
   if (g_wg_per_cu <= 0) {
     const char* s = getenv("TI_GEMV_WG_PER_CU");
     g_wg_per_cu = s && atoi(s) > 0 ? atoi(s) : 1;
@@ -100,7 +100,7 @@ __host__ inline int gemv_grid(int M, int N, int K, int num_cus, bool g32 = false
   const int NT = N >> 4;
   const int g = g_wg_per_cu * (num_cus > 0 ? num_cus : 256);
   int grid = NT < g ? NT : g;
-  while (grid < NT && gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid, g32) > 160 * 1024) grid += grid / 8 + 1;
+  while (grid < NT && gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid, g32, aff) > 160 * 1024) grid += grid / 8 + 1;
   return grid < NT ? grid : NT;
 }
 
@@ -114,24 +114,28 @@ __host__ inline int gemv_grid(int M, int N, int K, int num_cus, bool g32 = false
 //   es     epilogue inputs: residual [ntl][M][16] f32 (+ the fold weights of the same
 //          outputs, TI_EPI_RESID_F32 with fold_x), or RoPE (cos, sin) [M][hd] + pos [M]
 //   best   [16] u64                   argmax keys of the workgroup
+//   (affine group-32, TI_BITS_AFF: + the block minimums [ntl][K/128][4][16] fp16 after the scales
+//    and the blocks' sums of x [K/32][16] f32 after corr)
 struct GemvLds {
-  int x, sc, corr, slab, es, best, total;
+  int x, sc, corr, slab, es, best, total, mins, bsum;
 };
-__host__ __device__ inline GemvLds gemv_lds_layout(int M, int K, int ntl, bool g32 = false) {
+__host__ __device__ inline GemvLds gemv_lds_layout(int M, int K, int ntl, bool g32 = false, bool aff = false) {
   GemvLds l;
   const int gm = g32 ? 4 : 1;                  // scale / correction groups per 128 k
   l.x = 0;
   l.sc = l.x + align16(M * (K + 8) * 2);
-  l.corr = l.sc + align16(ntl * (K >> 7) * 32 * gm);
-  l.slab = l.corr + (K >> 7) * 16 * 4 * gm;    // int4 offset correction [K/128 (x4)][16 rows] f32
+  l.mins = l.sc + align16(ntl * (K >> 7) * 32 * gm);
+  l.corr = l.mins + (aff ? align16(ntl * (K >> 7) * 32 * gm) : 0);
+  l.bsum = l.corr + (K >> 7) * 16 * 4 * gm;
+  l.slab = l.bsum + (aff ? (K >> 7) * 16 * 4 * gm : 0);   // int4 offset correction [K/128 (x4)][16 rows] f32
   l.es = l.slab + (ntl + 1) * kGemvWaves * kWave * 16;
   const int es_bytes = 2 * ntl * M * 16 * 4 > M * 128 * 4 + 64 ? 2 * ntl * M * 16 * 4 : M * 128 * 4 + 64;
   l.best = l.es + align16(es_bytes);
   l.total = l.best + 16 * 8;
   return l;
 }
-__host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_wg, bool g32) {
-  return gemv_lds_layout(M, K, tiles_per_wg, g32).total;
+__host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_wg, bool g32, bool aff) {
+  return gemv_lds_layout(M, K, tiles_per_wg, g32, aff).total;
 }
 
 // ------------------------------------------------------------- x staging (LDS)
@@ -347,7 +351,7 @@ __device__ __forceinline__ void lds_barrier() {
 // G32: group-32 weights (TI_BITS_G32, GGUF Q4_0 / Q8_0 blocks): within a tile, lane l holds for
 // MFMA step s4 the 8 k = 32 s4 + 8 (l >> 4) + e, so each v_mfma_f32_16x16x32 reduces exactly one
 // 32-weight block; its scale (and, int4, its offset correction) is applied per step.
-template <int BITS, int XM, bool CH, bool STR, bool G32 = false>
+template <int BITS, int XM, bool CH, bool STR, bool G32 = false, bool AFF = false>
 __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* p_scales, const void* p_x,
                                           const float* p_aux, int p_mgk, int p_N, int p_kx, int p_ldo,
                                           const float* p_pre, GemvArgs a, const unsigned bid, const int t0_in,
@@ -375,7 +379,10 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   const int KW = wave < KT ? (KT - wave + kGemvWaves - 1) / kGemvWaves : 0;   // k-tiles per tile, this wave
   const int total = ntl * KW;
   static_assert(!G32 || (!STR && !CH && BITS != 16), "group-32 weights: int4 / int8, fused kernel only");
-  const GemvLds L = gemv_lds_layout(a.M, a.K, ntl, G32);
+  static_assert(!AFF || (G32 && BITS == 4), "affine blocks: group-32 int4");
+  const GemvLds L = gemv_lds_layout(a.M, a.K, ntl, G32, AFF);
+  uint16_t* ml = (uint16_t*)(smem + L.mins);       // AFF: block minimums, as sl
+  float* bsum = (float*)(smem + L.bsum);           // AFF: [K/32][16] sums of x per block and row
   f16* xl = (f16*)(smem + L.x);
   uint16_t* sl = (uint16_t*)(smem + L.sc);
   float* corr = (float*)(smem + L.corr);           // [K/128][16] (int4 only)
@@ -584,6 +591,10 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   if constexpr (BITS != 16) {
     for (int i = tid + kGemvThreads; i < n_sc; i += kGemvThreads) ((u32x4*)sl)[i] = sg[sc_off(i)];
   }
+  if constexpr (AFF) {   // the minimums follow all N/16 tiles' scales in the same buffer
+    const u32x4* mg = (const u32x4*)(a.scales + (size_t)NT * KT * 64 + (size_t)t0 * KT * 64);
+    for (int i = tid; i < n_sc; i += kGemvThreads) ((u32x4*)ml)[i] = mg[i];
+  }
   if constexpr (XM == XM_F16 || XM == XM_F16F) {
     if (nx16 > XPF * kGemvThreads) stage_x_generic<XM, CH>(a, xl, red, XPF * kGemvThreads);
   } else if constexpr (XM != XM_NORM1 && XM != XM_ATTN) {
@@ -606,7 +617,7 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
     const f16 s16 = (f16)0.0625f;
     for (int i0 = 0; i0 < a.M * K8; i0 += kGemvThreads) {
       const int idx = i0 + tid;
-      float part = 0.0f;
+      float part = 0.0f, sx = 0.0f;
       int m = 0, k8 = 0;
       if (idx < a.M * K8) {
         m = idx / K8;
@@ -617,10 +628,15 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
         const float lo = ((float)h[0] + (float)h[1]) + ((float)h[4] + (float)h[5]);
         const float hi = ((float)h[2] + (float)h[3]) + ((float)h[6] + (float)h[7]);
         part = 1032.0f * lo + 1152.0f * hi;
+        if constexpr (AFF) sx = lo + 16.0f * hi;   // the piece's sum of x (high slots were scaled by 1/16)
       }
       if constexpr (G32) {   // one 32-k block = 4 consecutive pieces
         part = group_sum<4>(part);
         if (idx < a.M * K8 && (lane & 3) == 0) corr[(k8 >> 2) * 16 + m] = part;
+        if constexpr (AFF) {
+          sx = group_sum<4>(sx);
+          if (idx < a.M * K8 && (lane & 3) == 0) bsum[(k8 >> 2) * 16 + m] = sx;
+        }
       } else {
         part = group_sum<16>(part);
         if (idx < a.M * K8 && (lane & 15) == 0) corr[(k8 >> 4) * 16 + m] = part;
@@ -664,6 +680,14 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
         acc[1] = fmaf(sc, tb[1], acc[1]);
         acc[2] = fmaf(sc, tb[2], acc[2]);
         acc[3] = fmaf(sc, tb[3], acc[3]);
+        if constexpr (AFF) {   // weight = d (q - 8) + (8 d + m): the offset term times the block's sum of x
+          const float mt = fmaf(8.0f, sc, h2f(ml[((ct * KT + kt) * 4 + s4) * 16 + r]));
+          const f32x4 bs = *(const f32x4*)(bsum + (kt * 4 + s4) * 16 + 4 * kq);
+          acc[0] = fmaf(mt, bs[0], acc[0]);
+          acc[1] = fmaf(mt, bs[1], acc[1]);
+          acc[2] = fmaf(mt, bs[2], acc[2]);
+          acc[3] = fmaf(mt, bs[3], acc[3]);
+        }
       }
     } else {
 #if TI_GEMV_EXP & 1   // diagnostic build (tools/probe_gemv.hip): stream only, no dequant / MFMA
@@ -832,12 +856,13 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   GEMV_TS(4);
 }
 
-template <int BITS, int XM, bool CH = false, bool G32 = false>
+template <int BITS, int XM, bool CH = false, bool G32 = false, bool AFF = false>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
                                                                    const void* p_x, const float* p_aux, int p_mgk,
                                                                    int p_N, int p_kx, int p_ldo, const float* p_pre,
                                                                    const GemvArgs a_in) {
-  gemv_body<BITS, XM, CH, false, G32>(p_tiles, p_scales, p_x, p_aux, p_mgk, p_N, p_kx, p_ldo, p_pre, a_in, blockIdx.x, 0, 0, 1);
+  gemv_body<BITS, XM, CH, false, G32, AFF>(p_tiles, p_scales, p_x, p_aux, p_mgk, p_N, p_kx, p_ldo, p_pre, a_in, blockIdx.x, 0,
+                                           0, 1);
 }
 
 // ============================================================ QKV + attention, one launch
@@ -1753,7 +1778,7 @@ __host__ inline int gemv_xmode(int x_kind, int M, int K) {
   return M == 1 && (K >> 3) <= kGemvThreads ? XM_NORM1 : XM_NORM;
 }
 
-template <int BITS, bool G32 = false>
+template <int BITS, bool G32 = false, bool AFF = false>
 static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid, const ti_chain* chain) {
   const float* pre = a.epi.kind == TI_EPI_RESID_F32 ? (const float*)a.epi.out
                      : a.epi.kind == TI_EPI_QKV_ROPE_KV ? (const float*)a.epi.pos : (const float*)a.x;
@@ -1776,12 +1801,12 @@ static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid, cons
     return TI_OK;
   }
   switch (xm) {
-    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_ATTN: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_ATTN, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_F16F: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16F, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM, false, G32>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_ATTN: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_ATTN, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F16F: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16F, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
   }
   TI_LAUNCH_CHECK("gemv_wq_kernel");
   return TI_OK;
@@ -2015,10 +2040,10 @@ static int fused_rows_pref(int bits) {
   }
   return bits == 4 ? g_fused_rows : 16;
 }
-static bool fused_fits(int M, int N, int K, bool g32 = false) {
+static bool fused_fits(int M, int N, int K, bool g32 = false, bool aff = false) {
   if (M > 16) return false;
-  const int NT = N >> 4, grid = ti::gemv_grid(M, N, K, query_cus(), g32);
-  return ti::gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid, g32) <= 160 * 1024;
+  const int NT = N >> 4, grid = ti::gemv_grid(M, N, K, query_cus(), g32, aff);
+  return ti::gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid, g32, aff) <= 160 * 1024;
 }
 static bool use_batched(int bits, int x_kind, int M, int N, int K) {
   const bool mb_ok = bits == 4 && x_kind == TI_X_F16;
@@ -2030,11 +2055,12 @@ extern "C" int ti_gemm_packed_rows(int bits, int M) { return bits == 4 && M > 16
 extern "C" int ti_gemm_max_rows(int bits, int x_kind, int N, int K) {
   if (N < 16 || K < 128) return 0;
   if (bits & TI_BITS_G32) {   // group-32 weights: the fused kernel; int4 fp16 rows also the tile kernel
+    const bool aff = (bits & TI_BITS_AFF) != 0;   // (affine blocks: fused pieces only)
     if (x_kind == TI_X_F16_PACKED) return 0;
-    if ((bits & ~TI_BITS_G32) == 4 && x_kind == TI_X_F16) return TI_GEMM_MAX_ROWS;   // 17..64: 16-row pieces
+    if ((bits & ~(TI_BITS_G32 | TI_BITS_AFF)) == 4 && x_kind == TI_X_F16) return TI_GEMM_MAX_ROWS;   // 16-row pieces
     int m = 16;
-    while (m > 1 && !fused_fits(m, N, K, true)) --m;
-    return fused_fits(m, N, K, true) ? m : 0;
+    while (m > 1 && !fused_fits(m, N, K, true, aff)) --m;
+    return fused_fits(m, N, K, true, aff) ? m : 0;
   }
   if (bits == 4 && (x_kind == TI_X_F16 || x_kind == TI_X_F16_PACKED)) return TI_GEMM_MAX_ROWS;
   if (x_kind == TI_X_F16_PACKED) return 0;
@@ -2070,16 +2096,17 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
                      ti_stream_t stream) {
   using namespace ti;
   if (!tiles || !x || !epi || !epi->out) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: null pointer");
-  const bool g32 = (bits & TI_BITS_G32) != 0;
-  if (g32) bits &= ~TI_BITS_G32;
-  if ((bits != 4 && bits != 8 && bits != 16) || (g32 && bits == 16))
-    return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: bits must be 4, 8 or 16 (+ TI_BITS_G32 for 4 / 8; got %d)", bits);
+  const bool g32 = (bits & TI_BITS_G32) != 0, aff = (bits & TI_BITS_AFF) != 0;
+  bits &= ~(TI_BITS_G32 | TI_BITS_AFF);
+  if ((bits != 4 && bits != 8 && bits != 16) || (g32 && bits == 16) || (aff && (!g32 || bits != 4)))
+    return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: bits must be 4, 8 or 16 (+ TI_BITS_G32 for 4 / 8, + TI_BITS_AFF "
+                        "for 4 | G32; got %d)", bits);
   // group-32: int4 fp16 rows from tile_rows() on run on the tile kernel, everything else on the
-  // fused kernel (more than 16 rows: in 16-row pieces, below)
-  const bool g32_tile = g32 && bits == 4 && x_kind == TI_X_F16 && M >= tile_rows() && !epi->out_packed;
+  // fused kernel (more than 16 rows: in 16-row pieces, below); affine blocks on the fused kernel only
+  const bool g32_tile = g32 && !aff && bits == 4 && x_kind == TI_X_F16 && M >= tile_rows() && !epi->out_packed;
   int g32_rows = 16;   // rows per fused launch (its LDS image holds the x rows)
-  while (g32 && g32_rows > 1 && !fused_fits(g32_rows, N, K, true)) --g32_rows;
-  if (g32 && (chain || x_kind == TI_X_F16_PACKED || (!g32_tile && !fused_fits(std::min(M, g32_rows), N, K, true))))
+  while (g32 && g32_rows > 1 && !fused_fits(g32_rows, N, K, true, aff)) --g32_rows;
+  if (g32 && (chain || x_kind == TI_X_F16_PACKED || (!g32_tile && !fused_fits(std::min(M, g32_rows), N, K, true, aff))))
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: group-32 weights: fused kernel rows (M=%d N=%d K=%d) "
                         "or int4 fp16 rows >= %d; no chain, no packed rows", M, N, K, tile_rows());
   if (bits != 16 && !scales) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: scales required for bits %d", bits);
@@ -2138,7 +2165,8 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
       if (ep.v_cache) ep.v_cache += (size_t)m0 * ep.kv_stream_stride;
       if (ep.argmax) ep.argmax += (size_t)m0 * TI_ARGMAX_SLOTS;
       if (m0 + mm < M) ep.step_ctr = nullptr;
-      const int rc = gemm_impl(tiles, scales, bits | TI_BITS_G32, static_cast<const char*>(x) + (size_t)m0 * ldx * x_elem,
+      const int rc = gemm_impl(tiles, scales, bits | TI_BITS_G32 | (aff ? TI_BITS_AFF : 0),
+                               static_cast<const char*>(x) + (size_t)m0 * ldx * x_elem,
                                x_kind, ldx, norm_w, eps, mm, N, K, &ep, nullptr, stream);
       if (rc != TI_OK) return rc;
     }
@@ -2179,8 +2207,8 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     grid = mb_grid(MB, N, K, query_cus(), &ntl);
     lds = mb_use_lds(MB) ? mb_lds_bytes(MB, ntl, K) : mbr_lds_bytes(MB, ntl, K);
   } else {
-    grid = gemv_grid(M, N, K, query_cus(), g32);
-    lds = gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid, g32);
+    grid = gemv_grid(M, N, K, query_cus(), g32, aff);
+    lds = gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid, g32, aff);
   }
   if (lds > 160 * 1024)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: LDS image %d B too large (M=%d N=%d K=%d)", lds, M, N, K);
@@ -2221,6 +2249,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   }
   if (rows) return launch_rows(a, rMB, rRG, ntl, grid, lds, s);
   if (batched) return launch_mb(a, M > 16 ? 2 : 1, grid, ntl, lds, s);
+  if (aff) return launch_gemv<4, true, true>(a, lds, s, grid, chain);
   if (g32) return bits == 4 ? launch_gemv<4, true>(a, lds, s, grid, chain) : launch_gemv<8, true>(a, lds, s, grid, chain);
   if (bits == 4) return launch_gemv<4>(a, lds, s, grid, chain);
   if (bits == 8) return launch_gemv<8>(a, lds, s, grid, chain);

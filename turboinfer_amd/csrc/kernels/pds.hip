@@ -45,6 +45,10 @@ namespace ti {
 #define TI_PDS_RING 8   // units (2 KiB per wave each) in flight per consumer wave
 #endif
 constexpr int kPdsRing = TI_PDS_RING;
+#ifndef TI_PDS_PRE
+#define TI_PDS_PRE 8   // ring units issued ahead of a hand-off, the rest after the input is staged (A/B: 8 best)
+#endif
+constexpr int kPdsPre = TI_PDS_PRE < TI_PDS_RING ? TI_PDS_PRE : TI_PDS_RING;
 constexpr int kPdsC = 8;                         // consumer waves
 constexpr int kPdsThreads = kPdsC * kWave;      // wave 7 is also the control wave
 constexpr int kPdsCThreads = kPdsC * kWave;
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
   ACur ac{};
   gc = gcur(0, PH_QKV);
 #pragma unroll
-  for (int s = 0; s < kPdsRing; ++s) grefill(gc, ring[s]);
+  for (int s = 0; s < kPdsPre; ++s) grefill(gc, ring[s]);
 
   // ---------------------------------------------------------------- X wave: setup
   uint32_t epoch = 0;
@@ -541,6 +545,8 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       else stage_f16_g(a.fxg, H, pds_tag(epoch, l - 1, PH_DN));
       if (is_x) rms = l == 0 ? fold_rms(a.n_ss0, H) : fold_rms_g(grid, H, pds_tag(epoch, l - 1, PH_DN));
       pds_barrier();
+#pragma unroll
+      for (int s = kPdsPre; s < kPdsRing; ++s) grefill(gc, ring[s]);   // the input is staged: the rest of the ring
       if (is_x) ts(l, PH_QKV, 2);
       ac = acur(l);   // the attention's first block: issued after the closing barrier
       gemv_phase(p);
@@ -584,7 +590,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       // would queue behind these in the CU's memory pipeline)
       pds_barrier();
 #pragma unroll
-      for (int s = 0; s < kPdsRing; ++s) arefill(ac, ring[s]);
+      for (int s = 0; s < kPdsPre; ++s) arefill(ac, ring[s]);
     }
 
     // ---------------- attention split (kvh, sp): partials as ti_attn_decode_partials
@@ -609,6 +615,8 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       }
       pds_barrier();
       pds_barrier();
+#pragma unroll
+      for (int s = kPdsPre; s < kPdsRing; ++s) arefill(ac, ring[s]);
       if (is_x) ts(l, PH_ATT, 2);
       {
         const int dl = lane & 15, kg = lane >> 4;
@@ -693,7 +701,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       // would queue behind these in the CU's memory pipeline)
       pds_barrier();
 #pragma unroll
-      for (int s = 0; s < kPdsRing; ++s) grefill(gc, ring[s]);
+      for (int s = 0; s < kPdsPre; ++s) grefill(gc, ring[s]);
     }
 
     // ---------------- O: x = the splits merged (gemv XM_ATTN staging), residual + fold (ffn_norm)
@@ -745,6 +753,8 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
         }
       }
       pds_barrier();
+#pragma unroll
+      for (int s = kPdsPre; s < kPdsRing; ++s) grefill(gc, ring[s]);
       if (is_x) ts(l, PH_O, 2);
       GCur gnx = gcur(l, PH_GU);
       gemv_phase(p);
@@ -759,7 +769,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       // would queue behind these in the CU's memory pipeline)
       pds_barrier();
 #pragma unroll
-      for (int s = 0; s < kPdsRing; ++s) grefill(gnx, ring[s]);
+      for (int s = 0; s < kPdsPre; ++s) grefill(gnx, ring[s]);
       gc = gnx;
     }
 
@@ -774,6 +784,8 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       stage_f16_g(a.fxg, H, pds_tag(epoch, l, PH_O));
       if (is_x) rms = fold_rms_g(grid, H, pds_tag(epoch, l, PH_O));
       pds_barrier();
+#pragma unroll
+      for (int s = kPdsPre; s < kPdsRing; ++s) grefill(gc, ring[s]);
       if (is_x) ts(l, PH_GU, 2);
       GCur gnx = gcur(l, PH_DN);
       gemv_phase(p);
@@ -796,7 +808,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       // would queue behind these in the CU's memory pipeline)
       pds_barrier();
 #pragma unroll
-      for (int s = 0; s < kPdsRing; ++s) grefill(gnx, ring[s]);
+      for (int s = 0; s < kPdsPre; ++s) grefill(gnx, ring[s]);
       gc = gnx;
     }
 
@@ -809,6 +821,8 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       pds_barrier();
       stage_f16_g(a.actg, I, pds_tag(epoch, l, PH_GU));
       pds_barrier();
+#pragma unroll
+      for (int s = kPdsPre; s < kPdsRing; ++s) grefill(gc, ring[s]);
       if (is_x) ts(l, PH_DN, 2);
       GCur gnx = gcur(l + 1, PH_QKV);
       gemv_phase(p);
@@ -825,7 +839,7 @@ __global__ __launch_bounds__(kPdsThreads, 1) void pds_kernel(const PdsArgs a) {
       // would queue behind these in the CU's memory pipeline)
       pds_barrier();
 #pragma unroll
-      for (int s = 0; s < kPdsRing; ++s) grefill(gnx, ring[s]);
+      for (int s = 0; s < kPdsPre; ++s) grefill(gnx, ring[s]);
       gc = gnx;
     }
   }
