@@ -234,7 +234,15 @@ typedef struct ti_epilogue {
   /* TI_EPI_STORE_F16 / TI_EPI_SILU_MUL_F16 of the batched-rows kernels (M > 16 or packed x):
    * write the fp16 output in TI_X_F16_PACKED order (K = ldo, ldo % 128 == 0) */
   int32_t out_packed;
+  /* Split-K workspace of the tile GEMM (int4 fp16 rows from TI_GEMM_TILE_ROWS on): device memory
+   * of splitk_bytes bytes whose first TI_SPLITK_TICKET_BYTES the owner zeroes once (every launch
+   * leaves them zeroed); the fp32 partial blocks follow.  With it, narrow outputs split K over
+   * workgroups to fill the chip (ti_gemm_tile_plan); NULL = no split.  One launch at a time per
+   * workspace (stream order). */
+  void* splitk_ws;
+  int64_t splitk_bytes;
 } ti_epilogue;
+#define TI_SPLITK_TICKET_BYTES (256 * 1024)
 
 int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind,
                    int ldx, const float* norm_w, float eps, int M, int N, int K,
@@ -254,6 +262,11 @@ int ti_gemm_max_rows(int bits, int x_kind, int N, int K);
  * operands are best given as TI_X_F16_PACKED.  From 65 rows (TI_GEMM_TILE_ROWS, env, <= 65) on
  * the LDS-tiled kernel takes TI_X_F16 rows. */
 int ti_gemm_packed_rows(int bits, int M);
+/* The tile GEMM's plan for an int4 (bits 4 or 4 | TI_BITS_G32) M x N x K call with a split-K
+ * workspace of ws_bytes (0 = none): row-waves, weight tiles per wave and k-slices (1 = no split;
+ * K is split only where one slice per column block would leave most CUs idle, TI_GEMM_SPLITK=0
+ * never).  TI_ERR_UNSUPPORTED when the call would not take the tile kernel. */
+int ti_gemm_tile_plan(int bits, int M, int N, int K, int64_t ws_bytes, int* wmr, int* tpw, int* n_ks);
 /* y[m][0:K] = fp16(rms_norm(x[m][0:K]) * w), tensor_engine.cpp:1452-1508 (the batched path's
  * activation prep; the same arithmetic as the fused TI_X_F32_RMSNORM prologue). */
 int ti_rmsnorm_f16(const float* x, int ldx, const float* w, float eps, uint16_t* y, int ldy, int M, int K,

@@ -18,10 +18,32 @@ pytestmark = pytest.mark.gpu
 f16, f32 = np.float16, np.float32
 
 
-def run(ti, tiles, scales, x16, M, N, K, ep):
+SPLITK_BYTES = 64 << 20
+TICKET_BYTES = 256 * 1024   # TI_SPLITK_TICKET_BYTES
+
+
+@pytest.fixture(scope="module")
+def splitk_ws(ti):
+    b = ti.DeviceBuffer(SPLITK_BYTES)
+    b.zero()
+    return b
+
+
+def tile_plan(ti, M, N, K, ws_bytes=SPLITK_BYTES, bits=4):
+    a, b, c = C.c_int(), C.c_int(), C.c_int()
+    rc = ti.lib().ti_gemm_tile_plan(bits, M, N, K, ws_bytes, C.byref(a), C.byref(b), C.byref(c))
+    return (a.value, b.value, c.value) if rc == 0 else None
+
+
+def run(ti, tiles, scales, x16, M, N, K, ep, ws=None):
+    """One call; with ws (the split-K workspace) its tickets must be left re-armed (zero)."""
     L = ti.lib()
+    if ws is not None:
+        ep.splitk_ws, ep.splitk_bytes = ws.ptr, ws.nbytes
     ti.check(L.ti_gemm_wq_a16(tiles.ptr, scales.ptr, 4, x16.ptr, ti.X_F16, K, None, 1e-5, M, N, K, C.byref(ep), None))
     ti.sync()
+    if ws is not None:
+        assert not ws.download(np.int32, (TICKET_BYTES // 4,)).any(), "split-K tickets not re-armed"
 
 
 # (M, K, N): rows 17-32 (two 16-row blocks), long K at few rows (one block), ragged tiles per
@@ -34,8 +56,14 @@ def run(ti, tiles, scales, x16, M, N, K, ep):
                                    (129, 384, 16),
                                    # tile kernel at prefill chunks: 128 / 64 columns per workgroup, ragged tiles and rows
                                    (512, 4096, 22016), (700, 4096, 12288 + 48), (1000, 1152, 4000 + 16),
-                                   (1024, 384, 16)])
-def test_batched_store(ti, oracle, M, K, N):
+                                   (1024, 384, 16),
+                                   # split K (with the workspace): narrow outputs at 65-128 rows, ragged slices
+                                   (65, 4096, 4096), (128, 11008, 4096 + 16), (100, 14336, 512), (96, 3200, 1040)])
+@pytest.mark.parametrize("splitk", [False, True])
+def test_batched_store(ti, oracle, splitk_ws, M, K, N, splitk):
+    """Without a workspace: the batched-rows kernels (<= 64 rows) and the tile kernel; with one
+    (the engine's form), the tile kernel splits K over workgroups where the plan
+    (ti_gemm_tile_plan) says so."""
     rng = np.random.RandomState(M * 7 + K + N)
     w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
     x = rng.standard_normal((M, K)).astype(f16)
@@ -44,14 +72,54 @@ def test_batched_store(ti, oracle, M, K, N):
     yd = ti.DeviceBuffer(M * N * 4)
     ep = ti.Epilogue()
     ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F32, N, yd.ptr
-    run(ti, dev(ti, tiles), dev(ti, scales), dev(ti, x), M, N, K, ep)
+    run(ti, dev(ti, tiles), dev(ti, scales), dev(ti, x), M, N, K, ep, splitk_ws if splitk else None)
     wf = deq(oracle, w, 4)
     xa = x.astype(f32)
     assert_close_dot(yd.download(f32, (M, N)), xa.astype(np.float64) @ wf.astype(np.float64), xa, wf)
 
 
-def test_batched_resid_silu_logits(ti, oracle):
+def test_splitk_plans_split_narrow_outputs(ti):
+    """Tile-kernel calls whose one-slice grid would leave most CUs idle (narrow outputs at 65-128
+    rows) split K, within the workspace; wide or tall calls and 17..64 rows do not."""
+    for M, N, K in [(65, 4096, 4096), (128, 4096, 4096), (128, 4096, 11008), (100, 512, 14336)]:
+        wmr, tpw, ks = tile_plan(ti, M, N, K)
+        assert ks > 1, (M, N, K)
+        n_cb = -(-(N // 16) // ((8 // wmr) * tpw))
+        n_rb = -(-M // (64 * wmr))
+        assert ks * n_cb * n_rb * 8 * tpw * 4 * 64 * 16 + TICKET_BYTES <= SPLITK_BYTES
+        assert tile_plan(ti, M, N, K, ws_bytes=0)[2] == 1            # no workspace: no split
+    assert tile_plan(ti, 512, 22016, 4096)[2] == 1
+    assert tile_plan(ti, 64, 4096, 4096) is None                      # batched-rows kernel
+    assert ti.lib().ti_gemm_packed_rows(4, 64) == 1
+
+
+def test_splitk_repeat_is_deterministic(ti, oracle, splitk_ws):
+    """The last arriver sums the k-slices in slice order: repeated calls give identical bits."""
+    M, K, N = 128, 11008, 4096
+    assert tile_plan(ti, M, N, K)[2] > 1
+    rng = np.random.RandomState(11)
+    w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
+    x = rng.standard_normal((M, K)).astype(f16)
+    tiles, scales = ti.wpack_host(w, 4)
+    td, sd, xd = dev(ti, tiles), dev(ti, scales), dev(ti, x)
+    outs = []
+    for _ in range(3):
+        yd = ti.DeviceBuffer(M * N * 4)
+        ep = ti.Epilogue()
+        ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F32, N, yd.ptr
+        run(ti, td, sd, xd, M, N, K, ep, splitk_ws)
+        outs.append(yd.download(f32, (M, N)))
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+    assert np.array_equal(outs[0].view(np.uint32), outs[2].view(np.uint32))
+    wf = deq(oracle, w, 4)
+    xa = x.astype(f32)
+    assert_close_dot(outs[0], xa.astype(np.float64) @ wf.astype(np.float64), xa, wf)
+
+
+@pytest.mark.parametrize("splitk", [False, True])
+def test_batched_resid_silu_logits(ti, oracle, splitk_ws, splitk):
     M, K = 57, 2048
+    ws = splitk_ws if splitk else None
     rng = np.random.RandomState(5)
     x = rng.standard_normal((M, K)).astype(f16)
     xd, xa = dev(ti, x), x.astype(np.float64)
@@ -63,7 +131,7 @@ def test_batched_resid_silu_logits(ti, oracle):
     rd = dev(ti, r)
     ep = ti.Epilogue()
     ep.kind, ep.ldo, ep.out = ti.EPI_RESID_F32, N, rd.ptr
-    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, N, K, ep)
+    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, N, K, ep, ws)
     wf = deq(oracle, w, 4)
     assert_close_dot(rd.download(f32, (M, N)) - r, xa @ wf.astype(np.float64), x.astype(f32), wf, rel=5e-5)
     # SiLU(gate) * up, gate/up interleaved 8 rows each per tile
@@ -75,7 +143,7 @@ def test_batched_resid_silu_logits(ti, oracle):
     yd = ti.DeviceBuffer(M * I * 2)
     ep = ti.Epilogue()
     ep.kind, ep.ldo, ep.out = ti.EPI_SILU_MUL_F16, I, yd.ptr
-    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, 2 * I, K, ep)
+    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, 2 * I, K, ep, ws)
     gg, uu = xa @ deq(oracle, g, 4).astype(np.float64), xa @ deq(oracle, u, 4).astype(np.float64)
     np.testing.assert_allclose(yd.download(f16, (M, I)).astype(np.float64), uu * (gg / (1 + np.exp(-gg))),
                                rtol=3e-3, atol=2e-3)
@@ -88,7 +156,7 @@ def test_batched_resid_silu_logits(ti, oracle):
     ctr = dev(ti, np.array([3], np.int32))
     ep = ti.Epilogue()
     ep.kind, ep.ldo, ep.out, ep.argmax, ep.step_ctr, ep.advance = ti.EPI_LOGITS_ARGMAX, V, ld.ptr, am.ptr, ctr.ptr, 2
-    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, V, K, ep)
+    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, V, K, ep, ws)
     logits = ld.download(f32, (M, V))
     keys = am.download(np.uint64, (M, ti.ARGMAX_SLOTS)).max(axis=1)
     np.testing.assert_array_equal((0xFFFFFFFF - (keys & 0xFFFFFFFF)).astype(np.int64), np.argmax(logits, axis=1))
@@ -96,8 +164,9 @@ def test_batched_resid_silu_logits(ti, oracle):
     np.testing.assert_allclose(logits, xa @ deq(oracle, w, 4).astype(np.float64), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("splitk", [False, True])
 @pytest.mark.parametrize("hd,nh,nkv", [(128, 4, 4), (64, 8, 2)])
-def test_batched_qkv_rope_kv_append(ti, oracle, hd, nh, nkv):
+def test_batched_qkv_rope_kv_append(ti, oracle, splitk_ws, hd, nh, nkv, splitk):
     M, H, max_seq, theta = 45, 512, 40, 10000.0
     qd, kvd = nh * hd, nkv * hd
     N = qd + 2 * kvd
@@ -118,7 +187,7 @@ def test_batched_qkv_rope_kv_append(ti, oracle, hd, nh, nkv):
     ep.kind, ep.ldo, ep.out = ti.EPI_QKV_ROPE_KV, qd, qbuf.ptr
     ep.q_dim, ep.kv_dim, ep.head_dim, ep.max_seq = qd, kvd, hd, max_seq
     ep.pos, ep.rope_cs, ep.k_cache, ep.v_cache, ep.kv_stream_stride = posd.ptr, csd.ptr, kc.ptr, vc.ptr, stride
-    run(ti, dev(ti, tiles), dev(ti, scales), dev(ti, x), M, N, H, ep)
+    run(ti, dev(ti, tiles), dev(ti, scales), dev(ti, x), M, N, H, ep, splitk_ws if splitk else None)
     q, k, v = (x.astype(np.float64) @ deq(oracle, w, 4).astype(np.float64) for w in ws)
     kcache = kc.download(f16, (M, nkv, max_seq, hd)).astype(f32)
     vcache = vc.download(f16, (M, nkv, max_seq, hd)).astype(f32)

@@ -111,6 +111,8 @@ struct ti_engine {
   float* draws = nullptr;      // [max_batch][draw_cap] uniform draws, per new token
   float* lps = nullptr;        // [max_batch][draw_cap] log p of the sampled tokens
   int draw_cap = 0;
+  void* splitk_ws = nullptr;   // tile GEMM split-K workspace (ti_epilogue.splitk_ws), int4 engines
+  size_t splitk_bytes = 0;
   void* samp_ws = nullptr;     // ti_sample_step_ws workspace (top_k > TI_SAMPLE_MAX_K)
   size_t samp_ws_bytes = 0;
   // prefill (forward_pass over prompt tokens): up to pf_rows prompt tokens of one stream run
@@ -291,6 +293,8 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
     if (ep.v_cache) ep.v_cache += (size_t)m0 * ep.kv_stream_stride;
     if (ep.argmax) ep.argmax += (size_t)m0 * TI_ARGMAX_SLOTS;
     if (!(last_gets_ctr && m0 + mm >= M)) ep.step_ctr = nullptr;
+    ep.splitk_ws = e->splitk_ws;
+    ep.splitk_bytes = (int64_t)e->splitk_bytes;
     const void* xm = static_cast<const char*>(x) + (size_t)m0 * ldx * x_elem;
     TI_TRY(ti_gemm_wq_a16(W.tiles, W.scales, c.bits, xm, x_kind, ldx, nw, c.eps, mm, W.N, W.K, &ep, e->s));
   }
@@ -891,6 +895,12 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
       return fail(rc);
     if (const char* env = getenv("TI_ATTN_PART")) e->part_on = atoi(env) != 0;
     if (const char* env = getenv("TI_FOLD")) e->fold_on = atoi(env) != 0;
+    if ((c.bits & ~TI_BITS_G32) == 4) {   // batched rows and prompt chunks: split-K tile GEMM (TI_SPLITK_MB, 0 = off)
+      const char* env = getenv("TI_SPLITK_MB");
+      const size_t mb = env ? (size_t)std::max(0, atoi(env)) : 64;
+      if (mb && (rc = e->alloc(&e->splitk_ws, mb << 20))) return fail(rc);
+      e->splitk_bytes = mb << 20;
+    }
     if ((rc = e->alloc_t(&e->qa_ctr, (size_t)c.heads * 16))) return fail(rc);
     if (const char* env = getenv("TI_QKV_ATTN")) e->qa_on = atoi(env) != 0;
     e->chain_slots = 2 + 5 * c.layers;

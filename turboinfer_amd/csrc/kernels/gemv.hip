@@ -1482,8 +1482,68 @@ __device__ __forceinline__ u32x4 ld_w_asm(const u32x4* p) {
   return v;
 }
 
+// Split-K merge of one wave's block (n_ks > 1): every k-slice's wave stores its fp32 partial
+// block write-through into the workspace and adds to the block's ticket after its stores have
+// drained; the last arriver reads the other slices back (sc1 loads, CH slices per round trip),
+// sums the n_ks slices in slice order (deterministic whatever the arrival order), re-arms the
+// ticket and runs the epilogue.  Workspace: ti_epilogue.splitk_ws (include/ti_hip.h).
+template <int TPW>
+__device__ __forceinline__ bool splitk_merge(const GemvArgs& a, f32x4 (&acc)[TPW][4], int wave_id, int n_waves, int ks,
+                                             int n_ks, int lane) {
+  char* ws = (char*)a.epi.splitk_ws;
+  int32_t* ticket = (int32_t*)ws + wave_id;
+  const __amdgpu_buffer_rsrc_t rs = sc1_rsrc(ws + TI_SPLITK_TICKET_BYTES);
+  constexpr int kSlab = TPW * 4 * kWave * 16;   // bytes per wave and slice
+  auto off = [&](int sl, int t, int b) {
+    return (uint32_t)(((size_t)sl * n_waves + wave_id) * kSlab + (size_t)((t * 4 + b) * kWave + lane) * 16);
+  };
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) __builtin_amdgcn_raw_buffer_store_b128(acc[t][b], rs, off(ks, t, b), 0, kAuxSc1Load);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int arrived = 0;
+  if (lane == 0) arrived = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  arrived = __builtin_amdgcn_readfirstlane(arrived);
+  if (arrived != n_ks - 1) return false;
+#if TI_GEMV_EXP & 1024   // diagnostic: no read-back (the last arriver keeps its own slice)
+  if (lane == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+#endif
+  constexpr int CH = TPW >= 4 ? 1 : 4 / TPW;   // slices per round trip (VGPR budget)
+  f32x4 sum[TPW][4];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) sum[t][b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+  for (int s0 = 0; s0 < n_ks; s0 += CH) {
+    f32x4 ld[CH][TPW][4];
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          ld[c][t][b] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off(min(s0 + c, n_ks - 1), t, b), 0, kAuxSc1Load));
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      if (s0 + c < n_ks)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) sum[t][b] += s0 + c == ks ? acc[t][b] : ld[c][t][b];
+  }
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[t][b] = sum[t][b];
+  if (lane == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
+  return true;
+}
+
 template <int TPW, bool G32 = false, int WMR = 2, int XB = 2>
-__global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb) {
+__global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb, int n_ks) {
   constexpr int WCOL = kGemvWaves / WMR, BM = 64 * WMR;   // column-waves, rows per workgroup
   static_assert(XB == 2 || (XB == 4 && TI_TILE_ASM), "deep activation ring: asm-issued DMA only");
   constexpr int XL = XB - 1;                               // groups of activations issued ahead
@@ -1491,19 +1551,23 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   const int KT = a.K >> 7, NT = a.N >> 4;
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, kq = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wave / WCOL, wn = wave % WCOL;
-  // blockIdx -> (row block, column block): the n_rb row blocks of a column block share an XCD
+  // blockIdx -> (row block, k-slice, column block): the n_rb row blocks and n_ks k-slices of a
+  // column block share an XCD; k-slice ks covers groups [kb, kb + nk)
   const int b8 = blockIdx.x & 7, rest = blockIdx.x >> 3;
-  const int rb = rest % n_rb, cb = (rest / n_rb) * 8 + b8;
+  const int rb = rest % n_rb, r2 = rest / n_rb, ks = r2 % n_ks, cb = (r2 / n_ks) * 8 + b8;
   if (cb >= n_cb) return;
+  const int kb = ks * KT / n_ks, nk = (ks + 1) * KT / n_ks - kb;
   const int m0 = rb * BM, t0 = cb * WCOL * TPW;
   f16* xb = (f16*)smem;                                       // [2][BM rows][128 k] swizzled
   constexpr int SG = G32 ? 4 : 1;                             // scales per tile row and group
   uint16_t* sl = (uint16_t*)(smem + XB * BM * 256);           // [WCOL TPW tiles][KT][SG][16]
-  const int n_sc = WCOL * TPW * KT * 2 * SG;                  // 16-byte pieces
+  const int n_sc = WCOL * TPW * nk * 2 * SG;                  // 16-byte pieces of this k-slice
   const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16 * SG);
   const int ntile_ok = min(WCOL * TPW, NT - t0);
-  for (int i = tid; i < n_sc; i += kGemvThreads)
-    ((u32x4*)sl)[i] = i < ntile_ok * KT * 2 * SG ? ld_w(sg + i) : (u32x4){0u, 0u, 0u, 0u};
+  for (int i = tid; i < n_sc; i += kGemvThreads) {
+    const int j = i / (nk * 2 * SG), p = (j * KT + kb) * 2 * SG + (i - j * nk * 2 * SG);   // tile j, piece in slice
+    ((u32x4*)sl)[p] = j < ntile_ok ? ld_w(sg + p) : (u32x4){0u, 0u, 0u, 0u};
+  }
 
   const f16* xg = (const f16*)a.x;
   const uint32_t xb_lds = (uint32_t)(uintptr_t)xb;   // LDS byte address of the staging buffers
@@ -1551,10 +1615,10 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   constexpr int kTileWR = TI_TILE_ASM ? 3 : (TPW == 4 ? 2 : 4);
   u32x4 W[kTileWR][TPW];
   if constexpr (!TI_TILE_ASM) {   // (the asm pipeline issues its first loads inside its loop)
-    if constexpr (TI_TILE_XREG) load_xr(0);
-    else issue_x(0);
+    if constexpr (TI_TILE_XREG) load_xr(kb);
+    else issue_x(kb);
 #pragma unroll
-    for (int u = 0; u < kTileWR - 1; ++u) load_w(W[u], u);
+    for (int u = 0; u < kTileWR - 1; ++u) load_w(W[u], kb + min(u, nk - 1));
   }
   f32x4 acc[TPW][4];
 #pragma unroll
@@ -1613,7 +1677,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   };
   // Per group kg: x(kg) and W(kg) were issued earlier; issue x(kg + 1) and W(kg + WR - 1),
   // wait until only those weight loads are younger than x(kg + 1)... (see below), compute kg.
-  const int KTP = (KT + kTileWR - 1) / kTileWR * kTileWR;
+  const int KTP = (nk + kTileWR - 1) / kTileWR * kTileWR;
   if constexpr (TI_TILE_ASM) {
     // Every group issues, in order, x(kg + XL) (2 WMR DMA instructions into buffer
     // (kg + XL) % XB, read last in group kg - 1) and W(kg + 2) (TPW loads into ring slot
@@ -1625,20 +1689,20 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
     //   W(kg): after group kg's own issue, two whole groups are younger -> vmcnt(NWT), then the
     //          slot's registers are tied ("+v") so nothing reads them earlier.
     constexpr int NX = (XL - 1) * (2 * WMR + TPW) + TPW, NWT = 2 * (2 * WMR + TPW);
-    for (int k0 = -kTileWR; k0 < KT; k0 += kTileWR) {
+    for (int k0 = -kTileWR; k0 < nk; k0 += kTileWR) {   // kg: group of this k-slice
 #pragma unroll
       for (int u = 0; u < kTileWR; ++u) {
         const int kg = k0 + u;
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NX) : "memory");   // x(kg): this wave's DMA
         lds_barrier();
-        issue_x(max(0, min(kg + XL, KT - 1)));
-        load_w(W[(u + 2) % kTileWR], max(0, kg + 2));
+        issue_x(kb + max(0, min(kg + XL, nk - 1)));
+        load_w(W[(u + 2) % kTileWR], kb + max(0, min(kg + 2, nk - 1)));
         // (also in the groups without compute: a slot's load is always consumed by its tie, so
         // hipcc never hands its registers to anything else while the load is in flight)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NWT) : "memory");   // W(kg)
 #pragma unroll
         for (int t = 0; t < TPW; ++t) asm volatile("" : "+v"(W[u][t]));
-        if (kg >= 0 && kg < KT) compute(W[u], kg);
+        if (kg >= 0 && kg < nk) compute(W[u], kb + kg);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped loads past the end
@@ -1654,27 +1718,33 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
       // x(kg) landed (the loads younger than it: W(kg + WR - 2), TPW instructions) and every
       // wave is past compute(kg - 1), so buffer (kg + 1) & 1 is free
       if constexpr (TI_TILE_XREG) {
-        if (kg < KT) store_xr(kg);
+        if (kg < nk) store_xr(kb + kg);
       }
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TPW) : "memory");
       lds_barrier();
-      if (kg < KT) {
-        if (kg + 1 < KT) {
-          if constexpr (TI_TILE_XREG) load_xr(kg + 1);
-          else issue_x(kg + 1);
+      if (kg < nk) {
+        if (kg + 1 < nk) {
+          if constexpr (TI_TILE_XREG) load_xr(kb + kg + 1);
+          else issue_x(kb + kg + 1);
         }
-        load_w(W[(u + kTileWR - 1) % kTileWR], kg + kTileWR - 1);
-        compute(W[u], kg);
+        load_w(W[(u + kTileWR - 1) % kTileWR], kb + min(kg + kTileWR - 1, nk - 1));
+        compute(W[u], kb + kg);
       }
     }
   }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if TI_GEMV_EXP & 512   // diagnostic: no split-K merge at all (every slice runs the epilogue)
+  const bool merged = true;
+#else
+  const bool merged = n_ks == 1 || splitk_merge<TPW>(a, acc, (cb * n_rb + rb) * kGemvWaves + wave,
+                                                      n_cb * n_rb * kGemvWaves, ks, n_ks, lane);
+#endif
   // epilogue straight from the accumulators (16 x 4 outputs per lane pattern of the MFMA); the
   // tile loop stays rolled (64 inlined epilogues are too large to unroll), so its accumulators
   // are picked by static selects and acc stays in registers
 #pragma unroll 1
-  for (int t = 0; t < TPW; ++t) {
+  for (int t = 0; t < (merged ? TPW : 0); ++t) {
     const int tn = t0 + wn * TPW + t;
     f32x4 av[4];
 #pragma unroll
@@ -1768,6 +1838,42 @@ __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
     }
   }
   return best;
+}
+
+// Tile GEMM plan with split-K (ti_epilogue.splitk_ws).  A split costs ≈ 5–14 µs of seam
+// (write-through partial stores, the ticket, the last arriver's read-back: tools/splitk_diag.sh)
+// and a tile workgroup carries ≈ 7 µs of fixed pipeline cost, so K is split only where the
+// one-slice grid would leave most of the chip idle: at most a quarter of the CUs busy, each
+// slice still at least 8 groups deep, the slices filling at most one round of workgroups.
+// (17..64 decode rows stay on the batched-rows kernel: split there measured slower, 5–14 µs of
+// seam against 12–50 µs launches.)  TI_GEMM_SPLITK=0 turns splitting off (A/B knob).
+static int g_splitk = -1;
+__host__ inline bool splitk_on() {
+  if (g_splitk < 0) {
+    const char* e = getenv("TI_GEMM_SPLITK");
+    g_splitk = e ? atoi(e) != 0 : 1;
+  }
+  return g_splitk != 0;
+}
+__host__ inline size_t splitk_slab_bytes(int n_ks, int n_cb, int n_rb, int tpw) {
+  return (size_t)n_ks * n_cb * n_rb * kGemvWaves * tpw * 4 * kWave * 16;
+}
+__host__ inline void tile_plan(int M, int N, int K, bool g32, int cus, int64_t ws_bytes, int* wmr_o, int* tpw_o,
+                               int* ks_o) {
+  const int shape = tile_shape(M, N, K, g32, cus);   // the one-slice choice (knobs applied there)
+  const int wmr = shape >> 3, tpw = shape & 7;
+  *wmr_o = wmr;
+  *tpw_o = tpw;
+  *ks_o = 1;
+  if (!splitk_on() || ws_bytes <= TI_SPLITK_TICKET_BYTES) return;
+  const int NT = N >> 4, KT = K >> 7, cols = (8 / wmr) * tpw;
+  const int n_cb = (NT + cols - 1) / cols, n_rb = (M + 64 * wmr - 1) / (64 * wmr);
+  const long wgs = (long)n_cb * n_rb;
+  if (wgs * 4 > cus || (size_t)wgs * kGemvWaves * 4 > TI_SPLITK_TICKET_BYTES) return;
+  int S = (int)(cus / wgs);
+  while (S > 1 && ((KT + S - 1) / S < 8 || splitk_slab_bytes(S, n_cb, n_rb, tpw) + TI_SPLITK_TICKET_BYTES > (size_t)ws_bytes))
+    --S;
+  *ks_o = S;
 }
 
 __host__ inline int gemv_xmode(int x_kind, int M, int K) {
@@ -2052,6 +2158,17 @@ static bool use_batched(int bits, int x_kind, int M, int N, int K) {
 
 extern "C" int ti_gemm_packed_rows(int bits, int M) { return bits == 4 && M > 16 && M < ti::tile_rows() ? 1 : 0; }
 
+extern "C" int ti_gemm_tile_plan(int bits, int M, int N, int K, int64_t ws_bytes, int* wmr, int* tpw, int* n_ks) {
+  const bool g32 = (bits & TI_BITS_G32) != 0;
+  if (!wmr || !tpw || !n_ks) return ti_set_error(TI_ERR_ARG, "ti_gemm_tile_plan: null pointer");
+  if ((bits & ~TI_BITS_G32) != 4 || M < ti::tile_rows() || M > TI_GEMM_MAX_ROWS || N < 16 || (N & 15) || K < 128 ||
+      (K & 127))
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_tile_plan: M=%d N=%d K=%d bits %d is not a tile-kernel call", M, N,
+                        K, bits);
+  ti::tile_plan(M, N, K, g32, query_cus(), ti::splitk_on() ? ws_bytes : 0, wmr, tpw, n_ks);
+  return TI_OK;
+}
+
 extern "C" int ti_gemm_max_rows(int bits, int x_kind, int N, int K) {
   if (N < 16 || K < 128) return 0;
   if (bits & TI_BITS_G32) {   // group-32 weights: the fused kernel; int4 fp16 rows also the tile kernel
@@ -2185,16 +2302,15 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
                         "ti_gemm_wq_a16: M=%d K=%d exceeds the fused kernel (ti_gemm_max_rows); the batched-rows "
                         "kernel needs bits 4 and fp16 rows (normalise with ti_rmsnorm_f16)", M, K);
   int grid = 0, lds = 0, ntl = 0, rMB = 0, rRG = 0;
+  const bool has_ws = epi->splitk_ws && epi->splitk_bytes > TI_SPLITK_TICKET_BYTES && splitk_on();
   const bool tile = batched && x_kind == TI_X_F16 && M >= tile_rows();
   const bool rows = !tile && batched && (packed_x || M > 32 || (M > 16 && rows_on()));
-  int n_cb = 0, n_rb = 0, tpw = 2, wmr = 2, xbuf = 2;
+  int n_cb = 0, n_rb = 0, n_ks = 1, tpw = 2, wmr = 2, xbuf = 2;
   if (tile) {
-    const int shape = tile_shape(M, N, K, g32, query_cus());   // the byte model (tile_shape)
-    wmr = shape >> 3;
-    tpw = shape & 7;
+    tile_plan(M, N, K, g32, query_cus(), has_ws ? epi->splitk_bytes : 0, &wmr, &tpw, &n_ks);   // (tile_plan)
     n_rb = (M + 64 * wmr - 1) / (64 * wmr);
     n_cb = ((N >> 4) + (8 / wmr) * tpw - 1) / ((8 / wmr) * tpw);
-    grid = (n_cb + 7) / 8 * 8 * n_rb;
+    grid = (n_cb + 7) / 8 * 8 * n_rb * n_ks;
     xbuf = tile_xb(K, tpw, g32, wmr);
     lds = tile_lds_bytes(K, tpw, g32, wmr, xbuf);
   } else if (rows) {
@@ -2242,7 +2358,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   hipStream_t s = (hipStream_t)stream;
   if (tile) {
     const void* f = tile_fn(tpw, g32, wmr, xbuf);
-    void* args[] = {&a, &n_cb, &n_rb};
+    void* args[] = {&a, &n_cb, &n_rb, &n_ks};
     TI_HIP_CHECK(hipLaunchKernel(f, dim3(grid), dim3(kGemvThreads), args, lds, s), "hipLaunchKernel(gemm_tile_kernel)");
     TI_LAUNCH_CHECK("gemm_tile_kernel");
     return TI_OK;
