@@ -941,8 +941,10 @@ __device__ __forceinline__ f16x8 deq_int4_signed(uint32_t w, uint32_t magic) {
   const f16x8 r = deq_int4_raw(w, magic);   // lanes (1024 + n) and (1024 + 16 n)
   const f16x2 lo_off = {(f16)-1032.0f, (f16)-1032.0f}, hi_mul = {(f16)0.0625f, (f16)0.0625f},
               hi_off = {(f16)-72.0f, (f16)-72.0f};
-  const f16x2 a = (f16x2){r[0], r[1]} + lo_off, b = (f16x2){r[2], r[3]} * hi_mul + hi_off;
-  const f16x2 c = (f16x2){r[4], r[5]} + lo_off, d = (f16x2){r[6], r[7]} * hi_mul + hi_off;
+  // (1024 + 16 n) / 16 - 72 = n - 8 exactly: one v_pk_fma_f16 (the build's -ffp-contract=off
+  // would otherwise split it into a multiply and an add)
+  const f16x2 a = (f16x2){r[0], r[1]} + lo_off, b = __builtin_elementwise_fma((f16x2){r[2], r[3]}, hi_mul, hi_off);
+  const f16x2 c = (f16x2){r[4], r[5]} + lo_off, d = __builtin_elementwise_fma((f16x2){r[6], r[7]}, hi_mul, hi_off);
   return (f16x8){a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
 }
 
@@ -1288,16 +1290,23 @@ __host__ __device__ inline int rows_lds_bytes(int mb_total, int ntl, int K) {
   return rows_slab_bytes(mb_total, ntl) + align16(ntl * (K >> 7) * 32);
 }
 
+// Workgroups: n_cg column groups x n_rb row blocks of 16 RG MB rows (narrow outputs split the
+// rows: a workgroup's activation bytes shrink with its rows, and its column group's weights are
+// re-read by the other row blocks from the same XCD's L2 -- blockIdx % 8 is the column group's
+// low bits, a speed placement only).
 template <int MB, int NTL, int RG, bool XP>
-__global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvArgs a, int grid) {
+__global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvArgs a, int n_cg, int n_rb) {
   constexpr int GW = RowsCfg<MB, NTL, RG>::kGroupWaves, WD = RowsCfg<MB, NTL, RG>::kWD;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KT = a.K >> 7, NT = a.N >> 4;
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, kq = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave / GW, gw = wave % GW;
-  const int t0 = (int)(blockIdx.x * (unsigned)NT / (unsigned)grid);
-  const int t1 = (int)((blockIdx.x + 1) * (unsigned)NT / (unsigned)grid);
+  const int rest = blockIdx.x >> 3, rb = rest % n_rb, cg = (rest / n_rb) * 8 + (blockIdx.x & 7);
+  if (cg >= n_cg) return;
+  const int b0 = rb * RG * MB;                       // first 16-row block of this workgroup
+  const int t0 = (int)(cg * (unsigned)NT / (unsigned)n_cg);
+  const int t1 = (int)((cg + 1) * (unsigned)NT / (unsigned)n_cg);
   const int ntl = t1 - t0;                           // NTL or NTL - 1
   const int NI = (KT + GW - 1) / GW, NIP = (NI + WD - 1) / WD * WD;
   ROWS_TS(0);
@@ -1329,12 +1338,12 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
 #pragma unroll
     for (int b = 0; b < MB; ++b) {
       if constexpr (XP) {   // TI_X_F16_PACKED: one contiguous KiB per (block, s4)
-        const int bb = min(grp * MB + b, (a.M - 1) >> 4);
+        const int bb = min(b0 + grp * MB + b, (a.M - 1) >> 4);
         const f16* xp = xg + ((size_t)(bb * KT + kt) * 4) * 512 + lane * 8;
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) x[b][s4] = *(const f16x8*)(xp + s4 * 512);
       } else {
-        const int m = min((grp * MB + b) * 16 + r, a.M - 1);
+        const int m = min((b0 + grp * MB + b) * 16 + r, a.M - 1);
         const f16* xr = xg + (size_t)m * a.ldx + kt * 128 + kq * 32;   // the tile's k order (A fragments)
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) x[b][s4] = *(const f16x8*)(xr + s4 * 8);
@@ -1416,7 +1425,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
     float v = 0.0f;
 #pragma unroll
     for (int w = 0; w < GW; ++w) v += sp[(g * GW + w) * kWave * 4];
-    const int m = bb * 16 + 4 * (lane >> 4) + i;
+    const int m = (b0 + bb) * 16 + 4 * (lane >> 4) + i;
     epilogue_mb(a, t0 + tl, m, n, v, ok && m < a.M);
   }
   ROWS_TS(5);
@@ -2040,31 +2049,73 @@ __host__ inline int rows_tiles_cap(int MB, int K) {
   const int lim = MB >= 2 ? 3 : 4, cap = 512 / (K >> 7);   // VGPR budget: no spills
   return cap < 1 ? 1 : (cap > lim ? lim : cap);
 }
-__host__ inline int rows_grid(int MB, int N, int K, int num_cus, int* ntl_out) {
-  const int NT = N >> 4, cap = rows_tiles_cap(MB, K);
-  int grid = NT < num_cus ? NT : num_cus;
-  if ((NT + grid - 1) / grid > cap) grid = (NT + cap - 1) / cap;
-  *ntl_out = (NT + grid - 1) / grid;
-  return grid;
+// Column groups for row blocks of MB blocks per group (one round of workgroups where the VGPR
+// cap on tiles per workgroup allows).
+__host__ inline int rows_grid(int MB, int N, int K, int num_cus, int* ntl_out, int n_rb = 1) {
+  const int NT = N >> 4, cap = rows_tiles_cap(MB, K), per = num_cus / n_rb > 0 ? num_cus / n_rb : 1;
+  int n_cg = NT < per ? NT : per;
+  if ((NT + n_cg - 1) / n_cg > cap) n_cg = (NT + cap - 1) / cap;
+  *ntl_out = (NT + n_cg - 1) / n_cg;
+  return n_cg;
+}
+// Rows per workgroup (16 RG MB): the fewest activation + weight bytes per workgroup over the
+// launch's rounds -- a workgroup streams its rows' activations (R K 2 bytes, L2) and its tiles'
+// weights (ntl 8 K bytes); narrow outputs (O, down) take 16-row blocks, wide ones all the rows.
+// TI_GEMM_ROWS_SPLIT=0 keeps all rows in one workgroup (A/B knob).
+static int g_rows_split = -1;
+__host__ inline void rows_plan(int M, int N, int K, int cus, int* MB, int* RG, int* n_rb, int* n_cg, int* ntl) {
+  if (g_rows_split < 0) {
+    const char* e = getenv("TI_GEMM_ROWS_SPLIT");
+    g_rows_split = e ? atoi(e) != 0 : 1;
+  }
+  rows_shape(M, MB, RG);   // all rows in one workgroup
+  *n_rb = 1;
+  *n_cg = rows_grid(*MB, N, K, cus, ntl);
+  if (!g_rows_split) return;
+  const int NT = N >> 4;
+  auto cost = [&](int mb, int rg, int nrb, int ncg, int nt) {
+    const long rounds = ((long)ncg * nrb + cus - 1) / cus;
+    return rounds * ((long)16 * rg * mb * K * 2 + (long)nt * 8 * K);
+  };
+  long best = cost(*MB, *RG, 1, *n_cg, *ntl);
+  const int shapes[2][2] = {{1, 1}, {2, 1}};   // 16 and 32 rows per workgroup
+  for (const auto& sh : shapes) {
+    const int mb = sh[0], rg = sh[1], rows = 16 * mb * rg;
+    if (rows >= M) continue;
+    const int nrb = (M + rows - 1) / rows;
+    int nt = 0;
+    const int ncg = rows_grid(mb, N, K, cus, &nt, nrb);
+    const long c = cost(mb, rg, nrb, ncg, nt);
+    if (c * 20 < best * 17 && nt <= NT) {   // a clear (15 %) win only: the model ignores round overlap
+      best = c;
+      *MB = mb;
+      *RG = rg;
+      *n_rb = nrb;
+      *n_cg = ncg;
+      *ntl = nt;
+    }
+  }
 }
 template <int MB, int RG, bool XP>
-static int launch_rows_t(const GemvArgs& a, int ntl, int grid, int lds, hipStream_t s) {
-  if (ntl == 1) hipLaunchKernelGGL((gemm_rows_kernel<MB, 1, RG, XP>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
-  else if (ntl == 2) hipLaunchKernelGGL((gemm_rows_kernel<MB, 2, RG, XP>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
-  else if (ntl == 3) hipLaunchKernelGGL((gemm_rows_kernel<MB, 3, RG, XP>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
-  else if constexpr (MB < 2) hipLaunchKernelGGL((gemm_rows_kernel<MB, 4, RG, XP>), dim3(grid), dim3(kGemvThreads), lds, s, a, grid);
+static int launch_rows_t(const GemvArgs& a, int ntl, int n_cg, int n_rb, int lds, hipStream_t s) {
+  const dim3 grid((unsigned)((n_cg + 7) / 8 * 8 * n_rb));
+  if (ntl == 1) hipLaunchKernelGGL((gemm_rows_kernel<MB, 1, RG, XP>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
+  else if (ntl == 2) hipLaunchKernelGGL((gemm_rows_kernel<MB, 2, RG, XP>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
+  else if (ntl == 3) hipLaunchKernelGGL((gemm_rows_kernel<MB, 3, RG, XP>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
+  else if constexpr (MB < 2) hipLaunchKernelGGL((gemm_rows_kernel<MB, 4, RG, XP>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
   else return ti_set_error(TI_ERR_ARG, "gemm_rows_kernel: %d tiles per workgroup at MB %d", ntl, MB);
   TI_LAUNCH_CHECK("gemm_rows_kernel");
   return TI_OK;
 }
 template <bool XP>
-static int launch_rows_x(const GemvArgs& a, int MB, int RG, int ntl, int grid, int lds, hipStream_t s) {
-  if (RG == 2) return MB == 1 ? launch_rows_t<1, 2, XP>(a, ntl, grid, lds, s) : launch_rows_t<2, 2, XP>(a, ntl, grid, lds, s);
-  return MB == 1 ? launch_rows_t<1, 1, XP>(a, ntl, grid, lds, s) : launch_rows_t<2, 1, XP>(a, ntl, grid, lds, s);
+static int launch_rows_x(const GemvArgs& a, int MB, int RG, int ntl, int n_cg, int n_rb, int lds, hipStream_t s) {
+  if (RG == 2)
+    return MB == 1 ? launch_rows_t<1, 2, XP>(a, ntl, n_cg, n_rb, lds, s) : launch_rows_t<2, 2, XP>(a, ntl, n_cg, n_rb, lds, s);
+  return MB == 1 ? launch_rows_t<1, 1, XP>(a, ntl, n_cg, n_rb, lds, s) : launch_rows_t<2, 1, XP>(a, ntl, n_cg, n_rb, lds, s);
 }
-static int launch_rows(const GemvArgs& a, int MB, int RG, int ntl, int grid, int lds, hipStream_t s) {
-  return a.x_kind == TI_X_F16_PACKED ? launch_rows_x<true>(a, MB, RG, ntl, grid, lds, s)
-                                     : launch_rows_x<false>(a, MB, RG, ntl, grid, lds, s);
+static int launch_rows(const GemvArgs& a, int MB, int RG, int ntl, int n_cg, int n_rb, int lds, hipStream_t s) {
+  return a.x_kind == TI_X_F16_PACKED ? launch_rows_x<true>(a, MB, RG, ntl, n_cg, n_rb, lds, s)
+                                     : launch_rows_x<false>(a, MB, RG, ntl, n_cg, n_rb, lds, s);
 }
 #define TI_ROWS_FNS1(MB, RG, XP)                                                                          \
   (const void*)gemm_rows_kernel<MB, 1, RG, XP>, (const void*)gemm_rows_kernel<MB, 2, RG, XP>,                \
@@ -2301,7 +2352,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     return ti_set_error(TI_ERR_UNSUPPORTED,
                         "ti_gemm_wq_a16: M=%d K=%d exceeds the fused kernel (ti_gemm_max_rows); the batched-rows "
                         "kernel needs bits 4 and fp16 rows (normalise with ti_rmsnorm_f16)", M, K);
-  int grid = 0, lds = 0, ntl = 0, rMB = 0, rRG = 0;
+  int grid = 0, lds = 0, ntl = 0, rMB = 0, rRG = 0, r_rb = 1;
   const bool has_ws = epi->splitk_ws && epi->splitk_bytes > TI_SPLITK_TICKET_BYTES && splitk_on();
   const bool tile = batched && x_kind == TI_X_F16 && M >= tile_rows();
   const bool rows = !tile && batched && (packed_x || M > 32 || (M > 16 && rows_on()));
@@ -2315,8 +2366,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     lds = tile_lds_bytes(K, tpw, g32, wmr, xbuf);
   } else if (rows) {
     rows_on();
-    rows_shape(M, &rMB, &rRG);
-    grid = rows_grid(rMB, N, K, query_cus(), &ntl);
+    rows_plan(M, N, K, query_cus(), &rMB, &rRG, &r_rb, &grid, &ntl);   // grid: column groups
     lds = rows_lds_bytes(rRG * rMB, ntl, K);
   } else if (batched) {
     const int MB = M > 16 ? 2 : 1;
@@ -2363,7 +2413,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     TI_LAUNCH_CHECK("gemm_tile_kernel");
     return TI_OK;
   }
-  if (rows) return launch_rows(a, rMB, rRG, ntl, grid, lds, s);
+  if (rows) return launch_rows(a, rMB, rRG, ntl, grid, r_rb, lds, s);
   if (batched) return launch_mb(a, M > 16 ? 2 : 1, grid, ntl, lds, s);
   if (aff) return launch_gemv<4, true, true>(a, lds, s, grid, chain);
   if (g32) return bits == 4 ? launch_gemv<4, true>(a, lds, s, grid, chain) : launch_gemv<8, true>(a, lds, s, grid, chain);
