@@ -1286,16 +1286,21 @@ struct RowsCfg {
 __host__ __device__ inline int rows_slab_bytes(int mb_total, int ntl) {
   return align16(ntl * mb_total * kGemvWaves * kWave * 16);
 }
-__host__ __device__ inline int rows_lds_bytes(int mb_total, int ntl, int K) {
-  return rows_slab_bytes(mb_total, ntl) + align16(ntl * (K >> 7) * 32);
+__host__ __device__ inline int rows_lds_bytes(int mb_total, int ntl, int K, bool g32 = false) {
+  return rows_slab_bytes(mb_total, ntl) + align16(ntl * (K >> 7) * 32 * (g32 ? 4 : 1));
 }
 
 // Workgroups: n_cg column groups x n_rb row blocks of 16 RG MB rows (narrow outputs split the
 // rows: a workgroup's activation bytes shrink with its rows, and its column group's weights are
 // re-read by the other row blocks from the same XCD's L2 -- blockIdx % 8 is the column group's
 // low bits, a speed placement only).
-template <int MB, int NTL, int RG, bool XP>
+// G32: group-32 int4 tiles (GGUF Q4_0 blocks, TI_BITS_G32; row-major x only): MFMA step s4 of a
+// k-tile reads k-chunk 32 s4 + 8 kq and is scaled by its own block's scale (4 per tile row and
+// k-tile), as in the fused and tile kernels.
+template <int MB, int NTL, int RG, bool XP, bool G32 = false>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvArgs a, int n_cg, int n_rb) {
+  static_assert(!(XP && G32), "group-32 rows take row-major activations");
+  constexpr int SG = G32 ? 4 : 1;   // scales per tile row and k-tile
   constexpr int GW = RowsCfg<MB, NTL, RG>::kGroupWaves, WD = RowsCfg<MB, NTL, RG>::kWD;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KT = a.K >> 7, NT = a.N >> 4;
@@ -1311,13 +1316,23 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
   const int NI = (KT + GW - 1) / GW, NIP = (NI + WD - 1) / WD * WD;
   ROWS_TS(0);
   f32x4* slab = (f32x4*)smem;                        // after the stream: [NTL][RG * MB][8][64]
-  uint16_t* sl = (uint16_t*)(smem + rows_slab_bytes(RG * MB, NTL));   // [ntl][KT][16]
+  uint16_t* sl = (uint16_t*)(smem + rows_slab_bytes(RG * MB, NTL));   // [ntl][KT][SG][16]
 
-  // the workgroup's group scales (ntl * KT <= 512: two 16-byte pieces per thread), first
-  const int n_sc = ntl * KT * 2;
-  const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16);
-  const u32x4 sc0 = ld_w(sg + (tid < n_sc ? tid : 0));
-  const u32x4 sc1 = ld_w(sg + (tid + kGemvThreads < n_sc ? tid + kGemvThreads : 0));
+  // the workgroup's group scales (ntl * KT * SG <= 512: 2 SG 16-byte pieces per thread), first
+  const int n_sc = ntl * KT * 2 * SG;
+  const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16 * SG);
+  u32x4 scr[2];
+  if constexpr (G32) {   // transposed to [ntl][KT][16 rows][4 blocks]: one 8-byte LDS read per tile and item
+    for (int i = tid; i < n_sc; i += kGemvThreads) {
+      const u32x4 v = ld_w(sg + i);
+      const int rr0 = (i & 1) * 8, s4 = (i >> 1) & 3, tk = i >> 3;   // piece: 8 rows of block s4 of (tile, kt)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sl[(tk * 16 + rr0 + e) * 4 + s4] = (uint16_t)(v[e >> 1] >> (16 * (e & 1)));
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) scr[j] = ld_w(sg + (tid + j * kGemvThreads < n_sc ? tid + j * kGemvThreads : 0));
+  }
 
   const f16* xg = (const f16*)a.x;
   const u32x4* tb = a.tiles + lane;
@@ -1344,9 +1359,10 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
         for (int s4 = 0; s4 < 4; ++s4) x[b][s4] = *(const f16x8*)(xp + s4 * 512);
       } else {
         const int m = min((b0 + grp * MB + b) * 16 + r, a.M - 1);
-        const f16* xr = xg + (size_t)m * a.ldx + kt * 128 + kq * 32;   // the tile's k order (A fragments)
+        // the tile's k order (A fragments): k = 128 kt + 32 kq + 8 s4 (+ e), group-32 32 s4 + 8 kq
+        const f16* xr = xg + (size_t)m * a.ldx + kt * 128 + kq * (G32 ? 8 : 32);
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) x[b][s4] = *(const f16x8*)(xr + s4 * 8);
+        for (int s4 = 0; s4 < 4; ++s4) x[b][s4] = *(const f16x8*)(xr + s4 * (G32 ? 32 : 8));
       }
     }
   };
@@ -1357,8 +1373,11 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
     load_w(W[u], u);
     load_x(X[u], u);
   }
-  if (tid < n_sc) ((u32x4*)sl)[tid] = sc0;
-  if (tid + kGemvThreads < n_sc) ((u32x4*)sl)[tid + kGemvThreads] = sc1;
+  if constexpr (!G32) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (tid + j * kGemvThreads < n_sc) ((u32x4*)sl)[tid + j * kGemvThreads] = scr[j];
+  }
   lds_barrier();
   ROWS_TS(1);
 
@@ -1375,6 +1394,27 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
     const int ktc = kvalid ? kt : KT - 1;
 #pragma unroll
     for (int tl = 0; tl < NTL; ++tl) {
+      if constexpr (G32) {   // one scale per 32-k block: each MFMA step scaled on its own
+        const uint2 s4p = *(const uint2*)(sl + ((min(tl, ntl - 1) * KT + ktc) * 16 + r) * 4);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const f16x8 bf = deq_int4_signed(w[tl][s4], magic);
+          f32x4 t[MB];
+#pragma unroll
+          for (int b = 0; b < MB; ++b)
+            t[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(x[b][s4], bf, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+          const uint32_t sp = s4 < 2 ? s4p.x : s4p.y;
+          const float sc = kvalid ? h2f((uint16_t)(sp >> (16 * (s4 & 1)))) : 0.0f;
+#pragma unroll
+          for (int b = 0; b < MB; ++b) {
+            acc[tl][b][0] = fmaf(sc, t[b][0], acc[tl][b][0]);
+            acc[tl][b][1] = fmaf(sc, t[b][1], acc[tl][b][1]);
+            acc[tl][b][2] = fmaf(sc, t[b][2], acc[tl][b][2]);
+            acc[tl][b][3] = fmaf(sc, t[b][3], acc[tl][b][3]);
+          }
+        }
+        continue;
+      }
       f32x4 t[MB];
 #pragma unroll
       for (int b = 0; b < MB; ++b) t[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
@@ -2035,6 +2075,14 @@ __host__ inline void rows_shape(int M, int* MB, int* RG) {
   *MB = mb;
   *RG = rg;
 }
+static int g_g32_rows = -1;
+__host__ inline bool g32_rows_on() {
+  if (g_g32_rows < 0) {
+    const char* e = getenv("TI_GEMM_G32_ROWS");
+    g_g32_rows = e ? atoi(e) != 0 : 1;
+  }
+  return g_g32_rows != 0;
+}
 // Tile kernel from this many rows on (TI_GEMM_TILE_ROWS in [17, 65], default 65: the rows
 // kernel takes at most 64 rows).
 static int g_tile_rows = 0;
@@ -2045,14 +2093,14 @@ static int tile_rows() {
   }
   return g_tile_rows;
 }
-__host__ inline int rows_tiles_cap(int MB, int K) {
-  const int lim = MB >= 2 ? 3 : 4, cap = 512 / (K >> 7);   // VGPR budget: no spills
+__host__ inline int rows_tiles_cap(int MB, int K, bool g32 = false) {
+  const int lim = MB >= 2 ? 3 : 4, cap = 512 / ((K >> 7) * (g32 ? 4 : 1));   // VGPR budget / scale pieces
   return cap < 1 ? 1 : (cap > lim ? lim : cap);
 }
 // Column groups for row blocks of MB blocks per group (one round of workgroups where the VGPR
 // cap on tiles per workgroup allows).
-__host__ inline int rows_grid(int MB, int N, int K, int num_cus, int* ntl_out, int n_rb = 1) {
-  const int NT = N >> 4, cap = rows_tiles_cap(MB, K), per = num_cus / n_rb > 0 ? num_cus / n_rb : 1;
+__host__ inline int rows_grid(int MB, int N, int K, int num_cus, int* ntl_out, int n_rb = 1, bool g32 = false) {
+  const int NT = N >> 4, cap = rows_tiles_cap(MB, K, g32), per = num_cus / n_rb > 0 ? num_cus / n_rb : 1;
   int n_cg = NT < per ? NT : per;
   if ((NT + n_cg - 1) / n_cg > cap) n_cg = (NT + cap - 1) / cap;
   *ntl_out = (NT + n_cg - 1) / n_cg;
@@ -2063,14 +2111,15 @@ __host__ inline int rows_grid(int MB, int N, int K, int num_cus, int* ntl_out, i
 // weights (ntl 8 K bytes); narrow outputs (O, down) take 16-row blocks, wide ones all the rows.
 // TI_GEMM_ROWS_SPLIT=0 keeps all rows in one workgroup (A/B knob).
 static int g_rows_split = -1;
-__host__ inline void rows_plan(int M, int N, int K, int cus, int* MB, int* RG, int* n_rb, int* n_cg, int* ntl) {
+__host__ inline void rows_plan(int M, int N, int K, int cus, int* MB, int* RG, int* n_rb, int* n_cg, int* ntl,
+                               bool g32 = false) {
   if (g_rows_split < 0) {
     const char* e = getenv("TI_GEMM_ROWS_SPLIT");
     g_rows_split = e ? atoi(e) != 0 : 1;
   }
   rows_shape(M, MB, RG);   // all rows in one workgroup
   *n_rb = 1;
-  *n_cg = rows_grid(*MB, N, K, cus, ntl);
+  *n_cg = rows_grid(*MB, N, K, cus, ntl, 1, g32);
   if (!g_rows_split) return;
   const int NT = N >> 4;
   auto cost = [&](int mb, int rg, int nrb, int ncg, int nt) {
@@ -2084,7 +2133,7 @@ __host__ inline void rows_plan(int M, int N, int K, int cus, int* MB, int* RG, i
     if (rows >= M) continue;
     const int nrb = (M + rows - 1) / rows;
     int nt = 0;
-    const int ncg = rows_grid(mb, N, K, cus, &nt, nrb);
+    const int ncg = rows_grid(mb, N, K, cus, &nt, nrb, g32);
     const long c = cost(mb, rg, nrb, ncg, nt);
     if (c * 20 < best * 17 && nt <= NT) {   // a clear (15 %) win only: the model ignores round overlap
       best = c;
@@ -2096,24 +2145,26 @@ __host__ inline void rows_plan(int M, int N, int K, int cus, int* MB, int* RG, i
     }
   }
 }
-template <int MB, int RG, bool XP>
+template <int MB, int RG, bool XP, bool G32>
 static int launch_rows_t(const GemvArgs& a, int ntl, int n_cg, int n_rb, int lds, hipStream_t s) {
   const dim3 grid((unsigned)((n_cg + 7) / 8 * 8 * n_rb));
-  if (ntl == 1) hipLaunchKernelGGL((gemm_rows_kernel<MB, 1, RG, XP>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
-  else if (ntl == 2) hipLaunchKernelGGL((gemm_rows_kernel<MB, 2, RG, XP>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
-  else if (ntl == 3) hipLaunchKernelGGL((gemm_rows_kernel<MB, 3, RG, XP>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
-  else if constexpr (MB < 2) hipLaunchKernelGGL((gemm_rows_kernel<MB, 4, RG, XP>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
+  if (ntl == 1) hipLaunchKernelGGL((gemm_rows_kernel<MB, 1, RG, XP, G32>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
+  else if (ntl == 2) hipLaunchKernelGGL((gemm_rows_kernel<MB, 2, RG, XP, G32>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
+  else if (ntl == 3) hipLaunchKernelGGL((gemm_rows_kernel<MB, 3, RG, XP, G32>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
+  else if constexpr (MB < 2) hipLaunchKernelGGL((gemm_rows_kernel<MB, 4, RG, XP, G32>), grid, dim3(kGemvThreads), lds, s, a, n_cg, n_rb);
   else return ti_set_error(TI_ERR_ARG, "gemm_rows_kernel: %d tiles per workgroup at MB %d", ntl, MB);
   TI_LAUNCH_CHECK("gemm_rows_kernel");
   return TI_OK;
 }
-template <bool XP>
+template <bool XP, bool G32 = false>
 static int launch_rows_x(const GemvArgs& a, int MB, int RG, int ntl, int n_cg, int n_rb, int lds, hipStream_t s) {
   if (RG == 2)
-    return MB == 1 ? launch_rows_t<1, 2, XP>(a, ntl, n_cg, n_rb, lds, s) : launch_rows_t<2, 2, XP>(a, ntl, n_cg, n_rb, lds, s);
-  return MB == 1 ? launch_rows_t<1, 1, XP>(a, ntl, n_cg, n_rb, lds, s) : launch_rows_t<2, 1, XP>(a, ntl, n_cg, n_rb, lds, s);
+    return MB == 1 ? launch_rows_t<1, 2, XP, G32>(a, ntl, n_cg, n_rb, lds, s) : launch_rows_t<2, 2, XP, G32>(a, ntl, n_cg, n_rb, lds, s);
+  return MB == 1 ? launch_rows_t<1, 1, XP, G32>(a, ntl, n_cg, n_rb, lds, s) : launch_rows_t<2, 1, XP, G32>(a, ntl, n_cg, n_rb, lds, s);
 }
-static int launch_rows(const GemvArgs& a, int MB, int RG, int ntl, int n_cg, int n_rb, int lds, hipStream_t s) {
+static int launch_rows(const GemvArgs& a, int MB, int RG, int ntl, int n_cg, int n_rb, int lds, hipStream_t s,
+                       bool g32 = false) {
+  if (g32) return launch_rows_x<false, true>(a, MB, RG, ntl, n_cg, n_rb, lds, s);
   return a.x_kind == TI_X_F16_PACKED ? launch_rows_x<true>(a, MB, RG, ntl, n_cg, n_rb, lds, s)
                                      : launch_rows_x<false>(a, MB, RG, ntl, n_cg, n_rb, lds, s);
 }
@@ -2272,9 +2323,13 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   // group-32: int4 fp16 rows from tile_rows() on run on the tile kernel, everything else on the
   // fused kernel (more than 16 rows: in 16-row pieces, below); affine blocks on the fused kernel only
   const bool g32_tile = g32 && !aff && bits == 4 && x_kind == TI_X_F16 && M >= tile_rows() && !epi->out_packed;
+  // group-32 int4 fp16 rows 17..64: the batched-rows kernel (TI_GEMM_G32_ROWS=0: fused pieces, A/B knob)
+  const bool g32_rowsk = g32 && !aff && bits == 4 && x_kind == TI_X_F16 && M > 16 && M < tile_rows() &&
+                         !epi->out_packed && !chain && g32_rows_on();
   int g32_rows = 16;   // rows per fused launch (its LDS image holds the x rows)
   while (g32 && g32_rows > 1 && !fused_fits(g32_rows, N, K, true, aff)) --g32_rows;
-  if (g32 && (chain || x_kind == TI_X_F16_PACKED || (!g32_tile && !fused_fits(std::min(M, g32_rows), N, K, true, aff))))
+  if (g32 && (chain || x_kind == TI_X_F16_PACKED ||
+              (!g32_tile && !g32_rowsk && !fused_fits(std::min(M, g32_rows), N, K, true, aff))))
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: group-32 weights: fused kernel rows (M=%d N=%d K=%d) "
                         "or int4 fp16 rows >= %d; no chain, no packed rows", M, N, K, tile_rows());
   if (bits != 16 && !scales) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: scales required for bits %d", bits);
@@ -2319,7 +2374,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     default:
       return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: unknown epilogue %d", epi->kind);
   }
-  if (g32 && !g32_tile && M > g32_rows) {   // pieces of g32_rows rows through the fused kernel
+  if (g32 && !g32_tile && !g32_rowsk && M > g32_rows) {   // pieces of g32_rows rows through the fused kernel
     if (x_kind == TI_X_ATTN_SPLITS || x_kind == TI_X_F16_FOLDED || epi->out_packed)
       return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: group-32 rows > 16 need plain x rows");
     const size_t x_elem = x_kind == TI_X_F16 ? 2 : 4;
@@ -2341,7 +2396,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     return TI_OK;
   }
   const bool packed_x = x_kind == TI_X_F16_PACKED;
-  const bool batched = g32 ? g32_tile : (packed_x || use_batched(bits, x_kind, M, N, K));
+  const bool batched = g32 ? (g32_tile || g32_rowsk) : (packed_x || use_batched(bits, x_kind, M, N, K));
   if (epi->out_packed && (!batched || (epi->kind != TI_EPI_STORE_F16 && epi->kind != TI_EPI_SILU_MUL_F16) ||
                           (epi->ldo & 127)))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: out_packed needs the batched-rows kernel, a fp16 store / SiLU "
@@ -2355,7 +2410,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   int grid = 0, lds = 0, ntl = 0, rMB = 0, rRG = 0, r_rb = 1;
   const bool has_ws = epi->splitk_ws && epi->splitk_bytes > TI_SPLITK_TICKET_BYTES && splitk_on();
   const bool tile = batched && x_kind == TI_X_F16 && M >= tile_rows();
-  const bool rows = !tile && batched && (packed_x || M > 32 || (M > 16 && rows_on()));
+  const bool rows = !tile && batched && (g32_rowsk || packed_x || M > 32 || (M > 16 && rows_on()));
   int n_cb = 0, n_rb = 0, n_ks = 1, tpw = 2, wmr = 2, xbuf = 2;
   if (tile) {
     tile_plan(M, N, K, g32, query_cus(), has_ws ? epi->splitk_bytes : 0, &wmr, &tpw, &n_ks);   // (tile_plan)
@@ -2366,8 +2421,8 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     lds = tile_lds_bytes(K, tpw, g32, wmr, xbuf);
   } else if (rows) {
     rows_on();
-    rows_plan(M, N, K, query_cus(), &rMB, &rRG, &r_rb, &grid, &ntl);   // grid: column groups
-    lds = rows_lds_bytes(rRG * rMB, ntl, K);
+    rows_plan(M, N, K, query_cus(), &rMB, &rRG, &r_rb, &grid, &ntl, g32);   // grid: column groups
+    lds = rows_lds_bytes(rRG * rMB, ntl, K, g32);
   } else if (batched) {
     const int MB = M > 16 ? 2 : 1;
     grid = mb_grid(MB, N, K, query_cus(), &ntl);
@@ -2413,7 +2468,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     TI_LAUNCH_CHECK("gemm_tile_kernel");
     return TI_OK;
   }
-  if (rows) return launch_rows(a, rMB, rRG, ntl, grid, r_rb, lds, s);
+  if (rows) return launch_rows(a, rMB, rRG, ntl, grid, r_rb, lds, s, g32);
   if (batched) return launch_mb(a, M > 16 ? 2 : 1, grid, ntl, lds, s);
   if (aff) return launch_gemv<4, true, true>(a, lds, s, grid, chain);
   if (g32) return bits == 4 ? launch_gemv<4, true>(a, lds, s, grid, chain) : launch_gemv<8, true>(a, lds, s, grid, chain);
