@@ -57,7 +57,8 @@ class TensorEngine {
   Tensor attention(const Tensor& query, const Tensor& key, const Tensor& value, const Tensor* mask = nullptr);
   Tensor attention_fast_incremental(const Tensor& query, const Tensor& key, const Tensor& value,
                                     const Tensor* mask = nullptr);
-  /// query [B,1,H], key/value [B,S,H] with num_heads heads of H/num_heads interleaved in H.
+  /// query [B,Sq,H] (any Sq), key/value [B,S,H] with num_heads heads of H/num_heads interleaved
+  /// in H, optional float mask [B,Sq,S] (0 = masked, the reference's -1e9 fill).
   Tensor multi_head_attention(const Tensor& query, const Tensor& key, const Tensor& value, size_t num_heads,
                               const Tensor* mask = nullptr);
   Tensor layer_norm(const Tensor& input, const Tensor& weight, const Tensor& bias, float eps = 1e-5f);
