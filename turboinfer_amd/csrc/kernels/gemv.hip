@@ -1744,14 +1744,26 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
         const int kg = k0 + u;
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NX) : "memory");   // x(kg): this wave's DMA
         lds_barrier();
+#if TI_GEMV_EXP & 4096   // diagnostic: the weight stream replaced by re-reads of the first group (L2)
+        issue_x(kb + max(0, min(kg + XL, nk - 1)));
+        load_w(W[(u + 2) % kTileWR], kb);
+#elif TI_GEMV_EXP & 8192   // diagnostic: the activation stream replaced by re-reads of the first group
+        issue_x(kb);
+        load_w(W[(u + 2) % kTileWR], kb + max(0, min(kg + 2, nk - 1)));
+#else
         issue_x(kb + max(0, min(kg + XL, nk - 1)));
         load_w(W[(u + 2) % kTileWR], kb + max(0, min(kg + 2, nk - 1)));
+#endif
         // (also in the groups without compute: a slot's load is always consumed by its tie, so
         // hipcc never hands its registers to anything else while the load is in flight)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NWT) : "memory");   // W(kg)
 #pragma unroll
         for (int t = 0; t < TPW; ++t) asm volatile("" : "+v"(W[u][t]));
+#if TI_GEMV_EXP & 2048   // diagnostic (tools/tile_diag.sh): operand streams only, no dequant / MFMA
+        if (kg >= 0 && kg < nk && lane == 64) compute(W[u], kb + kg);
+#else
         if (kg >= 0 && kg < nk) compute(W[u], kb + kg);
+#endif
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped loads past the end
@@ -2168,13 +2180,13 @@ static int launch_rows(const GemvArgs& a, int MB, int RG, int ntl, int n_cg, int
   return a.x_kind == TI_X_F16_PACKED ? launch_rows_x<true>(a, MB, RG, ntl, n_cg, n_rb, lds, s)
                                      : launch_rows_x<false>(a, MB, RG, ntl, n_cg, n_rb, lds, s);
 }
-#define TI_ROWS_FNS1(MB, RG, XP)                                                                          \
-  (const void*)gemm_rows_kernel<MB, 1, RG, XP>, (const void*)gemm_rows_kernel<MB, 2, RG, XP>,                \
-      (const void*)gemm_rows_kernel<MB, 3, RG, XP>
-#define TI_ROWS_FNS2(XP)                                                                                 \
-  TI_ROWS_FNS1(1, 1, XP), TI_ROWS_FNS1(2, 1, XP), TI_ROWS_FNS1(1, 2, XP), TI_ROWS_FNS1(2, 2, XP),         \
-      (const void*)gemm_rows_kernel<1, 4, 1, XP>, (const void*)gemm_rows_kernel<1, 4, 2, XP>
-#define TI_ROWS_FNS TI_ROWS_FNS2(false), TI_ROWS_FNS2(true)
+#define TI_ROWS_FNS1(MB, RG, XP, G)                                                                       \
+  (const void*)gemm_rows_kernel<MB, 1, RG, XP, G>, (const void*)gemm_rows_kernel<MB, 2, RG, XP, G>,          \
+      (const void*)gemm_rows_kernel<MB, 3, RG, XP, G>
+#define TI_ROWS_FNS2(XP, G)                                                                              \
+  TI_ROWS_FNS1(1, 1, XP, G), TI_ROWS_FNS1(2, 1, XP, G), TI_ROWS_FNS1(1, 2, XP, G), TI_ROWS_FNS1(2, 2, XP, G), \
+      (const void*)gemm_rows_kernel<1, 4, 1, XP, G>, (const void*)gemm_rows_kernel<1, 4, 2, XP, G>
+#define TI_ROWS_FNS TI_ROWS_FNS2(false, false), TI_ROWS_FNS2(true, false), TI_ROWS_FNS2(false, true)
 
 #define TI_MB_FNS1(K)                                                                                \
   (const void*)K<1, 1>, (const void*)K<1, 2>, (const void*)K<1, 3>, (const void*)K<1, 4>, (const void*)K<1, 5>, \
