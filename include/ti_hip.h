@@ -262,6 +262,9 @@ int ti_gemm_max_rows(int bits, int x_kind, int N, int K);
  * operands are best given as TI_X_F16_PACKED.  From 65 rows (TI_GEMM_TILE_ROWS, env, <= 65) on
  * the LDS-tiled kernel takes TI_X_F16 rows. */
 int ti_gemm_packed_rows(int bits, int M);
+/* The same for one M x N x K call: 0 also where 17..64 int4 rows of a wide output take the tile
+ * GEMM (rows x N >= TI_GEMM_TILE_WIDE_MN, env, default 850000), which needs TI_X_F16 rows. */
+int ti_gemm_packed_rows_for(int bits, int M, int N, int K);
 /* The tile GEMM's plan for an int4 (bits 4 or 4 | TI_BITS_G32) M x N x K call with a split-K
  * workspace of ws_bytes (0 = none): row-waves, weight tiles per wave and k-slices (1 = no split;
  * K is split only where one slice per column block would leave most CUs idle, TI_GEMM_SPLITK=0

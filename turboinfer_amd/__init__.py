@@ -73,7 +73,7 @@ EXPORTED = [
     "ti_device_sync", "ti_event_create", "ti_event_destroy", "ti_event_record", "ti_event_elapsed_ms",
     "ti_wpack_tile_bytes", "ti_wpack_scale_bytes", "ti_wpack_host", "ti_wsynth_device", "ti_fill_uniform_f16",
     "ti_fill_uniform_f32", "ti_fill_kv_uniform", "ti_kv_copy_slots", "ti_gemm_wq_a16", "ti_gemm_lds_bytes", "ti_gemm_prepare",
-    "ti_gemm_max_rows", "ti_gemm_packed_rows", "ti_gemm_tile_plan", "ti_rmsnorm_f16", "ti_rmsnorm_f16_packed", "ti_attn_decode_packed", "ti_attn_prefill",
+    "ti_gemm_max_rows", "ti_gemm_packed_rows", "ti_gemm_packed_rows_for", "ti_gemm_tile_plan", "ti_rmsnorm_f16", "ti_rmsnorm_f16_packed", "ti_attn_decode_packed", "ti_attn_prefill",
     "ti_attn_workspace_bytes", "ti_attn_decode", "ti_step_begin", "ti_matmul_f32", "ti_rms_norm_f32",
     "ti_rope_f32", "ti_silu_f32", "ti_relu_f32", "ti_add_f32", "ti_mul_f32", "ti_softmax_f32", "ti_attention_f32",
     "ti_argmax_f32", "ti_engine_create", "ti_engine_destroy", "ti_engine_get_stream", "ti_engine_memory", "ti_engine_set_tensor",
@@ -128,6 +128,7 @@ def lib() -> C.CDLL:
         L.ti_gemm_lds_bytes.argtypes = [i32, i32, i32]
         L.ti_gemm_max_rows.argtypes = [i32, i32, i32, i32]
         L.ti_gemm_packed_rows.argtypes = [i32, i32]
+        L.ti_gemm_packed_rows_for.argtypes = [i32, i32, i32, i32]
         L.ti_gemm_tile_plan.argtypes = [i32, i32, i32, i32, C.c_int64, vp, vp, vp]
         L.ti_rmsnorm_f16.argtypes = [vp, i32, vp, f32, vp, i32, i32, i32, vp]
         L.ti_rmsnorm_f16_packed.argtypes = [vp, i32, vp, f32, vp, i32, i32, vp]

@@ -269,7 +269,7 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
               const ti_epilogue& epi, size_t out_elem, bool last_gets_ctr) {
   const ti_engine_config& c = e->c;
   int rows = ti_gemm_max_rows(c.bits, x_kind, W.N, W.K);
-  if (x_kind == TI_X_F32_RMSNORM && packed_rows(e, M) && e->xn) {
+  if (x_kind == TI_X_F32_RMSNORM && ti_gemm_packed_rows_for(c.bits, M, W.N, W.K) && e->xn) {
     TI_TRY(ti_rmsnorm_f16_packed(static_cast<const float*>(x), ldx, nw, c.eps, e->xn, M, W.K, e->s));
     x = e->xn;
     x_kind = TI_X_F16_PACKED;

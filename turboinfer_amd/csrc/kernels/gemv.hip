@@ -1929,9 +1929,9 @@ __host__ inline void tile_plan(int M, int N, int K, bool g32, int cus, int64_t w
   if (!splitk_on() || ws_bytes <= TI_SPLITK_TICKET_BYTES) return;
   const int NT = N >> 4, KT = K >> 7, cols = (8 / wmr) * tpw;
   const int n_cb = (NT + cols - 1) / cols, n_rb = (M + 64 * wmr - 1) / (64 * wmr);
-  const long wgs = (long)n_cb * n_rb;
+  const long wgs = (long)n_cb * n_rb, grid1 = (long)(n_cb + 7) / 8 * 8 * n_rb;   // (launched: whole XCD rows)
   if (wgs * 4 > cus || (size_t)wgs * kGemvWaves * 4 > TI_SPLITK_TICKET_BYTES) return;
-  int S = (int)(cus / wgs);
+  int S = (int)(cus / grid1);
   while (S > 1 && ((KT + S - 1) / S < 8 || splitk_slab_bytes(S, n_cb, n_rb, tpw) + TI_SPLITK_TICKET_BYTES > (size_t)ws_bytes))
     --S;
   *ks_o = S;
@@ -2111,8 +2111,12 @@ __host__ inline int rows_tiles_cap(int MB, int K, bool g32 = false) {
 }
 // Column groups for row blocks of MB blocks per group (one round of workgroups where the VGPR
 // cap on tiles per workgroup allows).
+// The launch is ceil(n_cg / 8) * 8 * n_rb workgroups spread round-robin over the 8 XCDs, so with
+// row blocks the column groups per block are a multiple of 8 (3 row blocks x 85 groups = 264
+// workgroups put 33 on an XCD of 32 CUs: a second round, 1.7x the time, tools/rows_m_sweep.py).
 __host__ inline int rows_grid(int MB, int N, int K, int num_cus, int* ntl_out, int n_rb = 1, bool g32 = false) {
-  const int NT = N >> 4, cap = rows_tiles_cap(MB, K, g32), per = num_cus / n_rb > 0 ? num_cus / n_rb : 1;
+  const int NT = N >> 4, cap = rows_tiles_cap(MB, K, g32);
+  const int per = n_rb > 1 ? (num_cus / n_rb / 8 * 8 > 0 ? num_cus / n_rb / 8 * 8 : 8) : num_cus;
   int n_cg = NT < per ? NT : per;
   if ((NT + n_cg - 1) / n_cg > cap) n_cg = (NT + cap - 1) / cap;
   *ntl_out = (NT + n_cg - 1) / n_cg;
@@ -2135,7 +2139,7 @@ __host__ inline void rows_plan(int M, int N, int K, int cus, int* MB, int* RG, i
   if (!g_rows_split) return;
   const int NT = N >> 4;
   auto cost = [&](int mb, int rg, int nrb, int ncg, int nt) {
-    const long rounds = ((long)ncg * nrb + cus - 1) / cus;
+    const long rounds = ((long)(ncg + 7) / 8 * 8 * nrb + cus - 1) / cus;
     return rounds * ((long)16 * rg * mb * K * 2 + (long)nt * 8 * K);
   };
   long best = cost(*MB, *RG, 1, *n_cg, *ntl);
@@ -2270,7 +2274,24 @@ static bool use_batched(int bits, int x_kind, int M, int N, int K) {
   return !fused_fits(M, N, K) || (mb_ok && M > fused_rows_pref(bits));
 }
 
+// 17..64 int4 rows of a WIDE output take the tile GEMM, whose time is nearly flat there (≈ 27–31 µs
+// at 64 rows for N = 22016 .. 32000, K = 4096), instead of the batched-rows kernel, which moves
+// every row's activations per workgroup: rows x N >= TI_GEMM_TILE_WIDE_MN (env, default 850000;
+// 0 = off) -- the measured crossover (tools/rows_ab.sh: 64 x 12288 rows kernel 19.0 vs tile 26.5 us,
+// 32 x 28672 rows 36.5 vs tile 28.4, 64 x 22016 35.5 vs 28.3, 32 x 22016 25.7 vs 27.2).
+static long g_tile_wide_mn = -1;
+static bool wide_tile(int bits, int M, int N) {
+  if (g_tile_wide_mn < 0) {
+    const char* e = getenv("TI_GEMM_TILE_WIDE_MN");
+    g_tile_wide_mn = e ? atol(e) : 850000;
+  }
+  return bits == 4 && g_tile_wide_mn > 0 && M > 16 && M < ti::tile_rows() && (long)M * N >= g_tile_wide_mn;
+}
 extern "C" int ti_gemm_packed_rows(int bits, int M) { return bits == 4 && M > 16 && M < ti::tile_rows() ? 1 : 0; }
+extern "C" int ti_gemm_packed_rows_for(int bits, int M, int N, int K) {
+  (void)K;
+  return ti_gemm_packed_rows(bits, M) && !wide_tile(bits, M, N) ? 1 : 0;
+}
 
 extern "C" int ti_gemm_tile_plan(int bits, int M, int N, int K, int64_t ws_bytes, int* wmr, int* tpw, int* n_ks) {
   const bool g32 = (bits & TI_BITS_G32) != 0;
@@ -2421,7 +2442,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
                         "kernel needs bits 4 and fp16 rows (normalise with ti_rmsnorm_f16)", M, K);
   int grid = 0, lds = 0, ntl = 0, rMB = 0, rRG = 0, r_rb = 1;
   const bool has_ws = epi->splitk_ws && epi->splitk_bytes > TI_SPLITK_TICKET_BYTES && splitk_on();
-  const bool tile = batched && x_kind == TI_X_F16 && M >= tile_rows();
+  const bool tile = batched && x_kind == TI_X_F16 && (M >= tile_rows() || (!g32 && wide_tile(bits, M, N)));
   const bool rows = !tile && batched && (g32_rowsk || packed_x || M > 32 || (M > 16 && rows_on()));
   int n_cb = 0, n_rb = 0, n_ks = 1, tpw = 2, wmr = 2, xbuf = 2;
   if (tile) {
