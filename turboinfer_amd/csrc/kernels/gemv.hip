@@ -1890,8 +1890,9 @@ __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
           tile_lds_bytes(K, tpw, g32, wmr) > 160 * 1024)
         continue;
       const int cols = (8 / wmr) * tpw;
-      const long wgs = (long)(NT + cols - 1) / cols * ((M + 64 * wmr - 1) / (64 * wmr));
-      const long cost = (wgs + cus - 1) / cus * (16 * wmr + 8 * tpw);
+      // rounds as launched: ceil(column blocks / 8) x row blocks workgroups on each XCD's CUs
+      const long per_xcd = (long)((NT + cols - 1) / cols + 7) / 8 * ((M + 64 * wmr - 1) / (64 * wmr));
+      const long cost = (per_xcd + cus / 8 - 1) / (cus / 8) * (16 * wmr + 8 * tpw);
       if (best_cost < 0 || cost < best_cost) {
         best = 8 * wmr + tpw;
         best_cost = cost;
