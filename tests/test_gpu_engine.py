@@ -216,6 +216,14 @@ def test_engine_7b_64_streams(ti, oracle):
     _full_shape_streams(ti, oracle, CFG_7B, 2025, 64, [1, 17, 35, 49, 63], 4)
 
 
+def test_engine_7b_40_streams(ti, oracle):
+    """40 streams of the 7B shape: the batched-rows kernel in three 16-row blocks for the narrow
+    projections (O, down; whole XCD rows of column groups), the tile kernel for the wide ones
+    (gate/up, lm_head: rows x N >= TI_GEMM_TILE_WIDE_MN); a stream in each row block against the
+    oracle (the 64-stream test's streams, same caches and first tokens)."""
+    _full_shape_streams(ti, oracle, CFG_7B, 2025, 40, [1, 17, 35], 4)
+
+
 def test_engine_compat_plumbing_matches_reference_generate(ti, oracle, golden):
     """BASELINE config 1: the reference's own generate() on its benchmark model, exact tokens
     (fp32 bit-exact path + the reference sampler's tie order)."""
