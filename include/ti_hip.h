@@ -243,6 +243,8 @@ typedef struct ti_epilogue {
   int64_t splitk_bytes;
 } ti_epilogue;
 #define TI_SPLITK_TICKET_BYTES (256 * 1024)
+/* sizeof(ti_epilogue): a binding checks its mirror of the struct against it. */
+int ti_epilogue_bytes(void);
 
 int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind,
                    int ldx, const float* norm_w, float eps, int M, int N, int K,

@@ -47,6 +47,11 @@ def test_exports_every_declared_symbol(L):
     assert sorted(declared) == sorted(T.EXPORTED)
 
 
+def test_epilogue_mirror_matches_abi(L):
+    # the ctypes mirror of ti_epilogue must have the library's size (trailing fields included)
+    assert L.ti_epilogue_bytes() == C.sizeof(T.Epilogue)
+
+
 def test_argument_errors_are_reported_without_launch(L):
     ep = T.Epilogue()
     ep.kind = T.EPI_STORE_F32

@@ -29,7 +29,7 @@ EPI_STORE_F32, EPI_STORE_F16, EPI_RESID_F32, EPI_SILU_MUL_F16, EPI_QKV_ROPE_KV, 
 ARGMAX_SLOTS = 32
 GEMM_MAX_ROWS = 1024                # TI_GEMM_MAX_ROWS (include/ti_hip.h)
 BITS_G32 = 32                       # TI_BITS_G32 (include/ti_hip.h): group-32 weights (GGUF Q4_0 / Q8_0)
-BITS_AFF = 64                       # TI_BITS_AFF: affine group-32 int4 (GGUF Q4_1), with BITS_G32 | 4   # TI_ARGMAX_SLOTS (include/ti_hip.h)
+BITS_AFF = 64                       # TI_BITS_AFF: affine group-32 int4 (GGUF Q4_1), with BITS_G32 | 4
 SCALE_GROUP, SCALE_TENSOR, SCALE_UNIT = 0, 1, 2
 ROWS_CONCAT, ROWS_INTERLEAVE8 = 0, 1
 (W_Q, W_K, W_V, W_O, W_GATE, W_UP, W_DOWN, W_LM_HEAD, V_ATTN_NORM, V_FFN_NORM, V_OUT_NORM, E_EMBED) = range(12)
@@ -85,7 +85,7 @@ EXPORTED = [
     "ti_engine_beam_search", "ti_engine_serve", "ti_qkv_attn_fused", "ti_engine_set_qkv_attn",
     "ti_pds_decode", "ti_engine_set_pds", "ti_engine_pds_error", "ti_engine_pds_timestamps",
     "ti_wpack_q_host", "ti_engine_set_tensor_q", "ti_sample_workspace_bytes", "ti_sample_device_ws",
-    "ti_wpack_q1_host", "ti_engine_set_tensor_q1",
+    "ti_wpack_q1_host", "ti_engine_set_tensor_q1", "ti_epilogue_bytes",
     "ti_sample_step_ws", "ti_pds_granule_words",
 ]
 

@@ -2511,6 +2511,8 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   return launch_gemv<16>(a, lds, s, grid, chain);
 }
 
+extern "C" int ti_epilogue_bytes(void) { return (int)sizeof(ti_epilogue); }
+
 extern "C" int ti_gemm_grid(int M, int N, int K) {
   if (M < 1 || M > 16 || N < 16 || K < 128 || (N & 15) || (K & 127) || !fused_fits(M, N, K)) return 0;
   return ti::gemv_grid(M, N, K, query_cus());
