@@ -1,6 +1,7 @@
 #!/bin/bash
 # Fused-GEMV ring depth (TI_GEMV_RING_VGPRS 20 = product, exp/r24, exp/r32 builds) and two
 # workgroups per CU (TI_GEMV_WG_PER_CU=2) on the one-stream 7B and TinyLlama benches.
+# Variant builds: make BUILD=/tmp/build_rNN LIB=exp/rNN/libturboinfer_amd.so EXTRA=-DTI_GEMV_RING_VGPRS=NN
 set -e
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
