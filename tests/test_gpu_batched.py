@@ -93,6 +93,25 @@ def test_splitk_plans_split_narrow_outputs(ti):
     assert ti.lib().ti_gemm_packed_rows(4, 64) == 1
 
 
+@pytest.mark.parametrize("M,K,N", [(512, 1024, 12288), (256, 1152, 22016), (1000, 1024, 12288)])
+def test_tile_three_tiles_per_wave(ti, oracle, M, K, N):
+    """Shapes the planner gives 192-column workgroups (3 weight tiles per wave: the 7B QKV's 768
+    tiles at 64 rows as exactly 256 workgroups; gate/up at 256 rows), ragged rows included."""
+    plan = tile_plan(ti, M, N, K)
+    assert plan is not None and plan[1] == 3, plan
+    rng = np.random.RandomState(M + N)
+    w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
+    x = rng.standard_normal((M, K)).astype(f16)
+    tiles, scales = ti.wpack_host(w, 4)
+    yd = ti.DeviceBuffer(M * N * 4)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F32, N, yd.ptr
+    run(ti, dev(ti, tiles), dev(ti, scales), dev(ti, x), M, N, K, ep)
+    wf = deq(oracle, w, 4)
+    xa = x.astype(f32)
+    assert_close_dot(yd.download(f32, (M, N)), xa.astype(np.float64) @ wf.astype(np.float64), xa, wf)
+
+
 def test_splitk_repeat_is_deterministic(ti, oracle, splitk_ws):
     """The last arriver sums the k-slices in slice order: repeated calls give identical bits."""
     M, K, N = 128, 11008, 4096

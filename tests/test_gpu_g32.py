@@ -93,7 +93,8 @@ def test_gemm_g32_rmsnorm_prologue(ti, oracle, bits, M):
                                         (4, 200, 4096, 256), (4, 512, 1024, 4096 + 64), (8, 40, 4096, 256),
                                         # batched-rows kernel, row blocks split over workgroups (narrow N)
                                         (4, 33, 11008, 4096 + 16), (4, 48, 1152, 4000), (4, 64, 4096, 4096),
-                                        (4, 64, 4096, 12288)])   # (rows kernel LDS image above 64 KiB)
+                                        (4, 64, 4096, 12288),    # (rows kernel LDS image above 64 KiB)
+                                        (4, 512, 1024, 12288)])  # tile GEMM, 3 weight tiles per wave
 def test_gemm_g32_many_rows(ti, bits, M, K, N):
     """More rows than the fused kernel holds: int4 fp16 rows 17-64 run on the batched-rows
     kernel and from 65 on on the tile GEMM (group-32 k order and per-block scales in both),

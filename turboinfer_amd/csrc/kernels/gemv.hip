@@ -1495,7 +1495,8 @@ __host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, 
 
 // TPW: weight tiles per wave (2: 128 columns per workgroup; 1: 64 columns, twice the workgroups
 // for the narrow N = 4096 projections, which otherwise fill only 64 of 256 CUs at 256 rows;
-// 4: 256 columns, half the activation bytes per MFMA, when the rows give enough workgroups).
+// 4: 256 columns, half the activation bytes per MFMA, when the rows give enough workgroups;
+// 3: 192 columns, e.g. the 7B QKV's 768 tiles at 64 rows as exactly 256 workgroups).
 // G32: group-32 int4 tiles (TI_BITS_G32): MFMA step s4 of a group reads k-chunk 4 s4 + kq and
 // carries its own scale (one per 32-k block), so each step's product is scaled separately.
 #ifndef TI_TILE_ASM
@@ -1851,11 +1852,15 @@ __host__ inline bool tile_narrow_on() {
       (const void*)gemm_tile_kernel<2, true, 2, XB>, (const void*)gemm_tile_kernel<4, true, 2, XB>,            \
       (const void*)gemm_tile_kernel<1, false, 1, XB>, (const void*)gemm_tile_kernel<2, false, 1, XB>,          \
       (const void*)gemm_tile_kernel<4, false, 1, XB>, (const void*)gemm_tile_kernel<1, true, 1, XB>,           \
-      (const void*)gemm_tile_kernel<2, true, 1, XB>, (const void*)gemm_tile_kernel<4, true, 1, XB>
+      (const void*)gemm_tile_kernel<2, true, 1, XB>, (const void*)gemm_tile_kernel<4, true, 1, XB>,             \
+      (const void*)gemm_tile_kernel<3, false, 2, XB>, (const void*)gemm_tile_kernel<3, true, 2, XB>,           \
+      (const void*)gemm_tile_kernel<3, false, 1, XB>, (const void*)gemm_tile_kernel<3, true, 1, XB>
 #define TI_TILE_FNS TI_TILE_FNS_XB(2), TI_TILE_FNS_XB(TI_TILE_XB4)
 __host__ inline const void* tile_fn(int tpw, bool g32, int wmr, int xb) {
   static const void* const fns[] = {TI_TILE_FNS};
-  return fns[(xb == 4 ? 12 : 0) + (wmr == 1 ? 6 : 0) + (g32 ? 3 : 0) + (tpw == 1 ? 0 : tpw == 2 ? 1 : 2)];
+  const int base = xb == 4 ? 16 : 0;
+  if (tpw == 3) return fns[base + 12 + (wmr == 1 ? 2 : 0) + (g32 ? 1 : 0)];
+  return fns[base + (wmr == 1 ? 6 : 0) + (g32 ? 3 : 0) + (tpw == 1 ? 0 : tpw == 2 ? 1 : 2)];
 }
 // the deep activation ring when it fits the LDS (TI_TILE_XB=2 forces the double buffer: A/B knob)
 __host__ inline int tile_xb(int K, int tpw, bool g32, int wmr) {
@@ -1872,21 +1877,23 @@ __host__ inline int tile_xb(int K, int tpw, bool g32, int wmr) {
 // activations and WMR x (8 / WMR) TPW KiB of weights per group.  TI_TILE_WMR1=0 keeps 128-row
 // workgroups (A/B knob).  Returns 8 * WMR + TPW.
 __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
-  static int wide = -1, wmr1 = -1;
+  static int wide = -1, wmr1 = -1, tpw3 = -1;
   if (wide < 0) {
     const char* e = getenv("TI_TILE_WIDE");
     wide = e ? atoi(e) != 0 : 1;
     const char* f = getenv("TI_TILE_WMR1");
     wmr1 = f ? atoi(f) != 0 : 1;
+    const char* g = getenv("TI_TILE_TPW3");
+    tpw3 = g ? atoi(g) != 0 : 1;
   }
   const int NT = N >> 4;
   int best = 8 * 2 + 2;
   long best_cost = -1;
   for (int wmr : {2, 1}) {
     if (wmr == 1 && !wmr1) continue;
-    for (int tpw : {2, 1, 4}) {
+    for (int tpw : {2, 1, 4, 3}) {
       // (group-32 at TPW 4 spills to scratch: kept out, its asm-loaded weight ring must stay in VGPRs)
-      if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && (!wide || (g32 && TI_TILE_ASM))) ||
+      if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && (!wide || (g32 && TI_TILE_ASM))) || (tpw == 3 && !tpw3) ||
           tile_lds_bytes(K, tpw, g32, wmr) > 160 * 1024)
         continue;
       const int cols = (8 / wmr) * tpw;
