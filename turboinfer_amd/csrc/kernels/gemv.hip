@@ -1532,6 +1532,28 @@ __device__ __forceinline__ u32x4 ld_w_asm(const u32x4* p) {
   return v;
 }
 
+#if TI_GEMV_EXP & 16384   // diagnostic (tools/probe_tile.hip): per-wave cycles by loop phase
+__device__ unsigned long long g_tile_cy[4096 * 8 * 8];   // [workgroup][wave][phase]
+#define TILE_CY_DECL()                                \
+  unsigned long long cy_acc[6] = {0, 0, 0, 0, 0, 0}; \
+  unsigned long long cy_t = __builtin_readcyclecounter()
+#define TILE_CY(i)                                           \
+  do {                                                       \
+    const unsigned long long t_ = __builtin_readcyclecounter(); \
+    cy_acc[i] += t_ - cy_t;                                  \
+    cy_t = t_;                                               \
+  } while (0)
+#define TILE_CY_STORE()                                                                          \
+  do {                                                                                           \
+    if (lane == 0)                                                                               \
+      for (int i_ = 0; i_ < 6; ++i_) g_tile_cy[((size_t)blockIdx.x * 8 + wave) * 8 + i_] = cy_acc[i_]; \
+  } while (0)
+#else
+#define TILE_CY_DECL() do { } while (0)
+#define TILE_CY(i) do { } while (0)
+#define TILE_CY_STORE() do { } while (0)
+#endif
+
 // Split-K merge of one wave's block (n_ks > 1): every k-slice's wave stores its fp32 partial
 // block write-through into the workspace and adds to the block's ticket after its stores have
 // drained; the last arriver reads the other slices back (sc1 loads, CH slices per round trip),
@@ -1728,6 +1750,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   // Per group kg: x(kg) and W(kg) were issued earlier; issue x(kg + 1) and W(kg + WR - 1),
   // wait until only those weight loads are younger than x(kg + 1)... (see below), compute kg.
   const int KTP = (nk + kTileWR - 1) / kTileWR * kTileWR;
+  TILE_CY_DECL();
   if constexpr (TI_TILE_ASM) {
     // Every group issues, in order, x(kg + XL) (2 WMR DMA instructions into buffer
     // (kg + XL) % XB, read last in group kg - 1) and W(kg + 2) (TPW loads into ring slot
@@ -1744,7 +1767,9 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
       for (int u = 0; u < kTileWR; ++u) {
         const int kg = k0 + u;
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NX) : "memory");   // x(kg): this wave's DMA
+        TILE_CY(0);
         lds_barrier();
+        TILE_CY(1);
 #if TI_GEMV_EXP & 4096   // diagnostic: the weight stream replaced by re-reads of the first group (L2)
         issue_x(kb + max(0, min(kg + XL, nk - 1)));
         load_w(W[(u + 2) % kTileWR], kb);
@@ -1757,14 +1782,17 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #endif
         // (also in the groups without compute: a slot's load is always consumed by its tie, so
         // hipcc never hands its registers to anything else while the load is in flight)
+        TILE_CY(2);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NWT) : "memory");   // W(kg)
 #pragma unroll
         for (int t = 0; t < TPW; ++t) asm volatile("" : "+v"(W[u][t]));
+        TILE_CY(3);
 #if TI_GEMV_EXP & 2048   // diagnostic (tools/tile_diag.sh): operand streams only, no dequant / MFMA
         if (kg >= 0 && kg < nk && lane == 64) compute(W[u], kb + kg);
 #else
         if (kg >= 0 && kg < nk) compute(W[u], kb + kg);
 #endif
+        TILE_CY(4);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped loads past the end
@@ -1824,6 +1852,12 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   }
   if (a.epi.kind == TI_EPI_LOGITS_ARGMAX && a.epi.step_ctr && blockIdx.x == 0 && tid == 0)
     *a.epi.step_ctr += a.epi.advance;
+#if TI_GEMV_EXP & 16384
+  if constexpr (TI_TILE_ASM) {
+    TILE_CY(5);
+    TILE_CY_STORE();
+  }
+#endif
 }
 
 static int g_num_cus = 0;
