@@ -1490,7 +1490,8 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
 // the activation block and no weight tile loaded twice)
 // XB: activation-block buffers (2: double buffer; 4: issued three groups ahead, when the LDS holds them)
 __host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, int wmr = 2, int xb = 2) {
-  return xb * 64 * wmr * 256 + align16((8 / wmr) * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
+  const int n = xb * 64 * wmr * 256 + align16((8 / wmr) * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
+  return n > 8 * 64 * 20 * 4 ? n : 8 * 64 * 20 * 4;   // >= the epilogue's staging blocks (tile_epi_lds_bytes)
 }
 
 // TPW: weight tiles per wave (2: 128 columns per workgroup; 1: 64 columns, twice the workgroups
@@ -1612,6 +1613,71 @@ __device__ __forceinline__ bool splitk_merge(const GemvArgs& a, f32x4 (&acc)[TPW
     for (int b = 0; b < 4; ++b) acc[t][b] = sum[t][b];
   if (lane == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
   return true;
+}
+
+#ifndef TI_TILE_EPI_LDS
+#define TI_TILE_EPI_LDS 1   // 0: every epilogue per element from the MFMA layout (A/B knob)
+#endif
+constexpr int kTileEpiStride = 20;   // floats per row of a wave's 64 x 16 staging block (padded: no bank conflicts)
+__host__ __device__ constexpr int tile_epi_lds_bytes() { return kGemvWaves * 64 * kTileEpiStride * 4; }
+
+// Epilogue of weight tile tn (16 outputs) for rows mb .. mb + 63 of one wave, from its LDS block
+// stg[row][col] (row stride kTileEpiStride).  Same arithmetic as epilogue_mb, element for element.
+//   STORE_F32 / RESID_F32 / QKV_ROPE_KV: lane l owns columns 4 (l & 3) .. + 3 of rows 16 it + l / 4
+//   SILU_MUL_F16: lane l owns outputs 4 (l & 1) .. + 3 (gate columns, up = column + 8) of rows 32 it + l / 2
+__device__ __forceinline__ void tile_epilogue_lds(const GemvArgs& a, int tn, int mb, const float* stg, int lane) {
+  const ti_epilogue& e = a.epi;
+  if (e.kind == TI_EPI_SILU_MUL_F16) {
+    const int h = 4 * (lane & 1);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int row = 32 * it + (lane >> 1), m = mb + row;
+      const float4 g = *(const float4*)(stg + row * kTileEpiStride + h);
+      const float4 u = *(const float4*)(stg + row * kTileEpiStride + 8 + h);
+      if (m >= a.M) continue;
+      auto sm = [](float v, float up) { return f2h(up * (v / (1.0f + expf(-v)))); };
+      const uint32_t lo = sm(g.x, u.x) | ((uint32_t)sm(g.y, u.y) << 16), hi = sm(g.z, u.z) | ((uint32_t)sm(g.w, u.w) << 16);
+      *(uint2*)((uint16_t*)e.out + (size_t)m * e.ldo + tn * 8 + h) = make_uint2(lo, hi);
+    }
+    return;
+  }
+  const int c4 = 4 * (lane & 3), ng = tn * 16 + c4;
+  // QKV: the tile lies in one of q / k / v and one head (head_dim % 16 == 0)
+  const int hd = e.head_dim;
+  const bool in_q = ng < e.q_dim, in_k = !in_q && ng < e.q_dim + e.kv_dim;
+  const int c = in_q ? ng : in_k ? ng - e.q_dim : ng - e.q_dim - e.kv_dim;
+  const int kvh = e.kind == TI_EPI_QKV_ROPE_KV ? c / hd : 0, d = c - kvh * hd;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int row = 16 * it + (lane >> 2), m = mb + row;
+    const float4 v = *(const float4*)(stg + row * kTileEpiStride + c4);
+    if (m >= a.M) continue;
+    if (e.kind == TI_EPI_STORE_F32) {
+      *(float4*)((float*)e.out + (size_t)m * e.ldo + ng) = v;
+    } else if (e.kind == TI_EPI_RESID_F32) {
+      float4* o = (float4*)((float*)e.out + (size_t)m * e.ldo + ng);
+      const float4 h = *o;
+      *o = make_float4(h.x + v.x, h.y + v.y, h.z + v.z, h.w + v.w);
+    } else {   // TI_EPI_QKV_ROPE_KV
+      const int p = e.pos[m];
+      if (in_q || in_k) {
+        // (cos, sin) of pairs d / 2 and d / 2 + 1: even output fmaf(-odd, sin, even * cos), odd
+        // output fmaf(odd, cos, even * sin) (epilogue_mb with partner = the other of the pair)
+        const float4 cs = *(const float4*)(e.rope_cs + (size_t)p * hd + d);
+        const float r0 = fmaf(-v.y, cs.y, v.x * cs.x), r1 = fmaf(v.y, cs.x, v.x * cs.y);
+        const float r2 = fmaf(-v.w, cs.w, v.z * cs.z), r3 = fmaf(v.w, cs.z, v.z * cs.w);
+        if (in_q) {
+          *(float4*)((float*)e.out + (size_t)m * e.ldo + ng) = make_float4(r0, r1, r2, r3);
+        } else {
+          *(uint2*)(e.k_cache + (size_t)m * e.kv_stream_stride + ((size_t)kvh * e.max_seq + p) * hd + d) =
+              make_uint2(f2h(r0) | ((uint32_t)f2h(r1) << 16), f2h(r2) | ((uint32_t)f2h(r3) << 16));
+        }
+      } else {
+        *(uint2*)(e.v_cache + (size_t)m * e.kv_stream_stride + ((size_t)kvh * e.max_seq + p) * hd + d) =
+            make_uint2(f2h(v.x) | ((uint32_t)f2h(v.y) << 16), f2h(v.z) | ((uint32_t)f2h(v.w) << 16));
+      }
+    }
+  }
 }
 
 template <int TPW, bool G32 = false, int WMR = 2, int XB = 2>
@@ -1824,15 +1890,24 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // every wave is past its last read of the x / scale images (and every DMA into them has
+  // landed): the epilogue may stage through that LDS
+  lds_barrier();
 #if TI_GEMV_EXP & 512   // diagnostic: no split-K merge at all (every slice runs the epilogue)
   const bool merged = true;
 #else
   const bool merged = n_ks == 1 || splitk_merge<TPW>(a, acc, (cb * n_rb + rb) * kGemvWaves + wave,
                                                       n_cb * n_rb * kGemvWaves, ks, n_ks, lane);
 #endif
-  // epilogue straight from the accumulators (16 x 4 outputs per lane pattern of the MFMA); the
-  // tile loop stays rolled (64 inlined epilogues are too large to unroll), so its accumulators
-  // are picked by static selects and acc stays in registers
+  // Epilogue, one weight tile at a time (the loop stays rolled: 64 inlined epilogues are too large
+  // to unroll, so the tile's accumulators are picked by static selects and acc stays in
+  // registers).  Kinds with row-contiguous outputs go through the wave's own LDS block
+  // (tile_epilogue_lds: a lane then owns 4 consecutive outputs of a row, 8- / 16-byte accesses
+  // instead of 16 scattered 2- / 4-byte ones per tile); the rest per element from the MFMA layout.
+  const int ek = a.epi.kind;
+  const bool via_lds = TI_TILE_EPI_LDS && (ek == TI_EPI_STORE_F32 || ek == TI_EPI_RESID_F32 || ek == TI_EPI_QKV_ROPE_KV ||
+                                           (ek == TI_EPI_SILU_MUL_F16 && !a.epi.out_packed));
+  float* stg = (float*)smem + wave * (64 * kTileEpiStride);
 #pragma unroll 1
   for (int t = 0; t < (merged ? TPW : 0); ++t) {
     const int tn = t0 + wn * TPW + t;
@@ -1842,6 +1917,16 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
       if (tt == t)
 #pragma unroll
         for (int b = 0; b < 4; ++b) av[b] = acc[tt][b];
+    if (via_lds) {
+      // lane (r, kq) holds rows b*16 + 4 kq + i of column r; LDS program order within the wave
+      // makes the reads below see these writes, and the next tile's writes follow the reads
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) stg[(b * 16 + 4 * (lane >> 4) + i) * kTileEpiStride + r] = av[b][i];
+      if (tn < NT) tile_epilogue_lds(a, tn, m0 + wm * 64, stg, lane);
+      continue;
+    }
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
