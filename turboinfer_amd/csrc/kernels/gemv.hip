@@ -1615,6 +1615,13 @@ __device__ __forceinline__ bool splitk_merge(const GemvArgs& a, f32x4 (&acc)[TPW
   return true;
 }
 
+#ifndef TI_TILE_PAIR
+// asm pipeline with 4 activation buffers and one weight tile per wave: one barrier per pair of
+// groups (0: per group).  tools/probe_tile: TPW 1 (O, down at 512 rows) 6-9 % fewer cycles,
+// TPW 2-3 5 % more (the barrier's share stays, its per-pair wait doubles), so wider shapes keep
+// one barrier per group.
+#define TI_TILE_PAIR 1
+#endif
 #ifndef TI_TILE_EPI_LDS
 #define TI_TILE_EPI_LDS 1   // 0: every epilogue per element from the MFMA layout (A/B knob)
 #endif
@@ -1828,6 +1835,42 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
     //   W(kg): after group kg's own issue, two whole groups are younger -> vmcnt(NWT), then the
     //          slot's registers are tied ("+v") so nothing reads them earlier.
     constexpr int NX = (XL - 1) * (2 * WMR + TPW) + TPW, NWT = 2 * (2 * WMR + TPW);
+    if constexpr (TI_TILE_PAIR && XB == 4 && TPW == 1) {
+      // Pairs of groups per barrier (half the barriers): at the top of pair (kg, kg + 1), kg even,
+      // x(kg) and x(kg + 1) have landed in every wave and every wave is done with pair kg - 2, whose
+      // two buffers then take x(kg + 2) and x(kg + 3); W(kg + 2) goes out every group as before.
+      // Issue order: [pair top: 2 x 2 WMR DMAs, TPW weight loads] [odd group: TPW weight loads], so
+      //   x(kg + 1) at the pair top: the two groups' weight loads are younger -> vmcnt(2 TPW);
+      //   W(kg) after the group's own issue: one pair's worth -> vmcnt(4 WMR + 2 TPW).
+      // Slots: the loop runs in steps of 6 from -6 (k0 = 0 mod 2 and mod 3: static pair and slot
+      // positions); groups before -2 issue nothing (their waits pass at once).
+      constexpr int NX2 = 2 * TPW, NWT2 = 4 * WMR + 2 * TPW;
+      for (int k0 = -6; k0 < nk; k0 += 6) {
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+          const int kg = k0 + u, su = u % 3;
+          __builtin_amdgcn_sched_barrier(0);   // no interleaving across groups (register pressure)
+          if ((u & 1) == 0) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NX2) : "memory");   // x(kg), x(kg + 1)
+            TILE_CY(0);
+            lds_barrier();
+            TILE_CY(1);
+            if (kg >= -2) {
+              issue_x(kb + max(0, min(kg + 2, nk - 1)));
+              issue_x(kb + max(0, min(kg + 3, nk - 1)));
+            }
+          }
+          if (kg >= -2) load_w(W[(su + 2) % 3], kb + max(0, min(kg + 2, nk - 1)));
+          TILE_CY(2);
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NWT2) : "memory");   // W(kg)
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) asm volatile("" : "+v"(W[su][t]));
+          TILE_CY(3);
+          if (kg >= 0 && kg < nk) compute(W[su], kb + kg);
+          TILE_CY(4);
+        }
+      }
+    } else
     for (int k0 = -kTileWR; k0 < nk; k0 += kTileWR) {   // kg: group of this k-slice
 #pragma unroll
       for (int u = 0; u < kTileWR; ++u) {
