@@ -112,6 +112,66 @@ def test_tile_three_tiles_per_wave(ti, oracle, M, K, N):
     assert_close_dot(yd.download(f32, (M, N)), xa.astype(np.float64) @ wf.astype(np.float64), xa, wf)
 
 
+@pytest.mark.parametrize("M,K,N", [(32, 4096, 32000), (17, 1152, 50016), (25, 384, 34000)])
+def test_tile_32_row_waves(ti, oracle, M, K, N):
+    """Wide outputs at <= 32 rows take the tile kernel with 32-row waves (half the activation
+    block per group); ragged rows and tiles."""
+    L = ti.lib()   # the wide-output tile path (TI_GEMM_TILE_WIDE_MN), not the batched-rows kernel
+    assert L.ti_gemm_packed_rows(4, M) == 1 and L.ti_gemm_packed_rows_for(4, M, N, K) == 0
+    rng = np.random.RandomState(M + K)
+    w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
+    x = rng.standard_normal((M, K)).astype(f16)
+    tiles, scales = ti.wpack_host(w, 4)
+    yd = ti.DeviceBuffer(M * N * 4)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F32, N, yd.ptr
+    run(ti, dev(ti, tiles), dev(ti, scales), dev(ti, x), M, N, K, ep)
+    wf = deq(oracle, w, 4)
+    xa = x.astype(f32)
+    assert_close_dot(yd.download(f32, (M, N)), xa.astype(np.float64) @ wf.astype(np.float64), xa, wf)
+
+
+def test_tile_32_row_waves_epilogues(ti, oracle):
+    """Residual add, SiLU * up (LDS-staged epilogues) and logits + argmax (per element) on the
+    32-row-wave tile kernel."""
+    M, K, N = 29, 2048, 30016
+    assert ti.lib().ti_gemm_packed_rows_for(4, M, N, K) == 0   # (the SiLU call has 2 I = N outputs too)
+    rng = np.random.RandomState(29)
+    x = rng.standard_normal((M, K)).astype(f16)
+    xd, xa = dev(ti, x), x.astype(np.float64)
+    w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
+    tiles, scales = ti.wpack_host(w, 4)
+    r = rng.standard_normal((M, N)).astype(f32)
+    rd = dev(ti, r)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_RESID_F32, N, rd.ptr
+    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, N, K, ep)
+    wf = deq(oracle, w, 4)
+    assert_close_dot(rd.download(f32, (M, N)) - r, xa @ wf.astype(np.float64), x.astype(f32), wf, rel=5e-5)
+    I = N // 2
+    g = (rng.standard_normal((K, I)) * 0.05).astype(f32)
+    u = (rng.standard_normal((K, I)) * 0.05).astype(f32)
+    tiles, scales = ti.wpack_host(g, 4, n_total=2 * I, row_map=ti.ROWS_INTERLEAVE8, row_offset=0)
+    ti.wpack_host(u, 4, n_total=2 * I, row_map=ti.ROWS_INTERLEAVE8, row_offset=8, tiles=tiles, scales=scales)
+    yd = ti.DeviceBuffer(M * I * 2)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_SILU_MUL_F16, I, yd.ptr
+    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, 2 * I, K, ep)
+    gg, uu = xa @ deq(oracle, g, 4).astype(np.float64), xa @ deq(oracle, u, 4).astype(np.float64)
+    np.testing.assert_allclose(yd.download(f16, (M, I)).astype(np.float64), uu * (gg / (1 + np.exp(-gg))),
+                               rtol=3e-3, atol=2e-3)
+    ld, am = ti.DeviceBuffer(M * N * 4), ti.DeviceBuffer(M * ti.ARGMAX_SLOTS * 8)
+    am.zero()
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out, ep.argmax = ti.EPI_LOGITS_ARGMAX, N, ld.ptr, am.ptr
+    tiles, scales = ti.wpack_host(w, 4)
+    run(ti, dev(ti, tiles), dev(ti, scales), xd, M, N, K, ep)
+    logits = ld.download(f32, (M, N))
+    keys = am.download(np.uint64, (M, ti.ARGMAX_SLOTS)).max(axis=1)
+    np.testing.assert_array_equal((0xFFFFFFFF - (keys & 0xFFFFFFFF)).astype(np.int64), np.argmax(logits, axis=1))
+    np.testing.assert_allclose(logits, xa @ wf.astype(np.float64), rtol=1e-4, atol=1e-4)
+
+
 def test_splitk_repeat_is_deterministic(ti, oracle, splitk_ws):
     """The last arriver sums the k-slices in slice order: repeated calls give identical bits."""
     M, K, N = 128, 11008, 4096

@@ -1489,8 +1489,10 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
 // WMR: row-waves per workgroup (2: 128 rows x 4 column-waves; 1: 64 rows x 8 column-waves, half
 // the activation block and no weight tile loaded twice)
 // XB: activation-block buffers (2: double buffer; 4: issued three groups ahead, when the LDS holds them)
-__host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, int wmr = 2, int xb = 2) {
-  const int n = xb * 64 * wmr * 256 + align16((8 / wmr) * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
+// RB: 16-row blocks per row-wave (4: 64-row waves; 2: 32-row waves for calls of at most 32 rows,
+// half the activation block per group)
+__host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, int wmr = 2, int xb = 2, int rb = 4) {
+  const int n = xb * 16 * rb * wmr * 256 + align16((8 / wmr) * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
   return n > 8 * 64 * 20 * 4 ? n : 8 * 64 * 20 * 4;   // >= the epilogue's staging blocks (tile_epi_lds_bytes)
 }
 
@@ -1632,12 +1634,13 @@ __host__ __device__ constexpr int tile_epi_lds_bytes() { return kGemvWaves * 64 
 // stg[row][col] (row stride kTileEpiStride).  Same arithmetic as epilogue_mb, element for element.
 //   STORE_F32 / RESID_F32 / QKV_ROPE_KV: lane l owns columns 4 (l & 3) .. + 3 of rows 16 it + l / 4
 //   SILU_MUL_F16: lane l owns outputs 4 (l & 1) .. + 3 (gate columns, up = column + 8) of rows 32 it + l / 2
+template <int RB = 4>   // the wave's rows: 16 RB
 __device__ __forceinline__ void tile_epilogue_lds(const GemvArgs& a, int tn, int mb, const float* stg, int lane) {
   const ti_epilogue& e = a.epi;
   if (e.kind == TI_EPI_SILU_MUL_F16) {
     const int h = 4 * (lane & 1);
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+    for (int it = 0; it < RB / 2; ++it) {
       const int row = 32 * it + (lane >> 1), m = mb + row;
       const float4 g = *(const float4*)(stg + row * kTileEpiStride + h);
       const float4 u = *(const float4*)(stg + row * kTileEpiStride + 8 + h);
@@ -1655,7 +1658,7 @@ __device__ __forceinline__ void tile_epilogue_lds(const GemvArgs& a, int tn, int
   const int c = in_q ? ng : in_k ? ng - e.q_dim : ng - e.q_dim - e.kv_dim;
   const int kvh = e.kind == TI_EPI_QKV_ROPE_KV ? c / hd : 0, d = c - kvh * hd;
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
+  for (int it = 0; it < RB; ++it) {
     const int row = 16 * it + (lane >> 2), m = mb + row;
     const float4 v = *(const float4*)(stg + row * kTileEpiStride + c4);
     if (m >= a.M) continue;
@@ -1687,9 +1690,11 @@ __device__ __forceinline__ void tile_epilogue_lds(const GemvArgs& a, int tn, int
   }
 }
 
-template <int TPW, bool G32 = false, int WMR = 2, int XB = 2>
+template <int TPW, bool G32 = false, int WMR = 2, int XB = 2, int RB = 4>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb, int n_ks) {
-  constexpr int WCOL = kGemvWaves / WMR, BM = 64 * WMR;   // column-waves, rows per workgroup
+  constexpr int WCOL = kGemvWaves / WMR, BM = 16 * RB * WMR;   // column-waves, rows per workgroup
+  constexpr int ND = BM / 32;                                  // activation DMA instructions per wave and group
+  static_assert(RB == 4 || (RB == 2 && WMR == 1), "32-row waves: one row-wave per workgroup");
   static_assert(XB == 2 || (XB == 4 && TI_TILE_ASM), "deep activation ring: asm-issued DMA only");
   constexpr int XL = XB - 1;                               // groups of activations issued ahead
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1719,8 +1724,8 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   auto issue_x = [&](int kg) __attribute__((always_inline)) {   // BM / 4 DMA instructions per group
     f16* dst = xb + (kg & (XB - 1)) * BM * 128;
 #pragma unroll
-    for (int q = 0; q < 2 * WMR; ++q) {
-      const int j = wave * 2 * WMR + q, row = 4 * j + (lane >> 4), p = lane & 15, c = p ^ (row & 15);
+    for (int q = 0; q < ND; ++q) {
+      const int j = wave * ND + q, row = 4 * j + (lane >> 4), p = lane & 15, c = p ^ (row & 15);
       const int m = min(m0 + row, a.M - 1);
       if constexpr (TI_TILE_ASM)
         dma_1k_asm(xg + (size_t)m * a.ldx + kg * 128 + c * 8,
@@ -1732,18 +1737,18 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #ifndef TI_TILE_XREG
 #define TI_TILE_XREG 0   // 1: the activation block through VGPRs + ds_write instead of LDS-DMA
 #endif
-  u32x4 xreg[2 * WMR];
+  u32x4 xreg[ND];
   auto load_xr = [&](int kg) __attribute__((always_inline)) {
 #pragma unroll
-    for (int q = 0; q < 2 * WMR; ++q) {
-      const int j = wave * 2 * WMR + q, row = 4 * j + (lane >> 4), c = (lane & 15) ^ (row & 15);
+    for (int q = 0; q < ND; ++q) {
+      const int j = wave * ND + q, row = 4 * j + (lane >> 4), c = (lane & 15) ^ (row & 15);
       xreg[q] = *(const u32x4*)(xg + (size_t)min(m0 + row, a.M - 1) * a.ldx + kg * 128 + c * 8);
     }
   };
   auto store_xr = [&](int kg) __attribute__((always_inline)) {
 #pragma unroll
-    for (int q = 0; q < 2 * WMR; ++q)
-      *(u32x4*)(xb + (kg & 1) * BM * 128 + (wave * 2 * WMR + q) * 512 + lane * 8) = xreg[q];
+    for (int q = 0; q < ND; ++q)
+      *(u32x4*)(xb + (kg & 1) * BM * 128 + (wave * ND + q) * 512 + lane * 8) = xreg[q];
   };
   const u32x4* tb = a.tiles + lane;
   auto load_w = [&](u32x4 (&w)[TPW], int kg) __attribute__((always_inline)) {
@@ -1765,18 +1770,18 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #pragma unroll
     for (int u = 0; u < kTileWR - 1; ++u) load_w(W[u], kb + min(u, nk - 1));
   }
-  f32x4 acc[TPW][4];
+  f32x4 acc[TPW][RB];
 #pragma unroll
   for (int t = 0; t < TPW; ++t)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[t][b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    for (int b = 0; b < RB; ++b) acc[t][b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
   uint32_t magic;
   asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
   auto compute = [&](const u32x4 (&w)[TPW], int kg) __attribute__((always_inline)) {
-    const f16* xr = xb + (kg & (XB - 1)) * BM * 128 + (wm * 64 + r) * 128;
-    f16x8 xf[4][4];
+    const f16* xr = xb + (kg & (XB - 1)) * BM * 128 + (wm * 16 * RB + r) * 128;
+    f16x8 xf[RB][4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (int b = 0; b < RB; ++b)
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4)
         xf[b][s4] = *(const f16x8*)(xr + b * 16 * 128 + (((G32 ? s4 * 4 + kq : kq * 4 + s4) ^ r) * 8));
@@ -1786,13 +1791,13 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
           const f16x8 bf = deq_int4_signed(w[t][s4], magic);
-          f32x4 tmp[4];
+          f32x4 tmp[RB];
 #pragma unroll
-          for (int b = 0; b < 4; ++b)
+          for (int b = 0; b < RB; ++b)
             tmp[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[b][s4], bf, (f32x4){0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
           const float sc = h2f(sl[(((wn * TPW + t) * KT + kg) * 4 + s4) * 16 + r]);
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
+          for (int b = 0; b < RB; ++b) {
             acc[t][b][0] = fmaf(sc, tmp[b][0], acc[t][b][0]);
             acc[t][b][1] = fmaf(sc, tmp[b][1], acc[t][b][1]);
             acc[t][b][2] = fmaf(sc, tmp[b][2], acc[t][b][2]);
@@ -1801,18 +1806,18 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
         }
         continue;
       }
-      f32x4 tmp[4];
+      f32x4 tmp[RB];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) tmp[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+      for (int b = 0; b < RB; ++b) tmp[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         const f16x8 bf = deq_int4_signed(w[t][s4], magic);
 #pragma unroll
-        for (int b = 0; b < 4; ++b) tmp[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[b][s4], bf, tmp[b], 0, 0, 0);
+        for (int b = 0; b < RB; ++b) tmp[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[b][s4], bf, tmp[b], 0, 0, 0);
       }
       const float sc = h2f(sl[((wn * TPW + t) * KT + kg) * 16 + r]);
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
+      for (int b = 0; b < RB; ++b) {
         acc[t][b][0] = fmaf(sc, tmp[b][0], acc[t][b][0]);
         acc[t][b][1] = fmaf(sc, tmp[b][1], acc[t][b][1]);
         acc[t][b][2] = fmaf(sc, tmp[b][2], acc[t][b][2]);
@@ -1834,7 +1839,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
     //          -> vmcnt(NX), then the barrier makes every wave's part visible;
     //   W(kg): after group kg's own issue, two whole groups are younger -> vmcnt(NWT), then the
     //          slot's registers are tied ("+v") so nothing reads them earlier.
-    constexpr int NX = (XL - 1) * (2 * WMR + TPW) + TPW, NWT = 2 * (2 * WMR + TPW);
+    constexpr int NX = (XL - 1) * (ND + TPW) + TPW, NWT = 2 * (ND + TPW);
     if constexpr (TI_TILE_PAIR && XB == 4 && TPW == 1) {
       // Pairs of groups per barrier (half the barriers): at the top of pair (kg, kg + 1), kg even,
       // x(kg) and x(kg + 1) have landed in every wave and every wave is done with pair kg - 2, whose
@@ -1844,7 +1849,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
       //   W(kg) after the group's own issue: one pair's worth -> vmcnt(4 WMR + 2 TPW).
       // Slots: the loop runs in steps of 6 from -6 (k0 = 0 mod 2 and mod 3: static pair and slot
       // positions); groups before -2 issue nothing (their waits pass at once).
-      constexpr int NX2 = 2 * TPW, NWT2 = 4 * WMR + 2 * TPW;
+      constexpr int NX2 = 2 * TPW, NWT2 = 2 * ND + 2 * TPW;
       for (int k0 = -6; k0 < nk; k0 += 6) {
 #pragma unroll
         for (int u = 0; u < 6; ++u) {
@@ -1939,8 +1944,10 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #if TI_GEMV_EXP & 512   // diagnostic: no split-K merge at all (every slice runs the epilogue)
   const bool merged = true;
 #else
-  const bool merged = n_ks == 1 || splitk_merge<TPW>(a, acc, (cb * n_rb + rb) * kGemvWaves + wave,
-                                                      n_cb * n_rb * kGemvWaves, ks, n_ks, lane);
+  bool merged = n_ks == 1;   // (32-row waves never split: tile_plan)
+  if constexpr (RB == 4)
+    merged = merged || splitk_merge<TPW>(a, acc, (cb * n_rb + rb) * kGemvWaves + wave, n_cb * n_rb * kGemvWaves, ks,
+                                         n_ks, lane);
 #endif
   // Epilogue, one weight tile at a time (the loop stays rolled: 64 inlined epilogues are too large
   // to unroll, so the tile's accumulators are picked by static selects and acc stays in
@@ -1954,27 +1961,27 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #pragma unroll 1
   for (int t = 0; t < (merged ? TPW : 0); ++t) {
     const int tn = t0 + wn * TPW + t;
-    f32x4 av[4];
+    f32x4 av[RB];
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt)
       if (tt == t)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) av[b] = acc[tt][b];
+        for (int b = 0; b < RB; ++b) av[b] = acc[tt][b];
     if (via_lds) {
       // lane (r, kq) holds rows b*16 + 4 kq + i of column r; LDS program order within the wave
       // makes the reads below see these writes, and the next tile's writes follow the reads
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
+      for (int b = 0; b < RB; ++b)
 #pragma unroll
         for (int i = 0; i < 4; ++i) stg[(b * 16 + 4 * (lane >> 4) + i) * kTileEpiStride + r] = av[b][i];
-      if (tn < NT) tile_epilogue_lds(a, tn, m0 + wm * 64, stg, lane);
+      if (tn < NT) tile_epilogue_lds<RB>(a, tn, m0 + wm * 16 * RB, stg, lane);
       continue;
     }
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (int b = 0; b < RB; ++b)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = m0 + wm * 64 + b * 16 + 4 * (lane >> 4) + i;
+        const int m = m0 + wm * 16 * RB + b * 16 + 4 * (lane >> 4) + i;
         epilogue_mb(a, tn < NT ? tn : NT - 1, m, r, av[b][i], tn < NT && m < a.M);
       }
   }
@@ -2017,29 +2024,38 @@ __host__ inline bool tile_narrow_on() {
       (const void*)gemm_tile_kernel<2, true, 1, XB>, (const void*)gemm_tile_kernel<4, true, 1, XB>,             \
       (const void*)gemm_tile_kernel<3, false, 2, XB>, (const void*)gemm_tile_kernel<3, true, 2, XB>,           \
       (const void*)gemm_tile_kernel<3, false, 1, XB>, (const void*)gemm_tile_kernel<3, true, 1, XB>
-#define TI_TILE_FNS TI_TILE_FNS_XB(2), TI_TILE_FNS_XB(TI_TILE_XB4)
-__host__ inline const void* tile_fn(int tpw, bool g32, int wmr, int xb) {
+// 32-row waves (RB 2): one row-wave, the deep activation ring only
+#define TI_TILE_FNS_RB2                                                                                          \
+  (const void*)gemm_tile_kernel<1, false, 1, TI_TILE_XB4, 2>, (const void*)gemm_tile_kernel<2, false, 1, TI_TILE_XB4, 2>, \
+      (const void*)gemm_tile_kernel<3, false, 1, TI_TILE_XB4, 2>, (const void*)gemm_tile_kernel<4, false, 1, TI_TILE_XB4, 2>, \
+      (const void*)gemm_tile_kernel<1, true, 1, TI_TILE_XB4, 2>, (const void*)gemm_tile_kernel<2, true, 1, TI_TILE_XB4, 2>,  \
+      (const void*)gemm_tile_kernel<3, true, 1, TI_TILE_XB4, 2>
+#define TI_TILE_FNS TI_TILE_FNS_XB(2), TI_TILE_FNS_XB(TI_TILE_XB4), TI_TILE_FNS_RB2
+__host__ inline const void* tile_fn(int tpw, bool g32, int wmr, int xb, int rb = 4) {
   static const void* const fns[] = {TI_TILE_FNS};
+  if (rb == 2) return fns[32 + (g32 ? 4 : 0) + tpw - 1];   // (group-32 at TPW 4: never planned)
   const int base = xb == 4 ? 16 : 0;
   if (tpw == 3) return fns[base + 12 + (wmr == 1 ? 2 : 0) + (g32 ? 1 : 0)];
   return fns[base + (wmr == 1 ? 6 : 0) + (g32 ? 3 : 0) + (tpw == 1 ? 0 : tpw == 2 ? 1 : 2)];
 }
 // the deep activation ring when it fits the LDS (TI_TILE_XB=2 forces the double buffer: A/B knob)
-__host__ inline int tile_xb(int K, int tpw, bool g32, int wmr) {
+__host__ inline int tile_xb(int K, int tpw, bool g32, int wmr, int rb = 4) {
   static int force = -1;
   if (force < 0) {
     const char* e = getenv("TI_TILE_XB");
     force = e ? atoi(e) : 0;
   }
   if (TI_TILE_XB4 != 4 || force == 2) return 2;
-  return tile_lds_bytes(K, tpw, g32, wmr, 4) <= 160 * 1024 ? 4 : 2;
+  return tile_lds_bytes(K, tpw, g32, wmr, 4, rb) <= 160 * 1024 ? 4 : 2;
 }
 
-// Shapes considered: (row-waves WMR, tiles per wave TPW); a workgroup moves 16 WMR KiB of
-// activations and WMR x (8 / WMR) TPW KiB of weights per group.  TI_TILE_WMR1=0 keeps 128-row
-// workgroups (A/B knob).  Returns 8 * WMR + TPW.
+// Shapes considered: (row-waves WMR, 16-row blocks per row-wave RB, tiles per wave TPW); a
+// workgroup moves 4 RB WMR KiB of activations and WMR x (8 / WMR) TPW KiB of weights per group.
+// 32-row waves (WMR 1, RB 2) only for calls of at most 32 rows: the 64-row block's activation DMA
+// would move half padding (TI_TILE_RB2=0: A/B knob).  TI_TILE_WMR1=0 keeps 128-row workgroups
+// (A/B knob).  Returns 32 * (RB == 2) + 8 * WMR + TPW.
 __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
-  static int wide = -1, wmr1 = -1, tpw3 = -1;
+  static int wide = -1, wmr1 = -1, tpw3 = -1, rb2 = -1;
   if (wide < 0) {
     const char* e = getenv("TI_TILE_WIDE");
     wide = e ? atoi(e) != 0 : 1;
@@ -2047,23 +2063,27 @@ __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
     wmr1 = f ? atoi(f) != 0 : 1;
     const char* g = getenv("TI_TILE_TPW3");
     tpw3 = g ? atoi(g) != 0 : 1;
+    const char* h = getenv("TI_TILE_RB2");
+    rb2 = h ? atoi(h) != 0 : 1;
   }
   const int NT = N >> 4;
   int best = 8 * 2 + 2;
   long best_cost = -1;
-  for (int wmr : {2, 1}) {
+  for (int wr : {8, 4, 2}) {   // row-wave shape: 4 RB WMR (2 x 4, 1 x 4, 1 x 2)
+    const int wmr = wr == 8 ? 2 : 1, rb = wr == 2 ? 2 : 4;
     if (wmr == 1 && !wmr1) continue;
+    if (rb == 2 && (!rb2 || M > 32 || !wmr1 || TI_TILE_XB4 != 4)) continue;
     for (int tpw : {2, 1, 4, 3}) {
       // (group-32 at TPW 4 spills to scratch: kept out, its asm-loaded weight ring must stay in VGPRs)
       if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && (!wide || (g32 && TI_TILE_ASM))) || (tpw == 3 && !tpw3) ||
-          tile_lds_bytes(K, tpw, g32, wmr) > 160 * 1024)
+          tile_lds_bytes(K, tpw, g32, wmr, 2, rb) > 160 * 1024 || (rb == 2 && tile_xb(K, tpw, g32, wmr, rb) != 4))
         continue;
-      const int cols = (8 / wmr) * tpw;
+      const int cols = (8 / wmr) * tpw, bm = 16 * rb * wmr;
       // rounds as launched: ceil(column blocks / 8) x row blocks workgroups on each XCD's CUs
-      const long per_xcd = (long)((NT + cols - 1) / cols + 7) / 8 * ((M + 64 * wmr - 1) / (64 * wmr));
-      const long cost = (per_xcd + cus / 8 - 1) / (cus / 8) * (16 * wmr + 8 * tpw);
+      const long per_xcd = (long)((NT + cols - 1) / cols + 7) / 8 * ((M + bm - 1) / bm);
+      const long cost = (per_xcd + cus / 8 - 1) / (cus / 8) * (4 * rb * wmr + 8 * tpw);
       if (best_cost < 0 || cost < best_cost) {
-        best = 8 * wmr + tpw;
+        best = (rb == 2 ? 32 : 0) + 8 * wmr + tpw;
         best_cost = cost;
       }
     }
@@ -2090,13 +2110,14 @@ __host__ inline size_t splitk_slab_bytes(int n_ks, int n_cb, int n_rb, int tpw) 
   return (size_t)n_ks * n_cb * n_rb * kGemvWaves * tpw * 4 * kWave * 16;
 }
 __host__ inline void tile_plan(int M, int N, int K, bool g32, int cus, int64_t ws_bytes, int* wmr_o, int* tpw_o,
-                               int* ks_o) {
+                               int* ks_o, int* rb_o = nullptr) {
   const int shape = tile_shape(M, N, K, g32, cus);   // the one-slice choice (knobs applied there)
-  const int wmr = shape >> 3, tpw = shape & 7;
+  const int wmr = (shape >> 3) & 3, tpw = shape & 7, rb = shape & 32 ? 2 : 4;
   *wmr_o = wmr;
   *tpw_o = tpw;
   *ks_o = 1;
-  if (!splitk_on() || ws_bytes <= TI_SPLITK_TICKET_BYTES) return;
+  if (rb_o) *rb_o = rb;
+  if (rb == 2 || !splitk_on() || ws_bytes <= TI_SPLITK_TICKET_BYTES) return;   // (32-row waves never split)
   const int NT = N >> 4, KT = K >> 7, cols = (8 / wmr) * tpw;
   const int n_cb = (NT + cols - 1) / cols, n_rb = (M + 64 * wmr - 1) / (64 * wmr);
   const long wgs = (long)n_cb * n_rb, grid1 = (long)(n_cb + 7) / 8 * 8 * n_rb;   // (launched: whole XCD rows)
@@ -2614,14 +2635,14 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   const bool has_ws = epi->splitk_ws && epi->splitk_bytes > TI_SPLITK_TICKET_BYTES && splitk_on();
   const bool tile = batched && x_kind == TI_X_F16 && (M >= tile_rows() || (!g32 && wide_tile(bits, M, N)));
   const bool rows = !tile && batched && (g32_rowsk || packed_x || M > 32 || (M > 16 && rows_on()));
-  int n_cb = 0, n_rb = 0, n_ks = 1, tpw = 2, wmr = 2, xbuf = 2;
+  int n_cb = 0, n_rb = 0, n_ks = 1, tpw = 2, wmr = 2, xbuf = 2, trb = 4;
   if (tile) {
-    tile_plan(M, N, K, g32, query_cus(), has_ws ? epi->splitk_bytes : 0, &wmr, &tpw, &n_ks);   // (tile_plan)
-    n_rb = (M + 64 * wmr - 1) / (64 * wmr);
+    tile_plan(M, N, K, g32, query_cus(), has_ws ? epi->splitk_bytes : 0, &wmr, &tpw, &n_ks, &trb);   // (tile_plan)
+    n_rb = (M + 16 * trb * wmr - 1) / (16 * trb * wmr);
     n_cb = ((N >> 4) + (8 / wmr) * tpw - 1) / ((8 / wmr) * tpw);
     grid = (n_cb + 7) / 8 * 8 * n_rb * n_ks;
-    xbuf = tile_xb(K, tpw, g32, wmr);
-    lds = tile_lds_bytes(K, tpw, g32, wmr, xbuf);
+    xbuf = tile_xb(K, tpw, g32, wmr, trb);
+    lds = tile_lds_bytes(K, tpw, g32, wmr, xbuf, trb);
   } else if (rows) {
     rows_on();
     rows_plan(M, N, K, query_cus(), &rMB, &rRG, &r_rb, &grid, &ntl, g32);   // grid: column groups
@@ -2665,7 +2686,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   if (chain) chain->signaled = (uint32_t)grid;
   hipStream_t s = (hipStream_t)stream;
   if (tile) {
-    const void* f = tile_fn(tpw, g32, wmr, xbuf);
+    const void* f = tile_fn(tpw, g32, wmr, xbuf, trb);
     void* args[] = {&a, &n_cb, &n_rb, &n_ks};
     TI_HIP_CHECK(hipLaunchKernel(f, dim3(grid), dim3(kGemvThreads), args, lds, s), "hipLaunchKernel(gemm_tile_kernel)");
     TI_LAUNCH_CHECK("gemm_tile_kernel");
