@@ -38,7 +38,9 @@ for name, K, N in shapes:
         W.append((tiles, scales))
     for M in Ms:
         XK = T.X_F16 if ROWMAJOR or not T.lib().ti_gemm_packed_rows(4, M) else T.X_F16_PACKED
-        x16 = T.DeviceBuffer.from_array(np.random.RandomState(0).standard_normal((M, K)).astype(np.float16))
+        # (packed operands cover whole 16-row blocks: the buffer holds ceil(M / 16) * 16 rows)
+        MP = (M + 15) // 16 * 16 if XK == T.X_F16_PACKED else M
+        x16 = T.DeviceBuffer.from_array(np.random.RandomState(0).standard_normal((MP, K)).astype(np.float16))
         y = T.DeviceBuffer(M * N * 4)
         ep = T.Epilogue()
         ep.kind, ep.ldo, ep.out = T.EPI_STORE_F32, N, y.ptr
