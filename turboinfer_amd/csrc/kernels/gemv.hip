@@ -2049,13 +2049,23 @@ __host__ inline int tile_xb(int K, int tpw, bool g32, int wmr, int rb = 4) {
   return tile_lds_bytes(K, tpw, g32, wmr, 4, rb) <= 160 * 1024 ? 4 : 2;
 }
 
+// 32-row waves on (TI_TILE_RB2=0 keeps 64-row waves at every row count: A/B knob)
+static int g_tile_rb2 = -1;
+__host__ inline bool tile_rb2_on() {
+  if (g_tile_rb2 < 0) {
+    const char* e = getenv("TI_TILE_RB2");
+    g_tile_rb2 = e ? atoi(e) != 0 : 1;
+  }
+  return g_tile_rb2 != 0 && TI_TILE_XB4 == 4;
+}
+
 // Shapes considered: (row-waves WMR, 16-row blocks per row-wave RB, tiles per wave TPW); a
 // workgroup moves 4 RB WMR KiB of activations and WMR x (8 / WMR) TPW KiB of weights per group.
 // 32-row waves (WMR 1, RB 2) only for calls of at most 32 rows: the 64-row block's activation DMA
 // would move half padding (TI_TILE_RB2=0: A/B knob).  TI_TILE_WMR1=0 keeps 128-row workgroups
 // (A/B knob).  Returns 32 * (RB == 2) + 8 * WMR + TPW.
 __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
-  static int wide = -1, wmr1 = -1, tpw3 = -1, rb2 = -1;
+  static int wide = -1, wmr1 = -1, tpw3 = -1;
   if (wide < 0) {
     const char* e = getenv("TI_TILE_WIDE");
     wide = e ? atoi(e) != 0 : 1;
@@ -2063,8 +2073,6 @@ __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
     wmr1 = f ? atoi(f) != 0 : 1;
     const char* g = getenv("TI_TILE_TPW3");
     tpw3 = g ? atoi(g) != 0 : 1;
-    const char* h = getenv("TI_TILE_RB2");
-    rb2 = h ? atoi(h) != 0 : 1;
   }
   const int NT = N >> 4;
   int best = 8 * 2 + 2;
@@ -2072,7 +2080,7 @@ __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
   for (int wr : {8, 4, 2}) {   // row-wave shape: 4 RB WMR (2 x 4, 1 x 4, 1 x 2)
     const int wmr = wr == 8 ? 2 : 1, rb = wr == 2 ? 2 : 4;
     if (wmr == 1 && !wmr1) continue;
-    if (rb == 2 && (!rb2 || M > 32 || !wmr1 || TI_TILE_XB4 != 4)) continue;
+    if (rb == 2 && (!tile_rb2_on() || M > 32 || !wmr1)) continue;
     for (int tpw : {2, 1, 4, 3}) {
       // (group-32 at TPW 4 spills to scratch: kept out, its asm-loaded weight ring must stay in VGPRs)
       if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && (!wide || (g32 && TI_TILE_ASM))) || (tpw == 3 && !tpw3) ||
@@ -2470,13 +2478,21 @@ static bool use_batched(int bits, int x_kind, int M, int N, int K) {
 // every row's activations per workgroup: rows x N >= TI_GEMM_TILE_WIDE_MN (env, default 850000;
 // 0 = off) -- the measured crossover (tools/rows_ab.sh: 64 x 12288 rows kernel 19.0 vs tile 26.5 us,
 // 32 x 28672 rows 36.5 vs tile 28.4, 64 x 22016 35.5 vs 28.3, 32 x 22016 25.7 vs 27.2).
-static long g_tile_wide_mn = -1;
+// At 17..32 rows the tile kernel's 32-row waves (RB 2) move a quarter of the activation bytes the
+// batched-rows kernel does and win from N >= TI_GEMM_TILE_WIDE_N32 (env, default 16384) whatever the
+// rows (`profiles/r3c_tile_wide32.txt`: N = 22016 at 17-32 rows 25.1-25.5 -> 18.2-18.8 us, N = 32000
+// 36.1-36.4 -> 21.2-21.8; N = 12288 stays on the rows kernel, 13.8 vs 17.2).
+static long g_tile_wide_mn = -1, g_tile_wide_n32 = -1;
 static bool wide_tile(int bits, int M, int N) {
   if (g_tile_wide_mn < 0) {
     const char* e = getenv("TI_GEMM_TILE_WIDE_MN");
     g_tile_wide_mn = e ? atol(e) : 850000;
+    const char* f = getenv("TI_GEMM_TILE_WIDE_N32");
+    g_tile_wide_n32 = f ? atol(f) : 16384;
   }
-  return bits == 4 && g_tile_wide_mn > 0 && M > 16 && M < ti::tile_rows() && (long)M * N >= g_tile_wide_mn;
+  if (bits != 4 || g_tile_wide_mn <= 0 || M <= 16 || M >= ti::tile_rows()) return false;
+  if (M <= 32 && ti::tile_rb2_on() && g_tile_wide_n32 > 0 && N >= g_tile_wide_n32) return true;
+  return (long)M * N >= g_tile_wide_mn;
 }
 extern "C" int ti_gemm_packed_rows(int bits, int M) { return bits == 4 && M > 16 && M < ti::tile_rows() ? 1 : 0; }
 extern "C" int ti_gemm_packed_rows_for(int bits, int M, int N, int K) {
