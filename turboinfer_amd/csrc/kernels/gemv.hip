@@ -2065,8 +2065,12 @@ __host__ inline bool tile_rb2_on() {
 // would move half padding (TI_TILE_RB2=0: A/B knob).  TI_TILE_WMR1=0 keeps 128-row workgroups
 // (A/B knob).  Returns 32 * (RB == 2) + 8 * WMR + TPW.
 __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
-  static int wide = -1, wmr1 = -1, tpw3 = -1;
+  static int wide = -1, wmr1 = -1, tpw3 = -1, rb2_rows = -1, rb2_tie = -1;
   if (wide < 0) {
+    const char* r = getenv("TI_TILE_RB2_ROWS");   // A/B knobs: 32-row waves up to this many rows,
+    rb2_rows = r ? atoi(r) : 32;                   // and preferred on equal cost
+    const char* t = getenv("TI_TILE_RB2_TIE");
+    rb2_tie = t ? atoi(t) != 0 : 0;
     const char* e = getenv("TI_TILE_WIDE");
     wide = e ? atoi(e) != 0 : 1;
     const char* f = getenv("TI_TILE_WMR1");
@@ -2080,7 +2084,7 @@ __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
   for (int wr : {8, 4, 2}) {   // row-wave shape: 4 RB WMR (2 x 4, 1 x 4, 1 x 2)
     const int wmr = wr == 8 ? 2 : 1, rb = wr == 2 ? 2 : 4;
     if (wmr == 1 && !wmr1) continue;
-    if (rb == 2 && (!tile_rb2_on() || M > 32 || !wmr1)) continue;
+    if (rb == 2 && (!tile_rb2_on() || M > rb2_rows || !wmr1)) continue;
     for (int tpw : {2, 1, 4, 3}) {
       // (group-32 at TPW 4 spills to scratch: kept out, its asm-loaded weight ring must stay in VGPRs)
       if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && (!wide || (g32 && TI_TILE_ASM))) || (tpw == 3 && !tpw3) ||
@@ -2090,7 +2094,7 @@ __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
       // rounds as launched: ceil(column blocks / 8) x row blocks workgroups on each XCD's CUs
       const long per_xcd = (long)((NT + cols - 1) / cols + 7) / 8 * ((M + bm - 1) / bm);
       const long cost = (per_xcd + cus / 8 - 1) / (cus / 8) * (4 * rb * wmr + 8 * tpw);
-      if (best_cost < 0 || cost < best_cost) {
+      if (best_cost < 0 || cost < best_cost || (rb == 2 && rb2_tie && cost == best_cost)) {
         best = (rb == 2 ? 32 : 0) + 8 * wmr + tpw;
         best_cost = cost;
       }
