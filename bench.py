@@ -211,6 +211,9 @@ def main() -> int:
     import turboinfer_amd as T
 
     T.init(g.local_rank)
+    # same-run calibration of this box's HBM: every rate below can be read
+    # against it (1 GiB read by 2 workgroups per CU; device-to-device copy, read + write bytes)
+    hbm_read, hbm_copy = T.hbm_calibrate(1 << 30, 5)
     m = MODELS[args.model]
     V, H, layers, nh, nkv, hd, I, bits, theta = m
     B, L = args.batch, args.kv
@@ -237,31 +240,72 @@ def main() -> int:
     ms_per_step = dt / args.steps * 1000.0
     sb, wb = step_bytes(m, B, L)
 
-    # Dominant kernel: the W4 decode GEMM family (gemv_wq_kernel<4, *>), ~76 % of a step's
-    # bytes.  Live timing on the engine stream: each linear class as the step runs it (same
-    # kernel, x mode and epilogue), `kernel_reps` launches cycling through the layers so the
-    # weights come from HBM, captured into a graph and replayed back to back for several ms
-    # between two HIP events (ti_engine_time_kernel).  A step issues layers x (qkv, o,
-    # gate/up, down) + lm_head launches, weighted accordingly: achieved = sum(bytes) /
-    # sum(time) over those launches, which is what profiles/*_kernel_stats.txt gives as
-    # sum(calls x bytes) / total time over the gemv_wq_kernel<4, *> rows.
+    # Dominant kernel.  Live timing on the engine stream (ti_engine_time_kernel): the launches of
+    # one class as the step runs them (same kernel, x mode and epilogue), cycling through the
+    # layers so the weights come from HBM, captured into a graph and replayed back to back for
+    # several ms between two HIP events.
+    #  * one stream with the persistent decode layers on (the 7B default): pds_kernel, one
+    #    launch per step holding every layer's weights + K/V (~97 % of the step's bytes);
+    #  * otherwise the decode GEMM family: layers x (qkv, o, gate/up, down) + lm_head launches,
+    #    achieved = sum(bytes) / sum(time), which is what profiles/*_kernel_stats.txt gives as
+    #    sum(calls x bytes) / total time over the same rows; each class names its kernel.
     names = ["qkv", "o", "gate_up", "down", "lm_head"]
+    shapes = {"qkv": (nh * hd + 2 * nkv * hd, H), "o": (H, nh * hd), "gate_up": (2 * I, H), "down": (H, I),
+              "lm_head": (V, H)}
+    pds_on = B == 1 and e.set_pds(None)
+    fold_on = B == 1 and e.set_fold(None)
+    lib = T.lib()
+
+    def class_kernel(name):
+        N_, K_ = shapes[name]
+        if name in ("qkv", "gate_up", "lm_head"):
+            if fold_on:
+                xk = T.X_F16_FOLDED
+            elif bits == 4 and B > 1 and lib.ti_gemm_packed_rows_for(bits, B, N_, K_):
+                xk = T.X_F16_PACKED
+            elif lib.ti_gemm_max_rows(bits, T.X_F32_RMSNORM, N_, K_) < B:
+                xk = T.X_F16
+            else:
+                xk = T.X_F32_RMSNORM
+        elif name == "o" and B == 1:
+            xk = T.X_ATTN_SPLITS
+        else:
+            xk = T.X_F16_PACKED if bits == 4 and lib.ti_gemm_packed_rows(bits, B) else T.X_F16
+        return T.gemm_kernel_name(bits, xk, B, N_, K_)
+
     per = {}
     gemv_bytes = gemv_us = 0.0
     n_launch = 0
+    kernels_used = {}
     for w, name in enumerate(names):
         us, by = e.time_kernel(w, B, L, args.kernel_reps)
         cnt = 1 if name == "lm_head" else layers
-        per[name] = {"avg_us": round(us, 3), "bytes": int(by), "GBps": round(by / us / 1e3, 1)}
+        kname = class_kernel(name)
+        per[name] = {"avg_us": round(us, 3), "bytes": int(by), "GBps": round(by / us / 1e3, 1), "kernel": kname}
+        kernels_used.setdefault(kname, []).append(name)
+        if pds_on and name != "lm_head":
+            per[name]["note"] = "per-layer launch of the graph path (not run by the step: pds_kernel replaces it)"
         gemv_bytes += by * cnt
         gemv_us += us * cnt
         n_launch += cnt
     att_us, att_bytes = e.time_kernel(5, B, L, args.kernel_reps)
-    per["attention"] = {"avg_us": round(att_us, 3), "bytes": int(att_bytes), "GBps": round(att_bytes / att_us / 1e3, 1)}
-    achieved = gemv_bytes / gemv_us / 1e3   # GB/s
+    per["attention"] = {"avg_us": round(att_us, 3), "bytes": int(att_bytes), "GBps": round(att_bytes / att_us / 1e3, 1),
+                        "kernel": "attn_split_kernel"}
+    if pds_on:
+        pds_us, pds_bytes = e.time_kernel(6, B, L, 2)
+        per["pds"] = {"avg_us": round(pds_us, 3), "bytes": int(pds_bytes), "GBps": round(pds_bytes / pds_us / 1e3, 1),
+                      "kernel": "pds_kernel"}
+        dom = {"kernel": f"pds_kernel (persistent decode layers: {layers} x (QKV, attention, O, gate/up, down) in one "
+                         f"launch per step)", "bytes_per_launch": int(pds_bytes), "avg_launch_us": round(pds_us, 3)}
+        achieved = pds_bytes / pds_us / 1e3
+    else:
+        dom = {"kernel": " + ".join(f"{k} ({', '.join(v)})" for k, v in kernels_used.items()),
+               "bytes_per_launch": int(gemv_bytes / n_launch), "avg_launch_us": round(gemv_us / n_launch, 3)}
+        achieved = gemv_bytes / gemv_us / 1e3   # GB/s
     e.close()
 
-    traffic, traffic_src = pmc_traffic("gemv_wq_kernel<4>") if bits == 4 and B == 1 else (None, None)
+    traffic, traffic_src = pmc_traffic("pds_kernel" if pds_on else "gemv_wq_kernel<4>") if bits == 4 and B == 1 \
+        else (None, None)
     result = None
     if g.rank == 0:
         result = {
@@ -281,11 +325,16 @@ def main() -> int:
             "config": {"workload": f"{args.model} INT{bits} g128 decode, {B} stream(s)/GPU, KV {L}, replay at pos {L - 1}",
                        "model": args.model, "global_batch": B * g.world, "seq_len": L,
                        "parallelism": f"replicas{g.world} (request-sharded, no collectives)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernel": "gemv_wq_kernel<4>",
-                         "bytes_per_launch": int(gemv_bytes / n_launch), "avg_launch_us": round(gemv_us / n_launch, 3)},
+            "roofline": dict({"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                              "traffic_source": traffic_src}, **dom),
+            "attention_roofline": {"bound": "hbm", "kernel": "attn_split_kernel", "achieved": per["attention"]["GBps"],
+                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": round(per["attention"]["GBps"] / HBM_PEAK_GBS, 4),
+                                   "share_of_step_bytes": round(layers * att_bytes / sb, 4)},
+            "calibration": {"hbm_read_GBps": round(hbm_read, 1), "hbm_copy_GBps": round(hbm_copy, 1),
+                            "note": "same run, this GPU: 1 GiB streamed once by 2 workgroups per CU (read) and "
+                                    "hipMemcpyAsync device-to-device (read + write bytes); best of 5"},
             "step_roofline": {"bytes_per_step": int(sb), "weight_bytes": int(wb),
                               "achieved_GBps": round(sb / (ms_per_step * 1e-3) / 1e9, 1),
                               "frac": round(sb / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -172,9 +172,10 @@ int ti_engine_sync(ti_engine* e);
 int ti_engine_last_tokens(ti_engine* e, int n_streams, int32_t* tokens);
 
 /* Live per-kernel timing: the step's launches of class `which` (0 qkv, 1 o, 2 gate/up,
- * 3 down, 4 lm_head, 5 attention), `reps` of them cycling through the layers, captured into a
- * graph that is replayed back to back (several ms) between two HIP events on the engine
- * stream.  avg_us = average per launch; bytes = algorithmic HBM bytes per launch. */
+ * 3 down, 4 lm_head, 5 attention, 6 the persistent decode layers -- one launch for all layers,
+ * single stream, when persistent decode is on), `reps` of them cycling through the layers,
+ * captured into a graph that is replayed back to back (several ms) between two HIP events on
+ * the engine stream.  avg_us = average per launch; bytes = algorithmic HBM bytes per launch. */
 int ti_engine_time_kernel(ti_engine* e, int which, int n_streams, int kv_len, int reps, double* avg_us,
                           double* bytes);
 

@@ -353,6 +353,17 @@ int ti_qkv_attn_fused(const void* tiles, const uint16_t* scales, const uint16_t*
                       const ti_epilogue* epi, uint16_t* part_o, float* part_ml, uint32_t* counters,
                       uint32_t* abort_flag, ti_stream_t s);
 
+/* The kernel ti_gemm_wq_a16 launches for plain (not group-32) weights of this shape, e.g.
+ * "gemv_wq_kernel<4,4>", "gemm_rows_kernel", "gemm_tile_kernel" (bench / profile labels). */
+int ti_gemm_kernel_name(int bits, int x_kind, int M, int N, int K, char* buf, int len);
+
+/* Same-run HBM calibration (bench lines): best-of-`reps` read GB/s of a `bytes` buffer streamed
+ * once by 2 workgroups per CU, and hipMemcpyAsync device-to-device GB/s (read + write bytes).
+ * Not a reference interface: the reference's benchmark times wall clock only
+ * (benchmarks/benchmark_inference.cpp:309-384); this lets each measured rate be read against
+ * the box it ran on. */
+int ti_hbm_calibrate(size_t bytes, int reps, double* read_gbps, double* copy_gbps, ti_stream_t s);
+
 /* ----------------------------------------------------- persistent decode layers
  * All n_layers decode layers of ONE stream in one persistent launch (pds.hip): replaces the
  * per-layer QKV / attention / O / gate-up / down launches of forward_pass_incremental
@@ -394,6 +405,8 @@ typedef struct ti_pds_args {
   /* data-tagged hand-offs: 8-byte {payload, tag} granules, ti_pds_granule_words(...) of them,
    * zero before the first launch */
   unsigned long long* gran;
+  int32_t drop_wg;                   /* diagnostic: workgroup that withholds its first down-projection
+                                      * granules (a producer lost mid-launch); -1 = none */
 } ti_pds_args;
 size_t ti_pds_granule_words(int H, int I, int qd, int heads, int grid);
 #define TI_PDS_CTR_WORDS_PER_LAYER (5 * 8 * 32)

@@ -99,6 +99,8 @@ class Oracle:
         L.or_qmodel_synth.restype = C.c_void_p
         L.or_qmodel_free.argtypes = [C.c_void_p]
         L.or_qmodel_fill_kv.argtypes = [C.c_void_p, C.c_int, C.c_uint64]
+        L.or_qmodel_set_len.argtypes = [C.c_void_p, C.c_int]
+        L.or_qmodel_set_len.restype = C.c_int
         L.or_qmodel_step.argtypes = [C.c_void_p, C.c_int, _f32p]
         L.or_qmodel_step.restype = C.c_int
         L.or_half_to_float.argtypes = [C.c_uint16]
@@ -360,6 +362,11 @@ class OracleDeepModel:
     def fill_kv(self, n, seed):
         self.o.lib.or_qmodel_fill_kv(self.ptr, n, seed)
 
+    def set_len(self, n):
+        """Rewind the cache to n positions (the next step writes position n)."""
+        if self.o.lib.or_qmodel_set_len(self.ptr, int(n)) != n:
+            raise ValueError("or_qmodel_set_len: n beyond the cache")
+
     def step(self, token):
         logits = np.empty(self.cfg["vocab"], np.float32)
         t = self.o.lib.or_qmodel_step(self.ptr, int(token), logits)
@@ -402,6 +409,9 @@ class Reference:
         L.ref_quantize.argtypes = [_f32p, C.c_uint64, C.c_int, C.c_int, _i32p, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.ref_dequantize.argtypes = [_i32p, C.c_uint64, C.c_int, C.c_float, C.c_float, _f32p]
         L.ref_plumbing_generate.argtypes = [C.c_uint64] * 3 + [_i32p, C.c_uint64, C.c_uint64, _i32p, C.POINTER(C.c_uint64)]
+        L.ref_plumbing_generate_cfg.argtypes = [C.c_uint64] * 3 + [_i32p, C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64,
+                                                _i32p, C.POINTER(C.c_uint64), C.POINTER(C.c_int32),
+                                                C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.ref_plumbing_generate_sampled.argtypes = [C.c_uint64] * 3 + [_i32p, C.c_uint64, C.c_uint64, C.c_float,
                                                     C.c_uint64, C.c_float, _i32p, _f32p, C.POINTER(C.c_uint64)]
         L.ref_plumbing_beam_search.argtypes = [C.c_uint64] * 3 + [_i32p] + [C.c_uint64] * 3 + [
@@ -512,6 +522,18 @@ class Reference:
         n = C.c_uint64()
         self._chk(self.lib.ref_plumbing_generate(vocab, hidden, layers, p, p.size, max_new, out, C.byref(n)))
         return out[: n.value].tolist()
+
+    def plumbing_generate_cfg(self, vocab, hidden, layers, prompt, max_new, eos_token_id, max_len):
+        """The reference's greedy generate() with config.eos_token_id / max_sequence_length set:
+        (tokens, finished, stop code 0 eos_token / 1 max_length / 2 max_new_tokens, total_time_ms,
+        tokens_per_second)."""
+        p = np.ascontiguousarray(prompt, np.int32)
+        out = np.zeros(len(prompt) + max_new + 1, np.int32)
+        n, stop, ms, tps = C.c_uint64(), C.c_int32(), C.c_float(), C.c_float()
+        fin = self._chk(self.lib.ref_plumbing_generate_cfg(vocab, hidden, layers, p, p.size, max_new, eos_token_id,
+                                                           max_len, out, C.byref(n), C.byref(stop), C.byref(ms),
+                                                           C.byref(tps)))
+        return out[: n.value].tolist(), bool(fin), stop.value, ms.value, tps.value
 
     def plumbing_generate_sampled(self, vocab, hidden, layers, prompt, max_new, temperature, top_k, top_p):
         """The reference's generate(..., include_logprobs=true) with a sampling config: (all

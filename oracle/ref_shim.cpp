@@ -280,6 +280,34 @@ int ref_plumbing_generate(uint64_t vocab, uint64_t hidden, uint64_t layers, cons
   });
 }
 
+// The reference's generate() contract on the plumbing model, greedy, with a chosen
+// config.eos_token_id and max_sequence_length: tokens, stop_reason (0 eos_token, 1 max_length,
+// 2 max_new_tokens), finished, and its total_time_ms / tokens_per_second (inference_engine.cpp:734-802).
+int ref_plumbing_generate_cfg(uint64_t vocab, uint64_t hidden, uint64_t layers, const int32_t* prompt,
+                              uint64_t n_prompt, uint64_t max_new, int32_t eos_token_id, uint64_t max_len,
+                              int32_t* tokens_out, uint64_t* n_out, int32_t* stop_out, float* time_ms_out,
+                              float* tps_out) {
+  return guard([&] {
+    using namespace turboinfer::model;
+    ModelData data = plumbing_model(vocab, hidden, layers);
+    InferenceConfig cfg;
+    cfg.top_k = 1;
+    cfg.temperature = 1.0f;
+    cfg.eos_token_id = eos_token_id;
+    cfg.max_sequence_length = max_len;
+    cfg.device = ComputeDevice::kCPU;
+    InferenceEngine eng(data, cfg);
+    std::vector<int> p(prompt, prompt + n_prompt);
+    GenerationResult r = eng.generate(p, max_new, false);
+    for (size_t i = 0; i < r.tokens.size(); ++i) tokens_out[i] = r.tokens[i];
+    *n_out = r.tokens.size();
+    *stop_out = r.stop_reason == "eos_token" ? 0 : r.stop_reason == "max_length" ? 1 : r.stop_reason == "max_new_tokens" ? 2 : -1;
+    *time_ms_out = r.total_time_ms;
+    *tps_out = r.tokens_per_second;
+    return r.finished ? 1 : 0;
+  });
+}
+
 // The reference's generate() with a sampling configuration and include_logprobs = true on the
 // plumbing model: every step runs the reference's own sample_next_token
 // (inference_engine.cpp:1554-1673) with its clock-seeded mt19937 draw (:470-473), and the

@@ -190,6 +190,14 @@ void or_qmodel_fill_kv(or_qmodel* m, int n, uint64_t seed) {
 
 int or_qmodel_len(const or_qmodel* m) { return m->len; }
 
+/* Rewind the cache to n positions (0 <= n <= len): the next step writes position n.  Lets a fixture
+ * generator reuse a long prompt prefix for several candidate continuations. */
+int or_qmodel_set_len(or_qmodel* m, int n) {
+  if (n < 0 || n > m->len) return -1;
+  m->len = n;
+  return n;
+}
+
 static int argmax_lowest(const float* v, size_t n) {
   size_t best = 0;
   for (size_t i = 1; i < n; ++i) if (v[i] > v[best]) best = i;

@@ -20,6 +20,7 @@ void or_qmodel_free(or_qmodel* m);
 /* or_model_fill_kv */
 void or_qmodel_fill_kv(or_qmodel* m, int n, uint64_t seed);
 int or_qmodel_len(const or_qmodel* m);
+int or_qmodel_set_len(or_qmodel* m, int n);
 /* or_decode_step(kv_round_f16 = 1): logits [vocab], returns the argmax (-1 past max_seq) */
 int or_qmodel_step(or_qmodel* m, int token, float* logits);
 

@@ -214,6 +214,9 @@ static int run_generate(const model::ModelData& md, const std::string& prompts_f
   cfg.weight_bits = bits;
   cfg.max_sequence_length = 256;
   cfg.max_batch_size = 8;
+  // generate() contract checks (tests/test_cpp_api.py::test_generate_contract_matches_reference)
+  if (const char* v = std::getenv("TI_TEST_EOS")) cfg.eos_token_id = std::atoi(v);
+  if (const char* v = std::getenv("TI_TEST_MAXLEN")) cfg.max_sequence_length = (size_t)std::atoi(v);
   model::InferenceEngine eng(md, cfg);
   const auto res = eng.generate_batch(prompts, (size_t)n_new);
   size_t width = 0;
@@ -223,7 +226,10 @@ static int run_generate(const model::ModelData& md, const std::string& prompts_f
   for (size_t i = 0; i < n; ++i)
     for (size_t j = 0; j < res[i].tokens.size(); ++j) o.data_ptr<int32_t>()[i * width + j] = res[i].tokens[j];
   write_array(out, o);
-  std::cout << res[0].stop_reason << "\n" << eng.performance_stats();
+  std::cout << res[0].stop_reason << "\n";
+  std::printf("finished %d time_ms %.9g tokens_per_second %.9g\n", res[0].finished ? 1 : 0, (double)res[0].total_time_ms,
+              (double)res[0].tokens_per_second);
+  std::cout << eng.performance_stats();
   return 0;
 }
 

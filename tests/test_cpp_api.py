@@ -216,6 +216,58 @@ def test_inference_engine_plumbing_generate_exact(api_check, golden, tmp_path):
 
 
 @pytest.mark.gpu
+def test_generate_contract_matches_reference(api_check, golden, tmp_path, monkeypatch):
+    """generate()'s stop rules and timing fields against the compiled reference's own
+    GenerationResult (tests/golden/gen_generate_contract.py, inference_engine.cpp:734-802): EOS is
+    token 2 whatever config.eos_token_id says (eos_token_id 5 / 1 / 999 do not stop the run,
+    :759-760), max_sequence_length stops with "max_length", else "max_new_tokens";
+    total_time_ms is whole milliseconds and tokens_per_second = generated / (total_time_ms / 1000)
+    (inf under 1 ms), :778-782.  (`finished` after max_new_tokens is left uninitialised by the
+    reference, so it is not compared there.)"""
+    d = golden("generate_contract")
+    for i in range(int(d["n"][0])):
+        V, H, layers, max_new, eos, max_len = (int(v) for v in d[f"cfg{i}"])
+        mdir = tmp_path / f"plumb{i}"
+        mdir.mkdir()
+        _plumbing_dir(mdir, V, H, layers)
+        monkeypatch.setenv("TI_TEST_EOS", str(eos))
+        monkeypatch.setenv("TI_TEST_MAXLEN", str(max_len))
+        prompt = d[f"prompt{i}"].astype(np.int32)[None, :]
+        outp = api_check("generate", mdir, write(tmp_path / "p.bin", prompt), max_new, 1, 0, tmp_path / "o.bin")
+        got = [int(v) for v in read(tmp_path / "o.bin")[0] if v >= 0]
+        assert got == d[f"tokens{i}"].tolist(), (i, got)
+        stop, fin = (int(v) for v in d[f"stop{i}"])
+        lines = outp.splitlines()
+        assert lines[0] == ["eos_token", "max_length", "max_new_tokens"][stop], (i, lines[0])
+        f = lines[1].split()
+        assert f[0] == "finished" and f[2] == "time_ms" and f[4] == "tokens_per_second"
+        if stop != 2:
+            assert int(f[1]) == fin == 1
+        ms, tps = float(f[3]), float(f[5])
+        assert ms == int(ms)                                  # whole milliseconds
+        gen = len(got) - prompt.shape[1]
+        want = np.float32(gen) / (np.float32(ms) / np.float32(1000.0)) if ms > 0 else np.inf
+        assert tps == pytest.approx(float(want), rel=1e-6) if ms > 0 else np.isinf(tps)
+
+
+def _plumbing_dir(mdir, V, H, layers):
+    """The reference benchmark's create_test_model(V, H, layers) fill patterns
+    (benchmark_inference.cpp:145-225) as an api_check manifest (reference_compat path)."""
+    I = 4 * H
+    idx = np.arange(H * I)
+    up = ((((idx % 200).astype(f32) / f32(200.0)) - f32(0.5)) * f32(0.02)).astype(f32).reshape(H, I)
+    lm = ((((np.arange(H * V) % 500).astype(f32) / f32(500.0)) - f32(0.5)) * f32(0.01)).astype(f32).reshape(H, V)
+    lines = [f"meta {V} {H} {layers} {H // 64} {I} 10000.0"]
+    write(mdir / "up.bin", up)
+    write(mdir / "down.bin", up.reshape(-1).reshape(I, H))
+    write(mdir / "lm.bin", lm)
+    for l in range(layers):
+        lines += [f"layers.{l}.feed_forward.w1.weight up.bin", f"layers.{l}.feed_forward.w2.weight down.bin"]
+    lines.append("lm_head.weight lm.bin")
+    (mdir / "manifest.txt").write_text("\n".join(lines) + "\n")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["mini_gqa_w4", "mini_hd128_w8"])
 def test_inference_engine_llama_greedy_matches_reference(api_check, golden, oracle, tmp_path, name):
     """A Llama-shape ModelData (the oracle's weights under the reference's names) through

@@ -142,3 +142,28 @@ def test_deep_bench_replay(ti, golden, name):
         got.append(int(e.last_tokens(1)[0]))
     e.close()
     assert_greedy(got, d["replay_tokens"].tolist(), d["replay_logits"], f"{name} replay")
+
+
+@pytest.mark.parametrize("name", ["llama2_7b", "llama3_8b"])
+def test_deep_prefill_then_decode(ti, golden, name):
+    """prefill at full width and depth.  A 120-token prompt from an empty cache
+    (tests/golden/gen_deep_prefill.py): the engine runs its first 119 tokens as ONE prefill chunk --
+    the tile GEMM at 119 rows and the MFMA causal attention, at every one of the 32 layers, the KV they
+    write then read by the decode steps -- and decodes 3 greedy tokens from the last prompt token
+    (reference forward_pass + forward_pass_incremental, inference_engine.cpp:1429-1552).  Every
+    generated step's logits within TOL_DEEP * max|logit| of the full-depth oracle (which feeds the
+    prompt token by token), and every token equal."""
+    d = golden(f"deep_prefill_{name}")
+    cfg = json.loads(str(d["cfg"]))
+    prompt, ref, ref_lg = d["prompt"].tolist(), d["tokens"].tolist(), d["logits"]
+    e = engine_for(ti, cfg, max_batch=1)
+    e.synth(int(d["seed"][0]), 0.0)
+    worst = 0.0
+    for n in range(1, len(ref) + 1):   # logits of generated step n - 1 (each call prefills again)
+        got, lg = e.generate([prompt], n, want_logits=True)
+        r = ref_lg[n - 1].astype(np.float64)
+        worst = max(worst, float(np.max(np.abs(lg[0].astype(np.float64) - r))) / float(np.max(np.abs(r))))
+    e.close()
+    _log(dict(config=name, case="prefill120+decode3", layers=cfg["layers"], max_rel_err=worst, tol=TOL))
+    assert worst <= TOL, f"{name}: logit error {worst:.4g} * max|logit| > {TOL}"
+    assert_greedy(got[0].tolist(), ref, ref_lg, f"{name} prefill")

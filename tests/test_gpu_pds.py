@@ -96,3 +96,29 @@ def test_pds_timeout_is_fatal(ti, monkeypatch):
     with pytest.raises(ti.TiError, match="persistent decode"):
         e.step([5], [0])
     e.close()
+
+
+def test_pds_lost_producer_costs_one_timeout(ti, monkeypatch):
+    """A producer that never publishes mid-launch (TI_PDS_FORCE_ERR=2: workgroup 0 withholds its
+    layer-0 down-projection granules): every other workgroup waits on them, the first expiry (~50 ms)
+    marks the launch dead and every later wait of every workgroup passes at once.  The
+    call fails with the fatal hand-off error within a few timeouts, not one per wait, and the engine
+    falls back to the per-layer graph with correct results."""
+    import time
+    v, h, l, nh, nkv, hd, inter = CFGS["l2_shape"]
+    ref = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=4, max_seq=256, max_batch=1, attn_splits=8)
+    ref.synth(0x7157, 0.1)
+    want = np.asarray(ref.generate([[1, 2, 3]], 4))
+    ref.close()
+    e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=4, max_seq=256, max_batch=1, attn_splits=8)
+    e.synth(0x7157, 0.1)
+    monkeypatch.setenv("TI_PDS_FORCE_ERR", "2")
+    assert e.set_pds(True) is True
+    monkeypatch.delenv("TI_PDS_FORCE_ERR")
+    t0 = time.perf_counter()
+    with pytest.raises(ti.TiError, match="persistent decode"):
+        e.step([5], [0])
+    assert time.perf_counter() - t0 < 1.0
+    assert e.set_pds(None) is False
+    assert np.array_equal(np.asarray(e.generate([[1, 2, 3]], 4)), want)
+    e.close()

@@ -116,6 +116,17 @@ def test_plumbing_generate(oracle, golden):
         assert toks == d[f"tokens{i}"].tolist()
 
 
+def test_generate_contract_oracle(oracle, golden):
+    """The oracle's generate loop stops as the compiled reference does (gen_generate_contract.py):
+    on token id 2 (the config's eos_token_id is not consulted, inference_engine.cpp:759-760) or at
+    max_sequence_length (:767)."""
+    d = golden("generate_contract")
+    for i in range(int(d["n"][0])):
+        V, H, layers, max_new, _eos, max_len = (int(v) for v in d[f"cfg{i}"])
+        toks, _ = oracle.plumbing_generate(V, H, layers, d[f"prompt{i}"].tolist(), max_new, max_seq=max_len)
+        assert toks == d[f"tokens{i}"].tolist(), i
+
+
 @pytest.mark.parametrize("name", ["mini_gqa_w4", "mini_hd128_w8"])
 def test_decode_step_reference_composed(oracle, golden, name):
     """or_decode_step (fp32 cache) == the decode step composed from reference ops."""

@@ -86,7 +86,7 @@ EXPORTED = [
     "ti_pds_decode", "ti_engine_set_pds", "ti_engine_pds_error", "ti_engine_pds_timestamps",
     "ti_wpack_q_host", "ti_engine_set_tensor_q", "ti_sample_workspace_bytes", "ti_sample_device_ws",
     "ti_wpack_q1_host", "ti_engine_set_tensor_q1", "ti_epilogue_bytes",
-    "ti_sample_step_ws", "ti_pds_granule_words",
+    "ti_sample_step_ws", "ti_pds_granule_words", "ti_hbm_calibrate", "ti_gemm_kernel_name",
 ]
 
 _lib = None
@@ -196,6 +196,8 @@ def lib() -> C.CDLL:
         L.ti_engine_sync.argtypes = [vp]
         L.ti_engine_last_tokens.argtypes = [vp, i32, vp]
         L.ti_engine_time_kernel.argtypes = [vp, i32, i32, i32, i32, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.ti_hbm_calibrate.argtypes = [sz, i32, C.POINTER(C.c_double), C.POINTER(C.c_double), vp]
+        L.ti_gemm_kernel_name.argtypes = [i32, i32, i32, i32, i32, C.c_char_p, i32]
         L.ti_rope_table.argtypes = [vp, i32, i32, f32, vp]
         L.ti_sample_token.argtypes = [vp, i32, f32, i32, f32, f32, C.POINTER(C.c_int), C.POINTER(C.c_float)]
         _lib = L
@@ -261,6 +263,19 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+def hbm_calibrate(nbytes: int = 1 << 30, reps: int = 5) -> tuple[float, float]:
+    """(read GB/s, device-copy GB/s) of this GPU now: the same-run calibration of bench lines."""
+    r, c = C.c_double(), C.c_double()
+    check(lib().ti_hbm_calibrate(nbytes, reps, C.byref(r), C.byref(c), None))
+    return r.value, c.value
+
+
+def gemm_kernel_name(bits: int, x_kind: int, M: int, N: int, K: int) -> str:
+    buf = C.create_string_buffer(64)
+    check(lib().ti_gemm_kernel_name(bits, x_kind, M, N, K, buf, 64))
+    return buf.value.decode()
 
 
 def sync() -> None:

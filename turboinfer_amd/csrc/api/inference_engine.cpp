@@ -27,6 +27,10 @@ using api::check;
 
 namespace {
 
+// generate()'s end-of-sequence token: the reference tests `next_token == 2` (inference_engine.cpp:759-760),
+// not config.eos_token_id (which only its beam search reads, :2015)
+constexpr int kGenerateEos = 2;
+
 [[noreturn]] void off_path(const std::string& what, const char* row) {
   throw std::runtime_error("InferenceEngine::" + what + ": not part of the MI355X decode hot path (SURVEY.md 8(f) " +
                            row + ")");
@@ -480,7 +484,10 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
   const int V = im.cfg.vocab;
   std::vector<GenerationResult> results(batches.size());
   // The contract of generate() (inference_engine.cpp:734-802): stop after EOS or once the
-  // sequence reaches max_sequence_length; otherwise stop_reason "max_new_tokens".
+  // sequence reaches max_sequence_length; otherwise stop_reason "max_new_tokens".  EOS is token
+  // id 2 whatever config.eos_token_id says (:759-760 hard-codes it; only beam search reads the
+  // config, :2015).  total_time_ms is whole milliseconds (duration_cast<milliseconds>, :778-780)
+  // and tokens_per_second = generated / (total_time_ms / 1000), inf (or NaN) under 1 ms (:782).
   auto finish = [&](GenerationResult& r, const std::vector<int>& prompt, const std::vector<int>& fresh,
                     const std::vector<float>& lps, float ms) {
     r.tokens = prompt;
@@ -488,7 +495,7 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
     for (size_t i = 0; i < fresh.size(); ++i) {
       r.tokens.push_back(fresh[i]);
       if (i < lps.size()) r.logprobs.push_back(lps[i]);
-      if (fresh[i] == config_.eos_token_id) {
+      if (fresh[i] == kGenerateEos) {
         r.finished = true;
         r.stop_reason = "eos_token";
         break;
@@ -500,12 +507,12 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
       }
     }
     if (!r.finished) r.stop_reason = "max_new_tokens";
-    r.total_time_ms = ms;
+    r.total_time_ms = static_cast<float>(static_cast<long long>(ms));
     const size_t gen = r.tokens.size() - prompt.size();
-    r.tokens_per_second = ms > 0.0f ? gen / (ms / 1000.0f) : 0.0f;
+    r.tokens_per_second = gen / (r.total_time_ms / 1000.0f);
     im.total_generations++;
     im.total_tokens += gen;
-    im.total_time_ms += ms;
+    im.total_time_ms += r.total_time_ms;
     im.peak_tps = std::max(im.peak_tps, r.tokens_per_second);
   };
   // new tokens a request can take before max_length stops it (at least one is sampled)
@@ -531,7 +538,7 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
       for (size_t s = 0; s < n; ++s) {
         const int tok = im.sample(logits.data(), config_, include_logprobs ? &lps : nullptr);
         fresh.push_back(tok);
-        if (tok == config_.eos_token_id || p.size() + fresh.size() >= maxlen || s + 1 == n) break;
+        if (tok == kGenerateEos || p.size() + fresh.size() >= maxlen || s + 1 == n) break;
         check(ti_engine_compat_step(im.eng, 0, logits.data()), "ti_engine_compat_step");
         im.total_forward_passes++;
       }
@@ -601,7 +608,7 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
       for (size_t t = 0; t < std::min(b, steps_new); ++t) {
         fresh[0].push_back(out[t]);
         if (include_logprobs) lps[0].push_back(lp[t]);
-        if (out[t] == config_.eos_token_id || p.size() + fresh[0].size() >= maxlen) break;
+        if (out[t] == kGenerateEos || p.size() + fresh[0].size() >= maxlen) break;
       }
       im.rng = saved;
       im.rng.discard(fresh[0].size());
@@ -630,7 +637,7 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
           }
           const int t = im.sample(&logits[(size_t)m * V], config_, include_logprobs ? &lps[m] : nullptr);
           fresh[m].push_back(t);
-          if (t == config_.eos_token_id || fresh[m].size() >= budget(p.size())) done[m] = true;
+          if (t == kGenerateEos || fresh[m].size() >= budget(p.size())) done[m] = true;
           all_done = all_done && done[m];
         }
         if (all_done) break;

@@ -154,6 +154,7 @@ struct ti_engine {
   void* pds_zero = nullptr;             // 4 KiB of zeros, never written
   unsigned long long* pds_gran = nullptr;   // granule hand-offs (ti_pds_granule_words)
   unsigned long long* pds_ts = nullptr; // TI_PDS_TS=1: phase timestamps of the last launch
+  int pds_drop = -1;                    // diagnostic: workgroup that withholds a hand-off (TI_PDS_FORCE_ERR=2)
 
   int qd() const { return c.heads * c.head_dim; }
   int kvd() const { return c.kv_heads * c.head_dim; }
@@ -440,6 +441,7 @@ int chain_check(ti_engine* e) {
     TI_TRY(ti_memcpy_d2h(&err, e->pds_err, 4, e->s));
     if (err) {
       e->pds_on = false;
+      e->pds_drop = -1;
       for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
       e->graphs.clear();
       TI_TRY(ti_memset(e->pds_err, 0, 4, e->s));
@@ -508,12 +510,51 @@ bool pds_usable(ti_engine* e, int M) {
   if (!e->pds_on || !e->pds_layers || M != 1 || c.bits != 4 || c.compat) return false;
   if (!fold_usable(e, M) || !part_usable(e, M) || e->splits_for(M) != 8) return false;
   if (c.heads != c.kv_heads || c.head_dim != 128 || c.heads * 8 != c.hidden / 16 || c.heads * 8 > 256) return false;
+  // ti_pds_decode's other limits: granule tags hold 64 layers, <= 8 gate/up tiles per workgroup
+  if (c.layers > 64 || 2 * c.inter / 16 > 8 * c.heads * 8) return false;
   if (g_pds_cus == 0) {
     int dev = 0, n = 0;
     g_pds_cus = (hipGetDevice(&dev) == hipSuccess &&
                  hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) ? n : -1;
   }
   return g_pds_cus >= c.heads * 8;
+}
+
+// The persistent decode-layers launch (ti_pds_decode) of a single-stream step: input h / fx / ss
+// with the layer-0 fold of n_ss0 partials, output h and fx / ss folded with out_norm.
+int pds_launch(ti_engine* e, int n_ss0) {
+  const ti_engine_config& c = e->c;
+  ti_pds_args pa{};
+  pa.layers = e->pds_layers;
+  pa.n_layers = c.layers;
+  pa.grid = c.heads * 8;
+  pa.H = c.hidden;
+  pa.I = c.inter;
+  pa.qd = e->qd();
+  pa.heads = c.heads;
+  pa.kv_heads = c.kv_heads;
+  pa.head_dim = c.head_dim;
+  pa.max_seq = c.max_seq;
+  pa.n_ss0 = n_ss0;
+  pa.eps = c.eps;
+  pa.pos = e->pos;
+  pa.rope_cs = e->rope_cs;
+  pa.out_norm = e->out_norm;
+  pa.h = e->h;
+  pa.fx = e->fx;
+  pa.ss = e->ss;
+  pa.q = e->q;
+  pa.act = e->act;
+  pa.part_o = e->part_o;
+  pa.part_ml = e->part_ml;
+  pa.ctr = e->pds_ctr;
+  pa.launches = e->pds_launches;
+  pa.err = e->pds_err;
+  pa.zero = e->pds_zero;
+  pa.gran = e->pds_gran;
+  pa.ts = e->pds_ts;
+  pa.drop_wg = e->pds_drop;
+  return ti_pds_decode(&pa, e->s);
 }
 
 // One decode step for streams [0, M) on e->s.  Graph-capturable (no host sync / alloc).
@@ -572,37 +613,8 @@ int enqueue_step(ti_engine* e, int M, int advance) {
 
   const bool pds = pds_usable(e, M);
   if (pds) {   // every layer in one persistent launch; the lm_head stages its fold (grid partials)
-    ti_pds_args pa{};
-    pa.layers = e->pds_layers;
-    pa.n_layers = c.layers;
-    pa.grid = c.heads * 8;
-    pa.H = H;
-    pa.I = I;
-    pa.qd = qd;
-    pa.heads = c.heads;
-    pa.kv_heads = c.kv_heads;
-    pa.head_dim = c.head_dim;
-    pa.max_seq = c.max_seq;
-    pa.n_ss0 = n_ss;
-    pa.eps = c.eps;
-    pa.pos = e->pos;
-    pa.rope_cs = e->rope_cs;
-    pa.out_norm = e->out_norm;
-    pa.h = e->h;
-    pa.fx = e->fx;
-    pa.ss = e->ss;
-    pa.q = e->q;
-    pa.act = e->act;
-    pa.part_o = e->part_o;
-    pa.part_ml = e->part_ml;
-    pa.ctr = e->pds_ctr;
-    pa.launches = e->pds_launches;
-    pa.err = e->pds_err;
-    pa.zero = e->pds_zero;
-    pa.gran = e->pds_gran;
-    pa.ts = e->pds_ts;
-    TI_TRY(ti_pds_decode(&pa, e->s));
-    n_ss = pa.grid;
+    TI_TRY(pds_launch(e, n_ss));
+    n_ss = c.heads * 8;
   }
   for (int l = 0; l < (pds ? 0 : c.layers); ++l) {
     DevLayer& L = e->layer[l];
@@ -1682,10 +1694,18 @@ int ti_engine_set_pds(ti_engine* e, int on, int* active) {
     e->pds_on = on != 0;
   }
   // diagnostic (tests/test_gpu_pds.py): TI_PDS_FORCE_ERR=1 pre-sets the hand-off error word, so
-  // the next persistent launch runs without waits and the engine must report it as fatal
+  // the next persistent launch runs without waits and the engine must report it as fatal;
+  // TI_PDS_FORCE_ERR=2 makes workgroup 0 withhold its first down-projection granules in every
+  // launch (a producer lost mid-launch: every other workgroup's wait must end in one timeout)
   if (on > 0 && e->pds_err)
-    if (const char* env = getenv("TI_PDS_FORCE_ERR"))
-      if (atoi(env) != 0) TI_TRY(ti_memset(e->pds_err, 0xff, 4, e->s));
+    if (const char* env = getenv("TI_PDS_FORCE_ERR")) {
+      if (atoi(env) == 1) TI_TRY(ti_memset(e->pds_err, 0xff, 4, e->s));
+      if (atoi(env) == 2) {
+        e->pds_drop = 0;
+        for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
+        e->graphs.clear();
+      }
+    }
   if (active) *active = pds_usable(e, 1) ? 1 : 0;
   return TI_OK;
 }
@@ -1744,6 +1764,9 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
       case 4: W = &e->lm; x = e->h; xk = TI_X_F32_RMSNORM; ldx = H; nw = e->out_norm;
         ep.kind = TI_EPI_LOGITS_ARGMAX; ep.ldo = c.vocab; ep.out = e->logits; ep.argmax = e->argmax; break;
       case 5: break;
+      case 6:   // the persistent decode layers (one launch per step)
+        if (!pds_usable(e, n)) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_time_kernel: persistent decode off");
+        break;
       default: return ti_set_error(TI_ERR_ARG, "ti_engine_time_kernel: which=%d", which);
     }
     if (which == 1 || which == 3) {
@@ -1788,6 +1811,7 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
     cur = (cur + 1) % c.layers;
     TI_TRY(setup(L, W, x, xk, ldx, nw, ep));
     // (the one lm_head, 68 MB at 7B, fits the Infinity Cache: back-to-back it runs warm)
+    if (which == 6) return pds_launch(e, 1);
     if (which == 5 && part)
       return ti_attn_decode_partials(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, n, c.heads, c.kv_heads,
                                      c.head_dim, e->splits_for(n), e->part_o, e->part_ml, e->s);
@@ -1817,7 +1841,7 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
   const hipError_t ei = hipGraphInstantiate(&gx, graph, nullptr, nullptr, 0);
   hipGraphDestroy(graph);
   E_CHECK(ei, "hipGraphInstantiate");
-  const int rounds = std::max(4, 4096 / reps);
+  const int rounds = which == 6 ? std::max(4, 32 / reps) : std::max(4, 4096 / reps);
   hipEvent_t a = nullptr, b = nullptr;
   hipError_t el = hipEventCreate(&a);
   if (el == hipSuccess) el = hipEventCreate(&b);
@@ -1836,6 +1860,11 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
   *avg_us = (double)ms * 1000.0 / ((double)reps * rounds);
   if (which == 5) {
     *bytes = 2.0 * n * (double)kvd * kv_len * 2.0 + (double)n * qd * (4 + 2);
+  } else if (which == 6) {   // every layer's weights + scales, K/V read at kv_len, K/V row written
+    double wl = 0.0;
+    for (const DevLinear* L : {&e->layer[0].qkv, &e->layer[0].o, &e->layer[0].gu, &e->layer[0].down})
+      wl += (double)ti_wpack_tile_bytes(c.bits, L->K, L->N) + (double)ti_wpack_scale_bytes(c.bits, L->K, L->N);
+    *bytes = c.layers * (wl + 2.0 * (double)kvd * kv_len * 2.0 + 2.0 * kvd * 2.0);
   } else {
     const double wbytes = (double)ti_wpack_tile_bytes(c.bits, W->K, W->N) + (double)ti_wpack_scale_bytes(c.bits, W->K, W->N);
     *bytes = wbytes + (double)n * W->K * (xk == TI_X_F16 || xk == TI_X_F16_FOLDED ? 2 : 4);

@@ -24,6 +24,7 @@
 //     (deterministic) and the epilogue (residual add, SiLU*up, RoPE + KV append, logits +
 //     argmax) runs on the 16 x M results of each tile.
 #include <math.h>
+#include <atomic>
 #include <stdlib.h>
 
 #include "common.hpp"
@@ -2403,7 +2404,9 @@ static int launch_rows(const GemvArgs& a, int MB, int RG, int ntl, int n_cg, int
       (const void*)gemv_mb_kernel<2, 2>, (const void*)gemv_mb_kernel<2, 3>, (const void*)gemv_mb_kernel<2, 4>, \
       (const void*)gemv_mb_kernel<2, 5>, (const void*)gemv_mb_kernel<2, 6>
 
-static unsigned long long g_prepared = 0;   // devices (bit per ordinal) whose attributes are set
+// devices (bit per ordinal) whose attributes are set; engines may be driven from several threads
+// (test_gpu_threads.py): fetch_or, and a repeated setup by a racing first call is harmless
+static std::atomic<unsigned long long> g_prepared{0};
 
 }  // namespace ti
 
@@ -2426,7 +2429,7 @@ extern "C" int ti_gemm_prepare(void) {
   int dev = 0;
   TI_HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
   const unsigned long long bit = 1ull << (dev & 63);
-  if (g_prepared & bit) return TI_OK;
+  if (g_prepared.load(std::memory_order_acquire) & bit) return TI_OK;
   const void* fns[] = {
       (const void*)gemv_wq_kernel<4, XM_F16>,  (const void*)gemv_wq_kernel<4, XM_F32>,
       (const void*)gemv_wq_kernel<4, XM_NORM1>, (const void*)gemv_wq_kernel<4, XM_NORM>,
@@ -2444,7 +2447,7 @@ extern "C" int ti_gemm_prepare(void) {
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
-  g_prepared |= bit;
+  g_prepared.fetch_or(bit, std::memory_order_acq_rel);
   return TI_OK;
 }
 
@@ -2722,6 +2725,23 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
 }
 
 extern "C" int ti_epilogue_bytes(void) { return (int)sizeof(ti_epilogue); }
+
+// The kernel ti_gemm_wq_a16 launches for plain (not group-32) weights: the same predicates as
+// gemm_impl (use_batched, wide_tile, tile_rows, rows_on).  For bench / profile labels.
+extern "C" int ti_gemm_kernel_name(int bits, int x_kind, int M, int N, int K, char* buf, int len) {
+  using namespace ti;
+  if (!buf || len < 1) return ti_set_error(TI_ERR_ARG, "ti_gemm_kernel_name: null buffer");
+  if ((bits != 4 && bits != 8 && bits != 16) || M < 1 || M > TI_GEMM_MAX_ROWS || N < 16 || K < 128)
+    return ti_set_error(TI_ERR_ARG, "ti_gemm_kernel_name: bits %d M %d N %d K %d", bits, M, N, K);
+  const bool packed_x = x_kind == TI_X_F16_PACKED;
+  const bool batched = packed_x || use_batched(bits, x_kind, M, N, K);
+  const bool tile = batched && x_kind == TI_X_F16 && (M >= tile_rows() || wide_tile(bits, M, N));
+  const bool rows = !tile && batched && (packed_x || M > 32 || (M > 16 && rows_on()));
+  const char* name = tile ? "gemm_tile_kernel" : rows ? "gemm_rows_kernel" : batched ? (mb_use_lds(M > 16 ? 2 : 1) ? "gemv_mb_kernel" : "gemv_mbr_kernel") : nullptr;
+  if (name) snprintf(buf, (size_t)len, "%s", name);
+  else snprintf(buf, (size_t)len, "gemv_wq_kernel<%d,%d>", bits, gemv_xmode(x_kind, M, K));
+  return TI_OK;
+}
 
 extern "C" int ti_gemm_grid(int M, int N, int K) {
   if (M < 1 || M > 16 || N < 16 || K < 128 || (N & 15) || (K & 127) || !fused_fits(M, N, K)) return 0;

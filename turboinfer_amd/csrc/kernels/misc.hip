@@ -1,4 +1,5 @@
 // misc.hip -- device-side decode loop step, synthetic weight / KV generation.
+#include <algorithm>
 #include <math.h>
 
 #include "common.hpp"
@@ -251,6 +252,25 @@ __global__ __launch_bounds__(256) void kv_copy_kernel(uint16_t* const* tab, int6
   }
 }
 
+// HBM read calibration (ti_hbm_calibrate): every workgroup streams a contiguous slice with 16-byte
+// non-temporal loads, 4 in flight per thread, and folds them into one word (never 0 in practice).
+typedef uint32_t hbm_u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(512) void hbm_read_kernel(const hbm_u32x4* src, size_t n16, uint32_t* sink) {
+  const size_t per = (n16 + gridDim.x - 1) / gridDim.x, b0 = blockIdx.x * per, b1 = b0 + per < n16 ? b0 + per : n16;
+  uint32_t acc = 0;
+  for (size_t i = b0 + threadIdx.x; i < b1; i += 4 * blockDim.x) {
+    hbm_u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const size_t k = i + (size_t)j * blockDim.x;
+      v[j] = k < b1 ? __builtin_nontemporal_load(src + k) : (hbm_u32x4){0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc ^= v[j][0] ^ v[j][1] ^ v[j][2] ^ v[j][3];
+  }
+  if (acc == 0x9e3779b9u) sink[blockIdx.x] = acc;   // keeps the loads; practically never stores
+}
+
 }  // namespace ti
 
 extern "C" int ti_step_begin(const ti_step_args* a, ti_stream_t stream) {
@@ -363,5 +383,54 @@ extern "C" int ti_kv_copy_slots(uint16_t* const* tab, int n_tab, int64_t src_off
   hipLaunchKernelGGL(kv_copy_kernel, dim3(bx, rows, n_tab), dim3(256), 0, (hipStream_t)stream, tab, src_off, dst_off,
                      row_pitch, chunks);
   TI_LAUNCH_CHECK("kv_copy_kernel");
+  return TI_OK;
+}
+
+// Same-run HBM calibration for bench lines: the read rate of a `bytes` buffer
+// streamed by 4 waves per CU x 2 rounds, and hipMemcpyAsync device-to-device (read + write bytes),
+// each the best of `reps` timed passes after one warm pass.  Allocates and frees its buffers.
+extern "C" int ti_hbm_calibrate(size_t bytes, int reps, double* read_gbps, double* copy_gbps, ti_stream_t stream) {
+  if (!read_gbps || !copy_gbps || bytes < (1u << 20) || reps < 1) return ti_set_error(TI_ERR_ARG, "ti_hbm_calibrate: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  void *a = nullptr, *b = nullptr, *sink = nullptr;
+  int dev = 0, cus = 0;
+  TI_HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
+  TI_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
+  bytes &= ~(size_t)15;
+  hipError_t e = hipMalloc(&a, bytes);
+  if (e == hipSuccess) e = hipMalloc(&b, bytes);
+  if (e == hipSuccess) e = hipMalloc(&sink, 4096 * 4);
+  if (e == hipSuccess) e = hipMemsetAsync(a, 1, bytes, s);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  double best_r = 0.0, best_c = 0.0;
+  const int grid = 2 * (cus > 0 ? cus : 256);
+  for (int r = 0; r <= reps && e == hipSuccess; ++r) {
+    float ms = 0.0f;
+    e = hipEventRecord(e0, s);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(ti::hbm_read_kernel, dim3(grid), dim3(512), 0, s, (const ti::hbm_u32x4*)a, bytes / 16, (uint32_t*)sink);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipEventRecord(e1, s);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e == hipSuccess && r > 0 && ms > 0.0f) best_r = std::max(best_r, (double)bytes / (ms * 1e-3) / 1e9);
+    if (e == hipSuccess) e = hipEventRecord(e0, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipEventRecord(e1, s);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e == hipSuccess && r > 0 && ms > 0.0f) best_c = std::max(best_c, 2.0 * (double)bytes / (ms * 1e-3) / 1e9);
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  if (a) hipFree(a);
+  if (b) hipFree(b);
+  if (sink) hipFree(sink);
+  TI_HIP_CHECK(e, "ti_hbm_calibrate");
+  *read_gbps = best_r;
+  *copy_gbps = best_c;
   return TI_OK;
 }
