@@ -121,29 +121,15 @@ int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32
  * instead of one token per decode step.  Default: TI_GEMM_MAX_ROWS (int4) or 16; 0 = off. */
 int ti_engine_set_prefill(ti_engine* e, int rows);
 
-/* Chained decode steps (ti_hip.h ti_chain): single-stream steps are issued as launches that
- * order themselves in-kernel (hipExtAnyOrderLaunch) instead of a replayed hipGraph, so a
- * launch's weight stream starts while its predecessor finishes.  on = 1 (or env TI_CHAIN=1)
- * applies it wherever every launch of the step is chainable (one stream, fused GEMV kernel);
- * 0 (the default: measured 12 % slower than the replayed graph on MI355X)
- * always uses the graph; chaining also needs the fold off (ti_engine_set_fold); -1 leaves the setting.  *active (nullable) receives whether steps
- * of 1 stream will be chained. */
-int ti_engine_set_chain(ti_engine* e, int on, int* active);
-
 /* Fused hand-offs of single-stream steps: (1) the folded rms_norm (ti_hip.h TI_X_F16_FOLDED):
  * the epilogue that updates the residual also writes fp16(h * next norm weight) and
  * per-workgroup sums of h^2, and the next projection divides its outputs by the rms instead of
  * normalising its input first; (2) the attention's split partials (ti_attn_decode_partials)
  * merged by the O projection (TI_X_ATTN_SPLITS) when the step uses 2..8 splits.  Default on
- * (env TI_FOLD=0 / TI_ATTN_PART=0 turn them off one by one); chained steps need both off.
+ * (env TI_FOLD=0 / TI_ATTN_PART=0 turn them off one by one).
  * on = 0/1 sets both, -1 leaves them; *active (nullable) receives whether 1-stream steps fold. */
 int ti_engine_set_fold(ti_engine* e, int on, int* active);
 
-/* QKV projection + attention of single-stream steps in one launch (ti_hip.h
- * ti_qkv_attn_fused): applies on top of the fold and the attention partials (both on), int4
- * weights, heads == kv_heads, head_dim 64/128.  on = 1 (or env TI_QKV_ATTN=1) / 0 / -1 leaves
- * it; *active (nullable) receives whether 1-stream steps use it. */
-int ti_engine_set_qkv_attn(ti_engine* e, int on, int* active);
 /* Single-stream steps run every decode layer in ONE persistent launch (ti_pds_decode) when on
  * and the model qualifies (INT4, heads == kv_heads, head_dim 128, 8 splits, hidden = 128 *
  * heads, fold and split partials on); bit-identical to the per-layer launches.  -1 leaves the

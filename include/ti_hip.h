@@ -140,28 +140,6 @@ int ti_kv_copy_slots(uint16_t* const* tab, int n_tab, int64_t src_off, int64_t d
 int ti_fill_kv_uniform(uint64_t seed, uint32_t tensor_id, int n, int kv_heads, int head_dim, int max_seq,
                        uint16_t* dst, ti_stream_t s);
 
-/* ------------------------------------------------------------ chained launches
- * A decode step is a fixed sequence of dependent launches.  Chained, each launch is issued
- * with hipExtAnyOrderLaunch (the queue does not wait for the previous launch to retire) and
- * orders itself in-kernel instead: a workgroup first issues the loads that do not depend on
- * the previous launch (its packed weights), then waits until the predecessor's counter
- * reaches `wait_target`, and only then reads the predecessor's outputs.  Outputs are stored
- * write-through (sc1) and drained; one lane per workgroup then adds 1 to its shard
- * (blockIdx & 7) of `signal_ctr` (agent-scope atomic); dependent inputs are read with sc1
- * loads (MI355X_MICROARCH.md, "Hand-offs measured with sc1 loads").  A wait longer than
- * ~20 ms gives up, sets *abort_flag and proceeds (the caller must treat the step as failed).
- * `signaled` is an output: the workgroups of the launch, i.e. what it adds to signal_ctr. */
-#define TI_CHAIN_SHARDS 8
-typedef struct ti_chain {
-  const uint32_t* wait_ctr;          /* [TI_CHAIN_SHARDS] predecessor counter, NULL = no wait */
-  uint32_t wait_target;              /* proceed once the shards sum to >= wait_target */
-  uint32_t signaled;                 /* out: workgroups of this launch */
-  uint32_t* signal_ctr;              /* [TI_CHAIN_SHARDS] this launch's counter */
-  uint32_t* abort_flag;              /* device word, set when a wait times out */
-  int32_t any_order;                 /* 1: hipExtAnyOrderLaunch */
-  int32_t _pad;
-} ti_chain;
-
 /* ---------------------------------------------------- fused decode GEMM/GEMV
  * y[m][n] = sum_k xa[m][k] * W[k][n], m < M <= TI_GEMM_MAX_ROWS (see ti_gemm_max_rows), with
  *   xa = fp16(x)                               (x_kind TI_X_F16 / TI_X_F32), or
@@ -279,13 +257,6 @@ int ti_rmsnorm_f16(const float* x, int ldx, const float* w, float eps, uint16_t*
 /* ti_rmsnorm_f16 writing y in TI_X_F16_PACKED order (K % 128 == 0). */
 int ti_rmsnorm_f16_packed(const float* x, int ldx, const float* w, float eps, uint16_t* y, int M, int K,
                           ti_stream_t s);
-/* The same GEMM as one launch of a chain (see ti_chain): M == 1, fused kernel only
- * (TI_ERR_UNSUPPORTED otherwise, nothing launched). */
-int ti_gemm_wq_a16_chained(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind,
-                           int ldx, const float* norm_w, float eps, int M, int N, int K,
-                           const ti_epilogue* epi, ti_chain* chain, ti_stream_t s);
-/* 1 if ti_gemm_wq_a16_chained accepts this shape (M == 1, fused kernel, x staged in registers). */
-int ti_gemm_chainable(int bits, int x_kind, int M, int N, int K);
 /* Workgroups of the fused kernel for an M x N x K call: the fold_ss partials a
  * TI_EPI_RESID_F32 fold epilogue writes (0 = shape not taken by the fused kernel). */
 int ti_gemm_grid(int M, int N, int K);
@@ -341,17 +312,6 @@ int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, const uint1
 int ti_attn_prefill(const float* q, const uint16_t* k_cache, const uint16_t* v_cache, int max_seq,
                     const int32_t* pos, int M, int heads, int kv_heads, int head_dim, uint16_t* out,
                     ti_stream_t s);
-/* The QKV projection and ti_attn_decode_partials of one stream in ONE launch (int4 weights,
- * heads == kv_heads, head_dim 64/128): x is TI_X_F16_FOLDED (epi->ss_in / n_ss as for
- * ti_gemm_wq_a16), epi a TI_EPI_QKV_ROPE_KV epilogue (q to epi->out, K/V row appended at
- * pos).  Workgroup (head h, split s) computes tile s of head h in q, k and v, hands them to
- * the head's other workgroups through `counters` (per head 16 words, zero before the first
- * call and left zero by every call) and runs split s of head h's attention; partials as
- * ti_attn_decode_partials with splits = head_dim / 16.  A hand-off wait longer than ~20 ms
- * sets *abort_flag. */
-int ti_qkv_attn_fused(const void* tiles, const uint16_t* scales, const uint16_t* x, float eps, int K,
-                      const ti_epilogue* epi, uint16_t* part_o, float* part_ml, uint32_t* counters,
-                      uint32_t* abort_flag, ti_stream_t s);
 
 /* The kernel ti_gemm_wq_a16 launches for plain (not group-32) weights of this shape, e.g.
  * "gemv_wq_kernel<4,4>", "gemm_rows_kernel", "gemm_tile_kernel" (bench / profile labels). */
@@ -411,12 +371,6 @@ typedef struct ti_pds_args {
 size_t ti_pds_granule_words(int H, int I, int qd, int heads, int grid);
 #define TI_PDS_CTR_WORDS_PER_LAYER (5 * 8 * 32)
 int ti_pds_decode(const ti_pds_args* a, ti_stream_t s);
-/* One launch of a chain (ti_chain): the same attention; K/V, q and pos read with sc1 loads
- * after the wait, out stored write-through. */
-int ti_attn_decode_chained(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
-                           int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
-                           int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
-                           ti_chain* chain, ti_stream_t s);
 
 /* ------------------------------------------------------- step begin (device loop)
  * One block per stream: picks the token of this step (prompt token while step < n_in[m],
@@ -443,9 +397,6 @@ typedef struct ti_step_args {
   float* fold_ss;                    /* [M] */
 } ti_step_args;
 int ti_step_begin(const ti_step_args* a, ti_stream_t s);
-/* One launch of a chain (ti_chain): waits for the previous step's last launch (argmax keys,
- * step counter), stores h / pos / tokens write-through. */
-int ti_step_begin_chained(const ti_step_args* a, ti_chain* chain, ti_stream_t s);
 
 /* ------------------------------------------------------- on-device sampling
  * InferenceEngine::sample_next_token (inference_engine.cpp:1554-1673) per stream, the uniform

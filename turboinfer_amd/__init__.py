@@ -79,10 +79,10 @@ EXPORTED = [
     "ti_argmax_f32", "ti_engine_create", "ti_engine_destroy", "ti_engine_get_stream", "ti_engine_memory", "ti_engine_set_tensor",
     "ti_engine_synth", "ti_engine_fill_kv", "ti_engine_generate", "ti_engine_step", "ti_engine_compat_step",
     "ti_engine_replay_prepare", "ti_engine_set_prefill", "ti_engine_replay_run", "ti_engine_sync", "ti_engine_last_tokens",
-    "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token", "ti_gemm_wq_a16_chained", "ti_gemm_chainable",
-    "ti_attn_decode_chained", "ti_step_begin_chained", "ti_engine_set_chain", "ti_gemm_grid", "ti_engine_set_fold",
+    "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token", 
+    "ti_gemm_grid", "ti_engine_set_fold",
     "ti_attn_decode_partials", "ti_sample_device", "ti_sample_step", "ti_engine_generate_sampled",
-    "ti_engine_beam_search", "ti_engine_serve", "ti_qkv_attn_fused", "ti_engine_set_qkv_attn",
+    "ti_engine_beam_search", "ti_engine_serve", 
     "ti_pds_decode", "ti_engine_set_pds", "ti_engine_pds_error", "ti_engine_pds_timestamps",
     "ti_wpack_q_host", "ti_engine_set_tensor_q", "ti_sample_workspace_bytes", "ti_sample_device_ws",
     "ti_wpack_q1_host", "ti_engine_set_tensor_q1", "ti_epilogue_bytes",
@@ -151,9 +151,6 @@ def lib() -> C.CDLL:
                                                 C.POINTER(C.c_int)]
         if hasattr(L, "ti_attn_decode_partials"):
             L.ti_attn_decode_partials.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
-        if hasattr(L, "ti_qkv_attn_fused"):
-            L.ti_qkv_attn_fused.argtypes = [vp, vp, vp, f32, i32, C.POINTER(Epilogue), vp, vp, vp, vp, vp]
-            L.ti_engine_set_qkv_attn.argtypes = [vp, i32, C.POINTER(C.c_int)]
         if hasattr(L, "ti_engine_set_pds"):
             L.ti_engine_set_pds.argtypes = [vp, i32, C.POINTER(C.c_int)]
             L.ti_engine_pds_error.argtypes = [vp, C.POINTER(C.c_uint32)]
@@ -185,8 +182,6 @@ def lib() -> C.CDLL:
         L.ti_engine_generate.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp]
         L.ti_engine_step.argtypes = [vp, i32, vp, vp, vp]
         L.ti_engine_set_prefill.argtypes = [vp, i32]
-        L.ti_engine_set_chain.argtypes = [vp, i32, C.POINTER(C.c_int)]
-        L.ti_gemm_chainable.argtypes = [i32, i32, i32, i32, i32]
         if hasattr(L, "ti_engine_set_fold"):   # (older TI_LIB builds in A/B runs lack it)
             L.ti_gemm_grid.argtypes = [i32, i32, i32]
             L.ti_engine_set_fold.argtypes = [vp, i32, C.POINTER(C.c_int)]
@@ -440,23 +435,10 @@ class Engine:
         """Prompt tokens per prefill chunk (0 = consume prompts one token per decode step)."""
         check(lib().ti_engine_set_prefill(self.h, rows))
 
-    def set_chain(self, on=None) -> bool:
-        """Chained single-stream steps on/off (None: query); returns whether they are active."""
-        act = C.c_int(0)
-        check(lib().ti_engine_set_chain(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
-        return bool(act.value)
-
     def set_fold(self, on=None) -> bool:
         """Folded rms_norm hand-off on/off (None: query); returns whether 1-stream steps use it."""
         act = C.c_int(0)
         check(lib().ti_engine_set_fold(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
-        return bool(act.value)
-
-    def set_qkv_attn(self, on=None) -> bool:
-        """QKV projection + attention in one launch on/off (None: query); returns whether
-        1-stream steps use it (needs the fold and the attention partials)."""
-        act = C.c_int(0)
-        check(lib().ti_engine_set_qkv_attn(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
         return bool(act.value)
 
     def set_pds(self, on=None) -> bool:

@@ -98,10 +98,6 @@ struct ti_engine {
   // single-stream attention leaves its split merge to the O projection (ti_attn_decode_partials
   // + TI_X_ATTN_SPLITS): no arrival-ticket hand-off at the end of the attention launch
   bool part_on = true;         // TI_ATTN_PART=0 turns it off
-  // QKV projection + attention in one launch (ti_qkv_attn_fused) when the step folds and
-  // hands partials over: ti_engine_set_qkv_attn / TI_QKV_ATTN
-  bool qa_on = false;
-  uint32_t* qa_ctr = nullptr;  // [heads][16], zero between launches
   uint16_t* part_o = nullptr;  // [heads][TI_ATTN_MAX_PART_SPLITS][head_dim]
   float* part_ml = nullptr;    // [heads][TI_ATTN_MAX_PART_SPLITS][2]
   // on-device sampling (ti_engine_generate_sampled): the step graph ends with ti_sample_step
@@ -136,14 +132,6 @@ struct ti_engine {
   size_t weight_bytes = 0, kv_bytes = 0;
   std::map<std::pair<int, int>, hipGraphExec_t> graphs;  // (M, advance | sampled << 1)
   int replay_M = 0;
-  // chained single-stream steps (ti_hip.h ti_chain): launch slot k of a step signals
-  // chain_ctr[k][0..7]; chain_cum[k] = its cumulative workgroup count (the next wait target)
-  bool chain_on = false;       // TI_CHAIN=1 / ti_engine_set_chain (measured slower than the graph)
-  int chain_ok = -1;           // -1 unknown, 0/1: every launch of a 1-stream step chainable
-  int chain_slots = 0;
-  uint32_t* chain_ctr = nullptr;
-  uint32_t* chain_abort = nullptr;
-  std::vector<uint32_t> chain_cum;
   // all decode layers of a single-stream step in one persistent launch (ti_pds_decode,
   // pds.hip): ti_engine_set_pds / TI_PDS; needs the fold and the split partials
   bool pds_on = false;
@@ -302,136 +290,8 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
   return TI_OK;
 }
 
-// ------------------------------------------------------------- chained steps
-bool chain_usable(ti_engine* e, int M) {
-  const ti_engine_config& c = e->c;
-  // chained kernels have neither the folded rms_norm nor the split partials hand-off
-  if (!e->chain_on || M != 1 || c.compat || !e->chain_ctr || e->fold_on || e->part_on || e->samp_on) return false;
-  if (e->chain_ok < 0) {
-    const int H = c.hidden, I = c.inter, qd = e->qd(), kvd = e->kvd();
-    const int b = c.bits;
-    e->chain_ok = ti_gemm_chainable(b, TI_X_F32_RMSNORM, 1, qd + 2 * kvd, H) && ti_gemm_chainable(b, TI_X_F16, 1, H, qd) &&
-                  ti_gemm_chainable(b, TI_X_F32_RMSNORM, 1, 2 * I, H) && ti_gemm_chainable(b, TI_X_F16, 1, H, I) &&
-                  ti_gemm_chainable(b, TI_X_F32_RMSNORM, 1, c.vocab, H);
-  }
-  return e->chain_ok == 1;
-}
-
-// One single-stream decode step as chained launches: step_begin, 5 per layer, lm_head.  The
-// first step of a run is an ordinary (barrier) launch with no wait, so it follows whatever
-// the stream did before; every later launch waits in-kernel for the launch before it.
-int enqueue_step_chained(ti_engine* e, int advance, bool first) {
-  const ti_engine_config& c = e->c;
-  if (first) {
-    uint32_t mx = 0;
-    for (uint32_t v : e->chain_cum) mx = std::max(mx, v);
-    if (mx > (1u << 30)) {   // counters are monotonic u32: rewind while the stream drains
-      E_CHECK(hipMemsetAsync(e->chain_ctr, 0, (size_t)e->chain_slots * TI_CHAIN_SHARDS * 4, e->s), "hipMemsetAsync(chain)");
-      std::fill(e->chain_cum.begin(), e->chain_cum.end(), 0u);
-    }
-  }
-  int slot = 0, prev = first ? -1 : e->chain_slots - 1;
-  ti_chain ch{};
-  auto link = [&]() -> ti_chain* {
-    if (slot >= e->chain_slots) return nullptr;
-    ch = ti_chain{};
-    if (prev >= 0) {
-      ch.wait_ctr = e->chain_ctr + (size_t)prev * TI_CHAIN_SHARDS;
-      ch.wait_target = e->chain_cum[prev];
-      ch.any_order = 1;
-    }
-    ch.signal_ctr = e->chain_ctr + (size_t)slot * TI_CHAIN_SHARDS;
-    ch.abort_flag = e->chain_abort;
-    return &ch;
-  };
-  auto done = [&]() {
-    e->chain_cum[slot] += ch.signaled;
-    prev = slot++;
-  };
-  ti_step_args sa{};
-  sa.emb = e->emb;
-  sa.h = e->h;
-  sa.hidden = c.hidden;
-  sa.M = 1;
-  sa.vocab = c.vocab;
-  sa.in_stride = e->in_cap;
-  sa.out_stride = e->out_cap;
-  sa.placeholder_first = -1;
-  sa.in_tokens = e->in_tokens;
-  sa.n_in = e->n_in;
-  sa.argmax = e->argmax;
-  sa.out_tokens = e->out_tokens;
-  sa.pos = e->pos;
-  sa.base_pos = e->base_pos;
-  sa.step_ctr = e->step_ctr;
-  if (!link()) return ti_set_error(TI_ERR_ARG, "engine: chain slots");
-  TI_TRY(ti_step_begin_chained(&sa, &ch, e->s));
-  done();
-  const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
-  auto gemm = [&](const DevLinear& W, const void* x, int x_kind, int ldx, const float* nw, const ti_epilogue& ep) -> int {
-    if (!link()) return ti_set_error(TI_ERR_ARG, "engine: chain slots");
-    TI_TRY(ti_gemm_wq_a16_chained(W.tiles, W.scales, c.bits, x, x_kind, ldx, nw, c.eps, 1, W.N, W.K, &ep, &ch, e->s));
-    done();
-    return TI_OK;
-  };
-  for (int l = 0; l < c.layers; ++l) {
-    DevLayer& L = e->layer[l];
-    ti_epilogue ep{};
-    ep.kind = TI_EPI_QKV_ROPE_KV;
-    ep.ldo = qd;
-    ep.out = e->q;
-    ep.q_dim = qd;
-    ep.kv_dim = kvd;
-    ep.head_dim = c.head_dim;
-    ep.max_seq = c.max_seq;
-    ep.pos = e->pos;
-    ep.rope_cs = e->rope_cs;
-    ep.k_cache = L.kc;
-    ep.v_cache = L.vc;
-    ep.kv_stream_stride = e->kv_stride;
-    TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, L.attn_norm, ep));
-    if (!link()) return ti_set_error(TI_ERR_ARG, "engine: chain slots");
-    TI_TRY(ti_attn_decode_chained(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, 1, c.heads, c.kv_heads, c.head_dim,
-                                  e->splits_for(1), e->ws, e->attn, &ch, e->s));
-    done();
-    ti_epilogue eo{};
-    eo.kind = TI_EPI_RESID_F32;
-    eo.ldo = H;
-    eo.out = e->h;
-    TI_TRY(gemm(L.o, e->attn, TI_X_F16, qd, nullptr, eo));
-    ti_epilogue eg{};
-    eg.kind = TI_EPI_SILU_MUL_F16;
-    eg.ldo = I;
-    eg.out = e->act;
-    TI_TRY(gemm(L.gu, e->h, TI_X_F32_RMSNORM, H, L.ffn_norm, eg));
-    ti_epilogue ed{};
-    ed.kind = TI_EPI_RESID_F32;
-    ed.ldo = H;
-    ed.out = e->h;
-    TI_TRY(gemm(L.down, e->act, TI_X_F16, I, nullptr, ed));
-  }
-  ti_epilogue el{};
-  el.kind = TI_EPI_LOGITS_ARGMAX;
-  el.ldo = V;
-  el.out = e->logits;
-  el.argmax = e->argmax;
-  el.step_ctr = e->step_ctr;
-  el.advance = advance;
-  TI_TRY(gemm(e->lm, e->h, TI_X_F32_RMSNORM, H, e->out_norm, el));
-  return slot == e->chain_slots ? TI_OK : ti_set_error(TI_ERR_ARG, "engine: chain slot count %d != %d", slot, e->chain_slots);
-}
-
-// After a synchronisation: fail (and re-arm) if any chained wait timed out.
-int chain_check(ti_engine* e) {
-  if (e->chain_abort) {
-    uint32_t ab = 0;
-    TI_TRY(ti_memcpy_d2h(&ab, e->chain_abort, 4, e->s));
-    if (ab) {
-      TI_TRY(ti_memset(e->chain_abort, 0, 4, e->s));
-      TI_TRY(ti_stream_sync(e->s));
-      return ti_set_error(TI_ERR_HIP, "engine: a chained launch's in-kernel wait timed out (results invalid)");
-    }
-  }
+// After a synchronisation: fail (and re-arm) if a persistent launch's hand-off wait timed out.
+int handoff_check(ti_engine* e) {
   // The persistent decode launch (pds.hip) bounds every hand-off wait: a wait that times out sets
   // pds_err and the launch (and any later one) finishes without waiting, so its outputs are
   // invalid.  Fatal here: the caller gets an error instead of tokens, the engine drops back to
@@ -462,13 +322,9 @@ int chain_check(ti_engine* e) {
 
 int get_graph(ti_engine* e, int M, int advance, hipGraphExec_t* out);
 
-// n steps of M streams from the current device state: chained when possible, else the graph.
+// n steps of M streams from the current device state: the replayed step graph.
 int run_steps(ti_engine* e, int M, int advance, int n) {
   if (n <= 0) return TI_OK;
-  if (chain_usable(e, M)) {
-    for (int s = 0; s < n; ++s) TI_TRY(enqueue_step_chained(e, advance, s == 0));
-    return TI_OK;
-  }
   hipGraphExec_t g = nullptr;
   TI_TRY(get_graph(e, M, advance, &g));
   for (int s = 0; s < n; ++s) E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
@@ -492,14 +348,6 @@ bool part_usable(ti_engine* e, int M) {
   const int sp = e->splits_for(M);
   return e->part_on && e->part_o && M == 1 && !c.compat && sp >= 2 && sp <= TI_ATTN_MAX_PART_SPLITS &&
          e->qd() <= 4096;
-}
-
-// QKV + attention fused (ti_qkv_attn_fused): on top of the fold and the partials, int4,
-// heads == kv_heads, head_dim 64 / 128.
-bool qa_usable(ti_engine* e, int M) {
-  const ti_engine_config& c = e->c;
-  return e->qa_on && e->qa_ctr && e->part_on && e->part_o && fold_usable(e, M) && c.bits == 4 &&
-         c.heads == c.kv_heads && (c.head_dim == 64 || c.head_dim == 128) && e->qd() <= 4096;
 }
 
 // Persistent decode layers (ti_pds_decode): one stream with the fold and the split partials,
@@ -578,7 +426,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   sa.step_ctr = e->step_ctr;
   const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
   // fold (M == 1): every rms_norm input is handed over as fx + ss partials by its producer
-  const bool fold = fold_usable(e, M), part = part_usable(e, M), qa = qa_usable(e, M), pk = packed_rows(e, M);
+  const bool fold = fold_usable(e, M), part = part_usable(e, M), pk = packed_rows(e, M);
   auto next_norm = [&](int l) -> const float* { return l < c.layers ? e->layer[l].attn_norm : e->out_norm; };
   if (fold) {
     sa.fold_w = next_norm(0);
@@ -636,16 +484,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     eo.ldo = H;
     eo.out = e->h;
     fold_into(eo, L.ffn_norm);
-    if (qa) {   // one launch: QKV tiles of a head, hand-off within the head, its attention splits
-      ep.ss_in = e->ss;
-      ep.n_ss = n_ss;
-      TI_TRY(ti_qkv_attn_fused(L.qkv.tiles, L.qkv.scales, e->fx, c.eps, H, &ep, e->part_o, e->part_ml, e->qa_ctr,
-                               e->chain_abort, e->s));
-      eo.ss_in = e->part_ml;
-      eo.n_ss = c.head_dim / 16;
-      eo.head_dim = c.head_dim;
-      TI_TRY(gemm(L.o, e->part_o, TI_X_ATTN_SPLITS, qd, 2, nullptr, eo, 4, false));
-    } else if (part) {   // the O projection merges the attention's splits while staging its input
+    if (part) {   // the O projection merges the attention's splits while staging its input
       TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));
       TI_TRY(ti_attn_decode_partials(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M, c.heads, c.kv_heads,
                                      c.head_dim, e->splits_for(M), e->part_o, e->part_ml, e->s));
@@ -913,13 +752,6 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
       if (mb && (rc = e->alloc(&e->splitk_ws, mb << 20))) return fail(rc);
       e->splitk_bytes = mb << 20;
     }
-    if ((rc = e->alloc_t(&e->qa_ctr, (size_t)c.heads * 16))) return fail(rc);
-    if (const char* env = getenv("TI_QKV_ATTN")) e->qa_on = atoi(env) != 0;
-    e->chain_slots = 2 + 5 * c.layers;
-    e->chain_cum.assign((size_t)e->chain_slots, 0u);
-    if ((rc = e->alloc_t(&e->chain_ctr, (size_t)e->chain_slots * TI_CHAIN_SHARDS)) || (rc = e->alloc_t(&e->chain_abort, (size_t)1)))
-      return fail(rc);
-    if (const char* env = getenv("TI_CHAIN")) e->chain_on = atoi(env) != 0;
     std::vector<int32_t> ones(e->pf_rows, 1);
     if ((rc = ti_memcpy_h2d(e->pf_ones, ones.data(), ones.size() * 4, e->s)) || (rc = ti_memset(e->pf_zero, 0, 4, e->s)))
       return fail(rc);
@@ -1175,7 +1007,7 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
   TI_TRY(ti_memcpy_h2d(e->step_ctr, &s0, 4, e->s));
   TI_TRY(run_steps(e, n, 1, steps - s0));
   TI_TRY(ti_stream_sync(e->s));
-  TI_TRY(chain_check(e));
+  TI_TRY(handoff_check(e));
   std::vector<int32_t> outd((size_t)n * e->out_cap);
   std::vector<unsigned long long> am;
   TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
@@ -1533,7 +1365,7 @@ int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32
     TI_TRY(run_steps(e, B, 1, S));
     TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
     TI_TRY(read_argmax(e, B, am));   // synchronises the stream
-    TI_TRY(chain_check(e));          // before any token of the chunk is handed out
+    TI_TRY(handoff_check(e));          // before any token of the chunk is handed out
     for (int m = 0; m < B; ++m) {
       const int r = slot_req[m];
       if (r < 0) continue;
@@ -1580,7 +1412,7 @@ int ti_engine_step(ti_engine* e, int n, const int32_t* tokens, const int32_t* po
   TI_TRY(ti_memset(e->step_ctr, 0, 4, e->s));
   TI_TRY(run_steps(e, n, 1, 1));
   TI_TRY(ti_stream_sync(e->s));
-  TI_TRY(chain_check(e));
+  TI_TRY(handoff_check(e));
   if (logits) TI_TRY(ti_memcpy_d2h(logits, e->logits, (size_t)n * c.vocab * 4, e->s));
   return TI_OK;
 }
@@ -1647,16 +1479,9 @@ int ti_engine_sync(ti_engine* e) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_sync: null");
   DeviceScope bind_(e);
   TI_TRY(ti_stream_sync(e->s));
-  return chain_check(e);
+  return handoff_check(e);
 }
 
-int ti_engine_set_chain(ti_engine* e, int on, int* active) {
-  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_chain: null");
-  DeviceScope bind_(e);
-  if (on >= 0) e->chain_on = on != 0;
-  if (active) *active = chain_usable(e, 1) ? 1 : 0;
-  return TI_OK;
-}
 
 int ti_engine_set_fold(ti_engine* e, int on, int* active) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_fold: null");
@@ -1671,18 +1496,6 @@ int ti_engine_set_fold(ti_engine* e, int on, int* active) {
   return TI_OK;
 }
 
-int ti_engine_set_qkv_attn(ti_engine* e, int on, int* active) {
-  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_qkv_attn: null");
-  DeviceScope bind_(e);
-  if (on >= 0 && (on != 0) != e->qa_on) {
-    TI_TRY(ti_stream_sync(e->s));   // captured step graphs bake the setting in
-    for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
-    e->graphs.clear();
-    e->qa_on = on != 0;
-  }
-  if (active) *active = qa_usable(e, 1) ? 1 : 0;
-  return TI_OK;
-}
 
 int ti_engine_set_pds(ti_engine* e, int on, int* active) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_pds: null");

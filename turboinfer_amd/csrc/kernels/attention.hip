@@ -28,48 +28,42 @@
 
 namespace ti {
 
-template <int HD, int G, int R, bool HP, bool CH = false>
+template <int HD, int G, int R, bool HP>
 __global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnArgs a) {
-  attn_split_body<HD, G, R, HP, CH>(a, blockIdx.x, blockIdx.y, blockIdx.z,
-                                    (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
+  attn_split_body<HD, G, R, HP>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 template <int HD, int G, int R, bool HP>
-static int launch_one(const AttnArgs& a, hipStream_t s, const ti_chain* chain) {
+static int launch_one(const AttnArgs& a, hipStream_t s) {
   const dim3 grid(a.splits, a.kv_heads, a.M);
-  if (chain) {
-    TI_HIP_CHECK(ti_launch_ext(attn_split_kernel<HD, G, R, HP, true>, grid, dim3(kAttnThreads), 0, s, chain->any_order != 0, a),
-                 "hipExtLaunchKernel(attn_split_kernel chained)");
-    return TI_OK;
-  }
   hipLaunchKernelGGL((attn_split_kernel<HD, G, R, HP>), grid, dim3(kAttnThreads), 0, s, a);
   TI_LAUNCH_CHECK("attn_split_kernel");
   return TI_OK;
 }
 
 template <int HD, int G>
-static int launch_attn(const AttnArgs& a, hipStream_t s, const ti_chain* chain) {
+static int launch_attn(const AttnArgs& a, hipStream_t s) {
   const bool long_range = G >= 4 && a.max_seq / a.splits >= 1024;   // keys per split (upper bound)
 #ifndef TI_ATTN_HP
 #define TI_ATTN_HP 1   // head-parallel lanes for GQA groups of 4-8 over short ranges
 #endif
   if constexpr (TI_ATTN_HP && G >= 4 && HD / (64 / G) == 8) {
-    if (!long_range) return launch_one<HD, G, TI_ATTN_RING_HP, true>(a, s, chain);   // head-parallel lanes
+    if (!long_range) return launch_one<HD, G, TI_ATTN_RING_HP, true>(a, s);   // head-parallel lanes
   }
-  if (long_range) return launch_one<HD, G, TI_ATTN_RING_LONG, false>(a, s, chain);
+  if (long_range) return launch_one<HD, G, TI_ATTN_RING_LONG, false>(a, s);
   if constexpr (G == 1) {   // one stream, MHA (the 7B decode): 3 slots (bench A/B 745 vs 741 tok/s)
-    if (a.M == 1) return launch_one<HD, G, TI_ATTN_RING_M1, false>(a, s, chain);
+    if (a.M == 1) return launch_one<HD, G, TI_ATTN_RING_M1, false>(a, s);
   }
-  return launch_one<HD, G, TI_ATTN_RING, false>(a, s, chain);
+  return launch_one<HD, G, TI_ATTN_RING, false>(a, s);
 }
 
 template <int HD>
-static int dispatch_group(const AttnArgs& a, int G, hipStream_t s, const ti_chain* chain) {
+static int dispatch_group(const AttnArgs& a, int G, hipStream_t s) {
   switch (G) {
-    case 1: return launch_attn<HD, 1>(a, s, chain);
-    case 2: return launch_attn<HD, 2>(a, s, chain);
-    case 4: return launch_attn<HD, 4>(a, s, chain);
-    case 8: return launch_attn<HD, 8>(a, s, chain);
+    case 1: return launch_attn<HD, 1>(a, s);
+    case 2: return launch_attn<HD, 2>(a, s);
+    case 4: return launch_attn<HD, 4>(a, s);
+    case 8: return launch_attn<HD, 8>(a, s);
     default: return ti_set_error(TI_ERR_UNSUPPORTED, "ti_attn_decode: heads/kv_heads = %d not in {1,2,4,8}", G);
   }
 }
@@ -88,7 +82,7 @@ extern "C" size_t ti_attn_workspace_bytes(int M, int heads, int head_dim, int sp
 
 static int attn_impl(const float* q, const uint16_t* k_cache, const uint16_t* v_cache, int64_t kv_stream_stride,
                      int max_seq, const int32_t* pos, int M, int heads, int kv_heads, int head_dim, int splits,
-                     float* workspace, uint16_t* out, ti_chain* chain, ti_stream_t stream,
+                     float* workspace, uint16_t* out, ti_stream_t stream,
                      uint16_t* part_o = nullptr, float* part_ml = nullptr, bool packed = false) {
   using namespace ti;
   if (!q || !k_cache || !v_cache || !pos || ((!workspace || !out) && !part_o))
@@ -116,7 +110,7 @@ static int attn_impl(const float* q, const uint16_t* k_cache, const uint16_t* v_
   // splits only shape the work (results agree to rounding); the merge stages all partials
   // of a kv-head group in LDS, which bounds them.
   if (!part_o) splits = std::min(splits, std::max(1, ti::attn_max_splits(G, head_dim)));
-  if (packed && (((heads * head_dim) & 127) || chain || part_o))
+  if (packed && (((heads * head_dim) & 127) || part_o))
     return ti_set_error(TI_ERR_ARG, "ti_attn_decode_packed: heads * head_dim %d not a multiple of 128",
                         heads * head_dim);
   AttnArgs a;
@@ -138,16 +132,8 @@ static int attn_impl(const float* q, const uint16_t* k_cache, const uint16_t* v_
   a.kv_shift = kv_shift;
   a.splits = splits;
   a.scale = 1.0f / sqrtf((float)head_dim);   // tensor_engine.cpp:1288 (hidden = head_dim per head)
-  a.chain = chain_dev(chain);
-  if (chain) {
-    if (!chain->abort_flag || ((uintptr_t)out & 3))
-      return ti_set_error(TI_ERR_ARG, "ti_attn_decode_chained: abort_flag required, out 4-byte aligned");
-    if ((int64_t)max_seq * head_dim * 2 >= 0x7fffffffLL)
-      return ti_set_error(TI_ERR_UNSUPPORTED, "ti_attn_decode_chained: a (stream, kv-head) cache exceeds 2 GiB");
-    chain->signaled = (uint32_t)(splits * a.kv_heads * M);
-  }
   hipStream_t s = (hipStream_t)stream;
-  return head_dim == 128 ? dispatch_group<128>(a, G, s, chain) : dispatch_group<64>(a, G, s, chain);
+  return head_dim == 128 ? dispatch_group<128>(a, G, s) : dispatch_group<64>(a, G, s);
 }
 
 extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
@@ -155,7 +141,7 @@ extern "C" int ti_attn_decode(const float* q, const uint16_t* k_cache, const uin
                               int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
                               ti_stream_t stream) {
   return attn_impl(q, k_cache, v_cache, kv_stream_stride, max_seq, pos, M, heads, kv_heads, head_dim, splits, workspace,
-                   out, nullptr, stream);
+                   out, stream);
 }
 
 extern "C" int ti_attn_decode_packed(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
@@ -163,17 +149,9 @@ extern "C" int ti_attn_decode_packed(const float* q, const uint16_t* k_cache, co
                                      int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
                                      ti_stream_t stream) {
   return attn_impl(q, k_cache, v_cache, kv_stream_stride, max_seq, pos, M, heads, kv_heads, head_dim, splits, workspace,
-                   out, nullptr, stream, nullptr, nullptr, true);
+                   out, stream, nullptr, nullptr, true);
 }
 
-extern "C" int ti_attn_decode_chained(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
-                                      int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
-                                      int kv_heads, int head_dim, int splits, float* workspace, uint16_t* out,
-                                      ti_chain* chain, ti_stream_t stream) {
-  if (!chain) return ti_set_error(TI_ERR_ARG, "ti_attn_decode_chained: null chain");
-  return attn_impl(q, k_cache, v_cache, kv_stream_stride, max_seq, pos, M, heads, kv_heads, head_dim, splits, workspace,
-                   out, chain, stream);
-}
 
 extern "C" int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, const uint16_t* v_cache,
                                        int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
@@ -183,5 +161,5 @@ extern "C" int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, 
   if (splits < 2 || splits > TI_ATTN_MAX_PART_SPLITS)
     return ti_set_error(TI_ERR_ARG, "ti_attn_decode_partials: splits %d not in [2, %d]", splits, TI_ATTN_MAX_PART_SPLITS);
   return attn_impl(q, k_cache, v_cache, kv_stream_stride, max_seq, pos, M, heads, kv_heads, head_dim, splits, nullptr,
-                   nullptr, nullptr, stream, part_o, part_ml);
+                   nullptr, stream, part_o, part_ml);
 }

@@ -1,5 +1,5 @@
 // attention_body.hpp -- the split-K decode attention of attention.hip as a device function,
-// shared by attn_split_kernel (attention.hip) and the fused QKV + attention launch (gemv.hip).
+// used by attn_split_kernel (attention.hip).
 #pragma once
 #include <math.h>
 
@@ -20,7 +20,6 @@ struct AttnArgs {
   int64_t stride;
   int32_t max_seq, M, heads, kv_heads, splits;
   float scale;
-  ChainDev chain;   // chained launches only (CH)
   // partials mode (ti_attn_decode_partials): every split writes its normalised row and
   // (max, sum) and the merge is left to the consumer (the O projection's x staging)
   uint16_t* part_o;   // [M][heads][splits][HD] fp16, nullptr = merge in this launch
@@ -46,9 +45,6 @@ struct AttnArgs {
 #endif
 #ifndef TI_ATTN_RING_LONG
 #define TI_ATTN_RING_LONG 4
-#endif
-#ifndef TI_ATTN_CH_ALL_SC1
-#define TI_ATTN_CH_ALL_SC1 0   // chained: sc1 loads for every K/V row (else only the fresh one)
 #endif
 #ifndef TI_ATTN_EXP
 #define TI_ATTN_EXP 0   // product build; tools/probe_attn.hip: +4 = per-workgroup phase timestamps
@@ -117,14 +113,8 @@ __device__ __forceinline__ float groups_sum(float v) {
   else return v;
 }
 
-// CH: one launch of a chain (ti_chain): wait first, then pos, q and K/V with sc1 loads, the
-// output stored write-through in fp16 pairs, and every workgroup signals once.
-// EARLY (CH, not HP): pos was written before this launch, so a split whose range does not hold
-// the fresh row at pos issues its K/V ring before the wait (only q comes from the producer);
-// the split holding it waits first.
-template <int HD, int G, int R, bool HP, bool CH = false, bool EARLY = false>   // HP: head-parallel lanes (G >= 4, HD / (64 / G) == 8; see below)
-__device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, int kvh, int m, unsigned flat_block) {
-  static_assert(!EARLY || (CH && !HP), "EARLY: chained, lane-group layout");
+template <int HD, int G, int R, bool HP>   // HP: head-parallel lanes (G >= 4, HD / (64 / G) == 8; see below)
+__device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, int kvh, int m) {
   static_assert(!HP || (G >= 4 && HD / (64 / G) == 8), "head-parallel layout: 8 dims per lane");
   constexpr int LPK = HD / 8;       // lanes per key row
   constexpr int KPW = 64 / LPK;     // keys per slot (wave-load)
@@ -137,56 +127,19 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int dl = lane % LPK, kg = lane / LPK;
-  if constexpr (CH && !EARLY) chain_wait(a.chain);
-  const int L = (CH && !EARLY ? (int)__builtin_amdgcn_readfirstlane(ld_sc1_u32(a.pos + m)) : a.pos[m]) + 1;
+  const int L = a.pos[m] + 1;
   // K/V of this workgroup's (stream, kv-head): [max_seq][HD] fp16 from wg_off
   const int64_t wg_off = (int64_t)m * a.stride + (int64_t)(kvh >> a.kv_shift) * a.max_seq * HD;
-  const __amdgpu_buffer_rsrc_t rk = sc1_rsrc(a.kc + wg_off), rv = sc1_rsrc(a.vc + wg_off), rq = sc1_rsrc(a.q);
-  // Chained: only the row at L - 1 was written by the previous launch (the QKV epilogue of
-  // this step); rows before it were written by earlier steps and never change afterwards, so
-  // they keep the non-temporal loads and the fresh row is read with an sc1 load.
-  const int64_t fresh_lo = (int64_t)(L - 1) * HD, fresh_hi = fresh_lo + HD;
-  auto ld_k = [&](int64_t elem) -> u32x4 {   // elem: offset within the workgroup's K
-    if constexpr (CH) {
-#if TI_ATTN_CH_ALL_SC1
-      return __builtin_amdgcn_raw_buffer_load_b128(rk, (uint32_t)(elem * 2), 0, kAuxSc1Load);
-#else
-      if (elem >= fresh_lo && elem < fresh_hi) return __builtin_amdgcn_raw_buffer_load_b128(rk, (uint32_t)(elem * 2), 0, kAuxSc1Load);
-      return ld_kv((const u32x4*)(a.kc + wg_off + elem));
-#endif
-    } else {
-      return ld_kv((const u32x4*)(a.kc + wg_off + elem));
-    }
-  };
-  auto ld_v = [&](int64_t elem) -> u32x4 {
-    if constexpr (CH) {
-#if TI_ATTN_CH_ALL_SC1
-      return __builtin_amdgcn_raw_buffer_load_b128(rv, (uint32_t)(elem * 2), 0, kAuxSc1Load);
-#else
-      if (elem >= fresh_lo && elem < fresh_hi) return __builtin_amdgcn_raw_buffer_load_b128(rv, (uint32_t)(elem * 2), 0, kAuxSc1Load);
-      return ld_kv((const u32x4*)(a.vc + wg_off + elem));
-#endif
-    } else {
-      return ld_kv((const u32x4*)(a.vc + wg_off + elem));
-    }
-  };
-  auto ld_q4 = [&](size_t elem) -> float4 {
-    if constexpr (CH) return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(elem * 4), 0, kAuxSc1Load));
-    else return *(const float4*)(a.q + elem);
-  };
-  // fp16 output element idx (thread parity == idx parity): chained, lane pairs store 4 bytes
+  auto ld_k = [&](int64_t elem) -> u32x4 { return ld_kv((const u32x4*)(a.kc + wg_off + elem)); };
+  auto ld_v = [&](int64_t elem) -> u32x4 { return ld_kv((const u32x4*)(a.vc + wg_off + elem)); };
+  auto ld_q4 = [&](size_t elem) -> float4 { return *(const float4*)(a.q + elem); };
+  // fp16 output element idx
   auto store_out = [&](size_t idx, float val) {
-    if (a.out_kt > 0) {   // packed: row m = idx / K, column idx % K (parity kept: pairs stay adjacent)
+    if (a.out_kt > 0) {   // packed: row m = idx / K, column idx % K
       const int K = a.heads * HD, m = (int)(idx / (size_t)K), k = (int)(idx - (size_t)m * K);
       idx = TI_PACKED_INDEX(m, k, a.out_kt);
     }
-    const uint32_t hv = f2h(val);
-    if constexpr (CH) {
-      const uint32_t hp = (uint32_t)__shfl_xor((int)hv, 1, kWave);
-      if (!(idx & 1)) st_sc1_u32(a.out + idx, hv | (hp << 16));
-    } else {
-      a.out[idx] = (uint16_t)hv;
-    }
+    a.out[idx] = f2h(val);
   };
   const int chunk = (L + a.splits - 1) / a.splits;
   const int s0 = split * chunk, s1 = min(L, s0 + chunk);
@@ -271,15 +224,8 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
       kr[s] = ld_k((int64_t)key * HD + dl * 8);
       vr[s] = ld_v((int64_t)key * HD + dl * 8);
     };
-    const bool fresh_here = s1 == L && s1 > s0;   // workgroup-uniform
-    if constexpr (EARLY) {
-      if (fresh_here) chain_wait(a.chain);
-    }
   #pragma unroll
     for (int s = 0; s < R; ++s) refill(s);
-    if constexpr (EARLY) {
-      if (!fresh_here) chain_wait(a.chain);
-    }
 
     float q[G][8];
   #pragma unroll
@@ -396,10 +342,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
       s_part[g * row + HD + 3] = 0.0f;
     }
   }
-  if (a.splits == 1 || a.part_o) {
-    if constexpr (CH) chain_signal(a.chain, flat_block);
-    return;
-  }
+  if (a.splits == 1 || a.part_o) return;
   __syncthreads();
 
   ATTN_TS(2);
@@ -423,10 +366,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
   }
   __syncthreads();
   ATTN_TS(3);
-  if (!s_last) {
-    if constexpr (CH) chain_signal(a.chain, flat_block);
-    return;
-  }
+  if (!s_last) return;
   // all partials of the group's heads in one round trip: s_part[g][split][row]
   const int nv = G * a.splits * V4;
   for (int i = tid; i < nv; i += kAttnThreads) {
@@ -452,7 +392,6 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
     store_out((size_t)m * a.heads * HD + (size_t)h * HD + d, num / den);
   }
   if (tid == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-  if constexpr (CH) chain_signal(a.chain, flat_block);
   ATTN_TS(4);
 }
 

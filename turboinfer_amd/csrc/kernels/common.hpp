@@ -99,20 +99,8 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-// ------------------------------------------------------- chained launches (ti_chain)
-// Device half of the chain protocol of ti_hip.h: a launch waits in-kernel for its
-// predecessor's counter, reads the predecessor's outputs with sc1 loads and publishes its
-// own outputs with sc1 (write-through) stores, drained before the counter add
-// (MI355X_MICROARCH.md "Hand-offs measured with sc1 loads", first row: one lane per
-// workgroup adds after a barrier; the consumer's polling wave then releases the workgroup
-// through a barrier; every handed-off byte stored and loaded sc1, 4/8/16-byte accesses).
-struct ChainDev {
-  const uint32_t* wait_ctr;   // null: no wait
-  uint32_t* signal_ctr;       // null: no signal
-  uint32_t* abort_flag;
-  uint32_t wait_target;
-  uint32_t _pad;
-};
+// ------------------------------------------------------- write-through (sc1) accesses
+// (persistent decode hand-offs, split merges: MI355X_MICROARCH.md "Hand-offs measured with sc1 loads")
 constexpr int kAuxSc1Load = 16;   // buffer aux bit 4 = sc1 on gfx950
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t sc1_rsrc(const void* base) {
@@ -131,43 +119,6 @@ __device__ __forceinline__ void st_sc1_u32(void* p, uint32_t v) {
 __device__ __forceinline__ void st_sc1_f32(float* p, float v) { st_sc1_u32(p, __builtin_bit_cast(uint32_t, v)); }
 __device__ __forceinline__ void st_sc1_u64(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Wave 0 polls the predecessor's counter shards (one per lane 0..7) until they sum to the
-// target, with s_sleep between polls and a ~20 ms bound (then *abort_flag = 1 and go on);
-// the workgroup is released by a barrier that leaves outstanding loads (the weight ring)
-// in flight.
-__device__ __forceinline__ void chain_wait(const ChainDev& c) {
-  if (c.wait_ctr != nullptr) {
-    if (threadIdx.x < 64) {
-      const int lane = threadIdx.x;
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      while (true) {
-        uint32_t v = lane < TI_CHAIN_SHARDS ? ld_sc1_u32(c.wait_ctr + lane) : 0u;
-        v += __shfl_xor(v, 1, 64);
-        v += __shfl_xor(v, 2, 64);
-        v += __shfl_xor(v, 4, 64);
-        const uint32_t tot = __builtin_amdgcn_readfirstlane(v);
-        if (tot >= c.wait_target) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {   // 20 ms at 100 MHz
-          if (lane == 0) atomicOr(c.abort_flag, 1u);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
-}
-// Every wave drains its stores, then one lane adds to the workgroup's counter shard.
-__device__ __forceinline__ void chain_signal(const ChainDev& c, unsigned flat_block) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (c.signal_ctr != nullptr && threadIdx.x == 0)
-    __hip_atomic_fetch_add(c.signal_ctr + (flat_block & (TI_CHAIN_SHARDS - 1)), 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ----------------------------------------------------- synthetic model stream
@@ -213,31 +164,3 @@ extern "C++" int ti_check_hip(hipError_t e, const char* what);
   } while (0)
 #define TI_LAUNCH_CHECK(what) TI_HIP_CHECK(hipGetLastError(), what)
 
-// Launch with explicit AQL ordering: hipExtLaunchKernel with the kernel's exact parameter
-// types (args converted first), any_order -> hipExtAnyOrderLaunch (chained launches).
-#include <hip/hip_ext.h>
-
-#include <tuple>
-template <typename... P, typename... A>
-inline hipError_t ti_launch_ext(void (*fn)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t s, bool any_order,
-                                A&&... args) {
-  static_assert(sizeof...(P) == sizeof...(A), "ti_launch_ext: argument count");
-  std::tuple<P...> vals(static_cast<P>(args)...);
-  void* ptrs[sizeof...(P) > 0 ? sizeof...(P) : 1];
-  std::apply([&](auto&... v) {
-    int i = 0;
-    ((ptrs[i++] = (void*)&v), ...);
-  }, vals);
-  return hipExtLaunchKernel((const void*)fn, grid, block, ptrs, lds, s, nullptr, nullptr,
-                            any_order ? hipExtAnyOrderLaunch : 0);
-}
-inline ti::ChainDev chain_dev(const ti_chain* c) {
-  ti::ChainDev d{};
-  if (c) {
-    d.wait_ctr = c->wait_ctr;
-    d.signal_ctr = c->signal_ctr;
-    d.abort_flag = c->abort_flag;
-    d.wait_target = c->wait_target;
-  }
-  return d;
-}

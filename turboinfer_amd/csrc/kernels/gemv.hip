@@ -80,7 +80,6 @@ struct GemvArgs {
   float eps;
   int32_t x_kind, ldx, M, N, K;
   ti_epilogue epi;
-  ChainDev chain;   // chained launches only (gemv_wq_kernel<..., CH = true>)
 };
 
 __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
@@ -149,7 +148,7 @@ enum { XM_F16 = 0, XM_F32 = 1, XM_NORM1 = 2, XM_NORM = 3, XM_F16F = 4, XM_ATTN =
 
 // Generic staging (M > 1 with rms_norm, f32 rows, or rows longer than the register
 // prefetch covers).  Runs after the ring is issued, so its loads wait behind the ring.
-template <int XM, bool CH = false>
+template <int XM>
 __device__ __forceinline__ void stage_x_generic(const GemvArgs& a, f16* xl, float* red, int k8_from) {
   const int tid = threadIdx.x, K = a.K, xs = K + 8, K8 = K >> 3;
   if constexpr (XM == XM_NORM || XM == XM_NORM1) {
@@ -194,11 +193,7 @@ __device__ __forceinline__ void stage_x_generic(const GemvArgs& a, f16* xl, floa
   } else {
     for (int i = tid + k8_from; i < a.M * K8; i += kGemvThreads) {
       const int m = i / K8, k8 = i - m * K8;
-      if constexpr (CH)
-        *(u32x4*)(xl + m * xs + 8 * k8) =
-            __builtin_amdgcn_raw_buffer_load_b128(sc1_rsrc(a.x), ((size_t)m * a.ldx + 8 * k8) * 2, 0, kAuxSc1Load);
-      else
-        *(u32x4*)(xl + m * xs + 8 * k8) = *(const u32x4*)((const f16*)a.x + (size_t)m * a.ldx + 8 * k8);
+      *(u32x4*)(xl + m * xs + 8 * k8) = *(const u32x4*)((const f16*)a.x + (size_t)m * a.ldx + 8 * k8);
     }
   }
 }
@@ -213,11 +208,8 @@ __device__ __forceinline__ uint32_t float_order_key(float v) {
 // v_mfma_f32_16x16x32 C layout, reduced over the 8 waves); l is the lane or, for M <= 4,
 // n alone.  Partners of the shuffles below (n ^ 1, n + 8) sit in the same 16-lane group.  `best` is the
 // thread's running argmax key for LOGITS_ARGMAX.
-// Chained launches (CH) store write-through: 4-byte sc1 stores, fp16 outputs packed in pairs
-// (lane n even stores n and n + 1; its partner n ^ 1 sits in the same 16-lane group).
 // RESID with fold_x (M == 1): also the fp16 h * nw of the next projection's TI_X_F16_FOLDED input
 // (fold weights pre-staged at fw) and this thread's running sum of h^2 (ssacc).
-template <bool CH>
 __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int l, int i, float v, const float* es,
                                          unsigned long long& best, bool ok, const float* fw, float& ssacc) {
   const ti_epilogue& e = a.epi;
@@ -225,25 +217,16 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int 
   const bool live = ok && m < a.M;
   switch (e.kind) {
     case TI_EPI_STORE_F32:
-      if (live) {
-        if constexpr (CH) st_sc1_f32((float*)e.out + (size_t)m * e.ldo + ng, v);
-        else ((float*)e.out)[(size_t)m * e.ldo + ng] = v;
-      }
+      if (live) ((float*)e.out)[(size_t)m * e.ldo + ng] = v;
       break;
     case TI_EPI_STORE_F16:
-      if constexpr (CH) {
-        const uint32_t hv = f2h(v), hp = lane_xor_u32<1>(hv);
-        if (live && !(n & 1)) st_sc1_u32((uint16_t*)e.out + (size_t)m * e.ldo + ng, hv | (hp << 16));
-      } else if (live) {
-        ((uint16_t*)e.out)[(size_t)m * e.ldo + ng] = f2h(v);
-      }
+      if (live) ((uint16_t*)e.out)[(size_t)m * e.ldo + ng] = f2h(v);
       break;
     case TI_EPI_RESID_F32:   // add(residual, y), tensor_engine.cpp:1626-1678; residual pre-staged in LDS
       if (live) {
         const float r = es[(tl * a.M + m) * 16 + n] + v;
-        if constexpr (CH) st_sc1_f32((float*)e.out + (size_t)m * e.ldo + ng, r);
-        else ((float*)e.out)[(size_t)m * e.ldo + ng] = r;
-        if (!CH && e.fold_x) {
+        ((float*)e.out)[(size_t)m * e.ldo + ng] = r;
+        if (e.fold_x) {
           e.fold_x[ng] = f2h(r * fw[tl * 16 + n]);
           ssacc = fmaf(r, r, ssacc);
         }
@@ -253,12 +236,7 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int 
       // compute_ffn (inference_engine.cpp:386-391): multiply(up, silu(gate)).
       const float up = lane_xor<8>(v);   // lanes n < 8: the up row n + 8 of the same tile
       const float s = v / (1.0f + expf(-v));
-      if constexpr (CH) {
-        const uint32_t hv = f2h(up * s), hp = lane_xor_u32<1>(hv);
-        if (live && n < 8 && !(n & 1)) st_sc1_u32((uint16_t*)e.out + (size_t)m * e.ldo + nt * 8 + n, hv | (hp << 16));
-      } else if (live && n < 8) {
-        ((uint16_t*)e.out)[(size_t)m * e.ldo + nt * 8 + n] = f2h(up * s);
-      }
+      if (live && n < 8) ((uint16_t*)e.out)[(size_t)m * e.ldo + nt * 8 + n] = f2h(up * s);
       break;
     }
     case TI_EPI_QKV_ROPE_KV: {
@@ -278,26 +256,15 @@ __device__ __forceinline__ void epilogue(const GemvArgs& a, int nt, int tl, int 
           r = (d & 1) == 0 ? fmaf(-partner, cs.y, v * cs.x) : fmaf(v, cs.x, partner * cs.y);
         }
       }
-      uint32_t pair = 0;
-      if constexpr (CH) {
-        const uint32_t hv = f2h(r), hp = lane_xor_u32<1>(hv);
-        pair = hv | (hp << 16);
-      }
       if (!live) break;
       if (ng < e.q_dim) {
-        if constexpr (CH) st_sc1_f32((float*)e.out + (size_t)m * e.ldo + ng, r);
-        else ((float*)e.out)[(size_t)m * e.ldo + ng] = r;
+        ((float*)e.out)[(size_t)m * e.ldo + ng] = r;
       } else {
         const bool is_k = qk;
         const int c = ng - e.q_dim - (is_k ? 0 : e.kv_dim);
         const int kvh = c / hd, d = c - kvh * hd;
         uint16_t* cache = is_k ? e.k_cache : e.v_cache;
-        uint16_t* dst = cache + (size_t)m * e.kv_stream_stride + ((size_t)kvh * e.max_seq + p) * hd + d;
-        if constexpr (CH) {
-          if (!(d & 1)) st_sc1_u32(dst, pair);
-        } else {
-          *dst = f2h(r);
-        }
+        cache[(size_t)m * e.kv_stream_stride + ((size_t)kvh * e.max_seq + p) * hd + d] = f2h(r);
       }
       break;
     }
@@ -346,17 +313,16 @@ __device__ __forceinline__ void lds_barrier() {
 //          (max, sum) pairs (XM_ATTN), else NULL
 //   p_mgk: M | grid << 6 | epilogue kind << 18 | head_dim / 64 << 21 (XM_ATTN)
 //   p_kx:  K | (ldx, or n_ss for XM_F16F, or splits for XM_ATTN) << 16
-// The body is a device function: gemv_wq_kernel runs it over workgroup blockIdx.x's contiguous
-// tile range; STR (the fused QKV + attention launch below) over ntl_in tiles t0_in + i * tstr_in
-// chosen by the caller, bid standing in for blockIdx.x (argmax slot, counter shard, fold slot).
+// Workgroup blockIdx.x runs over its contiguous tile range.
 // G32: group-32 weights (TI_BITS_G32, GGUF Q4_0 / Q8_0 blocks): within a tile, lane l holds for
 // MFMA step s4 the 8 k = 32 s4 + 8 (l >> 4) + e, so each v_mfma_f32_16x16x32 reduces exactly one
 // 32-weight block; its scale (and, int4, its offset correction) is applied per step.
-template <int BITS, int XM, bool CH, bool STR, bool G32 = false, bool AFF = false>
-__device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* p_scales, const void* p_x,
-                                          const float* p_aux, int p_mgk, int p_N, int p_kx, int p_ldo,
-                                          const float* p_pre, GemvArgs a, const unsigned bid, const int t0_in,
-                                          const int ntl_in, const int tstr_in) {
+template <int BITS, int XM, bool G32 = false, bool AFF = false>
+__global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
+                                                                   const void* p_x, const float* p_aux, int p_mgk,
+                                                                   int p_N, int p_kx, int p_ldo, const float* p_pre,
+                                                                   GemvArgs a) {
+  const unsigned bid = blockIdx.x;
   a.tiles = p_tiles;
   a.scales = p_scales;
   a.x = p_x;
@@ -374,12 +340,11 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   const int KT = a.K >> 7, xs = a.K + 8, NT = a.N >> 4, K8 = a.K >> 3;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: counters live in SGPRs
-  const int tstr = STR ? tstr_in : 1;             // tile stride
-  const int t0 = STR ? t0_in : (int)(bid * (unsigned)NT / (unsigned)p_grid);   // NT * grid < 2^32
-  const int ntl = STR ? ntl_in : (int)((bid + 1) * (unsigned)NT / (unsigned)p_grid) - t0;
+  const int t0 = (int)(bid * (unsigned)NT / (unsigned)p_grid);   // NT * grid < 2^32
+  const int ntl = (int)((bid + 1) * (unsigned)NT / (unsigned)p_grid) - t0;
   const int KW = wave < KT ? (KT - wave + kGemvWaves - 1) / kGemvWaves : 0;   // k-tiles per tile, this wave
   const int total = ntl * KW;
-  static_assert(!G32 || (!STR && !CH && BITS != 16), "group-32 weights: int4 / int8, fused kernel only");
+  static_assert(!G32 || BITS != 16, "group-32 weights: int4 / int8");
   static_assert(!AFF || (G32 && BITS == 4), "affine blocks: group-32 int4");
   const GemvLds L = gemv_lds_layout(a.M, a.K, ntl, G32, AFF);
   uint16_t* ml = (uint16_t*)(smem + L.mins);       // AFF: block minimums, as sl
@@ -395,11 +360,6 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   // ---- 1. small inputs into registers, ahead of the ring
   const int n_sc = BITS == 16 ? 0 : ntl * KT * (G32 ? 8 : 2);  // u32x4 pieces of scales
   const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * (G32 ? 64 : 16));
-  auto sc_off = [&](int i) -> int {                // piece i of the dense [ntl][KT][2] image
-    if constexpr (!STR) return i;
-    const int tl = i / (2 * KT);
-    return i + tl * (tstr - 1) * 2 * KT;
-  };
   u32x4 sc_reg = {0u, 0u, 0u, 0u};
 #if TI_GEMV_EXP & 8   // diagnostic: no dependency on x / scales (constants instead of loads)
   const int nx16 = a.M * K8;
@@ -410,13 +370,12 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   auto load_x = [&]() {};
   if (false) {
 #else
-  if constexpr (BITS != 16) sc_reg = ld_w(sg + sc_off(tid < n_sc ? tid : 0));
+  if constexpr (BITS != 16) sc_reg = ld_w(sg + (tid < n_sc ? tid : 0));
 
   const int nx16 = a.M * K8;
   float4 v0, v1, w0, w1;
   u32x4 xr16[XPF];
-  // x rows and the epilogue input depend on the previous launch: loaded here, or -- chained
-  // (CH) -- after the in-kernel wait, with sc1 loads (load_x below).
+  // x rows and the epilogue input depend on the previous launch
   // XM_ATTN: this thread's 8 dims (one head) of every split, and the splits' (max, sum)
   constexpr int kPS = TI_ATTN_MAX_PART_SPLITS;
   u32x4 po[XM == XM_ATTN ? kPS : 1];
@@ -433,24 +392,15 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
       }
     } else if constexpr (XM == XM_NORM1) {
       const int k8 = tid < K8 ? tid : K8 - 1;
-      if constexpr (CH) {
-        const __amdgpu_buffer_rsrc_t rx = sc1_rsrc(a.x);
-        v0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, 32 * k8, 0, kAuxSc1Load));
-        v1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, 32 * k8 + 16, 0, kAuxSc1Load));
-      } else {
-        const float* xr = (const float*)a.x;
-        v0 = *(const float4*)(xr + 8 * k8);
-        v1 = *(const float4*)(xr + 8 * k8 + 4);
-      }
+      const float* xr = (const float*)a.x;
+      v0 = *(const float4*)(xr + 8 * k8);
+      v1 = *(const float4*)(xr + 8 * k8 + 4);
     } else if constexpr (XM == XM_F16 || XM == XM_F16F) {
 #pragma unroll
       for (int q = 0; q < XPF; ++q) {
         const int i = tid + q * kGemvThreads < nx16 ? tid + q * kGemvThreads : nx16 - 1;
         const int m = i / K8, k8 = i - m * K8;
-        if constexpr (CH)
-          xr16[q] = __builtin_amdgcn_raw_buffer_load_b128(sc1_rsrc(a.x), ((size_t)m * a.ldx + 8 * k8) * 2, 0, kAuxSc1Load);
-        else
-          xr16[q] = *(const u32x4*)((const f16*)a.x + (size_t)m * a.ldx + 8 * k8);
+        xr16[q] = *(const u32x4*)((const f16*)a.x + (size_t)m * a.ldx + 8 * k8);
       }
     }
   };
@@ -460,7 +410,7 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
     w0 = *(const float4*)(a.norm_w + 8 * k8);
     w1 = *(const float4*)(a.norm_w + 8 * k8 + 4);
   }
-  if constexpr (!CH) load_x();
+  load_x();
   // Epilogue input, one word per thread, loaded unconditionally (a branch here would make
   // the compiler wait at the join): a residual element of our tiles, this step's position
   // of row tid, or a dummy word of x.
@@ -471,14 +421,13 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   {
     const int idx = tid < n_res ? tid : 0;
     const int tl = idx / (a.M * 16), rem = idx - tl * a.M * 16, m = rem >> 4, n = rem & 15;
-    pre_p = kind == TI_EPI_RESID_F32 ? p_pre + (size_t)m * ldo + (t0 + tl * tstr) * 16 + n
+    pre_p = kind == TI_EPI_RESID_F32 ? p_pre + (size_t)m * ldo + (t0 + tl) * 16 + n
             : kind == TI_EPI_QKV_ROPE_KV ? p_pre + (tid < a.M ? tid : 0) : p_pre;
   }
-  float pre = 0.0f;
-  if constexpr (!CH) pre = *pre_p;
+  const float pre = *pre_p;
   // RESID with fold_x: the fold weight of the same output (one row), consumed by the epilogue
   // (its pointer comes from the kernarg struct: loaded after the ring is issued, below)
-  const bool fold = !CH && (XM == XM_F16 || XM == XM_ATTN) && kind == TI_EPI_RESID_F32 && a.epi.fold_x != nullptr;
+  const bool fold = (XM == XM_F16 || XM == XM_ATTN) && kind == TI_EPI_RESID_F32 && a.epi.fold_x != nullptr;
   float fw_pre = 0.0f;
   // XM_F16F: this lane's share of the producer's partial sums of squares (up to 256 of them),
   // clamped loads; masked and summed after the stream
@@ -493,10 +442,10 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   // items past the end re-load the last item (no branch around loads); coordinates advance
   // by counters (no integer division in the stream).
   const u32x4* tb = a.tiles + (size_t)t0 * KT * (kWave * C) + lane;
-  const size_t last_off = total > 0 ? ((size_t)(ntl - 1) * tstr * KT + wave + kGemvWaves * (KW - 1)) * (kWave * C) : 0;
+  const size_t last_off = total > 0 ? ((size_t)(ntl - 1) * KT + wave + kGemvWaves * (KW - 1)) * (kWave * C) : 0;
   int rt = 0, rk = 0, rj = 0;                      // refill cursor: tile, k index, item
   auto refill_off = [&]() -> size_t {
-    const size_t o = rj < total ? ((size_t)rt * tstr * KT + wave + kGemvWaves * rk) * (kWave * C) : last_off;
+    const size_t o = rj < total ? ((size_t)rt * KT + wave + kGemvWaves * rk) * (kWave * C) : last_off;
     ++rj;
     if (++rk == KW) { rk = 0; ++rt; }
     return o;
@@ -505,10 +454,7 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   // limited number of outstanding loads, so a wave issuing all R slots blocks in issue for
   // microseconds, and the barrier (hence the first MFMA) would wait for the slowest wave's
   // whole burst.  The rest of the ring is issued right after the barrier.
-#ifndef TI_CHAIN_R0
-#define TI_CHAIN_R0 2   // chained: ring slots issued before the wait (x loads queue behind them)
-#endif
-  constexpr int R0 = CH && !STR ? (TI_CHAIN_R0 < R ? TI_CHAIN_R0 : R) : (R >= 8 ? 4 : R);
+  constexpr int R0 = R >= 8 ? 4 : R;
   u32x4 ring[R][C];
 #if TI_GEMV_RING_DELAY > 0   // A/B knob: hold the ring back (x 64 clocks) behind the small loads
   __builtin_amdgcn_s_sleep(TI_GEMV_RING_DELAY);
@@ -519,14 +465,9 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
 #pragma unroll
     for (int c = 0; c < C; ++c) ring[s][c] = ld_w(tb + o + c * kWave);
   }
-  if constexpr (!CH && (XM == XM_F16 || XM == XM_ATTN)) {   // fold weight (consumed by the epilogue)
+  if constexpr (XM == XM_F16 || XM == XM_ATTN) {   // fold weight (consumed by the epilogue)
     const float* fw_p = fold ? a.epi.fold_w + (size_t)t0 * 16 + (tid < n_res ? tid : 0) : pre_p;
     fw_pre = *fw_p;
-  }
-  if constexpr (CH) {
-    chain_wait(a.chain);
-    load_x();
-    pre = ld_sc1_f32(pre_p);
   }
 
   GEMV_TS(1);
@@ -590,16 +531,15 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   }
   // rare shapes: what the register prefetch did not cover (these loads wait behind the ring)
   if constexpr (BITS != 16) {
-    for (int i = tid + kGemvThreads; i < n_sc; i += kGemvThreads) ((u32x4*)sl)[i] = sg[sc_off(i)];
+    for (int i = tid + kGemvThreads; i < n_sc; i += kGemvThreads) ((u32x4*)sl)[i] = sg[i];
   }
   if constexpr (AFF) {   // the minimums follow all N/16 tiles' scales in the same buffer
     const u32x4* mg = (const u32x4*)(a.scales + (size_t)NT * KT * 64 + (size_t)t0 * KT * 64);
     for (int i = tid; i < n_sc; i += kGemvThreads) ((u32x4*)ml)[i] = mg[i];
   }
   if constexpr (XM == XM_F16 || XM == XM_F16F) {
-    if (nx16 > XPF * kGemvThreads) stage_x_generic<XM, CH>(a, xl, red, XPF * kGemvThreads);
+    if (nx16 > XPF * kGemvThreads) stage_x_generic<XM>(a, xl, red, XPF * kGemvThreads);
   } else if constexpr (XM != XM_NORM1 && XM != XM_ATTN) {
-    static_assert(!CH, "chained launches stage x in registers (XM_F16 / XM_NORM1)");
     stage_x_generic<XM>(a, xl, red, 0);
   }
   if (a.epi.kind == TI_EPI_QKV_ROPE_KV && tid < a.M) ((int*)(es + a.M * a.epi.head_dim))[tid] = __builtin_bit_cast(int, pre);
@@ -768,9 +708,7 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
   // inputs past the one-per-thread prefetch (ntl * M * 16 or M * head_dim > 512): loaded now
   for (int i = tid + kGemvThreads; i < n_res; i += kGemvThreads) {
     const int tl = i / (a.M * 16), rem = i - tl * a.M * 16, m = rem >> 4, n = rem & 15;
-    const float* pp = p_pre + (size_t)m * ldo + (t0 + tl * tstr) * 16 + n;
-    if constexpr (CH) es[i] = ld_sc1_f32(pp);
-    else es[i] = *pp;
+    es[i] = p_pre[(size_t)m * ldo + (t0 + tl) * 16 + n];
     if (fold) es[n_res + i] = a.epi.fold_w[(size_t)t0 * 16 + i];
   }
   // XM_F16F: rms of the row from the producer's partials, the same fixed-order sum in every
@@ -803,7 +741,7 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
       for (int w = 1; w < kGemvWaves; ++w) v += sp[w * kWave];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (i < a.M) epilogue<CH>(a, t0 + tl * tstr, tl, n, i, XM == XM_F16F ? v[i] / rms : v[i], es, best[i], ok, fw_l, ssacc);
+        if (i < a.M) epilogue(a, t0 + tl, tl, n, i, XM == XM_F16F ? v[i] / rms : v[i], es, best[i], ok, fw_l, ssacc);
     }
   } else {
     const int i4 = wave & 3;
@@ -812,7 +750,7 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
       float v = 0.0f;
 #pragma unroll
       for (int w = 0; w < kGemvWaves; ++w) v += sp[w * kWave * 4];
-      epilogue<CH>(a, t0 + tl * tstr, tl, lane, i4, v, es, best[0], true, fw_l, ssacc);
+      epilogue(a, t0 + tl, tl, lane, i4, v, es, best[0], true, fw_l, ssacc);
     }
   }
   if (a.epi.kind == TI_EPI_LOGITS_ARGMAX) {
@@ -836,10 +774,7 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
     lds_barrier();
     if (tid < a.M && best_l[tid])
       atomicMax(a.epi.argmax + (size_t)tid * TI_ARGMAX_SLOTS + (bid & (TI_ARGMAX_SLOTS - 1)), best_l[tid]);
-    if (a.epi.step_ctr && bid == 0 && tid == 0) {
-      if constexpr (CH) __hip_atomic_fetch_add(a.epi.step_ctr, a.epi.advance, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else *a.epi.step_ctr += a.epi.advance;
-    }
+    if (a.epi.step_ctr && bid == 0 && tid == 0) *a.epi.step_ctr += a.epi.advance;
   }
   if (fold) {   // this workgroup's sum of h^2, waves in a fixed order (best_l: unused by RESID)
     float* red2 = (float*)best_l;
@@ -853,64 +788,8 @@ __device__ __forceinline__ void gemv_body(const u32x4* p_tiles, const uint16_t* 
       a.epi.fold_ss[bid] = t;
     }
   }
-  if constexpr (CH) chain_signal(a.chain, bid);
   GEMV_TS(4);
 }
-
-template <int BITS, int XM, bool CH = false, bool G32 = false, bool AFF = false>
-__global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
-                                                                   const void* p_x, const float* p_aux, int p_mgk,
-                                                                   int p_N, int p_kx, int p_ldo, const float* p_pre,
-                                                                   const GemvArgs a_in) {
-  gemv_body<BITS, XM, CH, false, G32, AFF>(p_tiles, p_scales, p_x, p_aux, p_mgk, p_N, p_kx, p_ldo, p_pre, a_in, blockIdx.x, 0,
-                                           0, 1);
-}
-
-// ============================================================ QKV + attention, one launch
-// ti_qkv_attn_fused (one stream, int4, kv_heads == heads): workgroup (head h, split s) of the
-// heads x S grid (S = HD / 16) first computes tile s of head h in each of the q, k and v
-// projections (tiles h*S + s + {0, 1, 2} * q_dim/16 of the folded-input QKV GEMV, RoPE + KV
-// append epilogue stored write-through), so the head's S workgroups together produce its q
-// row and its K/V row at pos; it then signals the head's counter, waits for the head's other
-// workgroups (chain_wait on the S shards) and runs split s of that head's attention in
-// partials mode (the O projection merges, TI_X_ATTN_SPLITS).  The launch boundary between
-// the QKV GEMV and the attention becomes a hand-off between the S workgroups of one head.
-// Counters: per head 8 shards + one pass count; the S-th workgroup past the wait re-arms them,
-// so they are zero between launches (zeroed once by the caller).
-#ifndef TI_QA_RING
-#define TI_QA_RING 4   // K/V slots per wave, issued before the hand-off wait
-#endif
-template <int HD>
-__global__ __launch_bounds__(kGemvThreads, 1) void qkv_attn_kernel(const u32x4* p_tiles, const uint16_t* p_scales,
-                                                                    const void* p_x, const float* p_aux, int p_mgk,
-                                                                    int p_N, int p_kx, int p_ldo, const float* p_pre,
-                                                                    const GemvArgs ga, const AttnArgs aa,
-                                                                    uint32_t* ctr) {
-  constexpr int S = HD / 16;
-  static_assert(S <= TI_CHAIN_SHARDS, "one counter shard per split");
-  const unsigned h = blockIdx.x / S, s = blockIdx.x - h * S;
-  uint32_t* hc = ctr + h * 16;
-  {
-    GemvArgs g = ga;
-    g.chain.wait_ctr = nullptr;
-    g.chain.signal_ctr = hc;
-    gemv_body<4, XM_F16F, true, true>(p_tiles, p_scales, p_x, p_aux, p_mgk, p_N, p_kx, p_ldo, p_pre, g, s, h * S + s, 3,
-                                      p_N / 48);
-  }
-  AttnArgs at = aa;
-  at.chain.wait_ctr = hc;
-  at.chain.signal_ctr = nullptr;
-  at.chain.wait_target = S;
-  attn_split_body<HD, 1, TI_QA_RING, false, true, true>(at, s, h, 0, blockIdx.x);
-  if (threadIdx.x == 0) {
-    const uint32_t n = __hip_atomic_fetch_add(hc + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (n == S - 1) {
-#pragma unroll
-      for (int i = 0; i <= 8; ++i) st_sc1_u32(hc + i, 0u);
-    }
-  }
-}
-
 
 // ================================================================= batched rows
 // gemv_mb_kernel<MB, NTL>: int4 weights x fp16 activations for M <= 16*MB rows (MB <= 2):
@@ -2150,7 +2029,7 @@ __host__ inline int gemv_xmode(int x_kind, int M, int K) {
 }
 
 template <int BITS, bool G32 = false, bool AFF = false>
-static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid, const ti_chain* chain) {
+static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid) {
   const float* pre = a.epi.kind == TI_EPI_RESID_F32 ? (const float*)a.epi.out
                      : a.epi.kind == TI_EPI_QKV_ROPE_KV ? (const float*)a.epi.pos : (const float*)a.x;
   const int xm = gemv_xmode(a.x_kind, a.M, a.K);
@@ -2159,25 +2038,13 @@ static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid, cons
   const int mgk = a.M | (grid << 6) | (a.epi.kind << 18) | (xm == XM_ATTN ? (a.epi.head_dim / 64) << 21 : 0);
   const int kx = a.K | ((xm == XM_F16F || xm == XM_ATTN ? a.epi.n_ss : a.ldx) << 16);
   const int ldo = a.epi.ldo;
-  if (chain) {   // chained: x staged in registers only (checked by the caller)
-    const bool ao = chain->any_order != 0;
-    hipError_t err;
-    if (xm == XM_F16)
-      err = ti_launch_ext(gemv_wq_kernel<BITS, XM_F16, true>, dim3(grid), dim3(kGemvThreads), lds, s, ao, a.tiles, a.scales,
-                          a.x, aux, mgk, a.N, kx, ldo, pre, a);
-    else
-      err = ti_launch_ext(gemv_wq_kernel<BITS, XM_NORM1, true>, dim3(grid), dim3(kGemvThreads), lds, s, ao, a.tiles,
-                          a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a);
-    TI_HIP_CHECK(err, "hipExtLaunchKernel(gemv_wq_kernel chained)");
-    return TI_OK;
-  }
   switch (xm) {
-    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_ATTN: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_ATTN, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_F16F: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16F, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM, false, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_ATTN: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_ATTN, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F16F: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16F, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
   }
   TI_LAUNCH_CHECK("gemv_wq_kernel");
   return TI_OK;
@@ -2437,9 +2304,6 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<8, XM_NORM1>, (const void*)gemv_wq_kernel<8, XM_NORM>,
       (const void*)gemv_wq_kernel<16, XM_F16>, (const void*)gemv_wq_kernel<16, XM_F32>,
       (const void*)gemv_wq_kernel<16, XM_NORM1>, (const void*)gemv_wq_kernel<16, XM_NORM>,
-      (const void*)gemv_wq_kernel<4, XM_F16, true>, (const void*)gemv_wq_kernel<4, XM_NORM1, true>,
-      (const void*)gemv_wq_kernel<8, XM_F16, true>, (const void*)gemv_wq_kernel<8, XM_NORM1, true>,
-      (const void*)gemv_wq_kernel<16, XM_F16, true>, (const void*)gemv_wq_kernel<16, XM_NORM1, true>,
       (const void*)gemv_wq_kernel<4, XM_F16F>, (const void*)gemv_wq_kernel<8, XM_F16F>,
       (const void*)gemv_wq_kernel<16, XM_F16F>, (const void*)gemv_wq_kernel<4, XM_ATTN>,
       (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS, TI_ROWS_FNS,
@@ -2558,7 +2422,7 @@ extern "C" int ti_rmsnorm_f16_packed(const float* x, int ldx, const float* w, fl
 }
 
 static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const void* x, int x_kind, int ldx,
-                     const float* norm_w, float eps, int M, int N, int K, const ti_epilogue* epi, ti_chain* chain,
+                     const float* norm_w, float eps, int M, int N, int K, const ti_epilogue* epi,
                      ti_stream_t stream) {
   using namespace ti;
   if (!tiles || !x || !epi || !epi->out) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: null pointer");
@@ -2572,13 +2436,13 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   const bool g32_tile = g32 && !aff && bits == 4 && x_kind == TI_X_F16 && M >= tile_rows() && !epi->out_packed;
   // group-32 int4 fp16 rows 17..64: the batched-rows kernel (TI_GEMM_G32_ROWS=0: fused pieces, A/B knob)
   const bool g32_rowsk = g32 && !aff && bits == 4 && x_kind == TI_X_F16 && M > 16 && M < tile_rows() &&
-                         !epi->out_packed && !chain && g32_rows_on();
+                         !epi->out_packed && g32_rows_on();
   int g32_rows = 16;   // rows per fused launch (its LDS image holds the x rows)
   while (g32 && g32_rows > 1 && !fused_fits(g32_rows, N, K, true, aff)) --g32_rows;
-  if (g32 && (chain || x_kind == TI_X_F16_PACKED ||
+  if (g32 && (x_kind == TI_X_F16_PACKED ||
               (!g32_tile && !g32_rowsk && !fused_fits(std::min(M, g32_rows), N, K, true, aff))))
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: group-32 weights: fused kernel rows (M=%d N=%d K=%d) "
-                        "or int4 fp16 rows >= %d; no chain, no packed rows", M, N, K, tile_rows());
+                        "or int4 fp16 rows >= %d; no packed rows", M, N, K, tile_rows());
   if (bits != 16 && !scales) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: scales required for bits %d", bits);
   if (M < 1 || M > TI_GEMM_MAX_ROWS)
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: M must be in [1,%d] (got %d)", TI_GEMM_MAX_ROWS, M);
@@ -2586,17 +2450,17 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: K %% 128 and N %% 16 must be 0 (K=%d N=%d)", K, N);
   if (x_kind < TI_X_F16 || x_kind > TI_X_F16_PACKED)
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: bad x_kind %d", x_kind);
-  if (x_kind == TI_X_F16_PACKED && (bits != 4 || chain))
+  if (x_kind == TI_X_F16_PACKED && bits != 4)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: TI_X_F16_PACKED needs bits 4 (batched-rows kernel)");
   if (x_kind == TI_X_ATTN_SPLITS &&
-      (M != 1 || chain || !epi->ss_in || epi->n_ss < 1 || epi->n_ss > TI_ATTN_MAX_PART_SPLITS ||
+      (M != 1 || !epi->ss_in || epi->n_ss < 1 || epi->n_ss > TI_ATTN_MAX_PART_SPLITS ||
        (epi->head_dim != 64 && epi->head_dim != 128) || K % epi->head_dim || K > 4096))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: TI_X_ATTN_SPLITS needs M == 1, ss_in, 1 <= n_ss <= %d, head_dim "
                         "64/128 and K <= 4096", TI_ATTN_MAX_PART_SPLITS);
-  if (x_kind == TI_X_F16_FOLDED && (M != 1 || chain || !epi->ss_in || epi->n_ss < 1 || epi->n_ss > 256))
+  if (x_kind == TI_X_F16_FOLDED && (M != 1 || !epi->ss_in || epi->n_ss < 1 || epi->n_ss > 256))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: TI_X_F16_FOLDED needs M == 1, ss_in and 1 <= n_ss <= 256");
   if (epi->kind == TI_EPI_RESID_F32 && epi->fold_x &&
-      (M != 1 || chain || !epi->fold_w || !epi->fold_ss || (x_kind != TI_X_F16 && x_kind != TI_X_ATTN_SPLITS)))
+      (M != 1 || !epi->fold_w || !epi->fold_ss || (x_kind != TI_X_F16 && x_kind != TI_X_ATTN_SPLITS)))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: fold_x needs M == 1, fp16 x, fold_w and fold_ss");
   if (K > 0xffff || ldx > 0xffff)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: K %d / ldx %d above 65535", K, ldx);
@@ -2637,7 +2501,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
       if (m0 + mm < M) ep.step_ctr = nullptr;
       const int rc = gemm_impl(tiles, scales, bits | TI_BITS_G32 | (aff ? TI_BITS_AFF : 0),
                                static_cast<const char*>(x) + (size_t)m0 * ldx * x_elem,
-                               x_kind, ldx, norm_w, eps, mm, N, K, &ep, nullptr, stream);
+                               x_kind, ldx, norm_w, eps, mm, N, K, &ep, stream);
       if (rc != TI_OK) return rc;
     }
     return TI_OK;
@@ -2682,14 +2546,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: LDS image %d B too large (M=%d N=%d K=%d)", lds, M, N, K);
   if (!batched && grid > 0xfff)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: %d workgroups (N=%d) above 4095", grid, N);
-  if (chain) {
-    const int xm = gemv_xmode(x_kind, M, K);
-    if (M != 1 || batched || (xm != XM_F16 && xm != XM_NORM1))
-      return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16_chained: M=%d K=%d x_kind=%d is not chainable", M, K, x_kind);
-    if (!chain->abort_flag || ((uintptr_t)epi->out & 3) || ((uintptr_t)epi->k_cache & 3) || ((uintptr_t)epi->v_cache & 3))
-      return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16_chained: abort_flag required, outputs 4-byte aligned");
-  }
-  if (lds > 64 * 1024 || chain) {   // no-op once this device is prepared
+  if (lds > 64 * 1024) {   // no-op once this device is prepared
     const int rc = ti_gemm_prepare();
     if (rc != TI_OK) return rc;
   }
@@ -2705,8 +2562,6 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   a.N = N;
   a.K = K;
   a.epi = *epi;
-  a.chain = chain_dev(chain);
-  if (chain) chain->signaled = (uint32_t)grid;
   hipStream_t s = (hipStream_t)stream;
   if (tile) {
     const void* f = tile_fn(tpw, g32, wmr, xbuf, trb);
@@ -2717,11 +2572,11 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   }
   if (rows) return launch_rows(a, rMB, rRG, ntl, grid, r_rb, lds, s, g32);
   if (batched) return launch_mb(a, M > 16 ? 2 : 1, grid, ntl, lds, s);
-  if (aff) return launch_gemv<4, true, true>(a, lds, s, grid, chain);
-  if (g32) return bits == 4 ? launch_gemv<4, true>(a, lds, s, grid, chain) : launch_gemv<8, true>(a, lds, s, grid, chain);
-  if (bits == 4) return launch_gemv<4>(a, lds, s, grid, chain);
-  if (bits == 8) return launch_gemv<8>(a, lds, s, grid, chain);
-  return launch_gemv<16>(a, lds, s, grid, chain);
+  if (aff) return launch_gemv<4, true, true>(a, lds, s, grid);
+  if (g32) return bits == 4 ? launch_gemv<4, true>(a, lds, s, grid) : launch_gemv<8, true>(a, lds, s, grid);
+  if (bits == 4) return launch_gemv<4>(a, lds, s, grid);
+  if (bits == 8) return launch_gemv<8>(a, lds, s, grid);
+  return launch_gemv<16>(a, lds, s, grid);
 }
 
 extern "C" int ti_epilogue_bytes(void) { return (int)sizeof(ti_epilogue); }
@@ -2748,88 +2603,9 @@ extern "C" int ti_gemm_grid(int M, int N, int K) {
   return ti::gemv_grid(M, N, K, query_cus());
 }
 
-extern "C" int ti_gemm_chainable(int bits, int x_kind, int M, int N, int K) {
-  using namespace ti;
-  if ((bits != 4 && bits != 8 && bits != 16) || M != 1 || N < 16 || K < 128 || (K & 127) || (N & 15)) return 0;
-  if (x_kind < TI_X_F16 || x_kind > TI_X_F32_RMSNORM || use_batched(bits, x_kind, M, N, K)) return 0;
-  const int xm = gemv_xmode(x_kind, M, K);
-  if (xm != XM_F16 && xm != XM_NORM1) return 0;
-  const int grid = gemv_grid(M, N, K, query_cus());
-  return gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid) <= 160 * 1024 ? 1 : 0;
-}
-
-extern "C" int ti_qkv_attn_fused(const void* tiles, const uint16_t* scales, const uint16_t* x, float eps, int K,
-                                 const ti_epilogue* epi, uint16_t* part_o, float* part_ml, uint32_t* counters,
-                                 uint32_t* abort_flag, ti_stream_t stream) {
-  using namespace ti;
-  if (!tiles || !scales || !x || !epi || !epi->out || !part_o || !part_ml || !counters || !abort_flag)
-    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_fused: null pointer");
-  const int hd = epi->head_dim, qd = epi->q_dim, N = qd + 2 * epi->kv_dim;
-  if (epi->kind != TI_EPI_QKV_ROPE_KV || !epi->pos || !epi->rope_cs || !epi->k_cache || !epi->v_cache ||
-      (hd != 64 && hd != 128) || epi->kv_dim != qd || qd % hd || epi->ldo < qd || epi->max_seq < 1 ||
-      epi->kv_stream_stride < (int64_t)qd * epi->max_seq)
-    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_fused: needs a QKV_ROPE_KV epilogue with kv_dim == q_dim, head_dim 64/128");
-  if (!epi->ss_in || epi->n_ss < 1 || epi->n_ss > 256)
-    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_fused: x is TI_X_F16_FOLDED: ss_in and 1 <= n_ss <= 256 required");
-  if (K < 128 || (K & 127) || K > 0xffff) return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_fused: bad K %d", K);
-  if (((uintptr_t)epi->out & 3) || ((uintptr_t)epi->k_cache & 3) || ((uintptr_t)epi->v_cache & 3))
-    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_fused: outputs must be 4-byte aligned");
-  if ((int64_t)epi->max_seq * hd * 2 >= 0x7fffffffLL)
-    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_fused: a head's cache exceeds 2 GiB");
-  const int S = hd / 16, heads = qd / hd, grid = heads * S;
-  const int lds = gemv_lds_bytes_tiles(1, K, 3);
-  if (lds > 96 * 1024 || grid > 0xfff)
-    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_fused: K %d / heads %d too large", K, heads);
-  GemvArgs a{};
-  a.tiles = (const u32x4*)tiles;
-  a.scales = scales;
-  a.x = x;
-  a.norm_w = nullptr;
-  a.eps = eps;
-  a.x_kind = TI_X_F16_FOLDED;
-  a.ldx = K;
-  a.M = 1;
-  a.N = N;
-  a.K = K;
-  a.epi = *epi;
-  a.chain = ChainDev{nullptr, nullptr, abort_flag, 0u, 0u};
-  AttnArgs t{};
-  t.q = (const float*)epi->out;
-  t.kc = epi->k_cache;
-  t.vc = epi->v_cache;
-  t.pos = epi->pos;
-  t.stride = epi->kv_stream_stride;
-  t.max_seq = epi->max_seq;
-  t.M = 1;
-  t.heads = heads;
-  t.kv_heads = heads;
-  t.splits = S;
-  t.scale = 1.0f / sqrtf((float)hd);   // tensor_engine.cpp:1288
-  t.chain = ChainDev{nullptr, nullptr, abort_flag, 0u, 0u};
-  t.part_o = part_o;
-  t.part_ml = part_ml;
-  const int mgk = 1 | (grid << 6) | (TI_EPI_QKV_ROPE_KV << 18);
-  const int kx = K | (epi->n_ss << 16);
-  hipStream_t s = (hipStream_t)stream;
-  if (hd == 128)
-    hipLaunchKernelGGL((qkv_attn_kernel<128>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, epi->ss_in,
-                       mgk, N, kx, epi->ldo, (const float*)epi->pos, a, t, counters);
-  else
-    hipLaunchKernelGGL((qkv_attn_kernel<64>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, epi->ss_in,
-                       mgk, N, kx, epi->ldo, (const float*)epi->pos, a, t, counters);
-  TI_LAUNCH_CHECK("qkv_attn_kernel");
-  return TI_OK;
-}
-
 extern "C" int ti_gemm_wq_a16(const void* tiles, const uint16_t* scales, int bits, const void* x,
                               int x_kind, int ldx, const float* norm_w, float eps, int M, int N, int K,
                               const ti_epilogue* epi, ti_stream_t stream) {
-  return gemm_impl(tiles, scales, bits, x, x_kind, ldx, norm_w, eps, M, N, K, epi, nullptr, stream);
+  return gemm_impl(tiles, scales, bits, x, x_kind, ldx, norm_w, eps, M, N, K, epi, stream);
 }
 
-extern "C" int ti_gemm_wq_a16_chained(const void* tiles, const uint16_t* scales, int bits, const void* x,
-                                      int x_kind, int ldx, const float* norm_w, float eps, int M, int N, int K,
-                                      const ti_epilogue* epi, ti_chain* chain, ti_stream_t stream) {
-  if (!chain) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16_chained: null chain");
-  return gemm_impl(tiles, scales, bits, x, x_kind, ldx, norm_w, eps, M, N, K, epi, chain, stream);
-}

@@ -10,18 +10,15 @@ namespace ti {
 // One block per stream m.  The decode loop runs entirely on the device: the token of
 // step s is the prompt token while s < n_in[m], else the previous step's greedy argmax
 // (the key packs (value, 0xFFFFFFFF - index), so the max is the lowest-index maximum).
-// CH: one launch of a chain (ti_chain): waits for the previous step's last launch, reads
-// the step counter and argmax keys with sc1 loads and stores h / pos / tokens write-through.
-template <bool CH>
-__global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a, const ChainDev chain) {
+__global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a) {
   __shared__ int s_tok;
   const int m = blockIdx.x, tid = threadIdx.x;
-  // Unchained with hidden % 8 == 0 (<= 8192): the embedding row moves in 16-byte pieces, all
+  // With hidden % 8 == 0 (<= 8192): the embedding row moves in 16-byte pieces, all
   // of a thread's loads in flight together; the fold weights (independent of the token) are
   // loaded before the token is decided.
   constexpr int kPT = 4;   // pieces of 8 per thread
   const int H8 = a.hidden >> 3;
-  const bool vec = !CH && (a.hidden & 7) == 0 && H8 <= 256 * kPT && a.placeholder_first < 0;
+  const bool vec = (a.hidden & 7) == 0 && H8 <= 256 * kPT && a.placeholder_first < 0;
   float4 fw[kPT][2];
   if (vec && a.fold_x) {
 #pragma unroll
@@ -31,13 +28,12 @@ __global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a, c
       fw[p][1] = *(const float4*)(a.fold_w + 8 * i8 + 4);
     }
   }
-  if constexpr (CH) chain_wait(chain);
-  const int s = CH ? (int)ld_sc1_u32(a.step_ctr) : *a.step_ctr;
+  const int s = *a.step_ctr;
   const int nin = a.n_in ? a.n_in[m] : 0;
   unsigned long long* am = a.argmax + (size_t)m * TI_ARGMAX_SLOTS;
   unsigned long long key = 0ull;
   if (tid < 64) {   // row m's key = max over its slots (wave 0)
-    key = tid < TI_ARGMAX_SLOTS ? (CH ? ld_sc1_u64(am + tid) : am[tid]) : 0ull;
+    key = tid < TI_ARGMAX_SLOTS ? am[tid] : 0ull;
 #pragma unroll
     for (int o = 1; o < TI_ARGMAX_SLOTS; o <<= 1) {
       const unsigned long long other = __shfl_xor(key, o, 64);
@@ -51,30 +47,22 @@ __global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a, c
     } else {
       tok = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
       if (a.out_tokens && s - nin < a.out_stride) {
-        int32_t* o = a.out_tokens + (size_t)m * a.out_stride + (s - nin);
-        if constexpr (CH) st_sc1_u32(o, (uint32_t)tok);
-        else *o = tok;
+        a.out_tokens[(size_t)m * a.out_stride + (s - nin)] = tok;
       }
     }
     if (tok < 0 || tok >= a.vocab) tok = 0;     // never index outside the table
     s_tok = tok;
-    if constexpr (CH) st_sc1_u32(a.pos + m, (uint32_t)(a.base_pos[m] + s));
-    else a.pos[m] = a.base_pos[m] + s;
+    a.pos[m] = a.base_pos[m] + s;
   }
   __syncthreads();   // every slot read before any is cleared
-  if (tid < TI_ARGMAX_SLOTS) {
-    if constexpr (CH) st_sc1_u64(am + tid, 0ull);
-    else am[tid] = 0ull;
-  }
+  if (tid < TI_ARGMAX_SLOTS) am[tid] = 0ull;
   float* h = a.h + (size_t)m * a.hidden;
   if (a.placeholder_first >= 0) {
     // forward_pass / forward_pass_incremental placeholder rows (inference_engine.cpp:1444-1448,
     // 1509-1512): 0.1f * (flat_index % 100).
     const size_t off = s == 0 ? (size_t)a.placeholder_first : 0;
     for (int i = tid; i < a.hidden; i += 256) {
-      const float v = 0.1f * (float)((off + (size_t)i) % 100);
-      if constexpr (CH) st_sc1_f32(h + i, v);
-      else h[i] = v;
+      h[i] = 0.1f * (float)((off + (size_t)i) % 100);
     }
   } else if (vec) {
     const uint16_t* e = a.emb + (size_t)s_tok * a.hidden;
@@ -114,17 +102,13 @@ __global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a, c
     float ss = 0.0f;
     for (int i = tid; i < a.hidden; i += 256) {
       const float v = h2f(e[i]);
-      if constexpr (CH) {
-        st_sc1_f32(h + i, v);
-      } else {
-        h[i] = v;
-        if (a.fold_x) {   // the first projection's TI_X_F16_FOLDED input (ti_hip.h)
-          a.fold_x[(size_t)m * a.hidden + i] = f2h(v * a.fold_w[i]);
-          ss = fmaf(v, v, ss);
-        }
+      h[i] = v;
+      if (a.fold_x) {   // the first projection's TI_X_F16_FOLDED input (ti_hip.h)
+        a.fold_x[(size_t)m * a.hidden + i] = f2h(v * a.fold_w[i]);
+        ss = fmaf(v, v, ss);
       }
     }
-    if (!CH && a.fold_x) {
+    if (a.fold_x) {
       __shared__ float s_red[4];
       ss = group_sum<64>(ss);
       if ((tid & 63) == 0) s_red[tid >> 6] = ss;
@@ -132,7 +116,6 @@ __global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a, c
       if (tid == 0) a.fold_ss[m] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
     }
   }
-  if constexpr (CH) chain_signal(chain, blockIdx.x);
 }
 
 // ---------------------------------------------------------- synthetic weights
@@ -281,25 +264,11 @@ extern "C" int ti_step_begin(const ti_step_args* a, ti_stream_t stream) {
   if (a->n_in && !a->in_tokens) return ti_set_error(TI_ERR_ARG, "ti_step_begin: in_tokens required");
   if (a->fold_x && (!a->fold_w || !a->fold_ss || a->placeholder_first >= 0))
     return ti_set_error(TI_ERR_ARG, "ti_step_begin: fold_x needs fold_w, fold_ss and the embedding gather");
-  hipLaunchKernelGGL(step_begin_kernel<false>, dim3(a->M), dim3(256), 0, (hipStream_t)stream, *a, ChainDev{});
+  hipLaunchKernelGGL(step_begin_kernel, dim3(a->M), dim3(256), 0, (hipStream_t)stream, *a);
   TI_LAUNCH_CHECK("step_begin_kernel");
   return TI_OK;
 }
 
-extern "C" int ti_step_begin_chained(const ti_step_args* a, ti_chain* chain, ti_stream_t stream) {
-  using namespace ti;
-  if (!a || !chain || !chain->abort_flag || !a->h || !a->argmax || !a->pos || !a->base_pos || !a->step_ctr || a->M < 1 ||
-      a->hidden < 1)
-    return ti_set_error(TI_ERR_ARG, "ti_step_begin_chained: bad arguments");
-  if (a->placeholder_first < 0 && !a->emb) return ti_set_error(TI_ERR_ARG, "ti_step_begin_chained: emb required");
-  if (a->n_in && !a->in_tokens) return ti_set_error(TI_ERR_ARG, "ti_step_begin_chained: in_tokens required");
-  if (a->fold_x) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_step_begin_chained: fold_x");
-  chain->signaled = (uint32_t)a->M;
-  TI_HIP_CHECK(ti_launch_ext(step_begin_kernel<true>, dim3(a->M), dim3(256), 0, (hipStream_t)stream,
-                             chain->any_order != 0, *a, chain_dev(chain)),
-               "hipExtLaunchKernel(step_begin_kernel chained)");
-  return TI_OK;
-}
 
 extern "C" int ti_wsynth_device(uint64_t seed, uint32_t tensor_id, int K, int N_src, int N_total, int bits,
                                 int row_map, int row_offset, void* tiles, uint16_t* scales, ti_stream_t stream) {

@@ -501,45 +501,77 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       }
       acc[0] = acc[1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
     };
-    for (int fi = 0; fi < nf; ++fi) {
-      const uint32_t fill = fbase + fi;
-      wait_full(fill);
-      const char* slot = smem + (fill % (uint32_t)a.n_slots) * kSlotBytes + lane * 16;
-      for (int j = 0; j < kFill; ++j) {
-        if (fi * kFill + j >= np) break;
-        if ((kt & 3) == c) {
-          if (tl != cur) {
-            flush();
-            cur = tl;
-          }
-          const u32x4 wv[1] = {*(const u32x4*)(slot + j * kPiece)};
-          f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) {
-            const f16x8 bf = dequant_step<4>(wv, s4, magic);
-            const f16x8 af = *(const f16x8*)(xrow + kt * 128 + s4 * 8);
-            t = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, t, 0, 0, 0);
-          }
-          t -= corr[kt];
-          const float sc = h2f(sl[(tl * KT + kt) * 16 + r]);
-          if ((kt >> 2) & 1) {   // virtual wave c + 4 (static register indices: no scratch)
-            acc[1][0] = fmaf(sc, t[0], acc[1][0]);
-            acc[1][1] = fmaf(sc, t[1], acc[1][1]);
-            acc[1][2] = fmaf(sc, t[2], acc[1][2]);
-            acc[1][3] = fmaf(sc, t[3], acc[1][3]);
-          } else {
-            acc[0][0] = fmaf(sc, t[0], acc[0][0]);
-            acc[0][1] = fmaf(sc, t[1], acc[0][1]);
-            acc[0][2] = fmaf(sc, t[2], acc[0][2]);
-            acc[0][3] = fmaf(sc, t[3], acc[0][3]);
-          }
-        }
-        if (++kt == KT) {
-          kt = 0;
-          ++tl;
-        }
+    // one item: 4 MFMAs on (x, dequantized W), the group's offset correction, the group scale
+    auto item = [&](const u32x4 w, int it, int ik) {
+      if (it != cur) {
+        flush();
+        cur = it;
       }
-      release(fill);
+      const u32x4 wv[1] = {w};
+      f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const f16x8 bf = dequant_step<4>(wv, s4, magic);
+        const f16x8 af = *(const f16x8*)(xrow + ik * 128 + s4 * 8);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, t, 0, 0, 0);
+      }
+      t -= corr[ik];
+      const float sc = h2f(sl[(it * KT + ik) * 16 + r]);
+      if ((ik >> 2) & 1) {   // virtual wave c + 4 (static register indices: no scratch)
+        acc[1][0] = fmaf(sc, t[0], acc[1][0]);
+        acc[1][1] = fmaf(sc, t[1], acc[1][1]);
+        acc[1][2] = fmaf(sc, t[2], acc[1][2]);
+        acc[1][3] = fmaf(sc, t[3], acc[1][3]);
+      } else {
+        acc[0][0] = fmaf(sc, t[0], acc[0][0]);
+        acc[0][1] = fmaf(sc, t[1], acc[0][1]);
+        acc[0][2] = fmaf(sc, t[2], acc[0][2]);
+        acc[0][3] = fmaf(sc, t[3], acc[0][3]);
+      }
+    };
+    if ((KT & 3) == 0 || ntl == 1) {
+      // k-tile == piece index (mod 4): this consumer's items sit at pieces c, c + 4, c + 8, c + 12 of
+      // every fill.  All four are read, the slot is released, then the math runs.
+      tl = 0;
+      kt = c;   // piece c of fill 0
+      for (int fi = 0; fi < nf; ++fi) {
+        const uint32_t fill = fbase + fi;
+        wait_full(fill);
+        const char* slot = smem + (fill % (uint32_t)a.n_slots) * kSlotBytes + lane * 16;
+        u32x4 w[4];
+        int itl[4], ikt[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          itl[u] = tl;
+          ikt[u] = kt;
+          w[u] = fi * kFill + c + 4 * u < np ? *(const u32x4*)(slot + (c + 4 * u) * kPiece) : (u32x4){0u, 0u, 0u, 0u};
+          kt += 4;
+          if (kt >= KT && ntl > 1) {
+            kt -= KT;
+            ++tl;
+          }
+        }
+        release(fill);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (fi * kFill + c + 4 * u < np) item(w[u], itl[u], ikt[u]);
+      }
+    } else {
+      // general shapes (K % 512 != 0 with several tiles): piece by piece
+      for (int fi = 0; fi < nf; ++fi) {
+        const uint32_t fill = fbase + fi;
+        wait_full(fill);
+        const char* slot = smem + (fill % (uint32_t)a.n_slots) * kSlotBytes + lane * 16;
+        for (int j = 0; j < kFill; ++j) {
+          if (fi * kFill + j >= np) break;
+          if ((kt & 3) == c) item(*(const u32x4*)(slot + j * kPiece), tl, kt);
+          if (++kt == KT) {
+            kt = 0;
+            ++tl;
+          }
+        }
+        release(fill);
+      }
     }
     if (np > 0) flush();
     fbase += nf;
@@ -647,14 +679,22 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         const uint32_t fill = fbase + fi;
         wait_full(fill);
         const char* slot = smem + (fill % (uint32_t)a.n_slots) * kSlotBytes + lane * 16;
+        u32x4 kr[2], vr[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int su = c + 4 * u, si = fi * 8 + su;
+          kr[u] = si < g.nslot ? *(const u32x4*)(slot + (2 * su) * kPiece) : (u32x4){0u, 0u, 0u, 0u};
+          vr[u] = si < g.nslot ? *(const u32x4*)(slot + (2 * su + 1) * kPiece) : (u32x4){0u, 0u, 0u, 0u};
+        }
+        release(fill);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int su = c + 4 * u, si = fi * 8 + su;   // slot of the split; virtual wave su
           if (si < g.nslot) {
             const int key = g.s0 + 4 * si + kg;
             const bool valid = key < g.s1;
-            u32x4 kv = *(const u32x4*)(slot + (2 * su) * kPiece);
-            u32x4 vv = valid ? *(const u32x4*)(slot + (2 * su + 1) * kPiece) : (u32x4){0u, 0u, 0u, 0u};
+            u32x4 kv = kr[u];
+            u32x4 vv = valid ? vr[u] : (u32x4){0u, 0u, 0u, 0u};
             if (valid && key == pos) {
               kv = *(const u32x4*)(kf_l + dl * 8);
               vv = *(const u32x4*)(vf_l + dl * 8);
@@ -676,7 +716,6 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
             for (int e = 0; e < 8; ++e) acc[u][e] = fmaf(pr, vf[e], acc[u][e] * alpha);
           }
         }
-        release(fill);
       }
       fbase += nf;
       // merge the lane groups of each virtual wave (attn_split_body, LPK = 16)
