@@ -178,8 +178,10 @@ struct ti_engine {
     weight_bytes += tb + sb;
     return TI_OK;
   }
-  int attn_target = 256;   // attention workgroups aimed at (env TI_ATTN_TARGET, A/B knob)
-  int gqa_part_splits = 8;   // env TI_ATTN_GQA_PART (0: off), see splits_for
+  // attention workgroups aimed at: one 8-wave workgroup per CU (128 / 256 / 512 measured 717 / 751 /
+  // 681 tok/s); GQA partials with 8 splits
+  static constexpr int attn_target = 256;
+  static constexpr int gqa_part_splits = 8;
   int splits_for(int M) const {
     if (c.attn_splits > 0) return c.attn_splits;
     // one stream of a GQA model (>= 4 q-heads per kv-head) with a small cache per kv-head
@@ -726,8 +728,6 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     for (int p = 0; p < c.max_seq; ++p) pv[p] = (float)p;
     if ((rc = ti_rope_table(pv.data(), c.max_seq, hd, c.rope_theta, cs.data()))) return fail(rc);
     if ((rc = ti_memcpy_h2d(e->rope_cs, cs.data(), cs.size() * 4, e->s))) return fail(rc);
-    if (const char* env = getenv("TI_ATTN_TARGET")) e->attn_target = std::max(1, atoi(env));
-    if (const char* env = getenv("TI_ATTN_GQA_PART")) e->gqa_part_splits = std::min(TI_ATTN_MAX_PART_SPLITS, atoi(env));
     if (const char* env = getenv("TI_ATTN_PART")) e->part_on = atoi(env) != 0;
     e->splits_max = e->splits_for(1);
     e->pf_rows = (c.bits & ~TI_BITS_G32) == 4 ? TI_GEMM_MAX_ROWS : 16;   // int4 (also group-32): the tile GEMM
@@ -744,7 +744,6 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
         (rc = e->alloc_t(&e->part_o, (size_t)c.heads * TI_ATTN_MAX_PART_SPLITS * hd)) ||
         (rc = e->alloc_t(&e->part_ml, (size_t)c.heads * TI_ATTN_MAX_PART_SPLITS * 2)))
       return fail(rc);
-    if (const char* env = getenv("TI_ATTN_PART")) e->part_on = atoi(env) != 0;
     if (const char* env = getenv("TI_FOLD")) e->fold_on = atoi(env) != 0;
     if ((c.bits & ~TI_BITS_G32) == 4) {   // batched rows and prompt chunks: split-K tile GEMM (TI_SPLITK_MB, 0 = off)
       const char* env = getenv("TI_SPLITK_MB");

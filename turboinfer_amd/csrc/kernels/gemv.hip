@@ -84,21 +84,31 @@ struct GemvArgs {
 
 __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
 
-// Workgroups per launch: one 8-wave workgroup per CU (each wave keeps 64 VGPRs of packed
-// weights in flight), never more than there are 16-row tiles.
-static int g_wg_per_cu = 0;   // TI_GEMV_WG_PER_CU (tuning knob), default 1
+// The GEMM's two remaining A/B knobs, read once per process (thread-safe static init).
+struct GemmKnobs {
+  bool splitk = true;       // TI_GEMM_SPLITK=0: no split-K for under-filled tile grids
+  bool rows_split = true;   // TI_GEMM_ROWS_SPLIT=0: all rows in one batched-rows workgroup
+};
+__host__ inline const GemmKnobs& gemm_knobs() {
+  static const GemmKnobs k = [] {
+    GemmKnobs v;
+    if (const char* e = getenv("TI_GEMM_SPLITK")) v.splitk = atoi(e) != 0;
+    if (const char* e = getenv("TI_GEMM_ROWS_SPLIT")) v.rows_split = atoi(e) != 0;
+    return v;
+  }();
+  return k;
+}
+
+// Workgroups per launch: one 8-wave workgroup per CU (a second workgroup per CU measured slower,
+// DESIGN 4.1), never more than there are 16-row tiles.
 
 __host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_wg, bool g32 = false, bool aff = false);
 
 // Tiles per workgroup are bounded by the LDS image (partial slabs and scales grow with
 // them): very wide outputs (a 128k vocabulary) get more workgroups than CUs.
 __host__ inline int gemv_grid(int M, int N, int K, int num_cus, bool g32 = false, bool aff = false) {
-  if (g_wg_per_cu <= 0) {
-    const char* s = getenv("TI_GEMV_WG_PER_CU");
-    g_wg_per_cu = s && atoi(s) > 0 ? atoi(s) : 1;
-  }
   const int NT = N >> 4;
-  const int g = g_wg_per_cu * (num_cus > 0 ? num_cus : 256);
+  const int g = num_cus > 0 ? num_cus : 256;
   int grid = NT < g ? NT : g;
   while (grid < NT && gemv_lds_bytes_tiles(M, K, (NT + grid - 1) / grid, g32, aff) > 160 * 1024) grid += grid / 8 + 1;
   return grid < NT ? grid : NT;
@@ -1876,15 +1886,6 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 }
 
 static int g_num_cus = 0;
-// TI_TILE_NARROW=0 keeps 128-column workgroups for every shape (A/B knob)
-static int g_tile_narrow = -1;
-__host__ inline bool tile_narrow_on() {
-  if (g_tile_narrow < 0) {
-    const char* e = getenv("TI_TILE_NARROW");
-    g_tile_narrow = e ? atoi(e) != 0 : 1;
-  }
-  return g_tile_narrow != 0;
-}
 
 // Tile kernel shape by a per-CU byte model: a CU streams a bounded number of bytes per
 // microsecond, a workgroup moves its activation block plus its weight tiles per
@@ -1918,26 +1919,14 @@ __host__ inline const void* tile_fn(int tpw, bool g32, int wmr, int xb, int rb =
   if (tpw == 3) return fns[base + 12 + (wmr == 1 ? 2 : 0) + (g32 ? 1 : 0)];
   return fns[base + (wmr == 1 ? 6 : 0) + (g32 ? 3 : 0) + (tpw == 1 ? 0 : tpw == 2 ? 1 : 2)];
 }
-// the deep activation ring when it fits the LDS (TI_TILE_XB=2 forces the double buffer: A/B knob)
+// the deep activation ring when it fits the LDS
 __host__ inline int tile_xb(int K, int tpw, bool g32, int wmr, int rb = 4) {
-  static int force = -1;
-  if (force < 0) {
-    const char* e = getenv("TI_TILE_XB");
-    force = e ? atoi(e) : 0;
-  }
-  if (TI_TILE_XB4 != 4 || force == 2) return 2;
+  if (TI_TILE_XB4 != 4) return 2;
   return tile_lds_bytes(K, tpw, g32, wmr, 4, rb) <= 160 * 1024 ? 4 : 2;
 }
 
-// 32-row waves on (TI_TILE_RB2=0 keeps 64-row waves at every row count: A/B knob)
-static int g_tile_rb2 = -1;
-__host__ inline bool tile_rb2_on() {
-  if (g_tile_rb2 < 0) {
-    const char* e = getenv("TI_TILE_RB2");
-    g_tile_rb2 = e ? atoi(e) != 0 : 1;
-  }
-  return g_tile_rb2 != 0 && TI_TILE_XB4 == 4;
-}
+// 32-row waves (they need the deep activation ring)
+__host__ inline bool tile_rb2_on() { return TI_TILE_XB4 == 4; }
 
 // Shapes considered: (row-waves WMR, 16-row blocks per row-wave RB, tiles per wave TPW); a
 // workgroup moves 4 RB WMR KiB of activations and WMR x (8 / WMR) TPW KiB of weights per group.
@@ -1945,36 +1934,25 @@ __host__ inline bool tile_rb2_on() {
 // would move half padding (TI_TILE_RB2=0: A/B knob).  TI_TILE_WMR1=0 keeps 128-row workgroups
 // (A/B knob).  Returns 32 * (RB == 2) + 8 * WMR + TPW.
 __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
-  static int wide = -1, wmr1 = -1, tpw3 = -1, rb2_rows = -1, rb2_tie = -1;
-  if (wide < 0) {
-    const char* r = getenv("TI_TILE_RB2_ROWS");   // A/B knobs: 32-row waves up to this many rows,
-    rb2_rows = r ? atoi(r) : 32;                   // and preferred on equal cost
-    const char* t = getenv("TI_TILE_RB2_TIE");
-    rb2_tie = t ? atoi(t) != 0 : 0;
-    const char* e = getenv("TI_TILE_WIDE");
-    wide = e ? atoi(e) != 0 : 1;
-    const char* f = getenv("TI_TILE_WMR1");
-    wmr1 = f ? atoi(f) != 0 : 1;
-    const char* g = getenv("TI_TILE_TPW3");
-    tpw3 = g ? atoi(g) != 0 : 1;
-  }
+  // 32-row waves only up to 32 rows: at 33-64 rows their second row block re-reads every weight
+  // tile (7-8 % slower on the wide outputs, profiles/r3c_tile_rb2_64rows.txt)
+  constexpr int rb2_rows = 32;
   const int NT = N >> 4;
   int best = 8 * 2 + 2;
   long best_cost = -1;
   for (int wr : {8, 4, 2}) {   // row-wave shape: 4 RB WMR (2 x 4, 1 x 4, 1 x 2)
     const int wmr = wr == 8 ? 2 : 1, rb = wr == 2 ? 2 : 4;
-    if (wmr == 1 && !wmr1) continue;
-    if (rb == 2 && (!tile_rb2_on() || M > rb2_rows || !wmr1)) continue;
+    if (rb == 2 && (!tile_rb2_on() || M > rb2_rows)) continue;
     for (int tpw : {2, 1, 4, 3}) {
       // (group-32 at TPW 4 spills to scratch: kept out, its asm-loaded weight ring must stay in VGPRs)
-      if ((tpw == 1 && !tile_narrow_on()) || (tpw == 4 && (!wide || (g32 && TI_TILE_ASM))) || (tpw == 3 && !tpw3) ||
+      if ((tpw == 4 && g32 && TI_TILE_ASM) ||
           tile_lds_bytes(K, tpw, g32, wmr, 2, rb) > 160 * 1024 || (rb == 2 && tile_xb(K, tpw, g32, wmr, rb) != 4))
         continue;
       const int cols = (8 / wmr) * tpw, bm = 16 * rb * wmr;
       // rounds as launched: ceil(column blocks / 8) x row blocks workgroups on each XCD's CUs
       const long per_xcd = (long)((NT + cols - 1) / cols + 7) / 8 * ((M + bm - 1) / bm);
       const long cost = (per_xcd + cus / 8 - 1) / (cus / 8) * (4 * rb * wmr + 8 * tpw);
-      if (best_cost < 0 || cost < best_cost || (rb == 2 && rb2_tie && cost == best_cost)) {
+      if (best_cost < 0 || cost < best_cost) {
         best = (rb == 2 ? 32 : 0) + 8 * wmr + tpw;
         best_cost = cost;
       }
@@ -1989,15 +1967,8 @@ __host__ inline int tile_shape(int M, int N, int K, bool g32, int cus) {
 // one-slice grid would leave most of the chip idle: at most a quarter of the CUs busy, each
 // slice still at least 8 groups deep, the slices filling at most one round of workgroups.
 // (17..64 decode rows stay on the batched-rows kernel: split there measured slower, 5–14 µs of
-// seam against 12–50 µs launches.)  TI_GEMM_SPLITK=0 turns splitting off (A/B knob).
-static int g_splitk = -1;
-__host__ inline bool splitk_on() {
-  if (g_splitk < 0) {
-    const char* e = getenv("TI_GEMM_SPLITK");
-    g_splitk = e ? atoi(e) != 0 : 1;
-  }
-  return g_splitk != 0;
-}
+// seam against 12–50 µs launches.)  TI_GEMM_SPLITK=0 turns splitting off (A/B knob, DESIGN 9).
+__host__ inline bool splitk_on() { return gemm_knobs().splitk; }
 __host__ inline size_t splitk_slab_bytes(int n_ks, int n_cb, int n_rb, int tpw) {
   return (size_t)n_ks * n_cb * n_rb * kGemvWaves * tpw * 4 * kWave * 16;
 }
@@ -2096,15 +2067,8 @@ __host__ inline int mb_grid(int MB, int N, int K, int num_cus, int* ntl_out) {
   return grid;
 }
 
-// One 16-row block: the register-fragment kernel unless TI_GEMM_MB_LDS=1 (A/B knob).
-static int g_mb_lds = -1;
-static bool mb_use_lds(int MB) {
-  if (g_mb_lds < 0) {
-    const char* s = getenv("TI_GEMM_MB_LDS");
-    g_mb_lds = s && atoi(s) > 0 ? 1 : 0;
-  }
-  return MB == 2 || g_mb_lds == 1;
-}
+// One 16-row block: the register-fragment kernel; two: the LDS-DMA one.
+static bool mb_use_lds(int MB) { return MB == 2; }
 template <int MB, int NTL>
 static int launch_mb_t(const GemvArgs& a, int grid, int lds, hipStream_t s) {
   if constexpr (MB == 1) {
@@ -2141,41 +2105,16 @@ static int launch_mb(const GemvArgs& a, int MB, int grid, int ntl, int lds, hipS
   }
 }
 // Rows kernel (M > 16): RG row groups x MB blocks per group, NTL tiles per workgroup.
-// TI_GEMM_ROWS=0 keeps the older 16/32-row kernels (A/B knob); TI_GEMM_ROWS_RG forces RG.
-static int g_rows_on = -1, g_rows_rg = -1;
-static bool rows_on() {
-  if (g_rows_on < 0) {
-    const char* s = getenv("TI_GEMM_ROWS");
-    g_rows_on = s ? (atoi(s) != 0) : 1;
-    const char* r = getenv("TI_GEMM_ROWS_RG");
-    g_rows_rg = r && (atoi(r) == 1 || atoi(r) == 2) ? atoi(r) : 0;
-  }
-  return g_rows_on == 1;
-}
+static bool rows_on() { return true; }
 __host__ inline void rows_shape(int M, int* MB, int* RG) {
-  const int rg = M > 32 ? 2 : (g_rows_rg > 0 ? g_rows_rg : 1);   // 64 rows: two groups of 32
+  const int rg = M > 32 ? 2 : 1;   // 64 rows: two groups of 32
   const int mb = (M + 16 * rg - 1) / (16 * rg);
   *MB = mb;
   *RG = rg;
 }
-static int g_g32_rows = -1;
-__host__ inline bool g32_rows_on() {
-  if (g_g32_rows < 0) {
-    const char* e = getenv("TI_GEMM_G32_ROWS");
-    g_g32_rows = e ? atoi(e) != 0 : 1;
-  }
-  return g_g32_rows != 0;
-}
-// Tile kernel from this many rows on (TI_GEMM_TILE_ROWS in [17, 65], default 65: the rows
-// kernel takes at most 64 rows).
-static int g_tile_rows = 0;
-static int tile_rows() {
-  if (g_tile_rows <= 0) {
-    const char* s = getenv("TI_GEMM_TILE_ROWS");
-    g_tile_rows = s && atoi(s) > 16 && atoi(s) <= 65 ? atoi(s) : 65;
-  }
-  return g_tile_rows;
-}
+__host__ inline bool g32_rows_on() { return true; }
+// Tile kernel from this many rows on (the rows kernel takes at most 64 rows).
+static int tile_rows() { return 65; }
 __host__ inline int rows_tiles_cap(int MB, int K, bool g32 = false) {
   const int lim = MB >= 2 ? 3 : 4, cap = 512 / ((K >> 7) * (g32 ? 4 : 1));   // VGPR budget / scale pieces
   return cap < 1 ? 1 : (cap > lim ? lim : cap);
@@ -2196,18 +2135,13 @@ __host__ inline int rows_grid(int MB, int N, int K, int num_cus, int* ntl_out, i
 // Rows per workgroup (16 RG MB): the fewest activation + weight bytes per workgroup over the
 // launch's rounds -- a workgroup streams its rows' activations (R K 2 bytes, L2) and its tiles'
 // weights (ntl 8 K bytes); narrow outputs (O, down) take 16-row blocks, wide ones all the rows.
-// TI_GEMM_ROWS_SPLIT=0 keeps all rows in one workgroup (A/B knob).
-static int g_rows_split = -1;
+// TI_GEMM_ROWS_SPLIT=0 keeps all rows in one workgroup (A/B knob, DESIGN 9).
 __host__ inline void rows_plan(int M, int N, int K, int cus, int* MB, int* RG, int* n_rb, int* n_cg, int* ntl,
                                bool g32 = false) {
-  if (g_rows_split < 0) {
-    const char* e = getenv("TI_GEMM_ROWS_SPLIT");
-    g_rows_split = e ? atoi(e) != 0 : 1;
-  }
   rows_shape(M, MB, RG);   // all rows in one workgroup
   *n_rb = 1;
   *n_cg = rows_grid(*MB, N, K, cus, ntl, 1, g32);
-  if (!g_rows_split) return;
+  if (!gemm_knobs().rows_split) return;
   const int NT = N >> 4;
   auto cost = [&](int mb, int rg, int nrb, int ncg, int nt) {
     const long rounds = ((long)(ncg + 7) / 8 * 8 * nrb + cus - 1) / cus;
@@ -2323,17 +2257,9 @@ extern "C" int ti_gemm_lds_bytes(int M, int N, int K) {
 
 // The fused kernel takes the rows while its LDS image fits; int4 with fp16 activations
 // also has the batched-rows kernel (up to TI_GEMM_MAX_ROWS rows, any K).
-// int4 with more than TI_GEMM_FUSED_ROWS rows (default 2; tuning knob) goes to the
-// batched-rows kernel: from 4 rows on it is faster at every 7B projection (bench.py
-// --batch 2..16, rocprof), at 2 rows the two tie.
-static int g_fused_rows = 0;
-static int fused_rows_pref(int bits) {
-  if (g_fused_rows <= 0) {
-    const char* s = getenv("TI_GEMM_FUSED_ROWS");
-    g_fused_rows = s && atoi(s) > 0 ? (atoi(s) < 16 ? atoi(s) : 16) : 2;
-  }
-  return bits == 4 ? g_fused_rows : 16;
-}
+// int4 with more than 2 rows goes to the batched-rows kernel: from 4 rows on it is faster at
+// every 7B projection (bench.py --batch 2..16, rocprof), at 2 rows the two tie.
+static int fused_rows_pref(int bits) { return bits == 4 ? 2 : 16; }
 static bool fused_fits(int M, int N, int K, bool g32 = false, bool aff = false) {
   if (M > 16) return false;
   const int NT = N >> 4, grid = ti::gemv_grid(M, N, K, query_cus(), g32, aff);
@@ -2350,20 +2276,14 @@ static bool use_batched(int bits, int x_kind, int M, int N, int K) {
 // 0 = off) -- the measured crossover (tools/rows_ab.sh: 64 x 12288 rows kernel 19.0 vs tile 26.5 us,
 // 32 x 28672 rows 36.5 vs tile 28.4, 64 x 22016 35.5 vs 28.3, 32 x 22016 25.7 vs 27.2).
 // At 17..32 rows the tile kernel's 32-row waves (RB 2) move a quarter of the activation bytes the
-// batched-rows kernel does and win from N >= TI_GEMM_TILE_WIDE_N32 (env, default 16384) whatever the
+// batched-rows kernel does and win from N >= 16384 whatever the
 // rows (`profiles/r3c_tile_wide32.txt`: N = 22016 at 17-32 rows 25.1-25.5 -> 18.2-18.8 us, N = 32000
 // 36.1-36.4 -> 21.2-21.8; N = 12288 stays on the rows kernel, 13.8 vs 17.2).
-static long g_tile_wide_mn = -1, g_tile_wide_n32 = -1;
 static bool wide_tile(int bits, int M, int N) {
-  if (g_tile_wide_mn < 0) {
-    const char* e = getenv("TI_GEMM_TILE_WIDE_MN");
-    g_tile_wide_mn = e ? atol(e) : 850000;
-    const char* f = getenv("TI_GEMM_TILE_WIDE_N32");
-    g_tile_wide_n32 = f ? atol(f) : 16384;
-  }
-  if (bits != 4 || g_tile_wide_mn <= 0 || M <= 16 || M >= ti::tile_rows()) return false;
-  if (M <= 32 && ti::tile_rb2_on() && g_tile_wide_n32 > 0 && N >= g_tile_wide_n32) return true;
-  return (long)M * N >= g_tile_wide_mn;
+  constexpr long kWideMN = 850000, kWideN32 = 16384;
+  if (bits != 4 || M <= 16 || M >= ti::tile_rows()) return false;
+  if (M <= 32 && ti::tile_rb2_on() && N >= kWideN32) return true;
+  return (long)M * N >= kWideMN;
 }
 extern "C" int ti_gemm_packed_rows(int bits, int M) { return bits == 4 && M > 16 && M < ti::tile_rows() ? 1 : 0; }
 extern "C" int ti_gemm_packed_rows_for(int bits, int M, int N, int K) {
