@@ -327,9 +327,9 @@ int ti_hbm_calibrate(size_t bytes, int reps, double* read_gbps, double* copy_gbp
 /* ----------------------------------------------------- persistent decode layers
  * All n_layers decode layers of ONE stream in one persistent launch (pds.hip): replaces the
  * per-layer QKV / attention / O / gate-up / down launches of forward_pass_incremental
- * (inference_engine.cpp:1493-1552, TransformerLayer::forward_incremental :203-279) for INT4
- * group-128 weights, heads == kv_heads, head_dim 128, grid = heads * 8 workgroups (<= the CU
- * count, one per CU) and hidden = 16 * grid.  Input: h, fx / ss as ti_step_begin leaves them
+ * (inference_engine.cpp:1493-1552, TransformerLayer::forward_incremental :203-279) for INT4 / INT8
+ * group-128 weights, head_dim 64 / 128, MHA or GQA, grid = heads * 8 workgroups (<= the CU
+ * count, one per CU; shapes: ti_pds_supported).  Input: h, fx / ss as ti_step_begin leaves them
  * with the layer-0 fold (n_ss0 partials); output: h and fx / ss folded with out_norm (n_ss =
  * grid partials) for the lm_head's TI_X_F16_FOLDED input.  Same arithmetic, bit for bit, as
  * the per-layer launches with the fold and split-partials hand-offs.  ctr (n_layers * 5 * 256
@@ -367,8 +367,13 @@ typedef struct ti_pds_args {
   unsigned long long* gran;
   int32_t drop_wg;                   /* diagnostic: workgroup that withholds its first down-projection
                                       * granules (a producer lost mid-launch); -1 = none */
+  int32_t bits;                      /* 4 or 8 (group-128 tiles) */
 } ti_pds_args;
 size_t ti_pds_granule_words(int H, int I, int qd, int heads, int grid);
+/* 1 if ti_pds_decode takes this shape: bits 4 / 8, head_dim 64 / 128, heads / kv_heads a power of
+ * two, grid = 8 * heads <= 256 workgroups (one per CU), hidden / 16 <= grid, layers <= 64, at most 4
+ * QKV and 8 gate/up tiles per workgroup. */
+int ti_pds_supported(int bits, int H, int I, int heads, int kv_heads, int head_dim, int grid, int layers);
 #define TI_PDS_CTR_WORDS_PER_LAYER (5 * 8 * 32)
 int ti_pds_decode(const ti_pds_args* a, ti_stream_t s);
 

@@ -12,17 +12,20 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 CFGS = {
-    # name: vocab, hidden, layers, heads, kv_heads, head_dim, inter   (hidden = 128 * heads)
-    "small": (512, 256, 2, 2, 2, 128, 512),
-    "l2_shape": (32000, 4096, 2, 32, 32, 128, 11008),
+    # name: vocab, hidden, layers, heads, kv_heads, head_dim, inter, bits
+    "small": (512, 256, 2, 2, 2, 128, 512, 4),                 # MHA head-group QKV mapping
+    "l2_shape": (32000, 4096, 2, 32, 32, 128, 11008, 4),       # Llama-2-7B layer shape
+    "tl_shape": (32000, 2048, 2, 32, 4, 64, 5632, 8),          # TinyLlama-1.1B: INT8, GQA 8, head_dim 64
+    "gqa_w4_hd64": (512, 256, 2, 4, 2, 64, 768, 4),            # GQA 2, hd 64, fewer O tiles than CUs
+    "gqa_w8_hd128": (1024, 512, 2, 4, 1, 128, 1024, 8),        # GQA 4, INT8, hd 128
 }
 
 
 def _twins(ti, name, max_seq):
-    v, h, l, nh, nkv, hd, inter = CFGS[name]
+    v, h, l, nh, nkv, hd, inter, bits = CFGS[name]
     eng = {}
     for on in (True, False):
-        e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=4, max_seq=max_seq, max_batch=1, attn_splits=8)
+        e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=bits, max_seq=max_seq, max_batch=1, attn_splits=8)
         e.synth(0x7157, 0.1)
         e.set_prefill(0)
         assert e.set_fold(True)
@@ -50,14 +53,15 @@ def test_pds_steps_bit_identical(ti, name):
         e.close()
 
 
-def test_pds_long_context_replay(ti):
+@pytest.mark.parametrize("name", ["l2_shape", "tl_shape"])
+def test_pds_long_context_replay(ti, name):
     """7B layer shape over a 2048-slot synthetic KV cache (the bench's configuration, 2 layers):
     replayed steps at position 2047 give the same argmax token with the persistent launch on and
     off, and repeated launches (monotonic hand-off counters) never time out."""
-    v, h, l, nh, nkv, hd, inter = CFGS["l2_shape"]
+    v, h, l, nh, nkv, hd, inter, bits = CFGS[name]
     toks = {}
     for on in (True, False):
-        e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=4, max_seq=2048, max_batch=1)
+        e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=bits, max_seq=2048, max_batch=1)
         e.synth(0x7157, 0.1)
         assert e.set_pds(on) is on
         e.fill_kv(0, 2047, 0x5eed)
@@ -75,7 +79,7 @@ def test_pds_timeout_is_fatal(ti, monkeypatch):
     """A hand-off wait that timed out (error word forced, TI_PDS_FORCE_ERR) must not hand back
     tokens: generate / step raise, the engine turns persistent decode off and resets the
     hand-off state, and the next call runs on the per-layer graph with correct results."""
-    v, h, l, nh, nkv, hd, inter = CFGS["l2_shape"]
+    v, h, l, nh, nkv, hd, inter, _bits = CFGS["l2_shape"]
     ref = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=4, max_seq=256, max_batch=1, attn_splits=8)
     ref.synth(0x7157, 0.1)
     want = np.asarray(ref.generate([[1, 2, 3]], 6))
@@ -105,7 +109,7 @@ def test_pds_lost_producer_costs_one_timeout(ti, monkeypatch):
     call fails with the fatal hand-off error within a few timeouts, not one per wait, and the engine
     falls back to the per-layer graph with correct results."""
     import time
-    v, h, l, nh, nkv, hd, inter = CFGS["l2_shape"]
+    v, h, l, nh, nkv, hd, inter, _bits = CFGS["l2_shape"]
     ref = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=4, max_seq=256, max_batch=1, attn_splits=8)
     ref.synth(0x7157, 0.1)
     want = np.asarray(ref.generate([[1, 2, 3]], 4))

@@ -22,7 +22,7 @@ def main():
     for r in rows:
         name = r["Kernel_Name"]
         key = "gemv_wq_kernel<4>" if "gemv_wq_kernel<4" in name else (
-            "attn_split_kernel" if "attn_split_kernel" in name else None)
+            "attn_split_kernel" if "attn_split_kernel" in name else ("pds_kernel" if "pds_kernel" in name else None))
         if key:
             fam[key].append(float(r["Counter_Value"]) * 1024.0 * 2.0)
     out = {"source": "rocprofv3 --pmc FETCH_SIZE (KiB, x2 gfx950 streaming-read correction)", "kernels": {}}

@@ -86,7 +86,7 @@ EXPORTED = [
     "ti_pds_decode", "ti_engine_set_pds", "ti_engine_pds_error", "ti_engine_pds_timestamps",
     "ti_wpack_q_host", "ti_engine_set_tensor_q", "ti_sample_workspace_bytes", "ti_sample_device_ws",
     "ti_wpack_q1_host", "ti_engine_set_tensor_q1", "ti_epilogue_bytes",
-    "ti_sample_step_ws", "ti_pds_granule_words", "ti_hbm_calibrate", "ti_gemm_kernel_name",
+    "ti_sample_step_ws", "ti_pds_granule_words", "ti_hbm_calibrate", "ti_gemm_kernel_name", "ti_pds_supported",
 ]
 
 _lib = None

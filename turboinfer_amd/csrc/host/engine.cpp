@@ -352,16 +352,15 @@ bool part_usable(ti_engine* e, int M) {
          e->qd() <= 4096;
 }
 
-// Persistent decode layers (ti_pds_decode): one stream with the fold and the split partials,
-// INT4, MHA with head_dim 128, heads * 8 == hidden / 16 <= the CU count (Llama-2-7B: 256).
+// Persistent decode layers (ti_pds_decode): one stream with the fold and the split partials (8
+// splits, so the persistent launch forms every partial as the per-layer launches do), INT4 / INT8,
+// the shapes ti_pds_supported takes (Llama-2-7B, TinyLlama-1.1B), grid = 8 heads <= the CU count.
 int g_pds_cus = 0;
 bool pds_usable(ti_engine* e, int M) {
   const ti_engine_config& c = e->c;
-  if (!e->pds_on || !e->pds_layers || M != 1 || c.bits != 4 || c.compat) return false;
+  if (!e->pds_on || !e->pds_layers || M != 1 || (c.bits != 4 && c.bits != 8) || c.compat) return false;
   if (!fold_usable(e, M) || !part_usable(e, M) || e->splits_for(M) != 8) return false;
-  if (c.heads != c.kv_heads || c.head_dim != 128 || c.heads * 8 != c.hidden / 16 || c.heads * 8 > 256) return false;
-  // ti_pds_decode's other limits: granule tags hold 64 layers, <= 8 gate/up tiles per workgroup
-  if (c.layers > 64 || 2 * c.inter / 16 > 8 * c.heads * 8) return false;
+  if (!ti_pds_supported(c.bits, c.hidden, c.inter, c.heads, c.kv_heads, c.head_dim, c.heads * 8, c.layers)) return false;
   if (g_pds_cus == 0) {
     int dev = 0, n = 0;
     g_pds_cus = (hipGetDevice(&dev) == hipSuccess &&
@@ -404,6 +403,7 @@ int pds_launch(ti_engine* e, int n_ss0) {
   pa.gran = e->pds_gran;
   pa.ts = e->pds_ts;
   pa.drop_wg = e->pds_drop;
+  pa.bits = c.bits;
   return ti_pds_decode(&pa, e->s);
 }
 
@@ -464,7 +464,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   const bool pds = pds_usable(e, M);
   if (pds) {   // every layer in one persistent launch; the lm_head stages its fold (grid partials)
     TI_TRY(pds_launch(e, n_ss));
-    n_ss = c.heads * 8;
+    n_ss = c.hidden / 16;   // one sum of h^2 per down tile (ti_pds_decode)
   }
   for (int l = 0; l < (pds ? 0 : c.layers); ++l) {
     DevLayer& L = e->layer[l];
@@ -759,7 +759,7 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     for (auto& L : e->layer) tab.push_back(L.vc);
     if ((rc = e->alloc_t(&e->kv_tab, tab.size())) || (rc = ti_memcpy_h2d(e->kv_tab, tab.data(), tab.size() * sizeof(void*), e->s)))
       return fail(rc);
-    if (c.bits == 4) {   // persistent decode layers (pds_usable decides per step)
+    if (c.bits == 4 || c.bits == 8) {   // persistent decode layers (pds_usable decides per step)
       std::vector<ti_pds_layer> pl((size_t)c.layers);
       for (int l = 0; l < c.layers; ++l) {
         DevLayer& L = e->layer[l];

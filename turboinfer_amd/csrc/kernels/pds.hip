@@ -4,9 +4,9 @@
 // Replaces the per-layer launch chain of the decode step (QKV, attention, O, gate/up, down:
 // TransformerLayer::forward_incremental, src/model/inference_engine.cpp:203-279, 291-368,
 // 376-401, with the matmuls of tensor_engine.cpp:594-640 and attention_fast_incremental
-// :1254-1388; the layer loop of forward_pass_incremental :1525-1530) for the configuration the
-// bench is quoted on: one stream, INT4 group-128 weights, multi-head attention with head_dim 128
-// and 8 * heads == the grid == hidden / 16 (Llama-2-7B: 256 workgroups, one per CU).
+// :1254-1388; the layer loop of forward_pass_incremental :1525-1530) for one stream with INT4 or
+// INT8 group-128 weights, head_dim 64 or 128, MHA or GQA, grid = 8 * heads workgroups (one per CU:
+// Llama-2-7B and TinyLlama-1.1B both 256).
 //
 // Why: a layer as five launches pays, per launch, the kernel boundary plus the latency from launch
 // to the first weight bytes (~4.1 us per launch, 5 per layer).  Here each CU's weight /
@@ -19,26 +19,27 @@
 //     instruction, "a piece") into a ring of n_slots 16 KiB slots in LDS; publishes a slot (LDS word
 //     FULL) behind a counted vmcnt that leaves up to 2 more slots in flight (1 while the CU gathers:
 //     gather-pass); reuses a slot once all four consumers released it (LDS words FREE[c]).
-//   * waves 0-3, the CONSUMERS: int4 dequant + v_mfma_f32_16x16x32_f16 out of the ring (GEMV
-//     phases) or the online softmax over K/V pieces (attention); they emulate the per-layer kernels'
-//     8 waves (virtual wave v = k-tile % 8, consumer v % 4), so every partial sum is formed in the
-//     same order as gemv_wq_kernel / attn_split_body and results are bit-identical to the graph path.
-//     Consumer 0 also runs the epilogues (tile sums in the fixed wave order, residual + folded
-//     rms_norm, RoPE + KV append, SiLU*up, the split merge) and publishes.  Consumers meet at LDS
-//     counter barriers (the loader never takes part in a barrier).
+//   * waves 0-3, the CONSUMERS: dequant + v_mfma_f32_16x16x32_f16 out of the ring (GEMV phases) or
+//     the online softmax over K/V pieces (attention); they emulate the per-layer kernels' 8 waves
+//     (virtual wave v = k-tile % 8 or key slot % 8, consumer v % 4), so every partial sum is formed
+//     in the same order as gemv_wq_kernel / attn_split_body and results are bit-identical to the
+//     graph path.  Consumer 0 also runs the epilogues (tile sums in the fixed wave order, residual +
+//     folded rms_norm, RoPE + KV append, SiLU*up, the split merge) and publishes.  Consumers meet at
+//     LDS counter barriers (the loader never takes part in a barrier).
 // Hand-offs: data-tagged 8-byte granules {payload, tag} (one sc1 store each, no flag, no fence),
 // gathered by the consumers with sc1 loads until every tag is this launch's (MI355X_MICROARCH.md
 // handoff-1to1 / allgather; cdna_hip_programming.md Guideline 16 R2).  Per layer:
-//   down(l-1) -> QKV: h folded with attn_norm (fp16 pairs) + one sum of h^2 per CU    all-to-all
-//   QKV -> attention: q / fresh K, V of head h from the 8 CUs of head h                 head group
-//   attention -> merge: split partials of 16 dims from the 8 splits of head h           head group
+//   down(l-1) -> QKV: h folded with attn_norm (fp16 pairs) + one sum of h^2 per tile    all-to-all
+//   QKV -> attention: q of head h, the fresh K, V row of its kv-head                     few-to-one
+//   attention -> merge: split partials of head h from its 8 splits                       head group
 //   merge -> O: the merged attention output (fp16 pairs)                                all-to-all
 //   O -> gate/up: h folded with ffn_norm + sums of h^2                                  all-to-all
 //   gate/up -> down: SiLU(gate) * up (fp16 pairs)                                       all-to-all
 // Workgroup b = (head h = b % heads, split s = b / heads): the 8 splits of a head share an XCD
-// (round-robin placement; speed only).  QKV: CU (h, s) computes q / k / v tile 8h + s of each, so
-// the attention's inputs come from its own head group; O / down: tile b; gate/up: tiles
-// [b NT / grid, (b + 1) NT / grid) -- the per-layer kernels' partition.
+// (round-robin placement; speed only).  QKV: for MHA with head_dim 128 and q_dim / 16 == grid, CU
+// (h, s) computes q / k / v tile 8h + s of each, so the attention's inputs come from its own head
+// group; otherwise tiles [b NT / grid, (b + 1) NT / grid).  O / down: tile b (b < hidden / 16);
+// gate/up: tiles [b NT / grid, (b + 1) NT / grid) -- the per-layer kernels' partition.
 // Every wait is bounded (~50 ms): on expiry the workgroup sets a shared LDS dead flag and *err, every
 // later wait of every wave passes at once, and every other workgroup leaves its waits on seeing *err,
 // so a broken hand-off costs one timeout per launch; the engine treats it as fatal.
@@ -62,8 +63,8 @@ constexpr int kFill = 16;                      // pieces per ring slot
 constexpr int kSlotBytes = kFill * kPiece;
 constexpr int kMaxSlots = 8;
 constexpr int kSplits = 8;
-constexpr int kHd = 128;
-constexpr int kPartG = kHd / 2 + 2;            // granules per split partial: 64 fp16 pairs + max + sum
+constexpr int kHdMax = 128;
+constexpr int kMaxQkvTiles = 4, kMaxGuTiles = 8;
 enum { PH_QKV = 0, PH_ATT, PH_O, PH_GU, PH_DN, PH_MRG, PH_N = 5 };
 enum { C_FULL = 0, C_FREE = 1, C_BAR = 5, C_GATHER = 6, C_DEAD = 7, C_EPOCH = 8, C_WORDS = 16 };
 #ifndef TI_PDS_THIN
@@ -78,14 +79,14 @@ typedef ti_pds_layer PdsLayerDev;
 
 struct PdsArgs {
   const PdsLayerDev* layers;
-  int n_layers, H, I, qd, max_seq, n_ss0, heads, grid, n_slots;
+  int n_layers, H, I, qd, kvd, max_seq, n_ss0, heads, kv_shift, grid, n_slots, nt_h, head_group;
   float eps, scale;
   const int32_t* pos;
   const float* rope_cs;     // [max_seq][hd] (cos, sin) pairs
   const float* out_norm;
   float* h;                 // [H] residual (read at start, written at end)
   uint16_t* fx;             // [H] fp16 h * next norm weight: layer 0's input, the lm_head's output
-  float* ss;                // [grid] sums of h^2 (likewise)
+  float* ss;                // [nt_h] sums of h^2 (likewise)
   uint32_t* launches;       // [grid] private launch counts (granule epochs)
   uint32_t* err;            // bit 0: a hand-off wait timed out
   const char* zero;         // >= 1 KiB of zeros, never written: dummy / masked DMA source
@@ -93,10 +94,10 @@ struct PdsArgs {
   int drop_wg;              // diagnostic: this workgroup withholds its layer-0 down granules (-1: none)
   // granules (8-byte {payload, tag}, one sc1 store / sc1 load each)
   unsigned long long* fxg;    // [H / 2]: fp16 pairs of the fold (O -> gate/up, down -> next QKV)
-  unsigned long long* ssg;    // [grid]: the fold's sums of h^2
+  unsigned long long* ssg;    // [nt_h]: the fold's sums of h^2, one per O / down tile
   unsigned long long* qg;     // [qd]: RoPE'd q, fp32
-  unsigned long long* kvg;    // [heads][2][hd / 2]: the fresh K, V rows (fp16 pairs)
-  unsigned long long* partg;  // [heads][8 splits][kPartG]: split partials
+  unsigned long long* kvg;    // [kv_heads][2][hd / 2]: the fresh K, V rows (fp16 pairs)
+  unsigned long long* partg;  // [heads][8 splits][hd / 2 + 2]: split partials
   unsigned long long* aog;    // [qd / 2]: the merged attention output (fp16 pairs)
   unsigned long long* actg;   // [I / 2]: SiLU * up (fp16 pairs)
   // LDS layout (bytes)
@@ -104,7 +105,8 @@ struct PdsArgs {
 };
 
 __host__ __device__ inline size_t pds_gran_words(int H, int I, int qd, int heads, int grid) {
-  return (size_t)H / 2 + (size_t)grid + (size_t)qd + (size_t)heads * kHd + (size_t)heads * kSplits * kPartG +
+  // (kv rows sized for MHA at head_dim 128: an upper bound for every supported shape)
+  return (size_t)H / 2 + (size_t)grid + (size_t)qd + (size_t)heads * kHdMax + (size_t)heads * kSplits * (kHdMax / 2 + 2) +
          (size_t)qd / 2 + (size_t)I / 2;
 }
 
@@ -135,14 +137,14 @@ __device__ __forceinline__ void cset(uint32_t* c, uint32_t v) { __hip_atomic_sto
 
 constexpr unsigned long long kSpinTicks = 5000000ull;   // ~50 ms of s_memrealtime (100 MHz)
 
-// One bounded wait.  `ready` is re-evaluated after each s_sleep; returns false (and the workgroup
-// is dead) on expiry or when the workgroup / another workgroup already failed.
+// One bounded wait: tick() once per unsuccessful poll; false = give up (this workgroup is dead:
+// its own expiry, an earlier one of another wave, or *err set by another workgroup).
 struct Spin {
   uint32_t* ctl;
   const uint32_t* err;
   unsigned long long t0 = 0;
   uint32_t n = 0;
-  __device__ bool tick() {   // call once per unsuccessful poll; false: give up
+  __device__ bool tick() {
     if (cget(ctl + C_DEAD)) return false;
     if (n == 0) t0 = __builtin_amdgcn_s_memrealtime();
     ++n;
@@ -181,41 +183,58 @@ __device__ __forceinline__ void dma_nt(const void* src_lane, uint32_t lds) {
 
 // Per-workgroup geometry, the same for every layer.
 struct PdsGeo {
-  int h, s;            // head, split
-  int L, s0, s1, nslot;
-  int KTh, KTq, KTi;   // k-tiles of H, qd, I
-  int gu0, gu_ntl;     // gate/up tiles
-  int tq[3];           // QKV tiles (q, k, v of head h, tile s)
+  int h, s, kvh;           // q-head, split, kv-head
+  int L, s0, s1, nslot;    // keys [s0, s1) of the split, in slots of KPW keys (one piece each)
+  int KTh, KTq, KTi;       // k-tiles of H, qd, I
+  int q0, qs, qn;          // QKV tiles q0 + t * qs, t < qn
+  int gu0, gun;            // gate/up tiles
+  int on;                  // O / down: tile bid (1) or none (0)
 };
+template <int HD>
 __device__ __forceinline__ PdsGeo pds_geo(const PdsArgs& a, int bid, int pos) {
+  constexpr int KPW = 64 / (HD / 8);
   PdsGeo g;
   g.h = bid % a.heads;
   g.s = bid / a.heads;
+  g.kvh = g.h >> a.kv_shift;
   g.L = pos + 1;
   const int chunk = (g.L + kSplits - 1) / kSplits;
   g.s0 = g.s * chunk;
   g.s1 = min(g.L, g.s0 + chunk);
-  g.nslot = g.s1 > g.s0 ? (g.s1 - g.s0 + 3) / 4 : 0;
+  g.nslot = g.s1 > g.s0 ? (g.s1 - g.s0 + KPW - 1) / KPW : 0;
   g.KTh = a.H >> 7;
   g.KTq = a.qd >> 7;
   g.KTi = a.I >> 7;
+  if (a.head_group) {   // MHA, head_dim 128, qd / 16 == grid: q / k / v tile 8h + s
+    g.q0 = g.h * (HD / 16) + g.s;
+    g.qs = a.qd >> 4;
+    g.qn = 3;
+  } else {
+    const int NT = (a.qd + 2 * a.kvd) >> 4;
+    g.q0 = (int)((unsigned)bid * (unsigned)NT / (unsigned)a.grid);
+    g.qn = (int)((unsigned)(bid + 1) * (unsigned)NT / (unsigned)a.grid) - g.q0;
+    g.qs = 1;
+  }
   const int NTg = (2 * a.I) >> 4;
   g.gu0 = (int)((unsigned)bid * (unsigned)NTg / (unsigned)a.grid);
-  g.gu_ntl = (int)((unsigned)(bid + 1) * (unsigned)NTg / (unsigned)a.grid) - g.gu0;
-  const int tph = kHd / 16;   // tiles per head
-  g.tq[0] = g.h * tph + g.s;
-  g.tq[1] = (a.qd >> 4) + g.tq[0];
-  g.tq[2] = 2 * (a.qd >> 4) + g.tq[0];
+  g.gun = (int)((unsigned)(bid + 1) * (unsigned)NTg / (unsigned)a.grid) - g.gu0;
+  g.on = bid < a.nt_h ? 1 : 0;
   return g;
 }
+// pieces of a phase (C pieces per weight item)
+template <int C>
 __device__ __forceinline__ int pds_pieces(const PdsGeo& g, int ph) {
-  return ph == PH_QKV ? 3 * g.KTh : ph == PH_ATT ? 2 * g.nslot : ph == PH_O ? g.KTq : ph == PH_GU ? g.gu_ntl * g.KTh : g.KTi;
+  return ph == PH_QKV ? g.qn * g.KTh * C : ph == PH_ATT ? 2 * g.nslot : ph == PH_O ? g.on * g.KTq * C
+         : ph == PH_GU ? g.gun * g.KTh * C : g.on * g.KTi * C;
 }
 __device__ __forceinline__ int pds_fills(int np) { return (np + kFill - 1) / kFill; }
 
 // ------------------------------------------------------------------------------------- loader
+template <int BITS, int HD>
 __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, int bid, int pos, uint32_t ring_lds,
                                            uint32_t* ctl, int lane) {
+  constexpr int C = BITS / 4;
+  constexpr int LPK = HD / 8, KPW = 64 / LPK;
   const int NS = a.n_slots;
   uint32_t f = 0, pub = 0;   // fills issued / published
   auto publish = [&](uint32_t upto) {
@@ -231,19 +250,20 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
     return m;
   };
   const char* zl = a.zero + lane * 16;
+  const size_t kv_off = ((size_t)g.kvh * a.max_seq) * HD * 2;   // bytes: this split's kv-head
   for (int l = 0; l < a.n_layers; ++l) {
     const PdsLayerDev& ly = a.layers[l];
     for (int ph = 0; ph < PH_N; ++ph) {
-      const int np = pds_pieces(g, ph), nf = pds_fills(np);
+      const int np = pds_pieces<C>(g, ph), nf = pds_fills(np);
       if (a.ts && lane == 0) a.ts[(((size_t)bid * a.n_layers + l) * PH_N + ph) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
-      // piece i's source for this lane
+      // GEMV phases: piece i = chunk i % C of item i / C = (tile t0 + (item / KT) * ts, k-tile item % KT)
       const char* wbase = nullptr;
-      int KT = 0;
-      if (ph == PH_QKV) { wbase = (const char*)ly.tiles[0]; KT = g.KTh; }
-      else if (ph == PH_O) { wbase = (const char*)ly.tiles[1] + (size_t)bid * g.KTq * kPiece; KT = g.KTq; }
-      else if (ph == PH_GU) { wbase = (const char*)ly.tiles[2] + (size_t)g.gu0 * g.KTh * kPiece; KT = g.KTh; }
-      else if (ph == PH_DN) { wbase = (const char*)ly.tiles[3] + (size_t)bid * g.KTi * kPiece; KT = g.KTi; }
-      const size_t kv_off = ((size_t)g.h * a.max_seq) * kHd * 2;   // bytes: head h of the cache
+      int KT = 1, t0 = 0, tstr = 1;
+      if (ph == PH_QKV) { wbase = (const char*)ly.tiles[0]; KT = g.KTh; t0 = g.q0; tstr = g.qs; }
+      else if (ph == PH_O) { wbase = (const char*)ly.tiles[1]; KT = g.KTq; t0 = bid; }
+      else if (ph == PH_GU) { wbase = (const char*)ly.tiles[2]; KT = g.KTh; t0 = g.gu0; }
+      else if (ph == PH_DN) { wbase = (const char*)ly.tiles[3]; KT = g.KTi; t0 = bid; }
+      const char* cbase = wbase + (size_t)t0 * KT * C * kPiece + lane * 16;   // tstr == 1: one contiguous run
       for (int fi = 0; fi < nf; ++fi) {
         // the slot must be released by every consumer
         if (f >= (uint32_t)NS) {
@@ -263,15 +283,15 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
           const char* src = zl;
           if (i < np) {
             if (ph == PH_ATT) {
-              const int slot = i >> 1, key = g.s0 + 4 * slot + (lane >> 4);
+              const int slot = i >> 1, key = g.s0 + KPW * slot + lane / LPK;
               // keys of the next split, past L, and the row this launch writes (pos) are not read
               if (key < g.s1 && key != pos)
-                src = (const char*)((i & 1) ? ly.v_cache : ly.k_cache) + kv_off + (size_t)key * kHd * 2 + (lane & 15) * 16;
-            } else if (ph == PH_QKV) {
-              const int seg = i / KT;
-              src = wbase + ((size_t)(g.tq[0] + seg * (a.qd >> 4)) * KT + (i - seg * KT)) * kPiece + lane * 16;
+                src = (const char*)((i & 1) ? ly.v_cache : ly.k_cache) + kv_off + (size_t)key * HD * 2 + (lane % LPK) * 16;
+            } else if (tstr == 1) {
+              src = cbase + (size_t)i * kPiece;
             } else {
-              src = wbase + (size_t)i * kPiece + lane * 16;
+              const int seg = i / (KT * C);
+              src = wbase + ((size_t)(t0 + seg * tstr) * KT * C + (i - seg * KT * C)) * kPiece + lane * 16;
             }
           }
           dma_nt(src, __builtin_amdgcn_readfirstlane(base + j * kPiece));
@@ -299,21 +319,27 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
 }
 
 // ----------------------------------------------------------------------------------- consumers
+template <int BITS, int HD>
 __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
+  constexpr int C = BITS / 4;                  // pieces per weight item (16 rows x 128 k)
+  constexpr int IPF = kFill / C;               // items per fill
+  constexpr int LPK = HD / 8, KPW = 64 / LPK;  // attention: lanes per key row, keys per slot (one piece)
+  constexpr int NPS = HD / 16;                 // fp16 pairs per split and CU in the head-group merge
+  constexpr int PG = HD / 2 + 2;               // granules per split partial
   extern __shared__ __attribute__((aligned(16))) char smem[];
   f16* xl = (f16*)(smem + a.l_x);
   uint16_t* sl = (uint16_t*)(smem + a.l_sc);
   float* corr = (float*)(smem + a.l_corr);
   float* slab = (float*)(smem + a.l_slab);          // [ntl][8 virtual waves][16]
-  float* s_acc = (float*)(smem + a.l_att);          // [8][128]
-  float* s_m = s_acc + kVW * kHd;                   // [8]
+  float* s_acc = (float*)(smem + a.l_att);          // [8][HD]
+  float* s_m = s_acc + kVW * kHdMax;                // [8]
   float* s_l = s_m + kVW;                           // [8]
-  float* q_l = s_l + kVW;                           // [128] q of the head
-  uint16_t* kf_l = (uint16_t*)(q_l + kHd);          // fresh K row [128], V row [128] fp16
-  uint16_t* vf_l = kf_l + kHd;
-  float* cs_l = (float*)(vf_l + kHd);               // RoPE (cos, sin) [128]
-  float* h_l = cs_l + kHd;                          // residual rows [16]
-  float* mg_o = h_l + 16;                           // split merge: [8 splits][16 dims]
+  float* q_l = s_l + kVW;                           // [HD] q of the head
+  uint16_t* kf_l = (uint16_t*)(q_l + kHdMax);       // fresh K row [HD], V row [HD] fp16
+  uint16_t* vf_l = kf_l + kHdMax;
+  float* cs_l = (float*)(vf_l + kHdMax);            // RoPE (cos, sin) [HD]
+  float* h_l = cs_l + kHdMax;                       // residual rows [16]
+  float* mg_o = h_l + 16;                           // split merge: [8 splits][HD / 8 dims]
   float* mg_ml = mg_o + kSplits * 16;               // [8][2]
   uint32_t* ctl = (uint32_t*)(smem + a.l_ctl);
   const uint32_t ring_lds = (uint32_t)(uintptr_t)smem;   // the ring starts the LDS image
@@ -322,8 +348,8 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bid = blockIdx.x;
   const int pos = __builtin_amdgcn_readfirstlane(gptr(a.pos)[0]);
-  const PdsGeo g = pds_geo(a, bid, pos);
-  const int H = a.H, I = a.I, qd = a.qd;
+  const PdsGeo g = pds_geo<HD>(a, bid, pos);
+  const int H = a.H, I = a.I, qd = a.qd, kvd = a.kvd;
 
   // ---- setup (the one workgroup barrier of the launch)
   if (wave == 0) {
@@ -335,12 +361,12 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     epoch = __builtin_amdgcn_readfirstlane(epoch);
     const uint32_t dead0 = ld_sc1_u32(a.err) != 0u ? 1u : 0u;
     if (lane < C_WORDS) ctl[lane] = lane == C_EPOCH ? epoch : lane == C_DEAD ? dead0 : 0u;
-    if (lane < 16) h_l[lane] = gptr(a.h)[bid * 16 + lane];
-    for (int j = lane; j < kHd; j += kWave) cs_l[j] = gptr(a.rope_cs)[(size_t)pos * kHd + j];
+    if (lane < 16 && g.on) h_l[lane] = gptr(a.h)[bid * 16 + lane];
+    for (int j = lane; j < HD; j += kWave) cs_l[j] = gptr(a.rope_cs)[(size_t)pos * HD + j];
   }
   __syncthreads();
   if (wave == kEC) {
-    pds_loader(a, g, bid, pos, ring_lds, ctl, lane);
+    pds_loader<BITS, HD>(a, g, bid, pos, ring_lds, ctl, lane);
     return;
   }
   const uint32_t epoch = __builtin_amdgcn_readfirstlane(cget(ctl + C_EPOCH));
@@ -357,9 +383,10 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
   const int r = lane & 15, kq = lane >> 4;
   uint32_t fbase = 0;   // ring fill of the current phase's first piece
 
-  // ---- gathers.  Granules g[0..n) into `out` (bounded re-polls); PL: plain / sc1 memory, no tags.
-  // fp16 vector of K (K/2 granules or K halves), staged into xl with the int4 pre-scaling and
-  // the offset correction corr[kt] (gemv_body's int4 pass, M = 1), by all four consumers.
+  // ---- gathers
+  // An fp16 vector of K (K/2 granules, or K halves in plain memory) staged into xl by all four
+  // consumers; int4: with the high-nibble slots pre-scaled by 1/16 and the offset correction corr[kt]
+  // (gemv_body's int4 pass, M = 1).
   auto stage_x = [&](const void* src, int K, uint32_t tag, bool plain) {
     const int K8 = K >> 3;
     constexpr int B = 6;
@@ -406,15 +433,19 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         if (idx < K8) {
           const u32x4 w = plain ? gv[b][0] : (u32x4){gv[b][0][0], gv[b][0][2], gv[b][1][0], gv[b][1][2]};
           f16x8 hx = __builtin_bit_cast(f16x8, w);
-          const f16 s16 = (f16)0.0625f;
-          hx[2] *= s16; hx[3] *= s16; hx[6] *= s16; hx[7] *= s16;
+          if constexpr (BITS == 4) {
+            const f16 s16 = (f16)0.0625f;
+            hx[2] *= s16; hx[3] *= s16; hx[6] *= s16; hx[7] *= s16;
+            const float lo = ((float)hx[0] + (float)hx[1]) + ((float)hx[4] + (float)hx[5]);
+            const float hi = ((float)hx[2] + (float)hx[3]) + ((float)hx[6] + (float)hx[7]);
+            part = 1032.0f * lo + 1152.0f * hi;
+          }
           *(f16x8*)(xl + 8 * idx) = hx;
-          const float lo = ((float)hx[0] + (float)hx[1]) + ((float)hx[4] + (float)hx[5]);
-          const float hi = ((float)hx[2] + (float)hx[3]) + ((float)hx[6] + (float)hx[7]);
-          part = 1032.0f * lo + 1152.0f * hi;
         }
-        part = group_sum<16>(part);
-        if (idx < K8 && (lane & 15) == 0) corr[idx >> 4] = part;
+        if constexpr (BITS == 4) {
+          part = group_sum<16>(part);
+          if (idx < K8 && (lane & 15) == 0) corr[idx >> 4] = part;
+        }
       }
     }
   };
@@ -451,7 +482,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     t = group_sum<kWave>(t);
     return sqrtf(t / (float)K + a.eps);
   };
-  // n (<= 64 per lane-set) single granules of one wave: g[idx(lane)] for lanes with want, bounded
+  // single granules of one wave: base[idx] for lanes with want, bounded
   auto gather1 = [&](const unsigned long long* base, int idx, bool want, uint32_t tag) -> uint32_t {
     unsigned long long v = want ? ld_sc1_u64(base + idx) : 0ull;
     Spin sp{ctl, a.err};
@@ -481,11 +512,11 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane == 0) cset(ctl + C_FREE + c, fill + 1);
   };
-  // GEMV phase: pieces (tile i / KT, k-tile i % KT); this consumer's items are k-tiles == c (mod 4),
-  // virtual wave kt % 8 in {c, c + 4}: the partial of (tile, virtual wave) accumulates exactly as
-  // wave kt % 8 of gemv_wq_kernel does, then lands in slab[tile][v] (lanes 0-15, output n = lane).
+  // GEMV phase over items (tile item / KT, k-tile item % KT): this consumer's items are k-tiles == c
+  // (mod 4), virtual wave kt % 8 in {c, c + 4}: the partial of (tile, virtual wave) accumulates
+  // exactly as wave kt % 8 of gemv_wq_kernel does, then lands in slab[tile][v] (lanes 0-15).
   auto gemv_phase = [&](int ntl, int KT) {
-    const int np = ntl * KT, nf = pds_fills(np);
+    const int ni = ntl * KT, nf = pds_fills(ni * C);
     const f16* xrow = xl + kq * 32;
     for (int t = 0; t < ntl; ++t)
       if (lane < 16) {
@@ -501,21 +532,20 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       }
       acc[0] = acc[1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
     };
-    // one item: 4 MFMAs on (x, dequantized W), the group's offset correction, the group scale
-    auto item = [&](const u32x4 w, int it, int ik) {
+    // one item: 4 MFMAs on (x, dequantized W), the int4 offset correction, the group scale
+    auto item = [&](const u32x4 (&wv)[C], int it, int ik) {
       if (it != cur) {
         flush();
         cur = it;
       }
-      const u32x4 wv[1] = {w};
       f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
-        const f16x8 bf = dequant_step<4>(wv, s4, magic);
+        const f16x8 bf = dequant_step<BITS>(wv, s4, magic);
         const f16x8 af = *(const f16x8*)(xrow + ik * 128 + s4 * 8);
         t = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, t, 0, 0, 0);
       }
-      t -= corr[ik];
+      if constexpr (BITS == 4) t -= corr[ik];
       const float sc = h2f(sl[(it * KT + ik) * 16 + r]);
       if ((ik >> 2) & 1) {   // virtual wave c + 4 (static register indices: no scratch)
         acc[1][0] = fmaf(sc, t[0], acc[1][0]);
@@ -530,21 +560,26 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       }
     };
     if ((KT & 3) == 0 || ntl == 1) {
-      // k-tile == piece index (mod 4): this consumer's items sit at pieces c, c + 4, c + 8, c + 12 of
-      // every fill.  All four are read, the slot is released, then the math runs.
+      // k-tile == item index (mod 4): this consumer's items sit at items c, c + 4, ... of every fill.
+      // They are all read, the slot is released, then the math runs.
+      constexpr int NU = IPF / 4;
       tl = 0;
-      kt = c;   // piece c of fill 0
+      kt = c;
       for (int fi = 0; fi < nf; ++fi) {
         const uint32_t fill = fbase + fi;
         wait_full(fill);
         const char* slot = smem + (fill % (uint32_t)a.n_slots) * kSlotBytes + lane * 16;
-        u32x4 w[4];
-        int itl[4], ikt[4];
+        u32x4 w[NU][C];
+        int itl[NU], ikt[NU];
+        bool live[NU];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < NU; ++u) {
           itl[u] = tl;
           ikt[u] = kt;
-          w[u] = fi * kFill + c + 4 * u < np ? *(const u32x4*)(slot + (c + 4 * u) * kPiece) : (u32x4){0u, 0u, 0u, 0u};
+          live[u] = fi * IPF + c + 4 * u < ni;
+#pragma unroll
+          for (int cc = 0; cc < C; ++cc)
+            w[u][cc] = live[u] ? *(const u32x4*)(slot + ((c + 4 * u) * C + cc) * kPiece) : (u32x4){0u, 0u, 0u, 0u};
           kt += 4;
           if (kt >= KT && ntl > 1) {
             kt -= KT;
@@ -553,18 +588,23 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         }
         release(fill);
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (fi * kFill + c + 4 * u < np) item(w[u], itl[u], ikt[u]);
+        for (int u = 0; u < NU; ++u)
+          if (live[u]) item(w[u], itl[u], ikt[u]);
       }
     } else {
-      // general shapes (K % 512 != 0 with several tiles): piece by piece
+      // general shapes (K % 512 != 0 with several tiles): item by item
       for (int fi = 0; fi < nf; ++fi) {
         const uint32_t fill = fbase + fi;
         wait_full(fill);
         const char* slot = smem + (fill % (uint32_t)a.n_slots) * kSlotBytes + lane * 16;
-        for (int j = 0; j < kFill; ++j) {
-          if (fi * kFill + j >= np) break;
-          if ((kt & 3) == c) item(*(const u32x4*)(slot + j * kPiece), tl, kt);
+        for (int j = 0; j < IPF; ++j) {
+          if (fi * IPF + j >= ni) break;
+          if ((kt & 3) == c) {
+            u32x4 w[C];
+#pragma unroll
+            for (int cc = 0; cc < C; ++cc) w[cc] = *(const u32x4*)(slot + (j * C + cc) * kPiece);
+            item(w, tl, kt);
+          }
           if (++kt == KT) {
             kt = 0;
             ++tl;
@@ -573,7 +613,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         release(fill);
       }
     }
-    if (np > 0) flush();
+    if (ni > 0) flush();
     fbase += nf;
   };
   // tile sums (the 8 virtual waves in order), output n of tile tl
@@ -616,38 +656,41 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     float rms = 1.0f;
     {
       ts(l, PH_QKV, 0);
-      stage_scales(ly.scales[0], g.tq[0], qd >> 4, 3, g.KTh);
+      stage_scales(ly.scales[0], g.q0, g.qs, g.qn, g.KTh);
       gathering(true);
       if (l == 0) stage_x(a.fx, H, 0u, true);
       else stage_x(a.fxg, H, pds_tag(epoch, l - 1, PH_DN), false);
-      if (c == 0) rms = l == 0 ? fold_rms(a.ss, a.n_ss0, H, 0u, true) : fold_rms(a.ssg, a.grid, H, pds_tag(epoch, l - 1, PH_DN), false);
+      if (c == 0) rms = l == 0 ? fold_rms(a.ss, a.n_ss0, H, 0u, true) : fold_rms(a.ssg, a.nt_h, H, pds_tag(epoch, l - 1, PH_DN), false);
       bar();
       gathering(false);
       ts(l, PH_QKV, 1);
-      gemv_phase(3, g.KTh);
+      gemv_phase(g.qn, g.KTh);
       bar();
       ts(l, PH_QKV, 2);
       if (c == 0) {
-        // outputs (tile tl = q / k / v, n) = lane < 48: TI_EPI_QKV_ROPE_KV, M = 1
+        // outputs (tile tl, n) = lane < 16 qn: TI_EPI_QKV_ROPE_KV, M = 1
         const int tl = lane >> 4, n = lane & 15;
-        const bool ok = tl < 3;
+        const bool ok = tl < g.qn;
         const float v = (ok ? tile_sum(tl, n) : 0.0f) / rms;
         const float partner = lane_xor<1>(v);
-        const int d = g.s * 16 + n;   // dim within the head
+        const int ng = (g.q0 + tl * g.qs) * 16 + n;
+        const bool qk = ng < qd + kvd;
+        const int base = ng < qd ? 0 : ng < qd + kvd ? qd : qd + kvd;
+        const int d = (ng - base) % HD, hh = (ng - base) / HD;
         float rv = v;
-        if (ok && tl < 2) {
+        if (ok && qk) {
           const float2 cs = *(const float2*)(cs_l + (d & ~1));
           rv = (d & 1) == 0 ? fmaf(-partner, cs.y, v * cs.x) : fmaf(v, cs.x, partner * cs.y);
         }
         const uint32_t hv = f2h(rv), hp = lane_xor_u32<1>(hv);
         const uint32_t tq = pds_tag(epoch, l, PH_QKV);
-        if (tl == 0) {
-          st_gran(a.qg + g.h * kHd + d, __builtin_bit_cast(uint32_t, rv), tq);
+        if (ok && ng < qd) {
+          st_gran(a.qg + ng, __builtin_bit_cast(uint32_t, rv), tq);
         } else if (ok && !(n & 1)) {
-          const bool is_k = tl == 1;
+          const bool is_k = qk;
           uint16_t* cache = is_k ? ly.k_cache : ly.v_cache;   // for later launches
-          gptr_w((uint32_t*)(cache + ((size_t)g.h * a.max_seq + pos) * kHd + d))[0] = hv | (hp << 16);
-          st_gran(a.kvg + ((size_t)g.h * 2 + (is_k ? 0 : 1)) * (kHd / 2) + d / 2, hv | (hp << 16), tq);
+          gptr_w((uint32_t*)(cache + ((size_t)hh * a.max_seq + pos) * HD + d))[0] = hv | (hp << 16);
+          st_gran(a.kvg + ((size_t)hh * 2 + (is_k ? 0 : 1)) * (HD / 2) + d / 2, hv | (hp << 16), tq);
         }
         ts(l, PH_QKV, 3);
       }
@@ -657,15 +700,15 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       ts(l, PH_ATT, 0);
       const uint32_t tq = pds_tag(epoch, l, PH_QKV);
       if (c == 0) {
-        q_l[lane] = __builtin_bit_cast(float, gather1(a.qg + g.h * kHd, lane, true, tq));
-        q_l[lane + kWave] = __builtin_bit_cast(float, gather1(a.qg + g.h * kHd, lane + kWave, true, tq));
+        q_l[lane] = __builtin_bit_cast(float, gather1(a.qg + g.h * HD, lane, lane < HD, tq));
+        if (HD > kWave) q_l[lane + kWave] = __builtin_bit_cast(float, gather1(a.qg + g.h * HD, lane + kWave, true, tq));
       } else if (c == 1 && pos >= g.s0 && pos < g.s1) {
-        ((uint32_t*)kf_l)[lane] = gather1(a.kvg + (size_t)g.h * kHd, lane, true, tq);
-        ((uint32_t*)vf_l)[lane] = gather1(a.kvg + (size_t)g.h * kHd + kHd / 2, lane, true, tq);
+        ((uint32_t*)kf_l)[lane] = gather1(a.kvg + (size_t)g.kvh * HD, lane, lane < HD / 2, tq);
+        ((uint32_t*)vf_l)[lane] = gather1(a.kvg + (size_t)g.kvh * HD + HD / 2, lane, lane < HD / 2, tq);
       }
       bar();
       ts(l, PH_ATT, 1);
-      const int dl = lane & 15, kg = lane >> 4;
+      const int dl = lane % LPK, kg = lane / LPK;
       float qv[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) qv[e] = q_l[dl * 8 + e] * a.scale;
@@ -691,7 +734,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         for (int u = 0; u < 2; ++u) {
           const int su = c + 4 * u, si = fi * 8 + su;   // slot of the split; virtual wave su
           if (si < g.nslot) {
-            const int key = g.s0 + 4 * si + kg;
+            const int key = g.s0 + KPW * si + kg;
             const bool valid = key < g.s1;
             u32x4 kv = kr[u];
             u32x4 vv = valid ? vr[u] : (u32x4){0u, 0u, 0u, 0u};
@@ -705,7 +748,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
             float d = 0.0f;
 #pragma unroll
             for (int e = 0; e < 8; ++e) d = fmaf(qv[e], kf[e], d);
-            d = group_sum<16>(d);
+            d = group_sum<LPK>(d);
             const float sc = valid ? d : -INFINITY;
             const float mn = fmaxf(mrun[u], sc);
             const float alpha = mrun[u] == mn ? 1.0f : __expf(mrun[u] - mn);
@@ -718,19 +761,19 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         }
       }
       fbase += nf;
-      // merge the lane groups of each virtual wave (attn_split_body, LPK = 16)
+      // merge the lane groups of each virtual wave (attn_split_body)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int v = c + 4 * u;
-        const float mx = groups_max<16>(mrun[u]);
+        const float mx = groups_max<LPK>(mrun[u]);
         const float f = mrun[u] == -INFINITY ? 0.0f : __expf(mrun[u] - mx);
-        const float lsum = groups_sum<16>(lrun[u] * f);
+        const float lsum = groups_sum<LPK>(lrun[u] * f);
         float o[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = groups_sum<16>(acc[u][e] * f);
-        if (lane < 16) {
+        for (int e = 0; e < 8; ++e) o[e] = groups_sum<LPK>(acc[u][e] * f);
+        if (lane < LPK) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) s_acc[v * kHd + dl * 8 + e] = o[e];
+          for (int e = 0; e < 8; ++e) s_acc[v * kHdMax + dl * 8 + e] = o[e];
         }
         if (lane == 0) {
           s_m[v] = mx;
@@ -740,7 +783,8 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       bar();
       ts(l, PH_ATT, 2);
       if (c == 0) {
-        // merge the 8 virtual waves: dims 2 lane, 2 lane + 1 of head h -> this split's partial
+        // merge the 8 virtual waves: dims 2 lane, 2 lane + 1 (lane < HD / 2) -> this split's partial
+        const int dd = lane < HD / 2 ? 2 * lane : 0;
         float mx = s_m[0];
 #pragma unroll
         for (int w = 1; w < kVW; ++w) mx = fmaxf(mx, s_m[w]);
@@ -749,32 +793,36 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
 #pragma unroll
           for (int w = 0; w < kVW; ++w) {
             const float f = s_m[w] == -INFINITY ? 0.0f : __expf(s_m[w] - mx);
-            o2[0] = fmaf(f, s_acc[w * kHd + 2 * lane], o2[0]);
-            o2[1] = fmaf(f, s_acc[w * kHd + 2 * lane + 1], o2[1]);
+            o2[0] = fmaf(f, s_acc[w * kHdMax + dd], o2[0]);
+            o2[1] = fmaf(f, s_acc[w * kHdMax + dd + 1], o2[1]);
             lsum = fmaf(f, s_l[w], lsum);
           }
         }
         const uint32_t ta = pds_tag(epoch, l, PH_ATT);
-        unsigned long long* pg = a.partg + ((size_t)g.h * kSplits + g.s) * kPartG;
+        unsigned long long* pg = a.partg + ((size_t)g.h * kSplits + g.s) * PG;
         const uint32_t lo = f2h(lsum > 0.0f ? o2[0] / lsum : 0.0f), hi = f2h(lsum > 0.0f ? o2[1] / lsum : 0.0f);
-        st_gran(pg + lane, lo | (hi << 16), ta);
+        if (lane < HD / 2) st_gran(pg + lane, lo | (hi << 16), ta);
         if (lane == 0) {
-          st_gran(pg + kHd / 2, __builtin_bit_cast(uint32_t, mx), ta);
-          st_gran(pg + kHd / 2 + 1, __builtin_bit_cast(uint32_t, lsum), ta);
+          st_gran(pg + HD / 2, __builtin_bit_cast(uint32_t, mx), ta);
+          st_gran(pg + HD / 2 + 1, __builtin_bit_cast(uint32_t, lsum), ta);
         }
         ts(l, PH_ATT, 3);
-        // the head group's split merge for dims [16 s, 16 s + 16): lane = split sp * 8 + pair j
-        // (the O projection's TI_X_ATTN_SPLITS staging arithmetic: weights l_s exp(m_s - max))
+        // the head group's split merge for dims [s HD / 8, (s + 1) HD / 8): lane = split sp * NPS +
+        // pair j (the O projection's TI_X_ATTN_SPLITS staging arithmetic: weights l_s exp(m_s - max))
         {
-          const int sp = lane >> 3, j = lane & 7;
-          const uint32_t pw = gather1(a.partg + ((size_t)g.h * kSplits + sp) * kPartG, g.s * 8 + j, true, ta);
-          const uint32_t mw = gather1(a.partg + ((size_t)g.h * kSplits + (lane >> 1)) * kPartG, kHd / 2 + (lane & 1),
-                                      lane < 16, ta);
+          const int sp = lane / NPS, j = lane % NPS;
+          const bool mine = lane < kSplits * NPS;
+          const uint32_t pw = gather1(a.partg + ((size_t)g.h * kSplits + (mine ? sp : 0)) * PG, g.s * NPS + j, mine, ta);
+          const uint32_t mw = gather1(a.partg + ((size_t)g.h * kSplits + (lane >> 1)) * PG, HD / 2 + (lane & 1),
+                                      lane < 2 * kSplits, ta);
           const f16x2 ph2 = __builtin_bit_cast(f16x2, pw);
-          mg_o[sp * 16 + 2 * j] = (float)ph2[0];
-          mg_o[sp * 16 + 2 * j + 1] = (float)ph2[1];
-          if (lane < 16) mg_ml[lane] = __builtin_bit_cast(float, mw);
+          if (mine) {
+            mg_o[sp * 16 + 2 * j] = (float)ph2[0];
+            mg_o[sp * 16 + 2 * j + 1] = (float)ph2[1];
+          }
+          if (lane < 2 * kSplits) mg_ml[lane] = __builtin_bit_cast(float, mw);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const int dm = lane % (HD / 8);
           float mxs = -INFINITY;
 #pragma unroll
           for (int q = 0; q < kSplits; ++q) mxs = fmaxf(mxs, mg_ml[2 * q]);
@@ -783,11 +831,11 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
           for (int q = 0; q < kSplits; ++q) {
             const float f = mg_ml[2 * q] != -INFINITY ? mg_ml[2 * q + 1] * __expf(mg_ml[2 * q] - mxs) : 0.0f;
             den += f;
-            num = fmaf(f, mg_o[q * 16 + (lane & 15)], num);
+            num = fmaf(f, mg_o[q * 16 + dm], num);
           }
           const uint32_t xv = f2h(den > 0.0f ? num / den : 0.0f), xp = lane_xor_u32<1>(xv);
-          if (lane < 16 && !(lane & 1))
-            st_gran(a.aog + (g.h * kHd + g.s * 16 + lane) / 2, xv | (xp << 16), pds_tag(epoch, l, PH_MRG));
+          if (lane < HD / 8 && !(lane & 1))
+            st_gran(a.aog + (g.h * HD + g.s * (HD / 8) + lane) / 2, xv | (xp << 16), pds_tag(epoch, l, PH_MRG));
         }
         ts(l, PH_ATT, 4);
       }
@@ -795,37 +843,35 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     // ============================================================== O: residual + fold (ffn_norm)
     {
       ts(l, PH_O, 0);
-      stage_scales(ly.scales[1], bid, 0, 1, g.KTq);
+      stage_scales(ly.scales[1], bid, 0, g.on, g.KTq);
       gathering(true);
       stage_x(a.aog, qd, pds_tag(epoch, l, PH_MRG), false);
       bar();
       gathering(false);
       ts(l, PH_O, 1);
-      gemv_phase(1, g.KTq);
+      gemv_phase(g.on, g.KTq);
       bar();
       ts(l, PH_O, 2);
-      if (c == 0) {
-        resid_fold(ly.ffn_norm, pds_tag(epoch, l, PH_O));
-        ts(l, PH_O, 3);
-      }
+      if (c == 0 && g.on) resid_fold(ly.ffn_norm, pds_tag(epoch, l, PH_O));
+      ts(l, PH_O, 3);
     }
     // ============================================================== gate/up: SiLU * up
     {
       ts(l, PH_GU, 0);
-      stage_scales(ly.scales[2], g.gu0, 1, g.gu_ntl, g.KTh);
+      stage_scales(ly.scales[2], g.gu0, 1, g.gun, g.KTh);
       gathering(true);
       stage_x(a.fxg, H, pds_tag(epoch, l, PH_O), false);
-      if (c == 0) rms = fold_rms(a.ssg, a.grid, H, pds_tag(epoch, l, PH_O), false);
+      if (c == 0) rms = fold_rms(a.ssg, a.nt_h, H, pds_tag(epoch, l, PH_O), false);
       bar();
       gathering(false);
       ts(l, PH_GU, 1);
-      gemv_phase(g.gu_ntl, g.KTh);
+      gemv_phase(g.gun, g.KTh);
       bar();
       ts(l, PH_GU, 2);
       if (c == 0) {
-        for (int tb = 0; tb < g.gu_ntl * 16; tb += kWave) {
+        for (int tb = 0; tb < g.gun * 16; tb += kWave) {
           const int t = tb + lane, tl = t >> 4, n = lane & 15;
-          const bool ok = t < g.gu_ntl * 16;
+          const bool ok = t < g.gun * 16;
           const float v = (ok ? tile_sum(tl, n) : 0.0f) / rms;
           const float up = lane_xor<8>(v);
           const float s = v / (1.0f + expf(-v));
@@ -839,57 +885,76 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     // ============================================================== down: residual + fold (next norm)
     {
       ts(l, PH_DN, 0);
-      stage_scales(ly.scales[3], bid, 0, 1, g.KTi);
+      stage_scales(ly.scales[3], bid, 0, g.on, g.KTi);
       gathering(true);
       stage_x(a.actg, I, pds_tag(epoch, l, PH_GU), false);
       bar();
       gathering(false);
       ts(l, PH_DN, 1);
-      gemv_phase(1, g.KTi);
+      gemv_phase(g.on, g.KTi);
       bar();
       ts(l, PH_DN, 2);
-      if (c == 0) {
-        // the last layer's fold goes to the lm_head launch: plain write-through stores
-        if (!(l == 0 && bid == a.drop_wg && l + 1 < a.n_layers))
-          resid_fold(l + 1 < a.n_layers ? a.layers[l + 1].attn_norm : a.out_norm,
-                     l + 1 < a.n_layers ? pds_tag(epoch, l, PH_DN) : 0u);
-        ts(l, PH_DN, 3);
-      }
+      // the last layer's fold goes to the lm_head launch: plain write-through stores
+      if (c == 0 && g.on && !(l == 0 && bid == a.drop_wg && l + 1 < a.n_layers))
+        resid_fold(l + 1 < a.n_layers ? a.layers[l + 1].attn_norm : a.out_norm,
+                   l + 1 < a.n_layers ? pds_tag(epoch, l, PH_DN) : 0u);
+      ts(l, PH_DN, 3);
     }
   }
-  if (c == 0 && lane < 16) gptr_w(a.h)[bid * 16 + lane] = h_l[lane];
+  if (c == 0 && lane < 16 && g.on) gptr_w(a.h)[bid * 16 + lane] = h_l[lane];
 }
 
 }  // namespace ti
 
 using namespace ti;
 
+namespace {
+template <int BITS, int HD>
+const void* pds_fn() { return (const void*)pds_kernel<BITS, HD>; }
+}  // namespace
+
 extern "C" {
 
 size_t ti_pds_granule_words(int H, int I, int qd, int heads, int grid) { return pds_gran_words(H, I, qd, heads, grid); }
+
+int ti_pds_supported(int bits, int H, int I, int heads, int kv_heads, int head_dim, int grid, int layers) {
+  if ((bits != 4 && bits != 8) || (head_dim != 64 && head_dim != 128) || heads < 1 || kv_heads < 1 || heads % kv_heads)
+    return 0;
+  int sh = 0;
+  while ((kv_heads << sh) < heads) ++sh;
+  if ((kv_heads << sh) != heads || grid != heads * kSplits || grid > 256 || layers < 1 || layers > 64) return 0;
+  const int qd = heads * head_dim, kvd = kv_heads * head_dim;
+  if (H % 128 || I % 128 || qd % 128 || H / 16 > grid) return 0;
+  const int nt_qkv = (qd + 2 * kvd) / 16, nt_gu = 2 * I / 16;
+  if ((nt_qkv + grid - 1) / grid > kMaxQkvTiles || (nt_gu + grid - 1) / grid > kMaxGuTiles) return 0;
+  return 1;
+}
 
 int ti_pds_decode(const ti_pds_args* h, ti_stream_t s) {
   if (!h || !h->layers || !h->pos || !h->h || !h->fx || !h->ss || !h->launches || !h->err || !h->zero ||
       !h->rope_cs || !h->out_norm || !h->gran)
     return ti_set_error(TI_ERR_ARG, "ti_pds_decode: null pointer");
-  if (h->n_layers < 1 || h->n_layers > 64)
-    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_pds_decode: %d layers (granule tags hold 64)", h->n_layers);
-  if (h->head_dim != kHd || h->heads != h->kv_heads || h->heads * kSplits != h->grid || h->grid > 256 ||
-      h->qd != h->heads * h->head_dim || h->H % 128 || h->I % 128 || h->H / 16 != h->grid || h->qd != h->H)
-    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_pds_decode: shape not supported (heads %d kv %d hd %d grid %d H %d I %d)",
-                        h->heads, h->kv_heads, h->head_dim, h->grid, h->H, h->I);
+  if (!ti_pds_supported(h->bits, h->H, h->I, h->heads, h->kv_heads, h->head_dim, h->grid, h->n_layers) ||
+      h->qd != h->heads * h->head_dim)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_pds_decode: shape not supported (bits %d heads %d kv %d hd %d grid %d H %d "
+                        "I %d layers %d)", h->bits, h->heads, h->kv_heads, h->head_dim, h->grid, h->H, h->I, h->n_layers);
+  const int HD = h->head_dim;
   PdsArgs a{};
   a.layers = (const PdsLayerDev*)h->layers;
   a.n_layers = h->n_layers;
   a.H = h->H;
   a.I = h->I;
   a.qd = h->qd;
+  a.kvd = h->kv_heads * HD;
   a.max_seq = h->max_seq;
   a.n_ss0 = h->n_ss0;
   a.heads = h->heads;
+  while ((h->kv_heads << a.kv_shift) < h->heads) ++a.kv_shift;
   a.grid = h->grid;
+  a.nt_h = h->H / 16;
+  a.head_group = HD == 128 && h->heads == h->kv_heads && h->qd / 16 == h->grid;
   a.eps = h->eps;
-  a.scale = 1.0f / sqrtf((float)h->head_dim);
+  a.scale = 1.0f / sqrtf((float)HD);
   a.pos = h->pos;
   a.rope_cs = h->rope_cs;
   a.out_norm = h->out_norm;
@@ -905,21 +970,21 @@ int ti_pds_decode(const ti_pds_args* h, ti_stream_t s) {
   a.ssg = a.fxg + h->H / 2;
   a.qg = a.ssg + h->grid;
   a.kvg = a.qg + h->qd;
-  a.partg = a.kvg + (size_t)h->heads * kHd;
-  a.aog = a.partg + (size_t)h->heads * kSplits * kPartG;
+  a.partg = a.kvg + (size_t)h->heads * kHdMax;
+  a.aog = a.partg + (size_t)h->heads * kSplits * (kHdMax / 2 + 2);
   a.actg = a.aog + h->qd / 2;
   // LDS: ring, x [max K + 8] fp16, scales, corr, slab, attention / control scratch
   const int KTh = h->H / 128, KTi = h->I / 128, KTq = h->qd / 128;
-  const int NTg = 2 * h->I / 16, gu_ntl = (NTg + h->grid - 1) / h->grid;
-  if (gu_ntl > 8) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_pds_decode: %d gate/up tiles per workgroup", gu_ntl);
+  const int nt_qkv = (a.qd + 2 * a.kvd) / 16, NTg = 2 * h->I / 16;
+  const int q_ntl = a.head_group ? 3 : (nt_qkv + h->grid - 1) / h->grid, gu_ntl = (NTg + h->grid - 1) / h->grid;
   const int kmax = std::max(h->H, std::max(h->I, h->qd));
-  const int sc_bytes = std::max(std::max(3 * KTh, gu_ntl * KTh), std::max(KTq, KTi)) * 32;
-  const int ntl_max = std::max(3, gu_ntl);
+  const int sc_bytes = std::max(std::max(q_ntl * KTh, gu_ntl * KTh), std::max(KTq, KTi)) * 32;
+  const int ntl_max = std::max(q_ntl, gu_ntl);
   auto al = [](int b) { return (b + 15) & ~15; };
+  const int att_bytes = (kVW * kHdMax + 2 * kVW + kHdMax) * 4 + 2 * kHdMax * 2 + kHdMax * 4 + 16 * 4 +
+                        kSplits * 16 * 4 + kSplits * 2 * 4;
   const int rest = al((kmax + 8) * 2) + al(sc_bytes) + al(std::max(KTh, std::max(KTi, KTq)) * 4) +
-                   al(ntl_max * kVW * 16 * 4) + al((kVW * kHd + 2 * kVW + kHd) * 4 + 2 * kHd * 2 + kHd * 4 + 16 * 4 +
-                                                   kSplits * 16 * 4 + kSplits * 2 * 4) +
-                   C_WORDS * 4;
+                   al(ntl_max * kVW * 16 * 4) + al(att_bytes) + C_WORDS * 4;
   const int lds_cap = 160 * 1024;
   const int n_slots = std::min(kMaxSlots, (lds_cap - rest) / kSlotBytes);
   if (n_slots < 3) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_pds_decode: LDS ring of %d slots", n_slots);
@@ -929,35 +994,40 @@ int ti_pds_decode(const ti_pds_args* h, ti_stream_t s) {
   a.l_corr = a.l_sc + al(sc_bytes);
   a.l_slab = a.l_corr + al(std::max(KTh, std::max(KTi, KTq)) * 4);
   a.l_att = a.l_slab + al(ntl_max * kVW * 16 * 4);
-  a.l_ctl = a.l_att + al((kVW * kHd + 2 * kVW + kHd) * 4 + 2 * kHd * 2 + kHd * 4 + 16 * 4 + kSplits * 16 * 4 +
-                         kSplits * 2 * 4);
+  a.l_ctl = a.l_att + al(att_bytes);
   a.l_total = a.l_ctl + C_WORDS * 4;
-  // per device: the LDS attribute and co-residency -- every wait needs all `grid` workgroups resident
-  // at once (one per CU): the occupancy query times the CU count must cover the grid, or nothing is
-  // launched (residency taken by other work at run time is caught by the bounded waits).
-  static std::atomic<unsigned long long> attr{0};
-  static std::atomic<int> resident[64];
+  const void* fn = h->bits == 4 ? (HD == 128 ? pds_fn<4, 128>() : pds_fn<4, 64>())
+                                : (HD == 128 ? pds_fn<8, 128>() : pds_fn<8, 64>());
+  const int variant = (h->bits == 8 ? 2 : 0) + (HD == 64 ? 1 : 0);
+  // per device and variant: the LDS attribute and co-residency -- every wait needs all `grid`
+  // workgroups resident at once (one per CU): the occupancy query times the CU count must cover
+  // the grid, or nothing is launched (residency taken by other work at run time is caught by the
+  // bounded waits).
+  static std::atomic<unsigned long long> prepared[4];
+  static std::atomic<int> resident[4][64];
   static std::mutex mu;
   int dev = 0;
   TI_HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
   dev &= 63;
-  if (!(attr.load() >> dev & 1ull)) {
+  if (!(prepared[variant].load() >> dev & 1ull)) {
     std::lock_guard<std::mutex> lk(mu);
-    if (!(attr.load() >> dev & 1ull)) {
-      TI_HIP_CHECK(hipFuncSetAttribute((const void*)pds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_cap),
+    if (!(prepared[variant].load() >> dev & 1ull)) {
+      TI_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_cap),
                    "hipFuncSetAttribute(pds_kernel)");
       int per_cu = 0, cus = 0;
-      TI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pds_kernel, kEThreads, lds_cap),
+      TI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kEThreads, lds_cap),
                    "hipOccupancyMaxActiveBlocksPerMultiprocessor(pds_kernel)");
       TI_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute(CUs)");
-      resident[dev].store(per_cu * cus);
-      attr.fetch_or(1ull << dev);
+      resident[variant][dev].store(per_cu * cus);
+      prepared[variant].fetch_or(1ull << dev);
     }
   }
-  if (resident[dev].load() < h->grid)
+  if (resident[variant][dev].load() < h->grid)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_pds_decode: %d workgroups cannot all be resident (%d)", h->grid,
-                        resident[dev].load());
-  hipLaunchKernelGGL(pds_kernel, dim3(h->grid), dim3(kEThreads), a.l_total, (hipStream_t)s, a);
+                        resident[variant][dev].load());
+  void* args[] = {&a};
+  TI_HIP_CHECK(hipLaunchKernel(fn, dim3(h->grid), dim3(kEThreads), args, a.l_total, (hipStream_t)s),
+               "hipLaunchKernel(pds_kernel)");
   TI_LAUNCH_CHECK("pds_kernel");
   return TI_OK;
 }
