@@ -200,12 +200,19 @@ typedef struct ti_epilogue {
   unsigned long long* argmax;        /* device [M][TI_ARGMAX_SLOTS] keys, zeroed before the call */
   int32_t* step_ctr;                 /* device counter += advance by one thread (nullable) */
   int32_t advance;
-  /* TI_X_F16_FOLDED input: n_ss partial sums of squares of the row at ss_in */
+  /* TI_X_F16_FOLDED input: n_ss partial sums of squares of the row at ss_in.
+   * Batched fold (17..64 int4 rows, TI_X_F16 / TI_X_F16_PACKED x holding fp16(h * nw), ss_in
+   * non-NULL): row m is normalised behind the GEMM, y[m] = (W . x[m]) / sqrt(sum over
+   * b < n_ss of ss_in[b * TI_FOLD_SS_ROWS + m] / K + eps) -- the batched-rows / tile kernels */
   int32_t n_ss;
   const float* ss_in;
   /* TI_EPI_RESID_F32, M == 1, fold_x non-NULL: besides h, write fold_x[n] = fp16(h[n] * fold_w[n])
    * and fold_ss[b] = sum of h[n]^2 over the outputs of workgroup b (b < ti_gemm_grid(...)): the
-   * next launch's TI_X_F16_FOLDED input */
+   * next launch's TI_X_F16_FOLDED input.
+   * M = 17..64 on the batched-rows kernel (TI_X_F16_PACKED x): fold_x[m][n] = fp16(h[m][n] *
+   * fold_w[n]) (TI_X_F16_PACKED order when fold_packed, else rows of ldo) and
+   * fold_ss[b * TI_FOLD_SS_ROWS + m] = sum of h[m][n]^2 over the columns of column group b
+   * (b < ti_gemm_fold_partials(...)): the next batched call's folded input */
   const float* fold_w;
   uint16_t* fold_x;
   float* fold_ss;
@@ -219,7 +226,9 @@ typedef struct ti_epilogue {
    * workspace (stream order). */
   void* splitk_ws;
   int64_t splitk_bytes;
+  int32_t fold_packed;
 } ti_epilogue;
+#define TI_FOLD_SS_ROWS 64
 #define TI_SPLITK_TICKET_BYTES (256 * 1024)
 /* sizeof(ti_epilogue): a binding checks its mirror of the struct against it. */
 int ti_epilogue_bytes(void);
@@ -260,6 +269,10 @@ int ti_rmsnorm_f16_packed(const float* x, int ldx, const float* w, float eps, ui
 /* Workgroups of the fused kernel for an M x N x K call: the fold_ss partials a
  * TI_EPI_RESID_F32 fold epilogue writes (0 = shape not taken by the fused kernel). */
 int ti_gemm_grid(int M, int N, int K);
+/* Column groups of the batched-rows kernel for an int4 TI_X_F16_PACKED M x N x K call (17..64
+ * rows): the fold_ss partials per row its TI_EPI_RESID_F32 fold epilogue writes (0 = the call
+ * does not take the batched-rows kernel). */
+int ti_gemm_fold_partials(int bits, int M, int N, int K);
 /* One-time kernel attribute setup; call before capturing ti_gemm_wq_a16 into a graph. */
 int ti_gemm_prepare(void);
 

@@ -376,3 +376,95 @@ def test_packed_operands_match_row_major(ti, oracle):
     ti.sync()
     np.testing.assert_array_equal(ti.unpack_rows(o_pk.download(np.uint16, Mp * heads * hd), M, heads * hd),
                                   o_rm.download(np.uint16, (M, heads * hd)))
+
+
+# ------------------------------------------------------- batched fold (17..64 rows)
+@pytest.mark.parametrize("M", [17, 32, 45, 64])
+@pytest.mark.parametrize("packed", [1, 0])
+def test_batched_fold_producer_consumer(ti, oracle, M, packed):
+    """The batched fold (ti_hip.h TI_FOLD_SS_ROWS): a batched-rows residual epilogue also writes
+    fp16(h * nw) (fragment-packed or row-major) and per-column-group sums of h^2 per row; the
+    next call takes those rows with ss_in and normalises behind its GEMM.  Against the rms_norm
+    prep path (ti_rmsnorm_f16[_packed] + the same GEMM): the two differ only in where the fp16
+    rounding of the normalised row happens (rtol 4e-3 on the outputs)."""
+    L = ti.lib()
+    K, H, N = 1152, 1024, 768 if packed else 25600   # consumer: rows kernel (packed) / tile kernel
+    assert L.ti_gemm_packed_rows_for(4, M, N, H) == packed
+    rng = np.random.RandomState(M + 100 * packed)
+    act = rng.standard_normal((M, K)).astype(f16)
+    wo = (rng.standard_normal((K, H)) * 0.03).astype(f32)
+    h0 = rng.standard_normal((M, H)).astype(f32)
+    nw = (1 + 0.1 * rng.standard_normal(H)).astype(f32)
+    to, so = ti.wpack_host(wo, 4)
+    tod, sod, actd, nwd = dev(ti, to), dev(ti, so), dev(ti, ti.pack_rows(act)), dev(ti, nw)
+    n_ss = L.ti_gemm_fold_partials(4, M, H, K)
+    assert 1 <= n_ss <= 4096
+    Mp = (M + 15) // 16 * 16
+    hd, fx, ss = dev(ti, h0), ti.DeviceBuffer(Mp * H * 2), ti.DeviceBuffer(n_ss * 64 * 4)
+    fx.zero()
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_RESID_F32, H, hd.ptr
+    ep.fold_w, ep.fold_x, ep.fold_ss, ep.fold_packed = nwd.ptr, fx.ptr, ss.ptr, packed
+    ti.check(L.ti_gemm_wq_a16(tod.ptr, sod.ptr, 4, actd.ptr, ti.X_F16_PACKED, K, None, 1e-5, M, H, K, C.byref(ep), None))
+    ti.sync()
+    h1 = hd.download(f32, (M, H))
+    assert_close_dot(h1 - h0, act.astype(np.float64) @ deq(oracle, wo, 4).astype(np.float64), act.astype(f32),
+                     deq(oracle, wo, 4), rel=5e-5)
+    # the folded outputs: exactly fp16(h * nw) of the stored h, and the row sums of h^2
+    fxr = fx.download(np.uint16, Mp * H)
+    fxr = ti.unpack_rows(fxr, M, H) if packed else fxr[: M * H].reshape(M, H)
+    np.testing.assert_array_equal(fxr, (h1 * nw).astype(f16).view(np.uint16))
+    ssr = ss.download(f32, (n_ss, 64))[:, :M].sum(axis=0)
+    np.testing.assert_allclose(ssr, (h1.astype(np.float64) ** 2).sum(axis=1), rtol=1e-5)
+    # consumer: folded rows + ss_in against the rms_norm prep of the same h
+    w2 = (rng.standard_normal((H, N)) * 0.03).astype(f32)
+    t2, s2 = ti.wpack_host(w2, 4)
+    t2d, s2d = dev(ti, t2), dev(ti, s2)
+    outs = []
+    for fold in (True, False):
+        yd = ti.DeviceBuffer(M * N * 4)
+        ep = ti.Epilogue()
+        ep.kind, ep.ldo, ep.out = ti.EPI_STORE_F32, N, yd.ptr
+        xk = ti.X_F16_PACKED if packed else ti.X_F16
+        if fold:
+            ep.ss_in, ep.n_ss = ss.ptr, n_ss
+            src = fx
+        else:
+            src = ti.DeviceBuffer(Mp * H * 2)
+            fn = L.ti_rmsnorm_f16_packed if packed else None
+            if packed:
+                ti.check(fn(hd.ptr, H, nwd.ptr, 1e-5, src.ptr, M, H, None))
+            else:
+                ti.check(L.ti_rmsnorm_f16(hd.ptr, H, nwd.ptr, 1e-5, src.ptr, H, M, H, None))
+        ti.check(L.ti_gemm_wq_a16(t2d.ptr, s2d.ptr, 4, src.ptr, xk, H, None, 1e-5, M, N, H, C.byref(ep), None))
+        ti.sync()
+        outs.append(yd.download(f32, (M, N)))
+    rms = np.sqrt((h1.astype(np.float64) ** 2).mean(axis=1) + 1e-5)
+    ref = ((h1 / rms[:, None]) * nw).astype(np.float64) @ deq(oracle, w2, 4).astype(np.float64)
+    scale = np.abs(ref).max()
+    assert np.abs(outs[0] - ref).max() <= 4e-3 * scale
+    assert np.abs(outs[0] - outs[1]).max() <= 4e-3 * scale
+    # a repeated folded call gives the same bits (fixed-order partial sums)
+    yd = ti.DeviceBuffer(M * N * 4)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out, ep.ss_in, ep.n_ss = ti.EPI_STORE_F32, N, yd.ptr, ss.ptr, n_ss
+    ti.check(L.ti_gemm_wq_a16(t2d.ptr, s2d.ptr, 4, fx.ptr, ti.X_F16_PACKED if packed else ti.X_F16, H, None, 1e-5, M,
+                              N, H, C.byref(ep), None))
+    ti.sync()
+    np.testing.assert_array_equal(yd.download(f32, (M, N)).view(np.uint32), outs[0].view(np.uint32))
+
+
+def test_batched_fold_refuses_other_kernels(ti):
+    """fold_x at M > 1 needs packed x (the batched-rows kernel); a folded input needs M <= 64."""
+    L = ti.lib()
+    M, K, N = 40, 1152, 512
+    buf = ti.DeviceBuffer(128 * 4096 * 4)
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out = ti.EPI_RESID_F32, N, buf.ptr
+    ep.fold_w, ep.fold_x, ep.fold_ss = buf.ptr, buf.ptr, buf.ptr
+    tiles, scales = ti.wpack_host(np.zeros((K, N), f32), 4)
+    td, sd = dev(ti, tiles), dev(ti, scales)
+    assert L.ti_gemm_wq_a16(td.ptr, sd.ptr, 4, buf.ptr, ti.X_F16, K, None, 1e-5, M, N, K, C.byref(ep), None) != 0
+    ep = ti.Epilogue()
+    ep.kind, ep.ldo, ep.out, ep.ss_in, ep.n_ss = ti.EPI_STORE_F32, N, buf.ptr, buf.ptr, 4
+    assert L.ti_gemm_wq_a16(td.ptr, sd.ptr, 4, buf.ptr, ti.X_F16, K, None, 1e-5, 100, N, K, C.byref(ep), None) != 0

@@ -46,7 +46,7 @@ class Epilogue(C.Structure):
                 ("kv_stream_stride", C.c_int64), ("argmax", C.c_void_p), ("step_ctr", C.c_void_p),
                 ("advance", C.c_int32), ("n_ss", C.c_int32), ("ss_in", C.c_void_p),
                 ("fold_w", C.c_void_p), ("fold_x", C.c_void_p), ("fold_ss", C.c_void_p), ("out_packed", C.c_int32),
-                ("splitk_ws", C.c_void_p), ("splitk_bytes", C.c_int64)]
+                ("splitk_ws", C.c_void_p), ("splitk_bytes", C.c_int64), ("fold_packed", C.c_int32)]
 
 
 class StepArgs(C.Structure):
@@ -87,6 +87,7 @@ EXPORTED = [
     "ti_wpack_q_host", "ti_engine_set_tensor_q", "ti_sample_workspace_bytes", "ti_sample_device_ws",
     "ti_wpack_q1_host", "ti_engine_set_tensor_q1", "ti_epilogue_bytes",
     "ti_sample_step_ws", "ti_pds_granule_words", "ti_hbm_calibrate", "ti_gemm_kernel_name", "ti_pds_supported",
+    "ti_gemm_fold_partials",
 ]
 
 _lib = None
@@ -125,6 +126,7 @@ def lib() -> C.CDLL:
         L.ti_fill_kv_uniform.argtypes = [u64, C.c_uint32, i32, i32, i32, i32, vp, vp]
         L.ti_kv_copy_slots.argtypes = [vp, i32, C.c_int64, C.c_int64, i32, C.c_int64, C.c_int64, vp]
         L.ti_gemm_wq_a16.argtypes = [vp, vp, i32, vp, i32, i32, vp, f32, i32, i32, i32, C.POINTER(Epilogue), vp]
+        L.ti_gemm_fold_partials.argtypes = [i32, i32, i32, i32]
         L.ti_gemm_lds_bytes.argtypes = [i32, i32, i32]
         L.ti_gemm_max_rows.argtypes = [i32, i32, i32, i32]
         L.ti_gemm_packed_rows.argtypes = [i32, i32]

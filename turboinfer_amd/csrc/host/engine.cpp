@@ -95,6 +95,9 @@ struct ti_engine {
   bool fold_on = true;         // TI_FOLD=0 / ti_engine_set_fold
   uint16_t* fx = nullptr;      // [hidden]
   float* ss = nullptr;         // [256]
+  // batched fold (17..64 int4 rows): the producers' (O, down) epilogues write xn = fp16(h * next
+  // norm weight) and per-column-group sums of h^2 per row [n_cg][TI_FOLD_SS_ROWS]
+  float* ss_rows = nullptr;
   // single-stream attention leaves its split merge to the O projection (ti_attn_decode_partials
   // + TI_X_ATTN_SPLITS): no arrival-ticket hand-off at the end of the attention launch
   bool part_on = true;         // TI_ATTN_PART=0 turns it off
@@ -344,6 +347,16 @@ bool fold_usable(ti_engine* e, int M) {
   return g_o > 0 && g_o <= 256 && g_d > 0 && g_d <= 256 && ti_gemm_max_rows(c.bits, TI_X_F16, H, qd) >= 1;
 }
 
+// The batched fold: 17..64 int4 rows on the batched-rows kernels (packed operands), the O / down
+// producers' column groups within the partial buffer.
+bool bfold_usable(ti_engine* e, int M) {
+  const ti_engine_config& c = e->c;
+  if (!e->fold_on || c.compat || c.bits != 4 || M <= 16 || M > TI_FOLD_SS_ROWS || !packed_rows(e, M) || !e->ss_rows)
+    return false;
+  const int po = ti_gemm_fold_partials(c.bits, M, c.hidden, e->qd()), pd = ti_gemm_fold_partials(c.bits, M, c.hidden, c.inter);
+  return po >= 1 && po <= 4096 && pd >= 1 && pd <= 4096;
+}
+
 // Split partials merged by the O projection: one stream, 2..8 splits, heads*head_dim <= 4096.
 bool part_usable(ti_engine* e, int M) {
   const ti_engine_config& c = e->c;
@@ -429,7 +442,12 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
   // fold (M == 1): every rms_norm input is handed over as fx + ss partials by its producer
   const bool fold = fold_usable(e, M), part = part_usable(e, M), pk = packed_rows(e, M);
+  // batched fold (17..64 rows): O / down write xn = fp16(h * next norm weight) and per-row sums of
+  // h^2; QKV (after layer 0), gate/up and the lm_head normalise behind their GEMM (ti_hip.h)
+  const bool bfold = !fold && bfold_usable(e, M);
+  int bn_ss = 0;   // partials per row the last batched producer wrote (0: none yet, rms_norm prep)
   auto next_norm = [&](int l) -> const float* { return l < c.layers ? e->layer[l].attn_norm : e->out_norm; };
+  auto next_n = [&](int l) -> int { return l < c.layers ? e->layer[l].qkv.N : e->lm.N; };
   if (fold) {
     sa.fold_w = next_norm(0);
     sa.fold_x = e->fx;
@@ -437,27 +455,43 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   }
   TI_TRY(ti_step_begin(&sa, e->s));
   int n_ss = 1;   // partials the last producer wrote (step_begin: one)
-  auto fold_into = [&](ti_epilogue& ep, const float* w) {   // producer side (RESID epilogue)
-    if (!fold) return;
-    ep.fold_w = w;
-    ep.fold_x = e->fx;
-    ep.fold_ss = e->ss;
+  // producer side (RESID epilogue); n_next: output width of the call that consumes the fold
+  auto fold_into = [&](ti_epilogue& ep, const float* w, int n_next) {
+    if (fold) {
+      ep.fold_w = w;
+      ep.fold_x = e->fx;
+      ep.fold_ss = e->ss;
+    } else if (bfold) {
+      ep.fold_w = w;
+      ep.fold_x = e->xn;
+      ep.fold_ss = e->ss_rows;
+      ep.fold_packed = ti_gemm_packed_rows_for(c.bits, M, n_next, H);
+    }
   };
-  auto norm_in = [&](const void*& x, int& xk, int& ldx, const float*& nw, ti_epilogue& ep) {   // consumer side
-    if (!fold) return;
-    x = e->fx;
-    xk = TI_X_F16_FOLDED;
-    ldx = H;
-    nw = nullptr;
-    ep.ss_in = e->ss;
-    ep.n_ss = n_ss;
+  auto norm_in = [&](const void*& x, int& xk, int& ldx, const float*& nw, ti_epilogue& ep, int n) {   // consumer side
+    if (fold) {
+      x = e->fx;
+      xk = TI_X_F16_FOLDED;
+      ldx = H;
+      nw = nullptr;
+      ep.ss_in = e->ss;
+      ep.n_ss = n_ss;
+    } else if (bfold && bn_ss > 0) {
+      x = e->xn;
+      xk = ti_gemm_packed_rows_for(c.bits, M, n, H) ? TI_X_F16_PACKED : TI_X_F16;
+      ldx = H;
+      nw = nullptr;
+      ep.ss_in = e->ss_rows;
+      ep.n_ss = bn_ss;
+    }
   };
 
   auto gemm = [&](const DevLinear& W, const void* x, int x_kind, int ldx, size_t /*x_elem*/, const float* nw,
                   ti_epilogue epi, size_t out_elem, bool last_gets_ctr) -> int {
-    if (x_kind == TI_X_F32_RMSNORM) norm_in(x, x_kind, ldx, nw, epi);
+    if (x_kind == TI_X_F32_RMSNORM) norm_in(x, x_kind, ldx, nw, epi, W.N);
     TI_TRY(gemm_rows(e, W, M, x, x_kind, ldx, nw, epi, out_elem, last_gets_ctr));
-    if (epi.fold_x) n_ss = ti_gemm_grid(M, W.N, W.K);
+    if (epi.fold_x && fold) n_ss = ti_gemm_grid(M, W.N, W.K);
+    if (epi.fold_x && bfold) bn_ss = ti_gemm_fold_partials(c.bits, M, W.N, W.K);
     return TI_OK;
   };
 
@@ -485,7 +519,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     eo.kind = TI_EPI_RESID_F32;
     eo.ldo = H;
     eo.out = e->h;
-    fold_into(eo, L.ffn_norm);
+    fold_into(eo, L.ffn_norm, L.gu.N);
     if (part) {   // the O projection merges the attention's splits while staging its input
       TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));
       TI_TRY(ti_attn_decode_partials(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M, c.heads, c.kv_heads,
@@ -513,7 +547,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     ed.kind = TI_EPI_RESID_F32;
     ed.ldo = H;
     ed.out = e->h;
-    fold_into(ed, next_norm(l + 1));
+    fold_into(ed, next_norm(l + 1), next_n(l + 1));
     TI_TRY(gemm(L.down, e->act, pk ? TI_X_F16_PACKED : TI_X_F16, I, 2, nullptr, ed, 4, false));
   }
   ti_epilogue el{};
@@ -740,7 +774,7 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
         (rc = e->alloc(reinterpret_cast<void**>(&e->ws), ws_bytes(e))) ||
         (rc = e->alloc_t(&e->pf_ones, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->pf_zero, (size_t)1)) ||
         (rc = e->alloc_t(&e->pf_base, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->fx, (size_t)H)) ||
-        (rc = e->alloc_t(&e->ss, (size_t)256)) ||
+        (rc = e->alloc_t(&e->ss, (size_t)256)) || (rc = e->alloc_t(&e->ss_rows, (size_t)4096 * TI_FOLD_SS_ROWS)) ||
         (rc = e->alloc_t(&e->part_o, (size_t)c.heads * TI_ATTN_MAX_PART_SPLITS * hd)) ||
         (rc = e->alloc_t(&e->part_ml, (size_t)c.heads * TI_ATTN_MAX_PART_SPLITS * 2)))
       return fail(rc);
@@ -1557,7 +1591,7 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
   DeviceScope bind_(e);
   const ti_engine_config& c = e->c;
   const int H = c.hidden, I = c.inter, qd = e->qd(), kvd = e->kvd();
-  const bool fold = fold_usable(e, n), part = part_usable(e, n);
+  const bool fold = fold_usable(e, n), part = part_usable(e, n), bfold = !fold && bfold_usable(e, n);
   // Launch r uses layer r % layers, so (as in a real step) its weights are not still in
   // the 256 MB Infinity Cache from the previous launch.
   int cur = 0;
@@ -1590,6 +1624,12 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
         ep.fold_w = L.ffn_norm;
         ep.fold_x = e->fx;
         ep.fold_ss = e->ss;
+      } else if (bfold) {   // the batched fold's producer form (enqueue_step)
+        ep.kind = TI_EPI_RESID_F32;
+        ep.fold_w = L.ffn_norm;
+        ep.fold_x = e->xn;
+        ep.fold_ss = e->ss_rows;
+        ep.fold_packed = ti_gemm_packed_rows_for(c.bits, n, which == 1 ? L.gu.N : L.qkv.N, H);
       }
       if (which == 1 && part) {   // O merges the attention's split partials
         x = e->part_o;
@@ -1607,6 +1647,12 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
       nw = nullptr;
       ep.ss_in = e->ss;
       ep.n_ss = ti_gemm_grid(1, H, which == 2 ? qd : I);
+    } else if (bfold && xk == TI_X_F32_RMSNORM) {   // the batched fold's consumer form
+      x = e->xn;
+      xk = ti_gemm_packed_rows_for(c.bits, n, W->N, H) ? TI_X_F16_PACKED : TI_X_F16;
+      nw = nullptr;
+      ep.ss_in = e->ss_rows;
+      ep.n_ss = ti_gemm_fold_partials(c.bits, n, H, which == 2 ? qd : I);
     }
     return TI_OK;
   };
@@ -1616,6 +1662,10 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
   const float* nw = nullptr;
   ti_epilogue ep{};
   TI_TRY(setup(e->layer[0], W, x, xk, ldx, nw, ep));
+  if (ep.ss_in == e->ss_rows && ep.n_ss > 0) {   // batched fold: partials of rms 1 per row
+    const float v = (float)H / (float)ep.n_ss;
+    TI_TRY(ti_fill_uniform_f32(1, 0, (uint64_t)ep.n_ss * TI_FOLD_SS_ROWS, 0.0f, v, e->ss_rows, e->s));
+  }
   std::vector<int32_t> base(n, kv_len - 1);
   TI_TRY(ti_memcpy_h2d(e->pos, base.data(), (size_t)n * 4, e->s));
   auto launch = [&]() -> int {

@@ -28,15 +28,15 @@
 
 namespace ti {
 
-template <int HD, int G, int R, bool HP>
-__global__ __launch_bounds__(kAttnThreads, 1) void attn_split_kernel(const AttnArgs a) {
-  attn_split_body<HD, G, R, HP>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+template <int HD, int G, int R, bool HP, int NW, bool ROT>
+__global__ __launch_bounds__(NW * kWave, 1) void attn_split_kernel(const AttnArgs a) {
+  attn_split_body<HD, G, R, HP, NW, ROT>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
-template <int HD, int G, int R, bool HP>
-static int launch_one(const AttnArgs& a, hipStream_t s) {
+template <int HD, int G, int R, bool HP, int NW = kAttnWaves, bool ROT = false>
+static int launch_one(const AttnArgs& a, hipStream_t s, size_t lds_pad = 0) {
   const dim3 grid(a.splits, a.kv_heads, a.M);
-  hipLaunchKernelGGL((attn_split_kernel<HD, G, R, HP>), grid, dim3(kAttnThreads), 0, s, a);
+  hipLaunchKernelGGL((attn_split_kernel<HD, G, R, HP, NW, ROT>), grid, dim3(NW * kWave), lds_pad, s, a);
   TI_LAUNCH_CHECK("attn_split_kernel");
   return TI_OK;
 }
@@ -50,7 +50,17 @@ static int launch_attn(const AttnArgs& a, hipStream_t s) {
   if constexpr (TI_ATTN_HP && G >= 4 && HD / (64 / G) == 8) {
     if (!long_range) return launch_one<HD, G, TI_ATTN_RING_HP, true>(a, s);   // head-parallel lanes
   }
-  if (long_range) return launch_one<HD, G, TI_ATTN_RING_LONG, false>(a, s);
+#ifndef TI_ATTN_LONG_WAVES
+#define TI_ATTN_LONG_WAVES 8
+#endif
+#ifndef TI_ATTN_LONG_PAD
+#define TI_ATTN_LONG_PAD 0   // dynamic LDS bytes added to the long-range launch (1 workgroup per CU)
+#endif
+#ifndef TI_ATTN_LONG_ROT
+#define TI_ATTN_LONG_ROT 0
+#endif
+  if (long_range)
+    return launch_one<HD, G, TI_ATTN_RING_LONG, false, TI_ATTN_LONG_WAVES, TI_ATTN_LONG_ROT != 0>(a, s, TI_ATTN_LONG_PAD);
   if constexpr (G == 1) {   // one stream, MHA (the 7B decode): 3 slots (bench A/B 745 vs 741 tok/s)
     if (a.M == 1) return launch_one<HD, G, TI_ATTN_RING_M1, false>(a, s);
   }

@@ -113,13 +113,13 @@ __device__ __forceinline__ float groups_sum(float v) {
   else return v;
 }
 
-template <int HD, int G, int R, bool HP>   // HP: head-parallel lanes (G >= 4, HD / (64 / G) == 8; see below)
+template <int HD, int G, int R, bool HP, int NW = kAttnWaves, bool ROT = false>   // HP: head-parallel lanes (G >= 4, HD / (64 / G) == 8; see below)
 __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, int kvh, int m) {
   static_assert(!HP || (G >= 4 && HD / (64 / G) == 8), "head-parallel layout: 8 dims per lane");
   constexpr int LPK = HD / 8;       // lanes per key row
   constexpr int KPW = 64 / LPK;     // keys per slot (wave-load)
-  __shared__ float s_m[kAttnWaves][G], s_l[kAttnWaves][G];
-  __shared__ __attribute__((aligned(16))) float s_acc[kAttnWaves][G][HD];
+  __shared__ float s_m[NW][G], s_l[NW][G];
+  __shared__ __attribute__((aligned(16))) float s_acc[NW][G][HD];
   __shared__ __attribute__((aligned(16))) float s_part[48 * 1024 / 4];   // merged rows, then all partials
   __shared__ int s_last;
 
@@ -144,7 +144,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
   const int chunk = (L + a.splits - 1) / a.splits;
   const int s0 = split * chunk, s1 = min(L, s0 + chunk);
   const int nslot = s1 > s0 ? (s1 - s0 + KPW - 1) / KPW : 0;               // slots of the chunk
-  const int total = wave < nslot ? (nslot - wave + kAttnWaves - 1) / kAttnWaves : 0;   // this wave's
+  const int total = wave < nslot ? (nslot - wave + NW - 1) / NW : 0;   // this wave's
 
   if constexpr (HP) {
     // head-parallel layout (G >= 4 q-heads per kv-head): lane l serves q-head l / LPH of the
@@ -153,11 +153,11 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
     constexpr int LPH = 64 / G;
     const int hg = lane / LPH, dh = lane % LPH;
     const int nkey = s1 > s0 ? s1 - s0 : 0;
-    const int total = wave < nkey ? (nkey - wave + kAttnWaves - 1) / kAttnWaves : 0;   // this wave's keys
+    const int total = wave < nkey ? (nkey - wave + NW - 1) / NW : 0;   // this wave's keys
     int rj = 0;
     u32x4 kr[R], vr[R];
     auto refill = [&](int s) {
-      const int key = min(s0 + wave + kAttnWaves * (rj < total ? rj : max(total - 1, 0)), max(s1 - 1, 0));
+      const int key = min(s0 + wave + NW * (rj < total ? rj : max(total - 1, 0)), max(s1 - 1, 0));
       ++rj;
       kr[s] = ld_k((int64_t)key * HD + dh * 8);
       vr[s] = ld_v((int64_t)key * HD + dh * 8);
@@ -216,7 +216,14 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
   } else {
     // the K/V ring first (nothing else to wait for), then q
     int rj = 0;
-    auto slot_key = [&](int i) { return s0 + (wave + kAttnWaves * i) * KPW + kg; };
+    // ROT: each workgroup starts its sweep at its own slot (wrapping), so the workgroups of a
+    // launch do not walk their equally aligned K/V ranges in lockstep
+    const int rot = ROT && nslot > 0 ? (int)(((unsigned)(m * a.kv_heads + kvh) * 61u) % (unsigned)nslot) : 0;
+    auto slot_key = [&](int i) {
+      int j = wave + NW * i;
+      if constexpr (ROT) j = j + rot >= nslot ? j + rot - nslot : j + rot;
+      return s0 + j * KPW + kg;
+    };
     u32x4 kr[R], vr[R];
     auto refill = [&](int s) {
       const int key = min(slot_key(rj < total ? rj : max(total - 1, 0)), max(s1 - 1, 0));
@@ -309,15 +316,15 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
 
   // merge the waves; one thread per (q-head of the group, dim)
   const int row = ws_row(HD);
-  for (int idx = tid; idx < G * HD; idx += kAttnThreads) {
+  for (int idx = tid; idx < G * HD; idx += (NW * kWave)) {
     const int g = idx / HD, d = idx - g * HD;
     float mx = s_m[0][g];
 #pragma unroll
-    for (int w = 1; w < kAttnWaves; ++w) mx = fmaxf(mx, s_m[w][g]);
+    for (int w = 1; w < NW; ++w) mx = fmaxf(mx, s_m[w][g]);
     float o = 0.0f, l = 0.0f;
     if (mx != -INFINITY) {
 #pragma unroll
-      for (int w = 0; w < kAttnWaves; ++w) {
+      for (int w = 0; w < NW; ++w) {
         const float f = s_m[w][g] == -INFINITY ? 0.0f : __expf(s_m[w][g] - mx);
         o = fmaf(f, s_acc[w][g][d], o);
         l = fmaf(f, s_l[w][g], l);
@@ -350,7 +357,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
   // (stream, head) are contiguous: [m][h][split][row].
   constexpr int V4 = (HD + 4) / 4;
   const __amdgpu_buffer_rsrc_t wsr = ws_rsrc(a.ws);
-  for (int i = tid; i < G * V4; i += kAttnThreads) {
+  for (int i = tid; i < G * V4; i += (NW * kWave)) {
     const int g = i / V4, c = i - g * V4, h = kvh * G + g;
     const int off = (((m * a.heads + h) * a.splits + split) * row + 4 * c) * 4;
     __builtin_amdgcn_raw_buffer_store_b128(*(const f32x4*)(s_part + g * row + 4 * c), wsr, off, 0, kAuxSc1);
@@ -369,7 +376,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
   if (!s_last) return;
   // all partials of the group's heads in one round trip: s_part[g][split][row]
   const int nv = G * a.splits * V4;
-  for (int i = tid; i < nv; i += kAttnThreads) {
+  for (int i = tid; i < nv; i += (NW * kWave)) {
     const int g = i / (a.splits * V4), rem = i - g * a.splits * V4;
     const int h = kvh * G + g;
     const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(wsr, ((m * a.heads + h) * a.splits * row + 4 * rem) * 4, 0,
@@ -377,7 +384,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
     *(f32x4*)(s_part + (size_t)g * a.splits * row + 4 * rem) = v;
   }
   __syncthreads();
-  for (int idx = tid; idx < G * HD; idx += kAttnThreads) {
+  for (int idx = tid; idx < G * HD; idx += (NW * kWave)) {
     const int g = idx / HD, d = idx - g * HD, h = kvh * G + g;
     const float* pb = s_part + (size_t)g * a.splits * row;
     float mx = -INFINITY;

@@ -1176,8 +1176,40 @@ struct RowsCfg {
 __host__ __device__ inline int rows_slab_bytes(int mb_total, int ntl) {
   return align16(ntl * mb_total * kGemvWaves * kWave * 16);
 }
-__host__ __device__ inline int rows_lds_bytes(int mb_total, int ntl, int K, bool g32 = false) {
+// batched fold (ti_hip.h TI_FOLD_SS_ROWS): per-thread partial sums [512] | 1 / rms per row [64] |
+// per-tile sums of h^2 per row [4][64], behind the slab and the scales
+constexpr int kFoldLdsBytes = 4096;
+__host__ __device__ inline int rows_fold_offset(int mb_total, int ntl, int K, bool g32 = false) {
   return rows_slab_bytes(mb_total, ntl) + align16(ntl * (K >> 7) * 32 * (g32 ? 4 : 1));
+}
+__host__ __device__ inline int rows_lds_bytes(int mb_total, int ntl, int K, bool g32 = false) {
+  return rows_fold_offset(mb_total, ntl, K, g32) + kFoldLdsBytes;
+}
+
+// Batched fold, consumer side: this thread's share of row `row`'s partial sums of h^2 (rows
+// of R per workgroup, 512 / R threads per row taking partials part, part + P, ...; loads issued
+// 8 at a time, summed in partial order).  fold_rms_finish turns the shares into rms per row.
+__device__ __forceinline__ float fold_share(const GemvArgs& a, int m, int part, int P) {
+  float t = 0.0f;
+  if (m >= a.M) return t;
+  const float* ss = a.epi.ss_in + m;
+  for (int b0 = part; b0 < a.epi.n_ss; b0 += 8 * P) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = b0 + j * P < a.epi.n_ss ? ss[(size_t)(b0 + j * P) * TI_FOLD_SS_ROWS] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t += v[j];
+  }
+  return t;
+}
+// part[512] holds every thread's share (thread = part * R + row); rms[row] = sqrt(sum / K + eps)
+// (the M == 1 fold's formula, gemv_wq_kernel XM_F16F).  Call between two workgroup barriers.
+__device__ __forceinline__ void fold_rms_finish(const GemvArgs& a, const float* part, float* rms, int R, int tid) {
+  if (tid < R) {
+    float t = 0.0f;
+    for (int p = 0; p < kGemvThreads / R; ++p) t += part[p * R + tid];
+    rms[tid] = sqrtf(t / (float)a.K + a.eps);
+  }
 }
 
 // Workgroups: n_cg column groups x n_rb row blocks of 16 RG MB rows (narrow outputs split the
@@ -1263,6 +1295,12 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
     load_w(W[u], u);
     load_x(X[u], u);
   }
+  // batched fold: the consumer's per-row rms shares (after the first ring loads: their wait
+  // costs nothing the first item would not wait for), the producer's per-tile h^2 sums
+  constexpr int R = 16 * RG * MB;
+  float* fold_l = (float*)(smem + rows_fold_offset(RG * MB, NTL, a.K, G32));
+  const bool fold_in = a.epi.ss_in != nullptr, fold_out = a.epi.kind == TI_EPI_RESID_F32 && a.epi.fold_x != nullptr;
+  const float share = fold_in ? fold_share(a, b0 * 16 + tid % R, tid / R, kGemvThreads / R) : 0.0f;
   if constexpr (!G32) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -1344,7 +1382,12 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
   for (int tl = 0; tl < NTL; ++tl)
 #pragma unroll
     for (int b = 0; b < MB; ++b) slab[((tl * RG * MB + grp * MB + b) * kGemvWaves + wave) * kWave + lane] = acc[tl][b];
+  if (fold_in) fold_l[tid] = share;
   lds_barrier();
+  if (fold_in) {
+    fold_rms_finish(a, fold_l, fold_l + kGemvThreads, R, tid);
+    lds_barrier();
+  }
   const int n = lane & 15, nblk = ntl * RG * MB * 4;
   const int nblk_pad = (nblk + kGemvWaves - 1) / kGemvWaves * kGemvWaves;
   for (int cb = wave; cb < nblk_pad; cb += kGemvWaves) {   // wave-uniform trip count (shuffles inside)
@@ -1355,8 +1398,31 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
     float v = 0.0f;
 #pragma unroll
     for (int w = 0; w < GW; ++w) v += sp[(g * GW + w) * kWave * 4];
-    const int m = (b0 + bb) * 16 + 4 * (lane >> 4) + i;
+    const int rl = bb * 16 + 4 * (lane >> 4) + i, m = b0 * 16 + rl;
+    if (fold_in) v = v / fold_l[kGemvThreads + rl];
+    if (fold_out) {   // residual add + the next call's folded input (fp16(h * w), sum of h^2 per row)
+      const ti_epilogue& e = a.epi;
+      const int ng = (t0 + tl) * 16 + n;
+      float hn = 0.0f;
+      if (ok && m < a.M) {
+        float* o = (float*)e.out + (size_t)m * e.ldo + ng;
+        hn = *o + v;
+        *o = hn;
+        e.fold_x[e.fold_packed ? TI_PACKED_INDEX(m, ng, e.ldo >> 7) : (size_t)m * e.ldo + ng] = f2h(hn * e.fold_w[ng]);
+      }
+      const float sq = group_sum<16>(hn * hn);
+      if (ok && n == 0) fold_l[kGemvThreads + 64 + tl * 64 + rl] = sq;
+      continue;
+    }
     epilogue_mb(a, t0 + tl, m, n, v, ok && m < a.M);
+  }
+  if (fold_out) {   // this column group's sum of h^2 per row, tiles in order
+    lds_barrier();
+    if (tid < R && b0 * 16 + tid < a.M) {
+      float t = 0.0f;
+      for (int tl = 0; tl < ntl; ++tl) t += fold_l[kGemvThreads + 64 + tl * 64 + tid];
+      a.epi.fold_ss[(size_t)cg * TI_FOLD_SS_ROWS + b0 * 16 + tid] = t;
+    }
   }
   ROWS_TS(5);
   if (a.epi.kind == TI_EPI_LOGITS_ARGMAX && a.epi.step_ctr && blockIdx.x == 0 && tid == 0)
@@ -1383,7 +1449,8 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
 // half the activation block per group)
 __host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, int wmr = 2, int xb = 2, int rb = 4) {
   const int n = xb * 16 * rb * wmr * 256 + align16((8 / wmr) * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
-  return n > 8 * 64 * 20 * 4 ? n : 8 * 64 * 20 * 4;   // >= the epilogue's staging blocks (tile_epi_lds_bytes)
+  // >= the epilogue's staging blocks (tile_epi_lds_bytes) + the batched fold's rms per row
+  return n > 8 * 64 * 20 * 4 + 512 ? n : 8 * 64 * 20 * 4 + 512;
 }
 
 // TPW: weight tiles per wave (2: 128 columns per workgroup; 1: 64 columns, twice the workgroups
@@ -1604,6 +1671,10 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   const int n_sc = WCOL * TPW * nk * 2 * SG;                  // 16-byte pieces of this k-slice
   const u32x4* sg = (const u32x4*)(a.scales + (size_t)t0 * KT * 16 * SG);
   const int ntile_ok = min(WCOL * TPW, NT - t0);
+  // batched fold (decode rows, ti_hip.h TI_FOLD_SS_ROWS): this thread's share of its row's rms
+  // (TPW 4, already short of registers: after the stream)
+  const bool fold_in = a.epi.ss_in != nullptr;
+  float share = fold_in && TPW < 4 ? fold_share(a, m0 + tid % BM, tid / BM, kGemvThreads / BM) : 0.0f;
   for (int i = tid; i < n_sc; i += kGemvThreads) {
     const int j = i / (nk * 2 * SG), p = (j * KT + kb) * 2 * SG + (i - j * nk * 2 * SG);   // tile j, piece in slice
     ((u32x4*)sl)[p] = j < ntile_ok ? ld_w(sg + p) : (u32x4){0u, 0u, 0u, 0u};
@@ -1831,6 +1902,14 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
   // every wave is past its last read of the x / scale images (and every DMA into them has
   // landed): the epilogue may stage through that LDS
   lds_barrier();
+  const float* rmsv = (const float*)(smem + tile_epi_lds_bytes());   // batched fold: rms per row
+  if (fold_in) {
+    if constexpr (TPW == 4) share = fold_share(a, m0 + tid % BM, tid / BM, kGemvThreads / BM);
+    ((float*)smem)[tid] = share;
+    lds_barrier();
+    fold_rms_finish(a, (const float*)smem, (float*)rmsv, BM, tid);
+    lds_barrier();
+  }
 #if TI_GEMV_EXP & 512   // diagnostic: no split-K merge at all (every slice runs the epilogue)
   const bool merged = true;
 #else
@@ -1857,6 +1936,11 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
       if (tt == t)
 #pragma unroll
         for (int b = 0; b < RB; ++b) av[b] = acc[tt][b];
+    if (fold_in)
+#pragma unroll
+      for (int b = 0; b < RB; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) av[b][i] = av[b][i] / rmsv[wm * 16 * RB + b * 16 + 4 * (lane >> 4) + i];
     if (via_lds) {
       // lane (r, kq) holds rows b*16 + 4 kq + i of column r; LDS program order within the wave
       // makes the reads below see these writes, and the next tile's writes follow the reads
@@ -2291,6 +2375,14 @@ extern "C" int ti_gemm_packed_rows_for(int bits, int M, int N, int K) {
   return ti_gemm_packed_rows(bits, M) && !wide_tile(bits, M, N) ? 1 : 0;
 }
 
+extern "C" int ti_gemm_fold_partials(int bits, int M, int N, int K) {
+  if (bits != 4 || M <= 16 || M >= ti::tile_rows() || M > TI_FOLD_SS_ROWS || N < 16 || (N & 15) || K < 128 || (K & 127))
+    return 0;
+  int MB = 0, RG = 0, n_rb = 0, n_cg = 0, ntl = 0;
+  ti::rows_plan(M, N, K, query_cus(), &MB, &RG, &n_rb, &n_cg, &ntl);
+  return n_cg;
+}
+
 extern "C" int ti_gemm_tile_plan(int bits, int M, int N, int K, int64_t ws_bytes, int* wmr, int* tpw, int* n_ks) {
   const bool g32 = (bits & TI_BITS_G32) != 0;
   if (!wmr || !tpw || !n_ks) return ti_set_error(TI_ERR_ARG, "ti_gemm_tile_plan: null pointer");
@@ -2379,9 +2471,18 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
                         "64/128 and K <= 4096", TI_ATTN_MAX_PART_SPLITS);
   if (x_kind == TI_X_F16_FOLDED && (M != 1 || !epi->ss_in || epi->n_ss < 1 || epi->n_ss > 256))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: TI_X_F16_FOLDED needs M == 1, ss_in and 1 <= n_ss <= 256");
-  if (epi->kind == TI_EPI_RESID_F32 && epi->fold_x &&
-      (M != 1 || !epi->fold_w || !epi->fold_ss || (x_kind != TI_X_F16 && x_kind != TI_X_ATTN_SPLITS)))
+  const bool fold_out = epi->kind == TI_EPI_RESID_F32 && epi->fold_x;
+  if (fold_out && M == 1 && (!epi->fold_w || !epi->fold_ss || (x_kind != TI_X_F16 && x_kind != TI_X_ATTN_SPLITS)))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: fold_x needs M == 1, fp16 x, fold_w and fold_ss");
+  if (fold_out && M > 1 && (!epi->fold_w || !epi->fold_ss || x_kind != TI_X_F16_PACKED || M > TI_FOLD_SS_ROWS ||
+                            (N & 127)))
+    return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: a batched fold_x needs TI_X_F16_PACKED x, M <= %d, fold_w, "
+                        "fold_ss and N %% 128 == 0", TI_FOLD_SS_ROWS);
+  // batched fold consumer: fp16(h * nw) rows normalised behind the GEMM (rows / tile kernels)
+  const bool fold_in = M > 1 && epi->ss_in && (x_kind == TI_X_F16 || x_kind == TI_X_F16_PACKED);
+  if (fold_in && (M > TI_FOLD_SS_ROWS || epi->n_ss < 1 || epi->n_ss > 4096))
+    return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: a batched folded input needs M <= %d and 1 <= n_ss <= 4096",
+                        TI_FOLD_SS_ROWS);
   if (K > 0xffff || ldx > 0xffff)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: K %d / ldx %d above 65535", K, ldx);
   if (x_kind == TI_X_F32_RMSNORM && !norm_w) return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: norm_w required");
@@ -2432,7 +2533,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
                           (epi->ldo & 127)))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: out_packed needs the batched-rows kernel, a fp16 store / SiLU "
                         "epilogue and ldo %% 128 == 0");
-  if (batched && epi->kind == TI_EPI_RESID_F32 && epi->fold_x)
+  if (batched && fold_out && M == 1)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: fold_x needs the fused kernel");
   if (batched && !(bits == 4 && (x_kind == TI_X_F16 || packed_x)))
     return ti_set_error(TI_ERR_UNSUPPORTED,
@@ -2462,6 +2563,9 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     grid = gemv_grid(M, N, K, query_cus(), g32, aff);
     lds = gemv_lds_bytes_tiles(M, K, ((N >> 4) + grid - 1) / grid, g32, aff);
   }
+  if ((fold_out && M > 1 && !rows) || (fold_in && !rows && !tile))
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: the batched fold runs on the batched-rows (fold_x) / "
+                        "rows or tile (folded input) kernels (M=%d N=%d K=%d)", M, N, K);
   if (lds > 160 * 1024)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: LDS image %d B too large (M=%d N=%d K=%d)", lds, M, N, K);
   if (!batched && grid > 0xfff)
