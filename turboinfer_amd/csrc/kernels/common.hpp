@@ -12,6 +12,15 @@ typedef _Float16 f16;
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// acc + sc * t as two packed fp32 FMAs (v_pk_fma_f32): the same fused roundings as four fmaf
+__device__ __forceinline__ f32x4 fma_scale4(float sc, f32x4 t, f32x4 acc) {
+  const f32x2 s2 = {sc, sc};
+  const f32x2 lo = __builtin_elementwise_fma(s2, (f32x2){t[0], t[1]}, (f32x2){acc[0], acc[1]});
+  const f32x2 hi = __builtin_elementwise_fma(s2, (f32x2){t[2], t[3]}, (f32x2){acc[2], acc[3]});
+  return (f32x4){lo[0], lo[1], hi[0], hi[1]};
+}
 
 constexpr int kWave = 64;
 

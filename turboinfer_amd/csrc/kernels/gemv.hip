@@ -1354,12 +1354,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
       }
       const float sc = kvalid ? h2f(sl[(min(tl, ntl - 1) * KT + ktc) * 16 + r]) : 0.0f;
 #pragma unroll
-      for (int b = 0; b < MB; ++b) {
-        acc[tl][b][0] = fmaf(sc, t[b][0], acc[tl][b][0]);
-        acc[tl][b][1] = fmaf(sc, t[b][1], acc[tl][b][1]);
-        acc[tl][b][2] = fmaf(sc, t[b][2], acc[tl][b][2]);
-        acc[tl][b][3] = fmaf(sc, t[b][3], acc[tl][b][3]);
-      }
+      for (int b = 0; b < MB; ++b) acc[tl][b] = fma_scale4(sc, t[b], acc[tl][b]);
     }
   };
   for (int i = 0; i < NIP; i += WD) {
@@ -1778,12 +1773,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
       }
       const float sc = h2f(sl[((wn * TPW + t) * KT + kg) * 16 + r]);
 #pragma unroll
-      for (int b = 0; b < RB; ++b) {
-        acc[t][b][0] = fmaf(sc, tmp[b][0], acc[t][b][0]);
-        acc[t][b][1] = fmaf(sc, tmp[b][1], acc[t][b][1]);
-        acc[t][b][2] = fmaf(sc, tmp[b][2], acc[t][b][2]);
-        acc[t][b][3] = fmaf(sc, tmp[b][3], acc[t][b][3]);
-      }
+      for (int b = 0; b < RB; ++b) acc[t][b] = fma_scale4(sc, tmp[b], acc[t][b]);
     }
   };
   // Per group kg: x(kg) and W(kg) were issued earlier; issue x(kg + 1) and W(kg + WR - 1),
