@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <queue>
 #include <cstdlib>
@@ -368,18 +369,20 @@ bool part_usable(ti_engine* e, int M) {
 // Persistent decode layers (ti_pds_decode): one stream with the fold and the split partials (8
 // splits, so the persistent launch forms every partial as the per-layer launches do), INT4 / INT8,
 // the shapes ti_pds_supported takes (Llama-2-7B, TinyLlama-1.1B), grid = 8 heads <= the CU count.
-int g_pds_cus = 0;
+std::atomic<int> g_pds_cus{0};   // CU count of the first device asked (engines may run on several threads)
 bool pds_usable(ti_engine* e, int M) {
   const ti_engine_config& c = e->c;
   if (!e->pds_on || !e->pds_layers || M != 1 || (c.bits != 4 && c.bits != 8) || c.compat) return false;
   if (!fold_usable(e, M) || !part_usable(e, M) || e->splits_for(M) != 8) return false;
   if (!ti_pds_supported(c.bits, c.hidden, c.inter, c.heads, c.kv_heads, c.head_dim, c.heads * 8, c.layers)) return false;
-  if (g_pds_cus == 0) {
+  int cus = g_pds_cus.load(std::memory_order_relaxed);
+  if (cus == 0) {
     int dev = 0, n = 0;
-    g_pds_cus = (hipGetDevice(&dev) == hipSuccess &&
-                 hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) ? n : -1;
+    cus = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) ? n : -1;
+    g_pds_cus.store(cus, std::memory_order_relaxed);   // (a racing first call stores the same value)
   }
-  return g_pds_cus >= c.heads * 8;
+  return cus >= c.heads * 8;
 }
 
 // The persistent decode-layers launch (ti_pds_decode) of a single-stream step: input h / fx / ss

@@ -1959,7 +1959,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #endif
 }
 
-static int g_num_cus = 0;
+static std::atomic<int> g_num_cus{0};   // (a racing first query stores the same value)
 
 // Tile kernel shape by a per-CU byte model: a CU streams a bounded number of bytes per
 // microsecond, a workgroup moves its activation block plus its weight tiles per
@@ -2287,15 +2287,15 @@ static std::atomic<unsigned long long> g_prepared{0};
 
 // Raise the dynamic-LDS cap of the GEMM instantiations (call before any stream capture).
 static int query_cus() {
-  if (ti::g_num_cus <= 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-      ti::g_num_cus = n;
-    else
-      ti::g_num_cus = 256;
+  int n = ti::g_num_cus.load(std::memory_order_relaxed);
+  if (n <= 0) {
+    int dev = 0;
+    if (!(hipGetDevice(&dev) == hipSuccess &&
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0))
+      n = 256;
+    ti::g_num_cus.store(n, std::memory_order_relaxed);
   }
-  return ti::g_num_cus;
+  return n;
 }
 
 extern "C" int ti_gemm_prepare(void) {
