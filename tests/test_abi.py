@@ -86,6 +86,18 @@ def test_argument_errors_are_reported_without_launch(L):
     assert rc == 1 and b"fold_x" in L.ti_last_error()
     assert L.ti_gemm_grid(1, 4096, 4096) >= 1 and L.ti_gemm_grid(1, 4096, 4096) <= 256
     assert L.ti_gemm_grid(0, 4096, 4096) == 0
+    # batched fold: producer partials for the configs[3] / [4] O and down shapes; none outside 17..64
+    # int4 rows; a batched fold_x needs packed x, a batched folded input at most 64 rows
+    for M, N, K in [(64, 4096, 4096), (64, 4096, 11008), (32, 4096, 4096), (32, 4096, 14336), (17, 4096, 4096)]:
+        assert 1 <= L.ti_gemm_fold_partials(4, M, N, K) <= 4096
+    assert L.ti_gemm_fold_partials(4, 16, 4096, 4096) == 0 and L.ti_gemm_fold_partials(4, 65, 4096, 4096) == 0
+    assert L.ti_gemm_fold_partials(8, 32, 4096, 4096) == 0
+    rc = L.ti_gemm_wq_a16(1, 1, 4, 1, T.X_F16, 4096, None, 1e-5, 32, 16, 4096, C.byref(fe), None)
+    assert rc == 1 and b"batched fold_x" in L.ti_last_error()
+    be = T.Epilogue()
+    be.kind, be.ldo, be.out, be.ss_in, be.n_ss = T.EPI_STORE_F32, 16, 1234, 1234, 8
+    rc = L.ti_gemm_wq_a16(1, 1, 4, 1, T.X_F16, 4096, None, 1e-5, 100, 16, 4096, C.byref(be), None)
+    assert rc == 1 and b"batched folded input" in L.ti_last_error()
     # attention head_dim unsupported
     rc = L.ti_attn_decode(1, 1, 1, 1 << 20, 16, 1, 1, 4, 4, 96, 1, 1, 1, None)
     assert rc == 3
