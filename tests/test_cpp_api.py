@@ -241,8 +241,10 @@ def test_generate_contract_matches_reference(api_check, golden, tmp_path, monkey
         assert lines[0] == ["eos_token", "max_length", "max_new_tokens"][stop], (i, lines[0])
         f = lines[1].split()
         assert f[0] == "finished" and f[2] == "time_ms" and f[4] == "tokens_per_second"
-        if stop != 2:
+        if stop in (0, 1):   # (-1: max_new_tokens, the reference's `finished` left uninitialised)
             assert int(f[1]) == fin == 1
+        else:
+            assert int(f[1]) == 0 and lines[0] == "max_new_tokens"
         ms, tps = float(f[3]), float(f[5])
         assert ms == int(ms)                                  # whole milliseconds
         gen = len(got) - prompt.shape[1]

@@ -1403,7 +1403,9 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
         float* o = (float*)e.out + (size_t)m * e.ldo + ng;
         hn = *o + v;
         *o = hn;
-        e.fold_x[e.fold_packed ? TI_PACKED_INDEX(m, ng, e.ldo >> 7) : (size_t)m * e.ldo + ng] = f2h(hn * e.fold_w[ng]);
+        float p = hn * e.fold_w[ng];
+        asm volatile("" : "+v"(p));   // fp16(fp32 product): no fused multiply-convert (one rounding less)
+        e.fold_x[e.fold_packed ? TI_PACKED_INDEX(m, ng, e.ldo >> 7) : (size_t)m * e.ldo + ng] = f2h(p);
       }
       const float sq = group_sum<16>(hn * hn);
       if (ok && n == 0) fold_l[kGemvThreads + 64 + tl * 64 + rl] = sq;

@@ -48,6 +48,7 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <vector>
 
 #include "common.hpp"
 #include "attention_body.hpp"
@@ -74,6 +75,23 @@ enum { C_FULL = 0, C_FREE = 1, C_BAR = 5, C_GATHER = 6, C_DEAD = 7, C_EPOCH = 8,
 #define TI_PDS_AHEAD 3  // slots in flight otherwise (vmcnt 16 * AHEAD <= 63)
 #endif
 static_assert(TI_PDS_AHEAD >= 1 && TI_PDS_AHEAD <= 3, "vmcnt immediate");
+#ifndef TI_PDS_FTRACE
+#define TI_PDS_FTRACE 0   // diagnostic build (tools/pds_ftrace.py): per-fill ring events of workgroups 0..3
+#endif
+#if TI_PDS_FTRACE
+constexpr int kFtWg = 4, kFtFills = 2048;
+// [wg][fill][k]: 0 loader issue begins, 1 loader publishes it (FULL > fill), 2 consumer 0's wait
+// for it ends, 3 consumer 0 releases it, 4 the loader starts waiting for a FREE slot before it,
+// 5 that wait ends
+static __device__ unsigned long long g_pds_ft[kFtWg][kFtFills][6];
+#define PDS_FT(f, k)                                                                                  \
+  do {                                                                                                \
+    if (blockIdx.x < kFtWg && (f) < (uint32_t)kFtFills && lane == 0)                                  \
+      g_pds_ft[blockIdx.x][(f)][(k)] = __builtin_amdgcn_s_memrealtime();                              \
+  } while (0)
+#else
+#define PDS_FT(f, k) do { } while (0)
+#endif
 
 typedef ti_pds_layer PdsLayerDev;
 
@@ -239,6 +257,9 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
   uint32_t f = 0, pub = 0;   // fills issued / published
   auto publish = [&](uint32_t upto) {
     if (upto > pub) {
+#if TI_PDS_FTRACE
+      for (uint32_t q = pub; q < upto; ++q) PDS_FT(q, 1);
+#endif
       pub = upto;
       cset(ctl + C_FULL, pub);
     }
@@ -269,13 +290,16 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
         if (f >= (uint32_t)NS) {
           const uint32_t need = f - NS + 1;
           if (min_free() < need) {
+            PDS_FT(f, 4);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             publish(f);
             Spin sp{ctl, a.err};
             while (min_free() < need)
               if (!sp.tick()) break;
+            PDS_FT(f, 5);
           }
         }
+        PDS_FT(f, 0);
         const uint32_t base = ring_lds + (uint32_t)(f % NS) * kSlotBytes;
 #pragma unroll 4
         for (int j = 0; j < kFill; ++j) {
@@ -507,10 +531,12 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     while (cget(ctl + C_FULL) <= fill)
       if (!sp.tick()) break;
     asm volatile("" ::: "memory");
+    if (c == 0) PDS_FT(fill, 2);
   };
   auto release = [&](uint32_t fill) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane == 0) cset(ctl + C_FREE + c, fill + 1);
+    if (c == 0) PDS_FT(fill, 3);
   };
   // GEMV phase over items (tile item / KT, k-tile item % KT): this consumer's items are k-tiles == c
   // (mod 4), virtual wave kt % 8 in {c, c + 4}: the partial of (tile, virtual wave) accumulates
@@ -929,6 +955,21 @@ int ti_pds_supported(int bits, int H, int I, int heads, int kv_heads, int head_d
   if ((nt_qkv + grid - 1) / grid > kMaxQkvTiles || (nt_gu + grid - 1) / grid > kMaxGuTiles) return 0;
   return 1;
 }
+
+#if TI_PDS_FTRACE
+// diagnostic build only: copy the fill trace ([4][2048][6] u64) to host and clear it
+int ti_pds_ftrace(unsigned long long* host, size_t n) {
+  const size_t bytes = sizeof(unsigned long long) * (size_t)ti::kFtWg * ti::kFtFills * 6;
+  if (!host || n * sizeof(unsigned long long) < bytes) return ti_set_error(TI_ERR_ARG, "ti_pds_ftrace: buffer");
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ti::g_pds_ft), bytes, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return ti_set_error(TI_ERR_HIP, "ti_pds_ftrace: copy");
+  static std::vector<unsigned long long> zero;
+  zero.assign(bytes / 8, 0ull);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(ti::g_pds_ft), zero.data(), bytes, 0, hipMemcpyHostToDevice) != hipSuccess)
+    return ti_set_error(TI_ERR_HIP, "ti_pds_ftrace: clear");
+  return TI_OK;
+}
+#endif
 
 int ti_pds_decode(const ti_pds_args* h, ti_stream_t s) {
   if (!h || !h->layers || !h->pos || !h->h || !h->fx || !h->ss || !h->launches || !h->err || !h->zero ||
