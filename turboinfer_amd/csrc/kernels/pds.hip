@@ -162,7 +162,7 @@ struct Spin {
   const uint32_t* err;
   unsigned long long t0 = 0;
   uint32_t n = 0;
-  __device__ bool tick() {
+  __device__ bool check() {
     if (cget(ctl + C_DEAD)) return false;
     if (n == 0) t0 = __builtin_amdgcn_s_memrealtime();
     ++n;
@@ -174,7 +174,20 @@ struct Spin {
         return false;
       }
     }
+    return true;
+  }
+  // polls of LDS words: a short sleep
+  __device__ bool tick() {
+    if (!check()) return false;
     __builtin_amdgcn_s_sleep(1);
+    return true;
+  }
+  // re-polls of granules in memory (sc1 loads that reach L2): every CU of the grid may be polling
+  // at once, and the re-loads compete with the weight streams for L2 / the CUs' load pipelines,
+  // so they back off ~0.2 us (s_sleep 8 = 512 clocks) and poll one batch at a time (stage_x)
+  __device__ bool tick_g() {
+    if (!check()) return false;
+    __builtin_amdgcn_s_sleep(8);
     return true;
   }
 };
@@ -435,14 +448,16 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         };
         Spin sp{ctl, a.err};
         while (true) {
-          bool ok = true;
+          // the first batch with a granule of an earlier launch in any lane (wave-uniform)
+          int first = -1;
 #pragma unroll
-          for (int b = 0; b < B; ++b) ok = ok && ok_b(b);
-          if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
-          if (!sp.tick()) break;
+          for (int b = 0; b < B; ++b)
+            if (first < 0 && __builtin_amdgcn_ballot_w64(!ok_b(b)) != 0ull) first = b;
+          if (first < 0) break;
+          if (!sp.tick_g()) break;
 #pragma unroll
           for (int b = 0; b < B; ++b) {
-            if (!ok_b(b)) {
+            if (b == first && !ok_b(b)) {
               const int idx = min(i0 + b * kEC * kWave + ctid, K8 - 1);
               gv[b][0] = ld_sc1_b128(src, (uint32_t)idx * 32u);
               gv[b][1] = ld_sc1_b128(src, (uint32_t)idx * 32u + 16u);
@@ -492,7 +507,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) ok = ok && (uint32_t)(v[j] >> 32) == tag;
         if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) break;
-        if (!sp.tick()) break;
+        if (!sp.tick_g()) break;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if ((uint32_t)(v[j] >> 32) != tag)
@@ -511,7 +526,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     unsigned long long v = want ? ld_sc1_u64(base + idx) : 0ull;
     Spin sp{ctl, a.err};
     while (__builtin_amdgcn_ballot_w64(want && (uint32_t)(v >> 32) != tag) != 0ull) {
-      if (!sp.tick()) break;
+      if (!sp.tick_g()) break;
       if (want && (uint32_t)(v >> 32) != tag) v = ld_sc1_u64(base + idx);
     }
     return (uint32_t)v;
