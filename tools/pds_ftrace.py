@@ -2,7 +2,8 @@
 -DTI_PDS_FTRACE=1, run with TI_LIB pointing at it) for workgroups 0..3 at the bench's 7B
 configuration.  Events per fill (s_memrealtime, 100 MHz): 0 loader issue begins, 1 published
 (FULL > fill), 2 consumer 0's wait ends, 3 consumer 0 releases it, 4/5 the loader's wait for a
-FREE slot before issuing it (start / end)."""
+FREE slot before issuing it (start / end), 6 its last piece issued.  DETAIL=0 skips the per-fill
+listing."""
 import ctypes as C
 import os
 import sys
@@ -23,10 +24,10 @@ e.replay_run(20)
 e.sync()
 L = ti.lib()
 L.ti_pds_ftrace.argtypes = [C.c_void_p, C.c_size_t]
-buf = np.zeros(4 * 2048 * 6, np.uint64)
+buf = np.zeros(4 * 2048 * 8, np.uint64)
 ti.check(L.ti_pds_ftrace(buf.ctypes.data_as(C.c_void_p), buf.size))
 e.close()
-tr = buf.reshape(4, 2048, 6).astype(np.int64)
+tr = buf.reshape(4, 2048, 8).astype(np.int64)
 KT_H, KT_Q, KT_I = H // 128, H // 128, I // 128
 names = ["QKV", "ATT", "O", "GU", "DN"]
 for b in range(4):
@@ -52,10 +53,13 @@ for b in range(4):
         blk = ((ev[:, 5] - ev[:, 4]) / 100)[blocked]
         # cadence: issue of fill k+1 - issue of fill k, within the phase
         cad = np.diff(t[idx, 0]) / 100
-        print(f"  {names[ph]:4s} issue->pub {pub_lat.mean():5.2f}  pub->acq {cons_lag.mean():6.2f}  acq->rel {hold.mean():5.2f}"
+        idur = (ev[:, 6] - ev[:, 0]) / 100
+        print(f"  {names[ph]:4s} issue {idur.mean():5.2f}  issue->pub {pub_lat.mean():5.2f}  pub->acq {cons_lag.mean():6.2f}  acq->rel {hold.mean():5.2f}"
               f"  issue cadence {np.median(cad):5.2f}  blocked {blocked.mean()*100:4.0f}% ({blk.mean() if blk.size else 0:5.2f} us)"
               f"  acq-issue {((ev[:, 2] - ev[:, 0]) / 100).mean():6.2f}")
     # one layer in detail (layer 5): fill, issue, pub, acq, rel relative to the layer's first issue
+    if os.environ.get("DETAIL", "1") == "0":
+        break
     l = 5
     base = l * per_layer
     tl0 = t[base, 0]

@@ -75,6 +75,16 @@ enum { C_FULL = 0, C_FREE = 1, C_BAR = 5, C_GATHER = 6, C_DEAD = 7, C_EPOCH = 8,
 #define TI_PDS_AHEAD 3  // slots in flight otherwise (vmcnt 16 * AHEAD <= 63)
 #endif
 static_assert(TI_PDS_AHEAD >= 1 && TI_PDS_AHEAD <= 3, "vmcnt immediate");
+#ifndef TI_PDS_NT
+#define TI_PDS_NT 1       // loader DMA non-temporal (0: default policy; diagnostic A/B)
+#endif
+#ifndef TI_PDS_PRIO
+#define TI_PDS_PRIO 0     // diagnostic: the loader wave at s_setprio 3
+#endif
+#ifndef TI_PDS_DIAG
+#define TI_PDS_DIAG 0     // diagnostic builds only: 1 consumers only acquire / release the ring (no math, no
+                          // hand-offs: garbage results); 2 the loader re-reads layer 0's QKV tiles (L2)
+#endif
 #ifndef TI_PDS_FTRACE
 #define TI_PDS_FTRACE 0   // diagnostic build (tools/pds_ftrace.py): per-fill ring events of workgroups 0..3
 #endif
@@ -82,8 +92,8 @@ static_assert(TI_PDS_AHEAD >= 1 && TI_PDS_AHEAD <= 3, "vmcnt immediate");
 constexpr int kFtWg = 4, kFtFills = 2048;
 // [wg][fill][k]: 0 loader issue begins, 1 loader publishes it (FULL > fill), 2 consumer 0's wait
 // for it ends, 3 consumer 0 releases it, 4 the loader starts waiting for a FREE slot before it,
-// 5 that wait ends
-static __device__ unsigned long long g_pds_ft[kFtWg][kFtFills][6];
+// 5 that wait ends, 6 the loader's last piece of it issued
+static __device__ unsigned long long g_pds_ft[kFtWg][kFtFills][8];
 #define PDS_FT(f, k)                                                                                  \
   do {                                                                                                \
     if (blockIdx.x < kFtWg && (f) < (uint32_t)kFtFills && lane == 0)                                  \
@@ -206,7 +216,11 @@ __device__ __forceinline__ void cbar(uint32_t* ctl, const uint32_t* err, uint32_
 // 64 lanes x 16 B -> LDS at the wave-uniform byte address lds, non-temporal (streamed once)
 __device__ __forceinline__ void dma_nt(const void* src_lane, uint32_t lds) {
   uint32_t keep;
+#if TI_PDS_NT
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+#else
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+#endif
                : "=&s"(keep)
                : "v"(src_lane), "s"(lds)
                : "memory");
@@ -283,6 +297,9 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
     for (int c = 1; c < kEC; ++c) m = min(m, cget(ctl + C_FREE + c));
     return m;
   };
+#if TI_PDS_PRIO
+  __builtin_amdgcn_s_setprio(3);
+#endif
   const char* zl = a.zero + lane * 16;
   const size_t kv_off = ((size_t)g.kvh * a.max_seq) * HD * 2;   // bytes: this split's kv-head
   for (int l = 0; l < a.n_layers; ++l) {
@@ -331,8 +348,12 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
               src = wbase + ((size_t)(t0 + seg * tstr) * KT * C + (i - seg * KT * C)) * kPiece + lane * 16;
             }
           }
+#if TI_PDS_DIAG & 2   // diagnostic: every piece from this CU's own 96 KiB of layer 0's QKV tiles (L2 hits)
+          src = (const char*)a.layers[0].tiles[0] + ((size_t)bid * 96 + (size_t)(i % 96)) * kPiece + lane * 16;
+#endif
           dma_nt(src, __builtin_amdgcn_readfirstlane(base + j * kPiece));
         }
+        PDS_FT(f, 6);
         ++f;
         if (TI_PDS_THIN && cget(ctl + C_GATHER)) {
           asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -553,6 +574,18 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     if (lane == 0) cset(ctl + C_FREE + c, fill + 1);
     if (c == 0) PDS_FT(fill, 3);
   };
+#if TI_PDS_DIAG & 1   // diagnostic: the ring alone (acquire / release every fill, nothing else)
+  {
+    uint32_t nf_all = 0;
+    for (int l = 0; l < a.n_layers; ++l)
+      for (int ph = 0; ph < PH_N; ++ph) nf_all += pds_fills(pds_pieces<C>(g, ph));
+    for (uint32_t f = 0; f < nf_all; ++f) {
+      wait_full(f);
+      release(f);
+    }
+    return;
+  }
+#endif
   // GEMV phase over items (tile item / KT, k-tile item % KT): this consumer's items are k-tiles == c
   // (mod 4), virtual wave kt % 8 in {c, c + 4}: the partial of (tile, virtual wave) accumulates
   // exactly as wave kt % 8 of gemv_wq_kernel does, then lands in slab[tile][v] (lanes 0-15).
@@ -972,9 +1005,9 @@ int ti_pds_supported(int bits, int H, int I, int heads, int kv_heads, int head_d
 }
 
 #if TI_PDS_FTRACE
-// diagnostic build only: copy the fill trace ([4][2048][6] u64) to host and clear it
+// diagnostic build only: copy the fill trace ([4][2048][8] u64) to host and clear it
 int ti_pds_ftrace(unsigned long long* host, size_t n) {
-  const size_t bytes = sizeof(unsigned long long) * (size_t)ti::kFtWg * ti::kFtFills * 6;
+  const size_t bytes = sizeof(unsigned long long) * (size_t)ti::kFtWg * ti::kFtFills * 8;
   if (!host || n * sizeof(unsigned long long) < bytes) return ti_set_error(TI_ERR_ARG, "ti_pds_ftrace: buffer");
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ti::g_pds_ft), bytes, 0, hipMemcpyDeviceToHost) != hipSuccess)
     return ti_set_error(TI_ERR_HIP, "ti_pds_ftrace: copy");
