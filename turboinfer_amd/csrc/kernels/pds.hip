@@ -56,8 +56,13 @@
 
 namespace ti {
 
+#ifndef TI_PDS_LOADERS
+#define TI_PDS_LOADERS 4   // loader waves (1, 2 or 4): one wave's VMEM issue is ~0.1 us per 1 KiB piece here
+#endif
 constexpr int kEC = 4;                         // consumer waves
-constexpr int kEThreads = (kEC + 1) * kWave;   // + the loader (wave kEC)
+constexpr int kNL = TI_PDS_LOADERS;            // loader waves kEC .. kEC + kNL - 1
+constexpr int kEThreads = (kEC + kNL) * kWave;
+static_assert(kNL == 1 || kNL == 2 || kNL == 4, "loader waves");
 constexpr int kVW = 8;                         // virtual waves: the per-layer kernels' 8 waves
 constexpr int kPiece = 1024;                   // bytes per LDS-DMA wave instruction
 constexpr int kFill = 16;                      // pieces per ring slot
@@ -67,14 +72,15 @@ constexpr int kSplits = 8;
 constexpr int kHdMax = 128;
 constexpr int kMaxQkvTiles = 4, kMaxGuTiles = 8;
 enum { PH_QKV = 0, PH_ATT, PH_O, PH_GU, PH_DN, PH_MRG, PH_N = 5 };
-enum { C_FULL = 0, C_FREE = 1, C_BAR = 5, C_GATHER = 6, C_DEAD = 7, C_EPOCH = 8, C_WORDS = 16 };
+// FULL: fills loader 0 has published (loaders w > 0: C_FULLX + w - 1); FREE + c: fills consumer c released
+enum { C_FULL = 0, C_FREE = 1, C_BAR = 5, C_GATHER = 6, C_DEAD = 7, C_EPOCH = 8, C_FULLX = 9, C_WORDS = 16 };
 #ifndef TI_PDS_THIN
 #define TI_PDS_THIN 1   // the loader keeps one slot in flight while its consumers gather (gather-pass)
 #endif
 #ifndef TI_PDS_AHEAD
 #define TI_PDS_AHEAD 3  // slots in flight otherwise (vmcnt 16 * AHEAD <= 63)
 #endif
-static_assert(TI_PDS_AHEAD >= 1 && TI_PDS_AHEAD <= 3, "vmcnt immediate");
+static_assert(TI_PDS_AHEAD >= 1 && TI_PDS_AHEAD * (16 / TI_PDS_LOADERS) <= 63, "vmcnt immediate");
 #ifndef TI_PDS_NT
 #define TI_PDS_NT 1       // loader DMA non-temporal (0: default policy; diagnostic A/B)
 #endif
@@ -277,18 +283,24 @@ __device__ __forceinline__ int pds_fills(int np) { return (np + kFill - 1) / kFi
 // ------------------------------------------------------------------------------------- loader
 template <int BITS, int HD>
 __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, int bid, int pos, uint32_t ring_lds,
-                                           uint32_t* ctl, int lane) {
+                                           uint32_t* ctl, int lane, int wl) {
+  // loader wl issues pieces wl, wl + kNL, ... of every fill (at kNL = 2 / 4 the attention's K and V
+  // pieces go to different waves) and publishes its own FULL word
   constexpr int C = BITS / 4;
   constexpr int LPK = HD / 8, KPW = 64 / LPK;
+  constexpr int PPL = kFill / kNL;   // pieces per loader and fill
   const int NS = a.n_slots;
+  const bool ft = wl == 0;           // the trace / timestamps: loader 0
+  uint32_t* full_w = ctl + (wl == 0 ? (int)C_FULL : (int)C_FULLX + wl - 1);
   uint32_t f = 0, pub = 0;   // fills issued / published
   auto publish = [&](uint32_t upto) {
     if (upto > pub) {
 #if TI_PDS_FTRACE
-      for (uint32_t q = pub; q < upto; ++q) PDS_FT(q, 1);
+      if (ft)
+        for (uint32_t q = pub; q < upto; ++q) PDS_FT(q, 1);
 #endif
       pub = upto;
-      cset(ctl + C_FULL, pub);
+      cset(full_w, pub);
     }
   };
   auto min_free = [&]() {
@@ -306,7 +318,7 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
     const PdsLayerDev& ly = a.layers[l];
     for (int ph = 0; ph < PH_N; ++ph) {
       const int np = pds_pieces<C>(g, ph), nf = pds_fills(np);
-      if (a.ts && lane == 0) a.ts[(((size_t)bid * a.n_layers + l) * PH_N + ph) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+      if (a.ts && ft && lane == 0) a.ts[(((size_t)bid * a.n_layers + l) * PH_N + ph) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
       // GEMV phases: piece i = chunk i % C of item i / C = (tile t0 + (item / KT) * ts, k-tile item % KT)
       const char* wbase = nullptr;
       int KT = 1, t0 = 0, tstr = 1;
@@ -314,26 +326,27 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
       else if (ph == PH_O) { wbase = (const char*)ly.tiles[1]; KT = g.KTq; t0 = bid; }
       else if (ph == PH_GU) { wbase = (const char*)ly.tiles[2]; KT = g.KTh; t0 = g.gu0; }
       else if (ph == PH_DN) { wbase = (const char*)ly.tiles[3]; KT = g.KTi; t0 = bid; }
-      const char* cbase = wbase + (size_t)t0 * KT * C * kPiece + lane * 16;   // tstr == 1: one contiguous run
+      const int SEG = KT * C;   // pieces per tile (>= 16: a fill spans at most two tiles)
       for (int fi = 0; fi < nf; ++fi) {
         // the slot must be released by every consumer
         if (f >= (uint32_t)NS) {
           const uint32_t need = f - NS + 1;
           if (min_free() < need) {
-            PDS_FT(f, 4);
+            if (ft) PDS_FT(f, 4);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             publish(f);
             Spin sp{ctl, a.err};
             while (min_free() < need)
               if (!sp.tick()) break;
-            PDS_FT(f, 5);
+            if (ft) PDS_FT(f, 5);
           }
         }
-        PDS_FT(f, 0);
+        if (ft) PDS_FT(f, 0);
         const uint32_t base = ring_lds + (uint32_t)(f % NS) * kSlotBytes;
-#pragma unroll 4
-        for (int j = 0; j < kFill; ++j) {
-          const int i = fi * kFill + j;
+        const int seg0 = tstr == 1 ? 0 : (fi * kFill) / SEG;   // (one division per fill)
+#pragma unroll
+        for (int jj = 0; jj < PPL; ++jj) {
+          const int j = wl + jj * kNL, i = fi * kFill + j;
           const char* src = zl;
           if (i < np) {
             if (ph == PH_ATT) {
@@ -341,11 +354,13 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
               // keys of the next split, past L, and the row this launch writes (pos) are not read
               if (key < g.s1 && key != pos)
                 src = (const char*)((i & 1) ? ly.v_cache : ly.k_cache) + kv_off + (size_t)key * HD * 2 + (lane % LPK) * 16;
-            } else if (tstr == 1) {
-              src = cbase + (size_t)i * kPiece;
             } else {
-              const int seg = i / (KT * C);
-              src = wbase + ((size_t)(t0 + seg * tstr) * KT * C + (i - seg * KT * C)) * kPiece + lane * 16;
+              int seg = seg0, ii = i - seg0 * SEG;
+              if (tstr != 1 && ii >= SEG) {
+                ++seg;
+                ii -= SEG;
+              }
+              src = wbase + ((size_t)(t0 + seg * tstr) * SEG + ii) * kPiece + lane * 16;
             }
           }
 #if TI_PDS_DIAG & 2   // diagnostic: every piece from this CU's own 96 KiB of layer 0's QKV tiles (L2 hits)
@@ -353,23 +368,17 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
 #endif
           dma_nt(src, __builtin_amdgcn_readfirstlane(base + j * kPiece));
         }
-        PDS_FT(f, 6);
+        if (ft) PDS_FT(f, 6);
         ++f;
         if (TI_PDS_THIN && cget(ctl + C_GATHER)) {
-          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPL) : "memory");
           publish(f - 1);
         } else {
-#if TI_PDS_AHEAD == 3
-          asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-#elif TI_PDS_AHEAD == 2
-          asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-#else
-          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-#endif
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPL * TI_PDS_AHEAD) : "memory");
           if (f >= TI_PDS_AHEAD) publish(f - TI_PDS_AHEAD);
         }
       }
-      if (a.ts && lane == 0) a.ts[(((size_t)bid * a.n_layers + l) * PH_N + ph) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+      if (a.ts && ft && lane == 0) a.ts[(((size_t)bid * a.n_layers + l) * PH_N + ph) * 8 + 7] = __builtin_amdgcn_s_memrealtime();
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -423,8 +432,8 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     for (int j = lane; j < HD; j += kWave) cs_l[j] = gptr(a.rope_cs)[(size_t)pos * HD + j];
   }
   __syncthreads();
-  if (wave == kEC) {
-    pds_loader<BITS, HD>(a, g, bid, pos, ring_lds, ctl, lane);
+  if (wave >= kEC) {
+    pds_loader<BITS, HD>(a, g, bid, pos, ring_lds, ctl, lane, wave - kEC);
     return;
   }
   const uint32_t epoch = __builtin_amdgcn_readfirstlane(cget(ctl + C_EPOCH));
@@ -564,7 +573,13 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
   // ---- ring consumption
   auto wait_full = [&](uint32_t fill) {
     Spin sp{ctl, a.err};
-    while (cget(ctl + C_FULL) <= fill)
+    auto full = [&]() {
+      uint32_t m = cget(ctl + C_FULL);
+#pragma unroll
+      for (int w = 1; w < kNL; ++w) m = min(m, cget(ctl + C_FULLX + w - 1));
+      return m;
+    };
+    while (full() <= fill)
       if (!sp.tick()) break;
     asm volatile("" ::: "memory");
     if (c == 0) PDS_FT(fill, 2);
