@@ -4,6 +4,8 @@
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
+timeout -k 10 120 exp/probe_ldsdma > gpurun_out/r4e_probe_ldsdma.txt 2>&1 || exit 1
+echo "probe ok"
 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_pds.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r4e_pds_tests.txt 2>&1 || exit 1
 echo "pds tests ok"
 : > gpurun_out/r4e_bench.txt

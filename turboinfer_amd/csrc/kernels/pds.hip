@@ -326,7 +326,7 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
       else if (ph == PH_O) { wbase = (const char*)ly.tiles[1]; KT = g.KTq; t0 = bid; }
       else if (ph == PH_GU) { wbase = (const char*)ly.tiles[2]; KT = g.KTh; t0 = g.gu0; }
       else if (ph == PH_DN) { wbase = (const char*)ly.tiles[3]; KT = g.KTi; t0 = bid; }
-      const int SEG = KT * C;   // pieces per tile (>= 16: a fill spans at most two tiles)
+      const int SEG = KT * C;   // pieces per tile
       for (int fi = 0; fi < nf; ++fi) {
         // the slot must be released by every consumer
         if (f >= (uint32_t)NS) {
@@ -343,7 +343,10 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
         }
         if (ft) PDS_FT(f, 0);
         const uint32_t base = ring_lds + (uint32_t)(f % NS) * kSlotBytes;
-        const int seg0 = tstr == 1 ? 0 : (fi * kFill) / SEG;   // (one division per fill)
+        // split tiles (tstr > 1): this loader's first piece of the fill as (tile seg, piece ii), one
+        // division per fill, then stepped (a fill may span several short tiles)
+        int seg = tstr == 1 ? 0 : (fi * kFill + wl) / SEG;
+        int ii = fi * kFill + wl - seg * SEG;
 #pragma unroll
         for (int jj = 0; jj < PPL; ++jj) {
           const int j = wl + jj * kNL, i = fi * kFill + j;
@@ -355,14 +358,15 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
               if (key < g.s1 && key != pos)
                 src = (const char*)((i & 1) ? ly.v_cache : ly.k_cache) + kv_off + (size_t)key * HD * 2 + (lane % LPK) * 16;
             } else {
-              int seg = seg0, ii = i - seg0 * SEG;
-              if (tstr != 1 && ii >= SEG) {
-                ++seg;
-                ii -= SEG;
-              }
               src = wbase + ((size_t)(t0 + seg * tstr) * SEG + ii) * kPiece + lane * 16;
             }
           }
+          ii += kNL;
+          if (tstr != 1)
+            while (ii >= SEG) {
+              ii -= SEG;
+              ++seg;
+            }
 #if TI_PDS_DIAG & 2   // diagnostic: every piece from this CU's own 96 KiB of layer 0's QKV tiles (L2 hits)
           src = (const char*)a.layers[0].tiles[0] + ((size_t)bid * 96 + (size_t)(i % 96)) * kPiece + lane * 16;
 #endif
