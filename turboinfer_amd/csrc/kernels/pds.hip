@@ -158,6 +158,12 @@ template <class T>
 __device__ __forceinline__ __attribute__((address_space(1))) T* gptr_w(T* p) {
   return (__attribute__((address_space(1))) T*)p;
 }
+// The layer table is read-only for the whole launch: read it through the constant address space, so
+// its fields come by scalar loads (lgkmcnt).  As plain global loads they were VECTOR loads whose
+// s_waitcnt vmcnt(0) drained every LDS-DMA in flight: once per phase, and once per attention piece
+// (the K / V base pointer), where it serialised the loader (fill trace: 6.4 us per 16 KiB fill).
+typedef const __attribute__((address_space(4))) PdsLayerDev* CLayer;
+__device__ __forceinline__ CLayer layer_c(const PdsLayerDev* t, int l) { return (CLayer)t + l; }
 __device__ __forceinline__ u32x4 ld_sc1_b128(const void* base, uint32_t byte_off) {
   return __builtin_amdgcn_raw_buffer_load_b128(sc1_rsrc(base), byte_off, 0, kAuxSc1Load);
 }
@@ -315,17 +321,19 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
   const char* zl = a.zero + lane * 16;
   const size_t kv_off = ((size_t)g.kvh * a.max_seq) * HD * 2;   // bytes: this split's kv-head
   for (int l = 0; l < a.n_layers; ++l) {
-    const PdsLayerDev& ly = a.layers[l];
+    const CLayer ly = layer_c(a.layers, l);
+    const char* const kcache = (const char*)ly->k_cache;
+    const char* const vcache = (const char*)ly->v_cache;
     for (int ph = 0; ph < PH_N; ++ph) {
       const int np = pds_pieces<C>(g, ph), nf = pds_fills(np);
       if (a.ts && ft && lane == 0) a.ts[(((size_t)bid * a.n_layers + l) * PH_N + ph) * 8 + 6] = __builtin_amdgcn_s_memrealtime();
       // GEMV phases: piece i = chunk i % C of item i / C = (tile t0 + (item / KT) * ts, k-tile item % KT)
       const char* wbase = nullptr;
       int KT = 1, t0 = 0, tstr = 1;
-      if (ph == PH_QKV) { wbase = (const char*)ly.tiles[0]; KT = g.KTh; t0 = g.q0; tstr = g.qs; }
-      else if (ph == PH_O) { wbase = (const char*)ly.tiles[1]; KT = g.KTq; t0 = bid; }
-      else if (ph == PH_GU) { wbase = (const char*)ly.tiles[2]; KT = g.KTh; t0 = g.gu0; }
-      else if (ph == PH_DN) { wbase = (const char*)ly.tiles[3]; KT = g.KTi; t0 = bid; }
+      if (ph == PH_QKV) { wbase = (const char*)ly->tiles[0]; KT = g.KTh; t0 = g.q0; tstr = g.qs; }
+      else if (ph == PH_O) { wbase = (const char*)ly->tiles[1]; KT = g.KTq; t0 = bid; }
+      else if (ph == PH_GU) { wbase = (const char*)ly->tiles[2]; KT = g.KTh; t0 = g.gu0; }
+      else if (ph == PH_DN) { wbase = (const char*)ly->tiles[3]; KT = g.KTi; t0 = bid; }
       const int SEG = KT * C;   // pieces per tile
       for (int fi = 0; fi < nf; ++fi) {
         // the slot must be released by every consumer
@@ -356,7 +364,7 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
               const int slot = i >> 1, key = g.s0 + KPW * slot + lane / LPK;
               // keys of the next split, past L, and the row this launch writes (pos) are not read
               if (key < g.s1 && key != pos)
-                src = (const char*)((i & 1) ? ly.v_cache : ly.k_cache) + kv_off + (size_t)key * HD * 2 + (lane % LPK) * 16;
+                src = ((i & 1) ? vcache : kcache) + kv_off + (size_t)key * HD * 2 + (lane % LPK) * 16;
             } else {
               src = wbase + ((size_t)(t0 + seg * tstr) * SEG + ii) * kPiece + lane * 16;
             }
@@ -368,7 +376,7 @@ __device__ __forceinline__ void pds_loader(const PdsArgs& a, const PdsGeo& g, in
               ++seg;
             }
 #if TI_PDS_DIAG & 2   // diagnostic: every piece from this CU's own 96 KiB of layer 0's QKV tiles (L2 hits)
-          src = (const char*)a.layers[0].tiles[0] + ((size_t)bid * 96 + (size_t)(i % 96)) * kPiece + lane * 16;
+          src = (const char*)layer_c(a.layers, 0)->tiles[0] + ((size_t)bid * 96 + (size_t)(i % 96)) * kPiece + lane * 16;
 #endif
           dma_nt(src, __builtin_amdgcn_readfirstlane(base + j * kPiece));
         }
@@ -744,12 +752,12 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
   };
 
   for (int l = 0; l < a.n_layers; ++l) {
-    const PdsLayerDev& ly = a.layers[l];
+    const CLayer ly = layer_c(a.layers, l);
     // ============================================================== QKV (RoPE + KV append)
     float rms = 1.0f;
     {
       ts(l, PH_QKV, 0);
-      stage_scales(ly.scales[0], g.q0, g.qs, g.qn, g.KTh);
+      stage_scales(ly->scales[0], g.q0, g.qs, g.qn, g.KTh);
       gathering(true);
       if (l == 0) stage_x(a.fx, H, 0u, true);
       else stage_x(a.fxg, H, pds_tag(epoch, l - 1, PH_DN), false);
@@ -781,7 +789,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
           st_gran(a.qg + ng, __builtin_bit_cast(uint32_t, rv), tq);
         } else if (ok && !(n & 1)) {
           const bool is_k = qk;
-          uint16_t* cache = is_k ? ly.k_cache : ly.v_cache;   // for later launches
+          uint16_t* cache = is_k ? ly->k_cache : ly->v_cache;   // for later launches
           gptr_w((uint32_t*)(cache + ((size_t)hh * a.max_seq + pos) * HD + d))[0] = hv | (hp << 16);
           st_gran(a.kvg + ((size_t)hh * 2 + (is_k ? 0 : 1)) * (HD / 2) + d / 2, hv | (hp << 16), tq);
         }
@@ -936,7 +944,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     // ============================================================== O: residual + fold (ffn_norm)
     {
       ts(l, PH_O, 0);
-      stage_scales(ly.scales[1], bid, 0, g.on, g.KTq);
+      stage_scales(ly->scales[1], bid, 0, g.on, g.KTq);
       gathering(true);
       stage_x(a.aog, qd, pds_tag(epoch, l, PH_MRG), false);
       bar();
@@ -945,13 +953,13 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       gemv_phase(g.on, g.KTq);
       bar();
       ts(l, PH_O, 2);
-      if (c == 0 && g.on) resid_fold(ly.ffn_norm, pds_tag(epoch, l, PH_O));
+      if (c == 0 && g.on) resid_fold(ly->ffn_norm, pds_tag(epoch, l, PH_O));
       ts(l, PH_O, 3);
     }
     // ============================================================== gate/up: SiLU * up
     {
       ts(l, PH_GU, 0);
-      stage_scales(ly.scales[2], g.gu0, 1, g.gun, g.KTh);
+      stage_scales(ly->scales[2], g.gu0, 1, g.gun, g.KTh);
       gathering(true);
       stage_x(a.fxg, H, pds_tag(epoch, l, PH_O), false);
       if (c == 0) rms = fold_rms(a.ssg, a.nt_h, H, pds_tag(epoch, l, PH_O), false);
@@ -978,7 +986,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     // ============================================================== down: residual + fold (next norm)
     {
       ts(l, PH_DN, 0);
-      stage_scales(ly.scales[3], bid, 0, g.on, g.KTi);
+      stage_scales(ly->scales[3], bid, 0, g.on, g.KTi);
       gathering(true);
       stage_x(a.actg, I, pds_tag(epoch, l, PH_GU), false);
       bar();
@@ -989,7 +997,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       ts(l, PH_DN, 2);
       // the last layer's fold goes to the lm_head launch: plain write-through stores
       if (c == 0 && g.on && !(l == 0 && bid == a.drop_wg && l + 1 < a.n_layers))
-        resid_fold(l + 1 < a.n_layers ? a.layers[l + 1].attn_norm : a.out_norm,
+        resid_fold(l + 1 < a.n_layers ? layer_c(a.layers, l + 1)->attn_norm : a.out_norm,
                    l + 1 < a.n_layers ? pds_tag(epoch, l, PH_DN) : 0u);
       ts(l, PH_DN, 3);
     }
