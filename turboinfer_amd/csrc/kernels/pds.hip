@@ -633,18 +633,22 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       }
       acc[0] = acc[1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
     };
-    // one item: 4 MFMAs on (x, dequantized W), the int4 offset correction, the group scale
-    auto item = [&](const u32x4 (&wv)[C], int it, int ik) {
-      if (it != cur) {
-        flush();
-        cur = it;
-      }
+    // one item's 4 MFMAs on (x, dequantized W)
+    auto item_mfma = [&](const u32x4 (&wv)[C], int ik) {
       f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         const f16x8 bf = dequant_step<BITS>(wv, s4, magic);
         const f16x8 af = *(const f16x8*)(xrow + ik * 128 + s4 * 8);
         t = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, t, 0, 0, 0);
+      }
+      return t;
+    };
+    // an item's MFMA result into its virtual wave's partial: the int4 offset correction, the group scale
+    auto item_acc = [&](f32x4 t, int it, int ik) {
+      if (it != cur) {
+        flush();
+        cur = it;
       }
       if constexpr (BITS == 4) t -= corr[ik];
       const float sc = h2f(sl[(it * KT + ik) * 16 + r]);
@@ -688,9 +692,22 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
           }
         }
         release(fill);
+        // the fill's NU MFMA chains interleaved (independent accumulators hide the MFMA latency),
+        // then accumulated in item order (the same sums, in the same order, as item by item)
+        f32x4 tv[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) tv[u] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int u = 0; u < NU; ++u) {
+            const f16x8 bf = dequant_step<BITS>(w[u], s4, magic);
+            const f16x8 af = *(const f16x8*)(xrow + (live[u] ? ikt[u] : 0) * 128 + s4 * 8);
+            tv[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, tv[u], 0, 0, 0);
+          }
 #pragma unroll
         for (int u = 0; u < NU; ++u)
-          if (live[u]) item(w[u], itl[u], ikt[u]);
+          if (live[u]) item_acc(tv[u], itl[u], ikt[u]);
       }
     } else {
       // general shapes (K % 512 != 0 with several tiles): item by item
@@ -704,7 +721,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
             u32x4 w[C];
 #pragma unroll
             for (int cc = 0; cc < C; ++cc) w[cc] = *(const u32x4*)(slot + (j * C + cc) * kPiece);
-            item(w, tl, kt);
+            item_acc(item_mfma(w, kt), tl, kt);
           }
           if (++kt == KT) {
             kt = 0;
