@@ -644,14 +644,14 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       }
       return t;
     };
-    // an item's MFMA result into its virtual wave's partial: the int4 offset correction, the group scale
-    auto item_acc = [&](f32x4 t, int it, int ik) {
+    // an item's MFMA result into its virtual wave's partial: the int4 offset correction cr, the group
+    // scale sc (both read from LDS before the MFMAs where the caller can)
+    auto item_acc2 = [&](f32x4 t, int it, int ik, float cr, float sc) {
       if (it != cur) {
         flush();
         cur = it;
       }
-      if constexpr (BITS == 4) t -= corr[ik];
-      const float sc = h2f(sl[(it * KT + ik) * 16 + r]);
+      if constexpr (BITS == 4) t -= cr;
       if ((ik >> 2) & 1) {   // virtual wave c + 4 (static register indices: no scratch)
         acc[1][0] = fmaf(sc, t[0], acc[1][0]);
         acc[1][1] = fmaf(sc, t[1], acc[1][1]);
@@ -663,6 +663,9 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         acc[0][2] = fmaf(sc, t[2], acc[0][2]);
         acc[0][3] = fmaf(sc, t[3], acc[0][3]);
       }
+    };
+    auto item_acc = [&](f32x4 t, int it, int ik) {
+      item_acc2(t, it, ik, BITS == 4 ? corr[ik] : 0.0f, h2f(sl[(it * KT + ik) * 16 + r]));
     };
     if ((KT & 3) == 0 || ntl == 1) {
       // k-tile == item index (mod 4): this consumer's items sit at items c, c + 4, ... of every fill.
@@ -691,6 +694,13 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
             ++tl;
           }
         }
+        // each item's correction and scale, read before the MFMAs (their LDS latency overlaps them)
+        float crv[NU], scv[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          crv[u] = BITS == 4 && live[u] ? corr[ikt[u]] : 0.0f;
+          scv[u] = live[u] ? h2f(sl[(itl[u] * KT + ikt[u]) * 16 + r]) : 0.0f;
+        }
         release(fill);
         // the fill's NU MFMA chains interleaved (independent accumulators hide the MFMA latency),
         // then accumulated in item order (the same sums, in the same order, as item by item)
@@ -707,7 +717,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
           }
 #pragma unroll
         for (int u = 0; u < NU; ++u)
-          if (live[u]) item_acc(tv[u], itl[u], ikt[u]);
+          if (live[u]) item_acc2(tv[u], itl[u], ikt[u], crv[u], scv[u]);
       }
     } else {
       // general shapes (K % 512 != 0 with several tiles): item by item
