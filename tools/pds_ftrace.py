@@ -54,9 +54,12 @@ for b in range(4):
         # cadence: issue of fill k+1 - issue of fill k, within the phase
         cad = np.diff(t[idx, 0]) / 100
         idur = (ev[:, 6] - ev[:, 0]) / 100
+        math = ((ev[:, 7] - ev[:, 3]) / 100)[ev[:, 7] > 0] if ph != 1 else np.zeros(1)
+        gapv = np.diff(ev[:, 2]) / 100   # consumer 0: acquire to next acquire within the phase
         print(f"  {names[ph]:4s} issue {idur.mean():5.2f}  issue->pub {pub_lat.mean():5.2f}  pub->acq {cons_lag.mean():6.2f}  acq->rel {hold.mean():5.2f}"
               f"  issue cadence {np.median(cad):5.2f}  blocked {blocked.mean()*100:4.0f}% ({blk.mean() if blk.size else 0:5.2f} us)"
-              f"  acq-issue {((ev[:, 2] - ev[:, 0]) / 100).mean():6.2f}")
+              f"  acq-issue {((ev[:, 2] - ev[:, 0]) / 100).mean():6.2f}  rel->math {math.mean():5.2f}"
+              f"  acq cadence {np.median(gapv) if gapv.size else 0:5.2f}")
     # one layer in detail (layer 5): fill, issue, pub, acq, rel relative to the layer's first issue
     if os.environ.get("DETAIL", "1") == "0":
         break

@@ -89,7 +89,8 @@ static_assert(TI_PDS_AHEAD >= 1 && TI_PDS_AHEAD * (16 / TI_PDS_LOADERS) <= 63, "
 #endif
 #ifndef TI_PDS_DIAG
 #define TI_PDS_DIAG 0     // diagnostic builds only: 1 consumers only acquire / release the ring (no math, no
-                          // hand-offs: garbage results); 2 the loader re-reads layer 0's QKV tiles (L2)
+                          // hand-offs: garbage results); 2 the loader re-reads layer 0's QKV tiles (L2);
+                          // 4 the GEMV phases skip their math (garbage results, hand-offs kept)
 #endif
 #ifndef TI_PDS_FTRACE
 #define TI_PDS_FTRACE 0   // diagnostic build (tools/pds_ftrace.py): per-fill ring events of workgroups 0..3
@@ -98,7 +99,7 @@ static_assert(TI_PDS_AHEAD >= 1 && TI_PDS_AHEAD * (16 / TI_PDS_LOADERS) <= 63, "
 constexpr int kFtWg = 4, kFtFills = 2048;
 // [wg][fill][k]: 0 loader issue begins, 1 loader publishes it (FULL > fill), 2 consumer 0's wait
 // for it ends, 3 consumer 0 releases it, 4 the loader starts waiting for a FREE slot before it,
-// 5 that wait ends, 6 the loader's last piece of it issued
+// 5 that wait ends, 6 the loader's last piece of it issued, 7 consumer 0's math on it done (GEMV)
 static __device__ unsigned long long g_pds_ft[kFtWg][kFtFills][8];
 #define PDS_FT(f, k)                                                                                  \
   do {                                                                                                \
@@ -702,6 +703,10 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
           scv[u] = live[u] ? h2f(sl[(itl[u] * KT + ikt[u]) * 16 + r]) : 0.0f;
         }
         release(fill);
+#if TI_PDS_DIAG & 4   // diagnostic: no GEMV math (garbage results; the ring and hand-offs only)
+        if (c == 0) PDS_FT(fill, 7);
+        continue;
+#endif
         // the fill's NU MFMA chains interleaved (independent accumulators hide the MFMA latency),
         // then accumulated in item order (the same sums, in the same order, as item by item)
         f32x4 tv[NU];
@@ -718,6 +723,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
 #pragma unroll
         for (int u = 0; u < NU; ++u)
           if (live[u]) item_acc2(tv[u], itl[u], ikt[u], crv[u], scv[u]);
+        if (c == 0) PDS_FT(fill, 7);
       }
     } else {
       // general shapes (K % 512 != 0 with several tiles): item by item
