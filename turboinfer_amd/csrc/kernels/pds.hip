@@ -59,10 +59,15 @@ namespace ti {
 #ifndef TI_PDS_LOADERS
 #define TI_PDS_LOADERS 4   // loader waves (1, 2 or 4): one wave's VMEM issue is ~0.1 us per 1 KiB piece here
 #endif
-constexpr int kEC = 4;                         // consumer waves
+#ifndef TI_PDS_CONSUMERS
+#define TI_PDS_CONSUMERS 4   // consumer waves (4 or 8): each runs 8 / kEC of the per-layer kernels' 8 waves
+#endif
+constexpr int kEC = TI_PDS_CONSUMERS;           // consumer waves
 constexpr int kNL = TI_PDS_LOADERS;            // loader waves kEC .. kEC + kNL - 1
 constexpr int kEThreads = (kEC + kNL) * kWave;
 static_assert(kNL == 1 || kNL == 2 || kNL == 4, "loader waves");
+static_assert(kEC == 4 || kEC == 8, "consumer waves");
+constexpr int kVPC = 8 / kEC;                  // virtual waves per consumer: c, c + kEC, ...
 constexpr int kVW = 8;                         // virtual waves: the per-layer kernels' 8 waves
 constexpr int kPiece = 1024;                   // bytes per LDS-DMA wave instruction
 constexpr int kFill = 16;                      // pieces per ring slot
@@ -73,7 +78,9 @@ constexpr int kHdMax = 128;
 constexpr int kMaxQkvTiles = 4, kMaxGuTiles = 8;
 enum { PH_QKV = 0, PH_ATT, PH_O, PH_GU, PH_DN, PH_MRG, PH_N = 5 };
 // FULL: fills loader 0 has published (loaders w > 0: C_FULLX + w - 1); FREE + c: fills consumer c released
-enum { C_FULL = 0, C_FREE = 1, C_BAR = 5, C_GATHER = 6, C_DEAD = 7, C_EPOCH = 8, C_FULLX = 9, C_WORDS = 16 };
+enum { C_FULL = 0, C_FREE = 1, C_BAR = 1 + kEC, C_GATHER = 2 + kEC, C_DEAD = 3 + kEC, C_EPOCH = 4 + kEC,
+       C_FULLX = 5 + kEC, C_WORDS = 16 };
+static_assert(C_FULLX + kNL - 1 <= C_WORDS, "control words");
 #ifndef TI_PDS_THIN
 #define TI_PDS_THIN 1   // the loader keeps one slot in flight while its consumers gather (gather-pass)
 #endif
@@ -615,24 +622,25 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
   }
 #endif
   // GEMV phase over items (tile item / KT, k-tile item % KT): this consumer's items are k-tiles == c
-  // (mod 4), virtual wave kt % 8 in {c, c + 4}: the partial of (tile, virtual wave) accumulates
+  // (mod kEC), virtual waves kt % 8 in {c, c + kEC, ...}: the partial of (tile, virtual wave) accumulates
   // exactly as wave kt % 8 of gemv_wq_kernel does, then lands in slab[tile][v] (lanes 0-15).
   auto gemv_phase = [&](int ntl, int KT) {
     const int ni = ntl * KT, nf = pds_fills(ni * C);
     const f16* xrow = xl + kq * 32;
     for (int t = 0; t < ntl; ++t)
-      if (lane < 16) {
-        slab[(t * kVW + c) * 16 + lane] = 0.0f;
-        slab[(t * kVW + c + 4) * 16 + lane] = 0.0f;
-      }
-    f32x4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+      if (lane < 16)
+#pragma unroll
+        for (int j = 0; j < kVPC; ++j) slab[(t * kVW + c + kEC * j) * 16 + lane] = 0.0f;
+    f32x4 acc[kVPC];
+#pragma unroll
+    for (int j = 0; j < kVPC; ++j) acc[j] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
     int cur = 0, tl = 0, kt = 0;
     auto flush = [&]() {
-      if (lane < 16) {
-        slab[(cur * kVW + c) * 16 + lane] = acc[0][0];
-        slab[(cur * kVW + c + 4) * 16 + lane] = acc[1][0];
-      }
-      acc[0] = acc[1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+      if (lane < 16)
+#pragma unroll
+        for (int j = 0; j < kVPC; ++j) slab[(cur * kVW + c + kEC * j) * 16 + lane] = acc[j][0];
+#pragma unroll
+      for (int j = 0; j < kVPC; ++j) acc[j] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
     };
     // one item's 4 MFMAs on (x, dequantized W)
     auto item_mfma = [&](const u32x4 (&wv)[C], int ik) {
@@ -653,11 +661,11 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         cur = it;
       }
       if constexpr (BITS == 4) t -= cr;
-      if ((ik >> 2) & 1) {   // virtual wave c + 4 (static register indices: no scratch)
-        acc[1][0] = fmaf(sc, t[0], acc[1][0]);
-        acc[1][1] = fmaf(sc, t[1], acc[1][1]);
-        acc[1][2] = fmaf(sc, t[2], acc[1][2]);
-        acc[1][3] = fmaf(sc, t[3], acc[1][3]);
+      if (kVPC == 2 && ((ik / kEC) & 1)) {   // virtual wave c + kEC (static register indices: no scratch)
+        acc[kVPC - 1][0] = fmaf(sc, t[0], acc[kVPC - 1][0]);
+        acc[kVPC - 1][1] = fmaf(sc, t[1], acc[kVPC - 1][1]);
+        acc[kVPC - 1][2] = fmaf(sc, t[2], acc[kVPC - 1][2]);
+        acc[kVPC - 1][3] = fmaf(sc, t[3], acc[kVPC - 1][3]);
       } else {
         acc[0][0] = fmaf(sc, t[0], acc[0][0]);
         acc[0][1] = fmaf(sc, t[1], acc[0][1]);
@@ -668,10 +676,10 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     auto item_acc = [&](f32x4 t, int it, int ik) {
       item_acc2(t, it, ik, BITS == 4 ? corr[ik] : 0.0f, h2f(sl[(it * KT + ik) * 16 + r]));
     };
-    if ((KT & 3) == 0 || ntl == 1) {
-      // k-tile == item index (mod 4): this consumer's items sit at items c, c + 4, ... of every fill.
-      // They are all read, the slot is released, then the math runs.
-      constexpr int NU = IPF / 4;
+    if (KT % kEC == 0 || ntl == 1) {
+      // k-tile == item index (mod kEC): this consumer's items sit at items c, c + kEC, ... of every
+      // fill.  They are all read, the slot is released, then the math runs.
+      constexpr int NU = IPF / kEC;
       tl = 0;
       kt = c;
       for (int fi = 0; fi < nf; ++fi) {
@@ -685,11 +693,11 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         for (int u = 0; u < NU; ++u) {
           itl[u] = tl;
           ikt[u] = kt;
-          live[u] = fi * IPF + c + 4 * u < ni;
+          live[u] = fi * IPF + c + kEC * u < ni;
 #pragma unroll
           for (int cc = 0; cc < C; ++cc)
-            w[u][cc] = live[u] ? *(const u32x4*)(slot + ((c + 4 * u) * C + cc) * kPiece) : (u32x4){0u, 0u, 0u, 0u};
-          kt += 4;
+            w[u][cc] = live[u] ? *(const u32x4*)(slot + ((c + kEC * u) * C + cc) * kPiece) : (u32x4){0u, 0u, 0u, 0u};
+          kt += kEC;
           if (kt >= KT && ntl > 1) {
             kt -= KT;
             ++tl;
@@ -733,7 +741,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         const char* slot = smem + (fill % (uint32_t)a.n_slots) * kSlotBytes + lane * 16;
         for (int j = 0; j < IPF; ++j) {
           if (fi * IPF + j >= ni) break;
-          if ((kt & 3) == c) {
+          if (kt % kEC == c) {
             u32x4 w[C];
 #pragma unroll
             for (int cc = 0; cc < C; ++cc) w[cc] = *(const u32x4*)(slot + (j * C + cc) * kPiece);
@@ -846,9 +854,14 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       float qv[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) qv[e] = q_l[dl * 8 + e] * a.scale;
-      float mrun[2] = {-INFINITY, -INFINITY}, lrun[2] = {0.0f, 0.0f}, acc[2][8];
+      float mrun[kVPC], lrun[kVPC], acc[kVPC][8];
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < kVPC; ++u) {
+        mrun[u] = -INFINITY;
+        lrun[u] = 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kVPC; ++u)
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[u][e] = 0.0f;
       const int np = 2 * g.nslot, nf = pds_fills(np);
@@ -856,17 +869,17 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
         const uint32_t fill = fbase + fi;
         wait_full(fill);
         const char* slot = smem + (fill % (uint32_t)a.n_slots) * kSlotBytes + lane * 16;
-        u32x4 kr[2], vr[2];
+        u32x4 kr[kVPC], vr[kVPC];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int su = c + 4 * u, si = fi * 8 + su;
+        for (int u = 0; u < kVPC; ++u) {
+          const int su = c + kEC * u, si = fi * 8 + su;
           kr[u] = si < g.nslot ? *(const u32x4*)(slot + (2 * su) * kPiece) : (u32x4){0u, 0u, 0u, 0u};
           vr[u] = si < g.nslot ? *(const u32x4*)(slot + (2 * su + 1) * kPiece) : (u32x4){0u, 0u, 0u, 0u};
         }
         release(fill);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int su = c + 4 * u, si = fi * 8 + su;   // slot of the split; virtual wave su
+        for (int u = 0; u < kVPC; ++u) {
+          const int su = c + kEC * u, si = fi * 8 + su;   // slot of the split; virtual wave su
           if (si < g.nslot) {
             const int key = g.s0 + KPW * si + kg;
             const bool valid = key < g.s1;
@@ -897,8 +910,8 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       fbase += nf;
       // merge the lane groups of each virtual wave (attn_split_body)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int v = c + 4 * u;
+      for (int u = 0; u < kVPC; ++u) {
+        const int v = c + kEC * u;
         const float mx = groups_max<LPK>(mrun[u]);
         const float f = mrun[u] == -INFINITY ? 0.0f : __expf(mrun[u] - mx);
         const float lsum = groups_sum<LPK>(lrun[u] * f);
