@@ -60,7 +60,7 @@ namespace ti {
 #define TI_PDS_LOADERS 4   // loader waves (1, 2 or 4): one wave's VMEM issue is ~0.1 us per 1 KiB piece here
 #endif
 #ifndef TI_PDS_CONSUMERS
-#define TI_PDS_CONSUMERS 4   // consumer waves (4 or 8): each runs 8 / kEC of the per-layer kernels' 8 waves
+#define TI_PDS_CONSUMERS 8   // consumer waves (4 or 8): each runs 8 / kEC of the per-layer kernels' 8 waves
 #endif
 constexpr int kEC = TI_PDS_CONSUMERS;           // consumer waves
 constexpr int kNL = TI_PDS_LOADERS;            // loader waves kEC .. kEC + kNL - 1
