@@ -97,7 +97,8 @@ static_assert(TI_PDS_AHEAD >= 1 && TI_PDS_AHEAD * (16 / TI_PDS_LOADERS) <= 63, "
 #ifndef TI_PDS_DIAG
 #define TI_PDS_DIAG 0     // diagnostic builds only: 1 consumers only acquire / release the ring (no math, no
                           // hand-offs: garbage results); 2 the loader re-reads layer 0's QKV tiles (L2);
-                          // 4 the GEMV phases skip their math (garbage results, hand-offs kept)
+                          // 4 the GEMV phases skip their math (garbage results, hand-offs kept);
+                          // 8 granule gathers take what they find (no tag waits: garbage results)
 #endif
 #ifndef TI_PDS_FTRACE
 #define TI_PDS_FTRACE 0   // diagnostic build (tools/pds_ftrace.py): per-fill ring events of workgroups 0..3
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
           gv[b][1] = ld_sc1_b128(src, (uint32_t)idx * 32u + 16u);
         }
       }
-      if (!plain) {
+      if (!plain && !(TI_PDS_DIAG & 8)) {
         auto ok_b = [&](int b) {
           return gv[b][0][1] == tag && gv[b][0][3] == tag && gv[b][1][1] == tag && gv[b][1][3] == tag;
         };
@@ -549,10 +550,11 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     }
     if (!plain) {
       unsigned long long v[4];
+      constexpr bool kPoll = !(TI_PDS_DIAG & 8);
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = ld_sc1_u64((const unsigned long long*)src + (lane + 64 * j < n_ss ? lane + 64 * j : 0));
       Spin sp{ctl, a.err};
-      while (true) {
+      while (kPoll) {
         bool ok = true;
 #pragma unroll
         for (int j = 0; j < 4; ++j) ok = ok && (uint32_t)(v[j] >> 32) == tag;
@@ -575,7 +577,7 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
   auto gather1 = [&](const unsigned long long* base, int idx, bool want, uint32_t tag) -> uint32_t {
     unsigned long long v = want ? ld_sc1_u64(base + idx) : 0ull;
     Spin sp{ctl, a.err};
-    while (__builtin_amdgcn_ballot_w64(want && (uint32_t)(v >> 32) != tag) != 0ull) {
+    while (!(TI_PDS_DIAG & 8) && __builtin_amdgcn_ballot_w64(want && (uint32_t)(v >> 32) != tag) != 0ull) {
       if (!sp.tick_g()) break;
       if (want && (uint32_t)(v >> 32) != tag) v = ld_sc1_u64(base + idx);
     }
