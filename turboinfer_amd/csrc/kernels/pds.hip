@@ -592,6 +592,25 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     }
   };
 
+  // The phase's group scales issued BEFORE its gather and written to LDS after it, so their load
+  // shares the gather's round trip (one 16-byte piece per consumer thread; larger phases stage
+  // them up front as before)
+  auto scales_issue = [&](const uint16_t* sc, int t0, int tstride, int ntl, int KT, u32x4& r) -> bool {
+    const int per = KT * 2, n = ntl * per;
+    if (n > kEC * kWave) {
+      stage_scales(sc, t0, tstride, ntl, KT);
+      return false;
+    }
+    if (ctid < n) {
+      const int t = ctid / per, p = ctid - t * per;
+      r = gptr((const u32x4*)(sc + (size_t)(t0 + t * tstride) * KT * 16))[p];
+    }
+    return true;
+  };
+  auto scales_commit = [&](int ntl, int KT, const u32x4& r, bool issued) {
+    if (issued && ctid < ntl * KT * 2) ((u32x4*)sl)[ctid] = r;
+  };
+
   // ---- ring consumption
   auto wait_full = [&](uint32_t fill) {
     Spin sp{ctl, a.err};
@@ -800,11 +819,13 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     float rms = 1.0f;
     {
       ts(l, PH_QKV, 0);
-      stage_scales(ly->scales[0], g.q0, g.qs, g.qn, g.KTh);
+      u32x4 scr = {0u, 0u, 0u, 0u};
+      const bool sci = scales_issue(ly->scales[0], g.q0, g.qs, g.qn, g.KTh, scr);
       gathering(true);
       if (l == 0) stage_x(a.fx, H, 0u, true);
       else stage_x(a.fxg, H, pds_tag(epoch, l - 1, PH_DN), false);
       if (c == 0) rms = l == 0 ? fold_rms(a.ss, a.n_ss0, H, 0u, true) : fold_rms(a.ssg, a.nt_h, H, pds_tag(epoch, l - 1, PH_DN), false);
+      scales_commit(g.qn, g.KTh, scr, sci);
       bar();
       gathering(false);
       ts(l, PH_QKV, 1);
@@ -992,9 +1013,11 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     // ============================================================== O: residual + fold (ffn_norm)
     {
       ts(l, PH_O, 0);
-      stage_scales(ly->scales[1], bid, 0, g.on, g.KTq);
+      u32x4 scr = {0u, 0u, 0u, 0u};
+      const bool sci = scales_issue(ly->scales[1], bid, 0, g.on, g.KTq, scr);
       gathering(true);
       stage_x(a.aog, qd, pds_tag(epoch, l, PH_MRG), false);
+      scales_commit(g.on, g.KTq, scr, sci);
       bar();
       gathering(false);
       ts(l, PH_O, 1);
@@ -1007,10 +1030,12 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     // ============================================================== gate/up: SiLU * up
     {
       ts(l, PH_GU, 0);
-      stage_scales(ly->scales[2], g.gu0, 1, g.gun, g.KTh);
+      u32x4 scr = {0u, 0u, 0u, 0u};
+      const bool sci = scales_issue(ly->scales[2], g.gu0, 1, g.gun, g.KTh, scr);
       gathering(true);
       stage_x(a.fxg, H, pds_tag(epoch, l, PH_O), false);
       if (c == 0) rms = fold_rms(a.ssg, a.nt_h, H, pds_tag(epoch, l, PH_O), false);
+      scales_commit(g.gun, g.KTh, scr, sci);
       bar();
       gathering(false);
       ts(l, PH_GU, 1);
@@ -1034,9 +1059,11 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     // ============================================================== down: residual + fold (next norm)
     {
       ts(l, PH_DN, 0);
-      stage_scales(ly->scales[3], bid, 0, g.on, g.KTi);
+      u32x4 scr = {0u, 0u, 0u, 0u};
+      const bool sci = scales_issue(ly->scales[3], bid, 0, g.on, g.KTi, scr);
       gathering(true);
       stage_x(a.actg, I, pds_tag(epoch, l, PH_GU), false);
+      scales_commit(g.on, g.KTi, scr, sci);
       bar();
       gathering(false);
       ts(l, PH_DN, 1);
