@@ -573,6 +573,31 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
     t = group_sum<kWave>(t);
     return sqrtf(t / (float)K + a.eps);
   };
+  // The fold's sums of h^2 (n_ss <= 32 kEC granules) gathered by every consumer beside its x sweep
+  // (consumer c: granules [32 c, 32 c + 32), its load issued before the sweep so both share one round
+  // trip) into LDS (the attention's s_acc, idle outside the attention phase); after the barrier
+  // consumer 0 forms the rms from them in fold_rms's order (bit-identical).
+  auto ss_issue = [&](int n_ss) -> unsigned long long {
+    const int i = c * 32 + lane;
+    return lane < 32 && i < n_ss ? ld_sc1_u64(a.ssg + i) : 0ull;
+  };
+  auto ss_finish = [&](unsigned long long v, int n_ss, uint32_t tag) {
+    const int i = c * 32 + lane;
+    const bool want = lane < 32 && i < n_ss;
+    Spin sp{ctl, a.err};
+    while (!(TI_PDS_DIAG & 8) && __builtin_amdgcn_ballot_w64(want && (uint32_t)(v >> 32) != tag) != 0ull) {
+      if (!sp.tick_g()) break;
+      if (want && (uint32_t)(v >> 32) != tag) v = ld_sc1_u64(a.ssg + i);
+    }
+    if (want) s_acc[i] = __builtin_bit_cast(float, (uint32_t)v);
+  };
+  auto rms_lds = [&](int n_ss, int K) {
+    float t = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t += lane + 64 * j < n_ss ? s_acc[lane + 64 * j] : 0.0f;
+    t = group_sum<kWave>(t);
+    return sqrtf(t / (float)K + a.eps);
+  };
   // single granules of one wave: base[idx] for lanes with want, bounded
   auto gather1 = [&](const unsigned long long* base, int idx, bool want, uint32_t tag) -> uint32_t {
     unsigned long long v = want ? ld_sc1_u64(base + idx) : 0ull;
@@ -822,11 +847,15 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       u32x4 scr = {0u, 0u, 0u, 0u};
       const bool sci = scales_issue(ly->scales[0], g.q0, g.qs, g.qn, g.KTh, scr);
       gathering(true);
+      const bool ssp = l > 0 && a.nt_h <= kEC * 32;   // the sums gathered by every consumer
+      const unsigned long long ssv = ssp ? ss_issue(a.nt_h) : 0ull;
       if (l == 0) stage_x(a.fx, H, 0u, true);
       else stage_x(a.fxg, H, pds_tag(epoch, l - 1, PH_DN), false);
-      if (c == 0) rms = l == 0 ? fold_rms(a.ss, a.n_ss0, H, 0u, true) : fold_rms(a.ssg, a.nt_h, H, pds_tag(epoch, l - 1, PH_DN), false);
+      if (ssp) ss_finish(ssv, a.nt_h, pds_tag(epoch, l - 1, PH_DN));
+      else if (c == 0) rms = l == 0 ? fold_rms(a.ss, a.n_ss0, H, 0u, true) : fold_rms(a.ssg, a.nt_h, H, pds_tag(epoch, l - 1, PH_DN), false);
       scales_commit(g.qn, g.KTh, scr, sci);
       bar();
+      if (ssp && c == 0) rms = rms_lds(a.nt_h, H);
       gathering(false);
       ts(l, PH_QKV, 1);
       gemv_phase(g.qn, g.KTh);
@@ -1033,10 +1062,14 @@ __global__ __launch_bounds__(kEThreads, 1) void pds_kernel(const PdsArgs a) {
       u32x4 scr = {0u, 0u, 0u, 0u};
       const bool sci = scales_issue(ly->scales[2], g.gu0, 1, g.gun, g.KTh, scr);
       gathering(true);
+      const bool ssp = a.nt_h <= kEC * 32;
+      const unsigned long long ssv = ssp ? ss_issue(a.nt_h) : 0ull;
       stage_x(a.fxg, H, pds_tag(epoch, l, PH_O), false);
-      if (c == 0) rms = fold_rms(a.ssg, a.nt_h, H, pds_tag(epoch, l, PH_O), false);
+      if (ssp) ss_finish(ssv, a.nt_h, pds_tag(epoch, l, PH_O));
+      else if (c == 0) rms = fold_rms(a.ssg, a.nt_h, H, pds_tag(epoch, l, PH_O), false);
       scales_commit(g.gun, g.KTh, scr, sci);
       bar();
+      if (ssp && c == 0) rms = rms_lds(a.nt_h, H);
       gathering(false);
       ts(l, PH_GU, 1);
       gemv_phase(g.gun, g.KTh);
