@@ -39,3 +39,25 @@ def test_deep_oracle_bit_identical_to_decode_step(oracle, name, jitter):
         b.step(tok)
     a.close()
     b.close()
+
+
+def test_long_fixture_consistent_and_reproduced(oracle, golden):
+    """tests/golden/deep_long_tinyllama_1b.npz (gen_deep_long.py): the stored top-k, margins and
+    full logits agree with each other, and the oracle reproduces its first steps bit for bit."""
+    import json
+    d = golden("deep_long_tinyllama_1b")
+    cfg = json.loads(str(d["cfg"]))
+    top_i, top_v, toks = d["top_idx"], d["top_val"], d["tokens"]
+    np.testing.assert_array_equal(top_i[:, 0], toks)
+    np.testing.assert_array_equal(d["margin"], top_v[:, 0] - top_v[:, 1])
+    for i, s in enumerate(d["full_at"]):
+        np.testing.assert_array_equal(d["full_logits"][i][top_i[s]], top_v[s])
+        assert float(np.abs(d["full_logits"][i]).max()) == float(d["maxabs"][s])
+    m = OracleDeepModel(oracle, cfg, int(d["seed"][0]), 0.0)
+    m.fill_kv(int(d["fill"][0]), int(d["stream"][1]))
+    t = int(d["stream"][0])
+    for step in range(2):
+        t, lg = m.step(t)
+        assert t == toks[step]
+        np.testing.assert_array_equal(lg.view(np.uint32), d["full_logits"][step].view(np.uint32))
+    m.close()
