@@ -88,14 +88,12 @@ __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
 struct GemmKnobs {
   bool splitk = true;       // TI_GEMM_SPLITK=0: no split-K for under-filled tile grids
   bool rows_split = true;   // TI_GEMM_ROWS_SPLIT=0: all rows in one batched-rows workgroup
-  int tile_w4 = 0;          // TI_TILE_W4=2|3: prefill tiles on 4-wave workgroups, 128-row waves, TPW 2|3 (A/B)
 };
 __host__ inline const GemmKnobs& gemm_knobs() {
   static const GemmKnobs k = [] {
     GemmKnobs v;
     if (const char* e = getenv("TI_GEMM_SPLITK")) v.splitk = atoi(e) != 0;
     if (const char* e = getenv("TI_GEMM_ROWS_SPLIT")) v.rows_split = atoi(e) != 0;
-    if (const char* e = getenv("TI_TILE_W4")) v.tile_w4 = atoi(e) == 2 || atoi(e) == 3 ? atoi(e) : 0;
     return v;
   }();
   return k;
@@ -1446,9 +1444,8 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvAr
 // XB: activation-block buffers (2: double buffer; 4: issued three groups ahead, when the LDS holds them)
 // RB: 16-row blocks per row-wave (4: 64-row waves; 2: 32-row waves for calls of at most 32 rows,
 // half the activation block per group)
-__host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, int wmr = 2, int xb = 2, int rb = 4,
-                                              int nwv = 8) {
-  const int n = xb * 16 * rb * wmr * 256 + align16((nwv / wmr) * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
+__host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, int wmr = 2, int xb = 2, int rb = 4) {
+  const int n = xb * 16 * rb * wmr * 256 + align16((8 / wmr) * tpw * (K >> 7) * 32 * (g32 ? 4 : 1));
   // >= the epilogue's staging blocks (tile_epi_lds_bytes) + the batched fold's rms per row
   return n > 8 * 64 * 20 * 4 + 512 ? n : 8 * 64 * 20 * 4 + 512;
 }
@@ -1647,14 +1644,11 @@ __device__ __forceinline__ void tile_epilogue_lds(const GemvArgs& a, int tn, int
   }
 }
 
-template <int TPW, bool G32 = false, int WMR = 2, int XB = 2, int RB = 4, int NWV = kGemvWaves>
-__global__ __launch_bounds__(64 * NWV, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb, int n_ks) {
-  constexpr int NTH = 64 * NWV;                                 // threads per workgroup
-  constexpr int WCOL = NWV / WMR, BM = 16 * RB * WMR;          // column-waves, rows per workgroup
-  constexpr int ND = BM / (4 * NWV);                           // activation DMA instructions per wave and group
-  static_assert(RB == 4 || (RB == 2 && WMR == 1) || (RB == 8 && NWV == 4), "32-row waves: one row-wave per workgroup");
-  static_assert(NWV == kGemvWaves || (NWV == 4 && RB == 8 && WMR == 1 && XB == 4 && !G32 && TPW <= 3),
-                "4-wave workgroups: 128-row waves, one row-wave, the deep activation ring, int4 g128");
+template <int TPW, bool G32 = false, int WMR = 2, int XB = 2, int RB = 4>
+__global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb, int n_ks) {
+  constexpr int WCOL = kGemvWaves / WMR, BM = 16 * RB * WMR;   // column-waves, rows per workgroup
+  constexpr int ND = BM / 32;                                  // activation DMA instructions per wave and group
+  static_assert(RB == 4 || (RB == 2 && WMR == 1), "32-row waves: one row-wave per workgroup");
   static_assert(XB == 2 || (XB == 4 && TI_TILE_ASM), "deep activation ring: asm-issued DMA only");
   constexpr int XL = XB - 1;                               // groups of activations issued ahead
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1676,9 +1670,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm_tile_kernel(const GemvArgs a
   const int ntile_ok = min(WCOL * TPW, NT - t0);
   // batched fold (decode rows, ti_hip.h TI_FOLD_SS_ROWS): this thread's share of its row's rms
   // (TPW 4, already short of registers: after the stream)
-  const bool fold_in = NWV == kGemvWaves && a.epi.ss_in != nullptr;   // (4-wave shapes: never planned with it)
-  float share = fold_in && TPW < 4 ? fold_share(a, m0 + tid % BM, tid / BM, NTH / BM) : 0.0f;
-  for (int i = tid; i < n_sc; i += NTH) {
+  const bool fold_in = a.epi.ss_in != nullptr;
+  float share = fold_in && TPW < 4 ? fold_share(a, m0 + tid % BM, tid / BM, kGemvThreads / BM) : 0.0f;
+  for (int i = tid; i < n_sc; i += kGemvThreads) {
     const int j = i / (nk * 2 * SG), p = (j * KT + kb) * 2 * SG + (i - j * nk * 2 * SG);   // tile j, piece in slice
     ((u32x4*)sl)[p] = j < ntile_ok ? ld_w(sg + p) : (u32x4){0u, 0u, 0u, 0u};
   }
@@ -1743,32 +1737,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm_tile_kernel(const GemvArgs a
   asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
   auto compute = [&](const u32x4 (&w)[TPW], int kg) __attribute__((always_inline)) {
     const f16* xr = xb + (kg & (XB - 1)) * BM * 128 + (wm * 16 * RB + r) * 128;
-    if constexpr (RB == 8) {
-      // 128-row waves (4-wave workgroups, up to 512 registers a wave): per k-chunk s4 the eight
-      // row blocks' fragments, each dequantized weight fragment feeding 8 MFMAs; every tile's
-      // group partials stay live until the group's scale FMAs (same products and order as RB 4)
-      f32x4 tmp[TPW][RB];
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        f16x8 xs[RB];
-#pragma unroll
-        for (int b = 0; b < RB; ++b) xs[b] = *(const f16x8*)(xr + b * 16 * 128 + (((kq * 4 + s4) ^ r) * 8));
-#pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-          const f16x8 bf = deq_int4_signed(w[t][s4], magic);
-#pragma unroll
-          for (int b = 0; b < RB; ++b)
-            tmp[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                xs[b], bf, s4 == 0 ? (f32x4){0.0f, 0.0f, 0.0f, 0.0f} : tmp[t][b], 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < TPW; ++t) {
-        const float sc = h2f(sl[((wn * TPW + t) * KT + kg) * 16 + r]);
-#pragma unroll
-        for (int b = 0; b < RB; ++b) acc[t][b] = fma_scale4(sc, tmp[t][b], acc[t][b]);
-      }
-    } else {
     f16x8 xf[RB][4];
 #pragma unroll
     for (int b = 0; b < RB; ++b)
@@ -1808,7 +1776,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm_tile_kernel(const GemvArgs a
       const float sc = h2f(sl[((wn * TPW + t) * KT + kg) * 16 + r]);
 #pragma unroll
       for (int b = 0; b < RB; ++b) acc[t][b] = fma_scale4(sc, tmp[b], acc[t][b]);
-    }
     }
   };
   // Per group kg: x(kg) and W(kg) were issued earlier; issue x(kg + 1) and W(kg + WR - 1),
@@ -1929,7 +1896,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm_tile_kernel(const GemvArgs a
   lds_barrier();
   const float* rmsv = (const float*)(smem + tile_epi_lds_bytes());   // batched fold: rms per row
   if (fold_in) {
-    if constexpr (TPW == 4) share = fold_share(a, m0 + tid % BM, tid / BM, NTH / BM);
+    if constexpr (TPW == 4) share = fold_share(a, m0 + tid % BM, tid / BM, kGemvThreads / BM);
     ((float*)smem)[tid] = share;
     lds_barrier();
     fold_rms_finish(a, (const float*)smem, (float*)rmsv, BM, tid);
@@ -1951,7 +1918,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void gemm_tile_kernel(const GemvArgs a
   const int ek = a.epi.kind;
   const bool via_lds = TI_TILE_EPI_LDS && (ek == TI_EPI_STORE_F32 || ek == TI_EPI_RESID_F32 || ek == TI_EPI_QKV_ROPE_KV ||
                                            (ek == TI_EPI_SILU_MUL_F16 && !a.epi.out_packed));
-  float* stg = (float*)smem + wave * ((RB > 4 ? 16 * RB : 64) * kTileEpiStride);
+  float* stg = (float*)smem + wave * (64 * kTileEpiStride);
 #pragma unroll 1
   for (int t = 0; t < (merged ? TPW : 0); ++t) {
     const int tn = t0 + wn * TPW + t;
@@ -2021,12 +1988,8 @@ static std::atomic<int> g_num_cus{0};   // (a racing first query stores the same
       (const void*)gemm_tile_kernel<1, true, 1, TI_TILE_XB4, 2>, (const void*)gemm_tile_kernel<2, true, 1, TI_TILE_XB4, 2>,  \
       (const void*)gemm_tile_kernel<3, true, 1, TI_TILE_XB4, 2>
 #define TI_TILE_FNS TI_TILE_FNS_XB(2), TI_TILE_FNS_XB(TI_TILE_XB4), TI_TILE_FNS_RB2
-__host__ inline const void* tile_fn(int tpw, bool g32, int wmr, int xb, int rb = 4, int nwv = 8) {
+__host__ inline const void* tile_fn(int tpw, bool g32, int wmr, int xb, int rb = 4) {
   static const void* const fns[] = {TI_TILE_FNS};
-#if TI_TILE_ASM
-  if (nwv == 4)   // 4-wave workgroups: 128-row waves, int4 g128, the deep activation ring
-    return tpw == 2 ? (const void*)gemm_tile_kernel<2, false, 1, 4, 8, 4> : (const void*)gemm_tile_kernel<3, false, 1, 4, 8, 4>;
-#endif
   if (rb == 2) return fns[32 + (g32 ? 4 : 0) + tpw - 1];   // (group-32 at TPW 4: never planned)
   const int base = xb == 4 ? 16 : 0;
   if (tpw == 3) return fns[base + 12 + (wmr == 1 ? 2 : 0) + (g32 ? 1 : 0)];
@@ -2354,11 +2317,7 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<4, XM_F16F>, (const void*)gemv_wq_kernel<8, XM_F16F>,
       (const void*)gemv_wq_kernel<16, XM_F16F>, (const void*)gemv_wq_kernel<4, XM_ATTN>,
       (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS, TI_ROWS_FNS,
-      TI_TILE_FNS,
-#if TI_TILE_ASM
-      tile_fn(2, false, 1, 4, 8, 4), tile_fn(3, false, 1, 4, 8, 4),
-#endif
-  };
+      TI_TILE_FNS};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
                  "hipFuncSetAttribute(gemv_wq_kernel)");
@@ -2576,18 +2535,14 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   const bool has_ws = epi->splitk_ws && epi->splitk_bytes > TI_SPLITK_TICKET_BYTES && splitk_on();
   const bool tile = batched && x_kind == TI_X_F16 && (M >= tile_rows() || (!g32 && wide_tile(bits, M, N)));
   const bool rows = !tile && batched && (g32_rowsk || packed_x || M > 32 || (M > 16 && rows_on()));
-  int n_cb = 0, n_rb = 0, n_ks = 1, tpw = 2, wmr = 2, xbuf = 2, trb = 4, nwv = kGemvWaves;
+  int n_cb = 0, n_rb = 0, n_ks = 1, tpw = 2, wmr = 2, xbuf = 2, trb = 4;
   if (tile) {
     tile_plan(M, N, K, g32, query_cus(), has_ws ? epi->splitk_bytes : 0, &wmr, &tpw, &n_ks, &trb);   // (tile_plan)
-    const int w4 = gemm_knobs().tile_w4;
-    if (TI_TILE_ASM && w4 && !g32 && !fold_in && M >= 128 && tile_lds_bytes(K, w4, false, 1, 4, 8, 4) <= 160 * 1024) {
-      nwv = 4, wmr = 1, trb = 8, tpw = w4, n_ks = 1;
-    }
     n_rb = (M + 16 * trb * wmr - 1) / (16 * trb * wmr);
-    n_cb = ((N >> 4) + (nwv / wmr) * tpw - 1) / ((nwv / wmr) * tpw);
+    n_cb = ((N >> 4) + (8 / wmr) * tpw - 1) / ((8 / wmr) * tpw);
     grid = (n_cb + 7) / 8 * 8 * n_rb * n_ks;
-    xbuf = nwv == 4 ? 4 : tile_xb(K, tpw, g32, wmr, trb);
-    lds = tile_lds_bytes(K, tpw, g32, wmr, xbuf, trb, nwv);
+    xbuf = tile_xb(K, tpw, g32, wmr, trb);
+    lds = tile_lds_bytes(K, tpw, g32, wmr, xbuf, trb);
   } else if (rows) {
     rows_on();
     rows_plan(M, N, K, query_cus(), &rMB, &rRG, &r_rb, &grid, &ntl, g32);   // grid: column groups
@@ -2625,9 +2580,9 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   a.epi = *epi;
   hipStream_t s = (hipStream_t)stream;
   if (tile) {
-    const void* f = tile_fn(tpw, g32, wmr, xbuf, trb, nwv);
+    const void* f = tile_fn(tpw, g32, wmr, xbuf, trb);
     void* args[] = {&a, &n_cb, &n_rb, &n_ks};
-    TI_HIP_CHECK(hipLaunchKernel(f, dim3(grid), dim3(64 * nwv), args, lds, s), "hipLaunchKernel(gemm_tile_kernel)");
+    TI_HIP_CHECK(hipLaunchKernel(f, dim3(grid), dim3(kGemvThreads), args, lds, s), "hipLaunchKernel(gemm_tile_kernel)");
     TI_LAUNCH_CHECK("gemm_tile_kernel");
     return TI_OK;
   }
