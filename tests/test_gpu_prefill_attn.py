@@ -75,6 +75,16 @@ def test_prefill_attention_7b_chunk(ti):
     np.testing.assert_allclose(got, dec, rtol=4e-3, atol=4e-3)
 
 
+@pytest.mark.parametrize("hd", [64, 128])
+def test_prefill_attention_chunk_beyond_one_wave_per_simd(ti, hd):
+    """A chunk with more waves than the chip has SIMDs (1024 rows x 32 heads = 2048 waves) takes the
+    3-deep K / V ring (two waves per SIMD); the chunks above take the deep ring (ti_attn_prefill)."""
+    pos = np.arange(1024, dtype=np.int32)
+    _, _, _, got, dec = _case(ti, 1024, 32, 32, hd, pos, 1024, seed=hd + 3)
+    assert np.all(np.isfinite(got))
+    np.testing.assert_allclose(got, dec, rtol=4e-3, atol=4e-3)
+
+
 def test_prefill_attention_rejects_bad_sizes(ti):
     L = ti.lib()
     assert L.ti_attn_prefill(1, 1, 1, 16, 1, 0, 4, 4, 128, 1, None) != 0

@@ -23,6 +23,8 @@
 // Queries are dealt longest-prefix first; a 4-block K / V ring per wave hides the loads.
 #include <math.h>
 
+#include <atomic>
+
 #include "common.hpp"
 
 namespace ti {
@@ -51,10 +53,13 @@ __device__ __forceinline__ void pf_split(float x, _Float16& hi, _Float16& lo) {
 }
 
 #ifndef TI_PF_RING
-#define TI_PF_RING 3   // K / V blocks in flight per wave (3: 248 VGPRs, two waves per SIMD)
+#define TI_PF_RING 3   // K / V blocks in flight per wave (3: 246 registers at hd 128, two waves per SIMD)
+#endif
+#ifndef TI_PF_RING_DEEP
+#define TI_PF_RING_DEEP 6   // the ring when every wave of the launch has a SIMD to itself (352 registers at hd 128)
 #endif
 
-template <int HD>
+template <int HD, int RING = TI_PF_RING>
 __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc, int max_seq,
                                                           const int32_t* __restrict__ pos, int M, int heads, int gsh,
@@ -109,7 +114,7 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
   const int nkb = kmax / 16 + 1;
   // K / V blocks in flight: a ring of kPfRing blocks, each slot refilled right after its block
   // is consumed (one or two waves per SIMD: the ring, not other waves, hides the load latency)
-  constexpr int kPfRing = TI_PF_RING;
+  constexpr int kPfRing = RING;
   KRaw kr[kPfRing];
   VRaw vr[kPfRing][4];
 #pragma unroll
@@ -218,12 +223,35 @@ extern "C" int ti_attn_prefill(const float* q, const uint16_t* k_cache, const ui
   const dim3 grid((M + qpw - 1) / qpw, kv_heads);
   const float scale = 1.0f / sqrtf((float)head_dim);   // tensor_engine.cpp:1288
   hipStream_t s = (hipStream_t)stream;
-  if (head_dim == 128)
-    hipLaunchKernelGGL(ti::attn_prefill_kernel<128>, grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq, pos, M, heads,
-                       gsh, scale, out);
-  else
-    hipLaunchKernelGGL(ti::attn_prefill_kernel<64>, grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq, pos, M, heads,
-                       gsh, scale, out);
+  // One wave per workgroup.  While the launch has at most one wave per SIMD (a 7B chunk of up to
+  // 512 rows: 1024 waves on 256 CUs x 4 SIMDs) nothing is gained by fitting two waves on a SIMD,
+  // so each wave keeps the deep ring: the longest rows' waves set the time, and their key
+  // stream is latency-bound (one block per ~1.1 us at 3 in flight).  Larger chunks keep the
+  // 3-deep ring, two waves per SIMD.
+  static std::atomic<int> simds{0};
+  int ns = simds.load(std::memory_order_relaxed);
+  if (ns == 0) {
+    int dev = 0, n = 0;
+    ns = hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess
+             ? 4 * n : -1;
+    simds.store(ns, std::memory_order_relaxed);   // (a racing first call stores the same value)
+  }
+  const bool deep = (long)grid.x * grid.y <= ns;
+  if (head_dim == 128) {
+    if (deep)
+      hipLaunchKernelGGL((ti::attn_prefill_kernel<128, TI_PF_RING_DEEP>), grid, dim3(64), 0, s, q, k_cache, v_cache,
+                         max_seq, pos, M, heads, gsh, scale, out);
+    else
+      hipLaunchKernelGGL((ti::attn_prefill_kernel<128, TI_PF_RING>), grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq,
+                         pos, M, heads, gsh, scale, out);
+  } else {
+    if (deep)
+      hipLaunchKernelGGL((ti::attn_prefill_kernel<64, TI_PF_RING_DEEP>), grid, dim3(64), 0, s, q, k_cache, v_cache,
+                         max_seq, pos, M, heads, gsh, scale, out);
+    else
+      hipLaunchKernelGGL((ti::attn_prefill_kernel<64, TI_PF_RING>), grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq,
+                         pos, M, heads, gsh, scale, out);
+  }
   TI_LAUNCH_CHECK("attn_prefill_kernel");
   return TI_OK;
 }
