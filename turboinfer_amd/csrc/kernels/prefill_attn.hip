@@ -16,10 +16,12 @@
 //                 S^T[key 4(l>>4)+i][column l&15]
 //   online softmax per column: 4 values per lane, two xor-shuffles across the lane groups;
 //                 masked keys (key > pos[row]) get p = 0
-//   O += P V      v_mfma_f32_16x16x16_f16: its A fragment (column l&15, keys 4(l>>4) + e) is
-//                 exactly the lane's own 4 p values (hi, lo); B for output tile t is V[key][dim
-//                 (l&15) hd/16 + t], half t of the lane's four 16-byte V loads (byte permutes)
-// Rows of O are rescaled by each block's alpha (read from the lane that owns that column).
+//   O^T += V^T P^T v_mfma_f32_16x16x16_f16: its B fragment (column l&15, keys 4(l>>4) + e) is
+//                 exactly the lane's own 4 p values (hi, lo); A for output tile t is V[key][dim
+//                 (l&15) hd/16 + t], half t of the lane's four 16-byte V loads (byte permutes);
+//                 D holds O^T[dim (4(l>>4) + i) hd/16 + t][column l&15]
+// So every accumulator row of a lane belongs to the lane's own column: each block's alpha rescales
+// it in place, and the lane writes hd/4 contiguous outputs of its column at the end.
 // Queries are dealt longest-prefix first; a 4-block K / V ring per wave hides the loads.
 #include <math.h>
 
@@ -56,7 +58,7 @@ __device__ __forceinline__ void pf_split(float x, _Float16& hi, _Float16& lo) {
 #define TI_PF_RING 3   // K / V blocks in flight per wave (3: 246 registers at hd 128, two waves per SIMD)
 #endif
 #ifndef TI_PF_RING_DEEP
-#define TI_PF_RING_DEEP 6   // the ring when every wave of the launch has a SIMD to itself (352 registers at hd 128)
+#define TI_PF_RING_DEEP 4   // the ring when every wave of the launch has a SIMD to itself (4 and 6 measured equal)
 #endif
 
 template <int HD, int RING = TI_PF_RING>
@@ -99,13 +101,12 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
   auto load = [&](int kb, KRaw& k, VRaw (&v)[4]) {
     const int kk = min(kb * 16 + r, max_seq - 1);
 #pragma unroll
-    for (int c = 0; c < KW; ++c) k[c] = *(const u32x4*)(kb0 + (size_t)kk * HD + 32 * c);
+    for (int c = 0; c < KW; ++c) k[c] = *(const u32x4*)(kb0 + (uint32_t)(kk * HD + 32 * c));
+    // keys past every column's prefix (kmax) may be unwritten (NaN): they read row kmax instead,
+    // finite, which their p = 0 then multiplies away exactly (no branch per load)
+    const int kl = min(kmax, max_seq - 1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int kv = kb * 16 + 4 * g + j;
-      // keys past every row's prefix may be unwritten: zero so that p = 0 times them stays 0
-      v[j] = kv <= kmax ? *(const VRaw*)(vb0 + (size_t)min(kv, max_seq - 1) * HD) : VRaw{};
-    }
+    for (int j = 0; j < 4; ++j) v[j] = *(const VRaw*)(vb0 + (uint32_t)(min(kb * 16 + 4 * g + j, kl) * HD));
   };
   f32x4 acc[DV];
 #pragma unroll
@@ -151,11 +152,9 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
       l_run = l_run * alpha + ps;
       m_run = mn;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float ar = __shfl(alpha, 4 * g + i, 64);   // alpha of query 4g + i (row i of O)
+      for (int t = 0; t < DV; ++t)   // O^T: every row of the lane's accumulators is its own column's
 #pragma unroll
-        for (int t = 0; t < DV; ++t) acc[t][i] *= ar;
-      }
+        for (int i = 0; i < 4; ++i) acc[t][i] *= alpha;
       f16x4 ph, pl;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -179,29 +178,31 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
         const uint32_t b01 = __builtin_amdgcn_perm(vw[1][t >> 1], vw[0][t >> 1], sel);
         const uint32_t b23 = __builtin_amdgcn_perm(vw[3][t >> 1], vw[2][t >> 1], sel);
         const f16x4 bf = __builtin_bit_cast(f16x4, ((unsigned long long)b23 << 32) | b01);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(ph, bf, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(pl, bf, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(bf, ph, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(bf, pl, acc[t], 0, 0, 0);
       }
       if (kb + kPfRing < nkb) load(kb + kPfRing, kr[u], vr[u]);
     }
   }
   float lt = l_run + __shfl_xor(l_run, 16, 64);
   lt += __shfl_xor(lt, 32, 64);
+  // lane (r, g) holds O^T[dim DV (4g + i) + t][column r] in acc[t][i]: dims 4g DV .. 4g DV + 4 DV - 1
+  // of column r's (row, head), contiguous
+  const float inv = 1.0f / lt;
+  const int row = q0 + (r >> gsh), hh = kvh * G + (r & (G - 1));
+  if (row < M) {
+    uint16_t* dst = out + ((size_t)row * heads + hh) * HD + 4 * g * DV;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float inv = 1.0f / __shfl(lt, 4 * g + i, 64);
-    const int col = 4 * g + i, row = q0 + (col >> gsh), hh = kvh * G + (col & (G - 1));
-    uint32_t o[DV / 2];
+    for (int i = 0; i < 4; ++i) {
+      uint32_t o[DV / 2];
 #pragma unroll
-    for (int t = 0; t < DV / 2; ++t) {
-      const uint16_t lo = __builtin_bit_cast(uint16_t, (_Float16)(acc[2 * t][i] * inv));
-      const uint16_t hi = __builtin_bit_cast(uint16_t, (_Float16)(acc[2 * t + 1][i] * inv));
-      o[t] = lo | ((uint32_t)hi << 16);
-    }
-    if (row < M) {
-      uint16_t* dst = out + ((size_t)row * heads + hh) * HD + r * DV;
-      if constexpr (HD == 128) *(ti::u32x4*)dst = (ti::u32x4){o[0], o[1], o[2], o[3]};
-      else *(uint2*)dst = make_uint2(o[0], o[1]);
+      for (int t = 0; t < DV / 2; ++t) {
+        const uint16_t lo = __builtin_bit_cast(uint16_t, (_Float16)(acc[2 * t][i] * inv));
+        const uint16_t hi = __builtin_bit_cast(uint16_t, (_Float16)(acc[2 * t + 1][i] * inv));
+        o[t] = lo | ((uint32_t)hi << 16);
+      }
+      if constexpr (HD == 128) *(ti::u32x4*)(dst + i * DV) = (ti::u32x4){o[0], o[1], o[2], o[3]};
+      else *(uint2*)(dst + i * DV) = make_uint2(o[0], o[1]);
     }
   }
 }
