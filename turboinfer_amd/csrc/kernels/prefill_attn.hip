@@ -120,68 +120,84 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
   VRaw vr[kPfRing][4];
 #pragma unroll
   for (int u = 0; u < kPfRing; ++u) load(u, kr[u], vr[u]);   // past nkb: clamped rows, zero V
+  // NB blocks (16 NB keys) per online-softmax step: one column max across the four lanes, one
+  // alpha and one rescale of O per step (2 when the ring divides into pairs); the wave's time is
+  // this chain, not the K / V stream
+  constexpr int NB = kPfRing % 2 == 0 ? 2 : 1;
   for (int kb0 = 0; kb0 < nkb; kb0 += kPfRing) {
 #pragma unroll
-    for (int u = 0; u < kPfRing; ++u) {
+    for (int u = 0; u < kPfRing; u += NB) {
       const int kb = kb0 + u;
       if (kb >= nkb) break;
-      f32x4 s = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+      f32x4 s[NB];
 #pragma unroll
-      for (int c = 0; c < KW; ++c) {
-        const f16x8 kf = __builtin_bit_cast(f16x8, kr[u][c]);
-        s = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[c], s, 0, 0, 0);
-        s = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[c], s, 0, 0, 0);
-      }
-      float pv[4], bm = -INFINITY;
+      for (int b = 0; b < NB; ++b) s[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool ok = kb * 16 + 4 * g + i <= p;
-        pv[i] = ok ? s[i] : -INFINITY;
-        bm = fmaxf(bm, pv[i]);
-      }
+      for (int c = 0; c < KW; ++c)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const f16x8 kf = __builtin_bit_cast(f16x8, kr[u + b][c]);
+          s[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[c], s[b], 0, 0, 0);
+          s[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[c], s[b], 0, 0, 0);
+        }
+      // keys past the column's position (and a second block past nkb: its keys are past kmax)
+      float pv[NB][4], bm = -INFINITY;
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool ok = (kb + b) * 16 + 4 * g + i <= p;
+          pv[b][i] = ok ? s[b][i] : -INFINITY;
+          bm = fmaxf(bm, pv[b][i]);
+        }
       bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
       bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
       const float mn = fmaxf(m_run, bm);   // finite: key 0 is in every row's prefix
       const float alpha = m_run == mn ? 1.0f : __expf(m_run - mn);
       float ps = 0.0f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        pv[i] = pv[i] == -INFINITY ? 0.0f : __expf(pv[i] - mn);
-        ps += pv[i];
-      }
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pv[b][i] = pv[b][i] == -INFINITY ? 0.0f : __expf(pv[b][i] - mn);
+          ps += pv[b][i];
+        }
       l_run = l_run * alpha + ps;
       m_run = mn;
 #pragma unroll
       for (int t = 0; t < DV; ++t)   // O^T: every row of the lane's accumulators is its own column's
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[t][i] *= alpha;
-      f16x4 ph, pl;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        _Float16 hi, lo;
-        pf_split(pv[e], hi, lo);
-        ph[e] = hi;
-        pl[e] = lo;
-      }
-      uint32_t vw[4][DV / 2];
+      for (int b = 0; b < NB; ++b) {
+        f16x4 ph, pl;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if constexpr (HD == 128) {
-          vw[j][0] = vr[u][j][0]; vw[j][1] = vr[u][j][1]; vw[j][2] = vr[u][j][2]; vw[j][3] = vr[u][j][3];
-        } else {
-          vw[j][0] = vr[u][j].x; vw[j][1] = vr[u][j].y;
+        for (int e = 0; e < 4; ++e) {
+          _Float16 hi, lo;
+          pf_split(pv[b][e], hi, lo);
+          ph[e] = hi;
+          pl[e] = lo;
         }
-      }
+        uint32_t vw[4][DV / 2];
 #pragma unroll
-      for (int t = 0; t < DV; ++t) {
-        const uint32_t sel = (t & 1) ? 0x07060302u : 0x05040100u;
-        const uint32_t b01 = __builtin_amdgcn_perm(vw[1][t >> 1], vw[0][t >> 1], sel);
-        const uint32_t b23 = __builtin_amdgcn_perm(vw[3][t >> 1], vw[2][t >> 1], sel);
-        const f16x4 bf = __builtin_bit_cast(f16x4, ((unsigned long long)b23 << 32) | b01);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(bf, ph, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(bf, pl, acc[t], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (HD == 128) {
+            vw[j][0] = vr[u + b][j][0]; vw[j][1] = vr[u + b][j][1]; vw[j][2] = vr[u + b][j][2]; vw[j][3] = vr[u + b][j][3];
+          } else {
+            vw[j][0] = vr[u + b][j].x; vw[j][1] = vr[u + b][j].y;
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < DV; ++t) {
+          const uint32_t sel = (t & 1) ? 0x07060302u : 0x05040100u;
+          const uint32_t b01 = __builtin_amdgcn_perm(vw[1][t >> 1], vw[0][t >> 1], sel);
+          const uint32_t b23 = __builtin_amdgcn_perm(vw[3][t >> 1], vw[2][t >> 1], sel);
+          const f16x4 bf = __builtin_bit_cast(f16x4, ((unsigned long long)b23 << 32) | b01);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(bf, ph, acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(bf, pl, acc[t], 0, 0, 0);
+        }
+        if (kb + b + kPfRing < nkb) load(kb + b + kPfRing, kr[u + b], vr[u + b]);
       }
-      if (kb + kPfRing < nkb) load(kb + kPfRing, kr[u], vr[u]);
     }
   }
   float lt = l_run + __shfl_xor(l_run, 16, 64);
