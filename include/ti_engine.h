@@ -78,6 +78,16 @@ int ti_engine_generate(ti_engine* e, int n_streams, const int32_t* prompts, cons
                        int prompt_stride, const int32_t* start_pos, int max_new, int32_t* out_tokens,
                        float* last_logits);
 
+/* Stop token of ti_engine_generate / ti_engine_generate_sampled (-1 = none, the default).  When
+ * set, the device loop runs in chunks of 4, 8, 16, 32, then 64 steps, and after each chunk the new
+ * tokens are read back; the loop ends once every stream has emitted the token, as the reference's
+ * generate() breaks at EOS (inference_engine.cpp:760-764, token id 2).  A stream's tokens end at its
+ * first stop token (included); the rest of its max_new entries are -1. */
+int ti_engine_set_stop(ti_engine* e, int32_t token);
+/* Step-graph replays (decode steps, each covering every stream of its call) and prompt chunks
+ * (prefill) this engine has run since it was created. */
+int ti_engine_counters(ti_engine* e, uint64_t* decode_steps, uint64_t* prefill_chunks);
+
 /* ti_engine_generate with the reference sampler on the device: after each
  * step's lm_head, ti_sample_step applies sample_next_token (inference_engine.cpp:1554-1673:
  * temperature, top-k, softmax, top-p, the draw) and feeds the token back, so the loop never

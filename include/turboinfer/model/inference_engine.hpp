@@ -16,9 +16,16 @@
 // prefilled in chunks of up to 1024 rows through the tile GEMM and the MFMA causal attention
 // (DESIGN 4.6).
 //
-// Binary layout: InferenceConfig carries two trailing fields (weight_bits, gpu_index) that the
-// reference's struct does not have, so this header is a source drop-in, not a layout drop-in:
-// code compiled against the reference's header must be recompiled against this one.
+// Binary layout: every public class has the reference's layout (InferenceConfig 48 bytes, the
+// engine's private members mirrored: tensor_engine_, impl_, the vocabulary maps), so a program
+// compiled against the reference's headers links and runs against this library unchanged
+// (tests/test_source_compat.py).  The two MI355X options live outside InferenceConfig, in the
+// model's metadata or the environment (ModelMetadata::extra_params first, then the variable):
+//   * "turboinfer.weight_bits" / TI_WEIGHT_BITS: the weight format below (default 0 = auto);
+//   * "turboinfer.gpu_index" / TI_GPU_INDEX: the HIP device the engine binds (default 0).
+// A ModelData with metadata but no tensors (the reference's test programs) builds the engine's
+// synthetic INT4 model of that shape (ti_engine_synth): the reference runs such a model on its
+// placeholder fallbacks instead.
 //
 // Model forms accepted (reference weight names, inference_engine.cpp:483-563):
 //   * llama: token_embeddings / embed_tokens, per-layer q/k/v/o, gate/up/down, both norms,
@@ -35,6 +42,8 @@
 #include <cstddef>
 #include <memory>
 #include <string>
+#include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "../core/tensor.hpp"
@@ -54,9 +63,6 @@ struct InferenceConfig {
   int eos_token_id = 2;
   bool use_cache = true;
   core::ComputeDevice device = core::ComputeDevice::kAuto;
-  // ---- MI355X additions (trailing, defaulted)
-  int weight_bits = 0;          ///< 4 / 8 / 16 (| 32 group-32, | 32 | 64 Q4_1); 0 = auto (fp32 -> 16, ints -> their width, GGUF blocks kept)
-  int gpu_index = 0;            ///< HIP device this engine binds
 };
 
 struct GenerationResult {
@@ -99,9 +105,14 @@ class InferenceEngine {
   std::string performance_stats() const;
 
  private:
+  // the reference's data members in its order (inference_engine.hpp:211-214, 318-320 there)
   ModelMetadata model_metadata_;
   InferenceConfig config_;
+  std::unique_ptr<core::TensorEngine> tensor_engine_;
   std::unique_ptr<class InferenceEngineImpl> impl_;
+  std::unordered_map<std::string, int> vocab_map_;      // (tokenizer: out of scope, kept empty)
+  std::unordered_map<int, std::string> id_to_token_;
+  std::vector<std::pair<std::string, std::string>> bpe_merges_;
   void validate_input_tokens(const std::vector<int>& tokens) const;
   void validate_batch_size(size_t batch_size) const;
 };

@@ -67,6 +67,7 @@ class Quantizer {
 
  private:
   QuantizationConfig config_;
+  std::unique_ptr<class QuantizerImpl> impl_;   ///< (layout of the reference's class; unused here)
 };
 
 const char* quantization_type_to_string(QuantizationType type);

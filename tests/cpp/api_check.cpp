@@ -203,15 +203,16 @@ static int generate_gguf(const std::string& path, const std::string& prompts_fil
   return run_generate(model::ModelLoader::load(path), prompts_file, n_new, top_k, bits, out);
 }
 
-static int run_generate(const model::ModelData& md, const std::string& prompts_file, int n_new, int top_k, int bits,
+static int run_generate(const model::ModelData& md_in, const std::string& prompts_file, int n_new, int top_k, int bits,
                         const std::string& out) {
+  model::ModelData md = md_in;
+  md.metadata().extra_params["turboinfer.weight_bits"] = std::to_string(bits);   // (the MI355X option)
   const Tensor pt = read_array(prompts_file);   // i32 [n][len]
   const size_t n = pt.shape().size(0), len = pt.shape().size(1);
   std::vector<std::vector<int>> prompts(n);
   for (size_t i = 0; i < n; ++i) prompts[i].assign(pt.data_ptr<int32_t>() + i * len, pt.data_ptr<int32_t>() + (i + 1) * len);
   model::InferenceConfig cfg;
   cfg.top_k = (size_t)top_k;
-  cfg.weight_bits = bits;
   cfg.max_sequence_length = 256;
   cfg.max_batch_size = 8;
   // generate() contract checks (tests/test_cpp_api.py::test_generate_contract_matches_reference)

@@ -113,6 +113,9 @@ def test_engine_config_validation(L):
     assert rc != 0   # vocab 1000 not a multiple of 16 (or no device here)
     cfg = T.EngineConfig(1024, 256, 2, 6, 4, 64, 512, 1e4, 1e-5, 4, 64, 1, 0, 0, 0)
     assert L.ti_engine_create(C.byref(cfg), C.byref(h)) != 0  # heads % kv_heads
+    # generate()'s stop token and the step counters need an engine
+    assert L.ti_engine_set_stop(None, 2) == 1 and b"ti_engine_set_stop" in L.ti_last_error()
+    assert L.ti_engine_counters(None, None, None) == 1
 
 
 @pytest.mark.parametrize("bits", [4, 8, 16])

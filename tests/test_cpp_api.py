@@ -305,6 +305,72 @@ def test_inference_engine_llama_greedy_matches_reference(api_check, golden, orac
             assert g == r, f"token {i}: C++ API {g} reference {r}"
 
 
+# Seeds of a small GQA INT4 model (prompt 1 17 42) whose greedy decode emits EOS (token 2) as its
+# k-th new token, every step's top-2 margin above 3x the logits tolerance (searched with the oracle).
+_EOS_CFG = {"vocab": 128, "hidden": 256, "layers": 2, "heads": 4, "kv_heads": 2, "head_dim": 64, "inter": 512,
+            "rope_theta": 10000.0, "eps": 1e-05, "bits": 4, "group": 128, "max_seq": 256}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,k", [(78, 3), (87, 5), (114, 10)])
+def test_generate_stops_the_device_loop_at_eos(api_check, oracle, tmp_path, seed, k):
+    """generate() breaks at EOS (inference_engine.cpp:760-764): the device loop stops within one
+    chunk of the EOS step (ti_engine_set_stop: chunks of 4, 8, 16, ... steps), so a request that
+    ends at its k-th token out of max_new = 200 runs the k steps rounded up to the chunk schedule,
+    not 200 (the engine's own step counter, reported as performance_stats' forward passes), and
+    its time covers only those steps."""
+    from pyoracle import OracleModel
+    prompt = [1, 17, 42]
+    m = OracleModel(oracle, _EOS_CFG, seed, 0.1)
+    w = m.weights()
+    for t in prompt[:-1]:
+        m.step(t)
+    want, tok = [], prompt[-1]
+    for _ in range(k):
+        tok, lg = m.step(tok)
+        s = np.sort(lg)
+        assert s[-1] - s[-2] > 6e-3 * float(np.max(np.abs(lg)))
+        want.append(int(tok))
+    m.close()
+    assert want[-1] == 2 and 2 not in want[:-1], want
+    c = _EOS_CFG
+    mdir = tmp_path / "eos"
+    mdir.mkdir()
+    lines = [f"meta {c['vocab']} {c['hidden']} {c['layers']} {c['heads']} {c['inter']} {c['rope_theta']!r}"]
+    for j, (name, v) in enumerate(w.items()):
+        write(mdir / f"t{j}.bin", v.astype(f32))
+        lines.append(f"{name} t{j}.bin")
+    (mdir / "manifest.txt").write_text("\n".join(lines) + "\n")
+    outp = api_check("generate", mdir, write(tmp_path / "p.bin", np.array([prompt], np.int32)), 200, 1, 4,
+                     tmp_path / "o.bin")
+    got = [int(v) for v in read(tmp_path / "o.bin")[0] if v >= 0]
+    assert got == prompt + want
+    out = outp.splitlines()
+    assert out[0] == "eos_token"
+    steps = 0
+    for chunk in (4, 8, 16, 32):      # the chunk schedule until the EOS step is covered
+        steps += chunk
+        if steps >= k:
+            break
+    passes = [ln for ln in out if "Forward Passes:" in ln]
+    assert passes and int(passes[0].split(":")[1]) == steps + 1, (passes, steps)   # + the prompt's prefill chunk
+
+
+@pytest.mark.gpu
+def test_reference_built_program_runs_against_our_library():
+    """Binary drop-in: the reference's tests/test_inference_engine.cpp, compiled against the
+    REFERENCE's headers (tests/test_source_compat.py builds it in the build container), runs
+    against libturboinfer_amd.so: engine from metadata only (the synthetic INT4 model of that
+    shape), generate with logprobs, set_config, repeated generations."""
+    exe = os.path.join(ROOT, "tests", "cpp", "bin", "ref_test_inference_engine")
+    assert os.path.exists(exe), "build it with tests/test_source_compat.py or __graft_entry__.build()"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    assert "Test completed successfully" in r.stdout
+    gen = [ln for ln in r.stdout.splitlines() if "Generated tokens:" in ln]
+    assert gen and 1 <= int(gen[0].split(":")[1]) <= 10, gen   # (sampled: an EOS may end it early)
+
+
 # ---------------------------------------------------------------- TINQ (SURVEY 8(f) rank 3)
 def _tinq_module():
     import importlib.util

@@ -87,7 +87,7 @@ EXPORTED = [
     "ti_wpack_q_host", "ti_engine_set_tensor_q", "ti_sample_workspace_bytes", "ti_sample_device_ws",
     "ti_wpack_q1_host", "ti_engine_set_tensor_q1", "ti_epilogue_bytes",
     "ti_sample_step_ws", "ti_pds_granule_words", "ti_hbm_calibrate", "ti_gemm_kernel_name", "ti_pds_supported",
-    "ti_gemm_fold_partials",
+    "ti_gemm_fold_partials", "ti_engine_set_stop", "ti_engine_counters",
 ]
 
 _lib = None
@@ -184,6 +184,9 @@ def lib() -> C.CDLL:
         L.ti_engine_generate.argtypes = [vp, i32, vp, vp, i32, vp, i32, vp, vp]
         L.ti_engine_step.argtypes = [vp, i32, vp, vp, vp]
         L.ti_engine_set_prefill.argtypes = [vp, i32]
+        if hasattr(L, "ti_engine_set_stop"):
+            L.ti_engine_set_stop.argtypes = [vp, C.c_int32]
+            L.ti_engine_counters.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         if hasattr(L, "ti_engine_set_fold"):   # (older TI_LIB builds in A/B runs lack it)
             L.ti_gemm_grid.argtypes = [i32, i32, i32]
             L.ti_engine_set_fold.argtypes = [vp, i32, C.POINTER(C.c_int)]
@@ -436,6 +439,17 @@ class Engine:
     def set_prefill(self, rows):
         """Prompt tokens per prefill chunk (0 = consume prompts one token per decode step)."""
         check(lib().ti_engine_set_prefill(self.h, rows))
+
+    def set_stop(self, token=-1):
+        """Stop token of generate / generate_sampled (-1: none): the device loop ends in chunks once
+        every stream has emitted it (ti_engine_set_stop)."""
+        check(lib().ti_engine_set_stop(self.h, token))
+
+    def counters(self):
+        """(decode step-graph replays, prefill chunks) run by this engine (ti_engine_counters)."""
+        a, b = C.c_uint64(0), C.c_uint64(0)
+        check(lib().ti_engine_counters(self.h, C.byref(a), C.byref(b)))
+        return int(a.value), int(b.value)
 
     def set_fold(self, on=None) -> bool:
         """Folded rms_norm hand-off on/off (None: query); returns whether 1-stream steps use it."""

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <map>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <iomanip>
 #include <random>
@@ -30,6 +31,18 @@ namespace {
 // generate()'s end-of-sequence token: the reference tests `next_token == 2` (inference_engine.cpp:759-760),
 // not config.eos_token_id (which only its beam search reads, :2015)
 constexpr int kGenerateEos = 2;
+
+// The reference's public layouts are kept (a program built against its headers links against
+// this library): InferenceConfig has no room for the MI355X options, so they come from the model's
+// extra_params, then the environment, then the default (inference_engine.hpp header note).
+static_assert(sizeof(InferenceConfig) == 48 && sizeof(GenerationResult) == 96, "reference layout (LP64)");
+static_assert(sizeof(InferenceEngine) == 400, "reference layout (LP64)");
+int engine_option(const ModelMetadata& md, const char* key, const char* env, int dflt) {
+  const auto it = md.extra_params.find(key);
+  if (it != md.extra_params.end()) return std::atoi(it->second.c_str());
+  if (const char* v = std::getenv(env)) return std::atoi(v);
+  return dflt;
+}
 
 [[noreturn]] void off_path(const std::string& what, const char* row) {
   throw std::runtime_error("InferenceEngine::" + what + ": not part of the MI355X decode hot path (SURVEY.md 8(f) " +
@@ -311,6 +324,45 @@ class InferenceEngineImpl {
     check(ti_engine_set_tensor(eng, slot, layer, v.data(), TI_SCALE_UNIT), "ti_engine_set_tensor");
   }
 
+  // The device engine of cfg (filled in by the caller but for the stream capacity).
+  void create(const InferenceConfig& c) {
+    cfg.attn_splits = 0;
+    // streams held at once: the configured batch, bounded to 64 GiB of fp16 KV
+    const double kv_stream = 2.0 * cfg.layers * cfg.kv_heads * cfg.head_dim * 2.0 * cfg.max_seq;
+    capacity = (int)std::max<size_t>(1, std::min<size_t>(c.max_batch_size, (size_t)(64.0 * (1ull << 30) / kv_stream)));
+    capacity = std::min(capacity, 64);
+    cfg.max_batch = compat ? 1 : capacity;
+    check(ti_init(cfg.device), "ti_init");
+    check(ti_engine_create(&cfg, &eng), "ti_engine_create");
+    // generate() ends its device loop at EOS (token id 2, inference_engine.cpp:759-764)
+    if (!compat) check(ti_engine_set_stop(eng, kGenerateEos), "ti_engine_set_stop");
+  }
+
+  // Metadata without tensors (the reference's own test programs build engines this way and run
+  // them on its placeholder fallbacks, inference_engine.cpp:293-296, 377-380, 672-684): the
+  // engine's seeded synthetic llama model of that shape (ti_engine_synth), INT4 unless the
+  // weight_bits option says 8 or 16.
+  void build_synthetic(const ModelMetadata& md, const InferenceConfig& c, int gpu) {
+    const int H = (int)md.hidden_size, nh = (int)md.num_heads;
+    cfg.vocab = (int)md.vocab_size;
+    cfg.hidden = H;
+    cfg.layers = (int)md.num_layers;
+    cfg.heads = nh;
+    cfg.kv_heads = nh;
+    cfg.head_dim = H / nh;
+    cfg.inter = md.intermediate_size ? (int)md.intermediate_size : 4 * H;
+    cfg.rope_theta = md.rope_theta > 0.0f ? md.rope_theta : 10000.0f;
+    cfg.eps = 1e-5f;
+    const int bits = engine_option(md, "turboinfer.weight_bits", "TI_WEIGHT_BITS", 0);
+    cfg.bits = bits == 8 || bits == 16 ? bits : 4;
+    cfg.max_seq = (int)std::max<size_t>(1, c.max_sequence_length);
+    cfg.compat = 0;
+    cfg.device = gpu;
+    compat = false;
+    create(c);
+    check(ti_engine_synth(eng, 0x7475726269ull, 0.0f), "ti_engine_synth");
+  }
+
   void build(const ModelData& m, const InferenceConfig& c) {
     if (gguf_named(m)) {
       gguf_src = true;
@@ -321,6 +373,8 @@ class InferenceEngineImpl {
     size_t I = md.intermediate_size;
     if (!H || !L || !nh || !V || H % nh) throw std::runtime_error("InferenceEngine: incomplete model metadata");
     const size_t hd = H / nh;
+    const int gpu = engine_option(md, "turboinfer.gpu_index", "TI_GPU_INDEX", 0);
+    if (m.num_tensors() == 0) return build_synthetic(md, c, gpu);
     const core::Tensor* q0 = layer_tensor(m, 0, "self_attn.q_proj.weight", "attention.q_proj.weight");
     const core::Tensor* k0 = layer_tensor(m, 0, "self_attn.k_proj.weight", "attention.k_proj.weight");
     const core::Tensor* up0 = layer_tensor(m, 0, "mlp.up_proj.weight", "feed_forward.w1.weight");
@@ -330,7 +384,7 @@ class InferenceEngineImpl {
     compat = (q0 == nullptr);
 
     // weight format
-    int bits = c.weight_bits;
+    int bits = engine_option(md, "turboinfer.weight_bits", "TI_WEIGHT_BITS", 0);
     if (bits == 0) {
       bits = 16;
       if (is_int(*up0)) {
@@ -366,15 +420,8 @@ class InferenceEngineImpl {
     cfg.bits = compat ? 16 : bits;
     cfg.max_seq = (int)std::max<size_t>(1, c.max_sequence_length);
     cfg.compat = compat ? 1 : 0;
-    cfg.device = c.gpu_index;
-    cfg.attn_splits = 0;
-    // streams held at once: the configured batch, bounded to 64 GiB of fp16 KV
-    const double kv_stream = 2.0 * L * cfg.kv_heads * hd * 2.0 * cfg.max_seq;
-    capacity = (int)std::max<size_t>(1, std::min<size_t>(c.max_batch_size, (size_t)(64.0 * (1ull << 30) / kv_stream)));
-    capacity = std::min(capacity, 64);
-    cfg.max_batch = compat ? 1 : capacity;
-    check(ti_init(c.gpu_index), "ti_init");
-    check(ti_engine_create(&cfg, &eng), "ti_engine_create");
+    cfg.device = gpu;
+    create(c);
 
     for (size_t l = 0; l < L; ++l) {
       const int li = (int)l;
@@ -442,10 +489,8 @@ InferenceEngine::InferenceEngine(InferenceEngine&&) noexcept = default;
 InferenceEngine& InferenceEngine::operator=(InferenceEngine&&) noexcept = default;
 
 void InferenceEngine::set_config(const InferenceConfig& config) {
-  if (config.max_sequence_length != config_.max_sequence_length || config.weight_bits != config_.weight_bits ||
-      config.gpu_index != config_.gpu_index)
-    throw std::runtime_error("InferenceEngine::set_config: max_sequence_length / weight_bits / gpu_index are fixed "
-                             "when the device engine is built");
+  if (config.max_sequence_length != config_.max_sequence_length)
+    throw std::runtime_error("InferenceEngine::set_config: max_sequence_length is fixed when the device engine is built");
   config_ = config;
 }
 
@@ -569,8 +614,14 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
     }
     std::vector<std::vector<int>> fresh(n);
     std::vector<std::vector<float>> lps(n);
+    // forward passes = the engine's decode steps + prompt chunks actually run (the device loop
+    // stops at EOS in chunks, so this is not the planned step count)
+    uint64_t d0 = 0, p0 = 0, d1 = 0, p1 = 0;
+    check(ti_engine_counters(im.eng, &d0, &p0), "ti_engine_counters");
+    const bool device_loop = greedy || (n == 1 && config_.top_k >= 1 && config_.top_k <= (size_t)V);
     if (greedy) {
-      // the whole token loop on the device (argmax feedback), EOS / length applied after
+      // the whole token loop on the device (argmax feedback); it stops once every request of the
+      // group emitted EOS (ti_engine_set_stop), the length limit is applied after
       std::vector<int32_t> prompts((size_t)n * stride, 0), lens(n), out((size_t)n * want);
       for (int m = 0; m < n; ++m) {
         const auto& p = batches[c0 + m];
@@ -582,7 +633,6 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
       check(ti_engine_generate(im.eng, n, prompts.data(), lens.data(), (int)stride, nullptr, (int)steps_new, out.data(),
                                nullptr),
             "ti_engine_generate");
-      im.total_forward_passes += stride + steps_new - 1;
       for (int m = 0; m < n; ++m) {
         const size_t b = budget(batches[c0 + m].size());
         for (size_t t = 0; t < std::min(b, steps_new); ++t) fresh[m].push_back(out[(size_t)m * steps_new + t]);
@@ -603,7 +653,6 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
                                        config_.temperature, (int)config_.top_k, config_.top_p, draws.data(), out.data(),
                                        lp.data()),
             "ti_engine_generate_sampled");
-      im.total_forward_passes += p.size() + steps_new - 1;
       const size_t b = budget(p.size());
       for (size_t t = 0; t < std::min(b, steps_new); ++t) {
         fresh[0].push_back(out[t]);
@@ -644,6 +693,10 @@ std::vector<GenerationResult> InferenceEngine::generate_batch(const std::vector<
       }
     }
     const float ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (device_loop) {   // (the host-sampler loop counts its own steps)
+      check(ti_engine_counters(im.eng, &d1, &p1), "ti_engine_counters");
+      im.total_forward_passes += (size_t)((d1 - d0) + (p1 - p0));
+    }
     for (int m = 0; m < n; ++m) finish(results[c0 + m], batches[c0 + m], fresh[m], lps[m], ms);
   }
   return results;

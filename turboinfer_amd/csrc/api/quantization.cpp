@@ -101,6 +101,10 @@ QuantizationInfo saved_tensor_info(const core::Tensor& t, QuantizationType type)
 }
 }  // namespace
 
+// (the reference's pimpl, kept for its class layout; this Quantizer needs no state beyond config_)
+class QuantizerImpl {};
+static_assert(sizeof(Quantizer) == 56, "reference layout (LP64)");
+
 Quantizer::Quantizer(const QuantizationConfig& config) : config_(config) {}
 Quantizer::~Quantizer() = default;
 void Quantizer::set_config(const QuantizationConfig& config) { config_ = config; }

@@ -130,6 +130,11 @@ struct ti_engine {
   int32_t* in_tokens = nullptr;
   int32_t* out_tokens = nullptr;
   int in_cap = 0, out_cap = 0;
+  // generate() stop token (ti_engine_set_stop): the device loop runs in chunks and ends once every
+  // stream has emitted it (the reference's `break` at EOS, inference_engine.cpp:760-764); -1 = none
+  int32_t stop_token = -1;
+  uint64_t n_decode_steps = 0;   // step-graph replays (ti_engine_counters)
+  uint64_t n_prefill_chunks = 0; // prompt chunks through enqueue_prefill
   int splits_max = 1;
   int64_t kv_stride = 0;
   uint16_t** kv_tab = nullptr;   // device [2 * layers]: every layer's K then V cache base (ti_kv_copy_slots)
@@ -334,6 +339,7 @@ int run_steps(ti_engine* e, int M, int advance, int n) {
   hipGraphExec_t g = nullptr;
   TI_TRY(get_graph(e, M, advance, &g));
   for (int s = 0; s < n; ++s) E_CHECK(hipGraphLaunch(g, e->s), "hipGraphLaunch");
+  e->n_decode_steps += (uint64_t)n;
   return TI_OK;
 }
 
@@ -596,6 +602,7 @@ static bool prefill_attn_on() {
 
 int enqueue_prefill(ti_engine* e, int m, int t0, int rows, int base) {
   const ti_engine_config& c = e->c;
+  ++e->n_prefill_chunks;
   std::vector<int32_t> bp(rows);
   for (int j = 0; j < rows; ++j) bp[j] = base + t0 + j;
   TI_TRY(ti_memcpy_h2d(e->pf_base, bp.data(), (size_t)rows * 4, e->s));
@@ -1041,20 +1048,49 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
       for (int t0 = 0; t0 < s0; t0 += e->pf_rows) TI_TRY(enqueue_prefill(e, m, t0, std::min(e->pf_rows, s0 - t0), base[m]));
   }
   TI_TRY(ti_memcpy_h2d(e->step_ctr, &s0, 4, e->s));
-  TI_TRY(run_steps(e, n, 1, steps - s0));
-  TI_TRY(ti_stream_sync(e->s));
-  TI_TRY(handoff_check(e));
   std::vector<int32_t> outd((size_t)n * e->out_cap);
   std::vector<unsigned long long> am;
-  TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
-  TI_TRY(read_argmax(e, n, am));
+  // generated token t of stream m once `ran` steps have run: the step feed record holds every
+  // token but the last, which is still in the argmax slots
+  auto token_at = [&](int m, int t, int ran) -> int32_t {
+    const int produced = ran - nin[m] + 1;
+    if (t < produced - 1) return outd[(size_t)m * e->out_cap + t];
+    if (t == produced - 1) return (int32_t)(0xFFFFFFFFu - (uint32_t)(am[m] & 0xFFFFFFFFull));
+    return -1;
+  };
+  int ran = steps;
+  if (e->stop_token < 0) {
+    TI_TRY(run_steps(e, n, 1, steps - s0));
+    TI_TRY(ti_stream_sync(e->s));
+    TI_TRY(handoff_check(e));
+    TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
+    TI_TRY(read_argmax(e, n, am));
+  } else {
+    // chunks of 4, 8, 16, 32, then 64 steps; after each, every stream's new tokens are read back
+    // (one small copy) and the loop ends once each has emitted the stop token
+    ran = s0;
+    for (int chunk = 4; ran < steps; chunk = std::min(chunk * 2, 64)) {
+      const int S = std::min(chunk, steps - ran);
+      TI_TRY(run_steps(e, n, 1, S));
+      ran += S;
+      TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
+      TI_TRY(read_argmax(e, n, am));   // (synchronises the stream)
+      TI_TRY(handoff_check(e));
+      bool all = true;
+      for (int m = 0; m < n && all; ++m) {
+        bool hit = false;
+        const int produced = ran - nin[m] + 1;
+        for (int t = 0; t < std::min(produced, max_new) && !hit; ++t) hit = token_at(m, t, ran) == e->stop_token;
+        all = hit || produced >= max_new;
+      }
+      if (all) break;
+    }
+  }
   for (int m = 0; m < n; ++m) {
-    const int produced = steps - nin[m] + 1;   // generated tokens of stream m
+    bool stopped = false;
     for (int t = 0; t < max_new; ++t) {
-      int32_t tok;
-      if (t < produced - 1) tok = outd[(size_t)m * e->out_cap + t];
-      else if (t == produced - 1) tok = (int32_t)(0xFFFFFFFFu - (uint32_t)(am[m] & 0xFFFFFFFFull));
-      else tok = -1;
+      const int32_t tok = stopped ? -1 : token_at(m, t, ran);
+      stopped = stopped || (e->stop_token >= 0 && tok == e->stop_token);
       out_tokens[(size_t)m * max_new + t] = tok;
     }
   }
@@ -1420,6 +1456,19 @@ int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32
       if (slot_req[m] >= 0) slot_pos[m] += S;
     }
   }
+  return TI_OK;
+}
+
+int ti_engine_set_stop(ti_engine* e, int32_t token) {
+  if (!e || token < -1 || token >= e->c.vocab) return ti_set_error(TI_ERR_ARG, "ti_engine_set_stop: token %d", token);
+  e->stop_token = token;
+  return TI_OK;
+}
+
+int ti_engine_counters(ti_engine* e, uint64_t* decode_steps, uint64_t* prefill_chunks) {
+  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_counters: null");
+  if (decode_steps) *decode_steps = e->n_decode_steps;
+  if (prefill_chunks) *prefill_chunks = e->n_prefill_chunks;
   return TI_OK;
 }
 
