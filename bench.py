@@ -108,21 +108,28 @@ def cpu_baseline(m, L):
                       f"change it); host {os.uname().machine}, {os.cpu_count()} logical CPUs"}
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed FETCH_SIZE pass
-    (profiles/r*_pmc_traffic.json, written by tools/pmc_traffic.py from a separate
-    `rocprofv3 --pmc FETCH_SIZE` run of this bench), or None."""
+def pmc_traffic(kernel: str, model: str, batch: int):
+    """HBM bytes per launch of `kernel` from the newest committed FETCH_SIZE pass of this
+    configuration (profiles/r*_pmc_traffic*.json, written by tools/pmc_traffic.py from a separate
+    `rocprofv3 --pmc FETCH_SIZE` run of this bench; files without a "config" are the default
+    llama2-7b one-stream pass), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
-    if not files:
-        return None, None
-    try:
-        d = json.load(open(files[-1]))
-        k = d["kernels"][kernel]
-        v = k.get("step_weighted_traffic_bytes_per_launch", k["traffic_bytes_per_launch"])
-        return int(v), os.path.relpath(files[-1], ROOT)
-    except (KeyError, ValueError, OSError):
-        return None, None
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic*.json")):
+        try:
+            d = json.load(open(f))
+            c = d.get("config", {"model": "llama2-7b", "batch": 1})
+            if c.get("model") != model or int(c.get("batch", 1)) != batch or kernel not in d["kernels"]:
+                continue
+            k = d["kernels"][kernel]
+            v = int(k.get("step_weighted_traffic_bytes_per_launch", k["traffic_bytes_per_launch"]))
+        except (KeyError, ValueError, OSError):
+            continue
+        tag = os.path.basename(f).split("_")[0]          # r<N>: newest round wins
+        rank = (int(tag[1:]) if tag[1:].isdigit() else 0, f)
+        if best is None or rank > best[0]:
+            best = (rank, v, os.path.relpath(f, ROOT))
+    return (best[1], best[2]) if best else (None, None)
 
 
 def dry_run(g: "Group", args) -> int:
@@ -304,8 +311,8 @@ def main() -> int:
         achieved = gemv_bytes / gemv_us / 1e3   # GB/s
     e.close()
 
-    traffic, traffic_src = pmc_traffic("pds_kernel" if pds_on else "gemv_wq_kernel<4>") if bits == 4 and B == 1 \
-        else (None, None)
+    traffic, traffic_src = pmc_traffic("pds_kernel" if pds_on else (f"gemv_wq_kernel<{bits}>" if B == 1 else "gemm_family"),
+                                       args.model, B)
     result = None
     if g.rank == 0:
         result = {

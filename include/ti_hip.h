@@ -242,7 +242,7 @@ int ti_gemm_lds_bytes(int M, int N, int K);
  * Two kernels: the fused one (rms_norm prologue, any bits) takes up to 16 rows while its LDS
  * image fits; for bits 4 with TI_X_F16 rows the batched-rows kernel takes up to
  * TI_GEMM_MAX_ROWS rows at any K (batched decode, generate_batch inference_engine.cpp:804-828)
- * and is used above TI_GEMM_FUSED_ROWS (env, default 2) rows.  An int4 caller with more rows
+ * and is used above 2 rows (a fixed crossover).  An int4 caller with more rows
  * than this returns for TI_X_F32_RMSNORM should normalise them with ti_rmsnorm_f16 and pass
  * TI_X_F16 rows.  0 = shape unsupported. */
 #define TI_GEMM_MAX_ROWS 1024

@@ -13,6 +13,11 @@ max|logit|, so the GPU test (TOL 5e-3) can assert every token.
 
     python tests/golden/gen_deep_prefill.py            # both configs (~10 min, 8 threads)
     python tests/golden/gen_deep_prefill.py llama2_7b
+    TI_PF_PROMPT=640 python tests/golden/gen_deep_prefill.py   # deep_prefill640_*.npz
+
+The 640-token variant is the prefill the benchmark times: with the engine's 512-row chunk limit the
+first 639 prompt tokens run as a 512-row chunk then a 127-row chunk that attends over the first
+chunk's K/V, both through the tile GEMM and the MFMA causal attention.
 """
 from __future__ import annotations
 
@@ -30,7 +35,8 @@ sys.path.insert(0, HERE)
 from pyoracle import Oracle, OracleDeepModel  # noqa: E402
 from gen_deep import CONFIGS  # noqa: E402
 
-N_PROMPT, N_GEN, MARGIN = 120, 3, 0.016
+N_PROMPT, N_GEN, MARGIN = int(os.environ.get("TI_PF_PROMPT", "120")), 3, 0.016
+SUFFIX = "" if N_PROMPT == 120 else str(N_PROMPT)
 PROMPT_SEED = {"llama2_7b": 7001, "llama3_8b": 7003}
 
 
@@ -70,11 +76,11 @@ def make(name: str, oracle: Oracle) -> None:
     rel = out["margin"] / np.abs(lgs).max(axis=1)
     print(f"{name}: last prompt token {prompt[-1]}, tokens {toks}, margin/max {np.round(rel, 4).tolist()}", flush=True)
     m.close()
-    np.savez_compressed(os.path.join(HERE, f"deep_prefill_{name}.npz"), **out)
+    np.savez_compressed(os.path.join(HERE, f"deep_prefill{SUFFIX}_{name}.npz"), **out)
     man = os.path.join(HERE, "manifest.json")
     with open(man) as f:
         manifest = json.load(f)
-    manifest["files"][f"deep_prefill_{name}.npz"] = (
+    manifest["files"][f"deep_prefill{SUFFIX}_{name}.npz"] = (
         f"full-depth oracle prefill + decode (tests/golden/gen_deep_prefill.py, oracle/ti_oracle_deep.c), {what}: "
         f"engine seed {seed}, unit norms, a {N_PROMPT}-token prompt (seeded, last token searched for margins "
         f"> {MARGIN} of max|logit|) from an empty cache, {N_GEN} greedy tokens with their logits")

@@ -20,6 +20,8 @@
 //   5  as 1, and before the wait every wave but the poller also DMAs the first kPF items of its
 //      next phase into LDS (global_load_lds_dwordx4 nt, 1 KiB each), consumed from LDS after the edge
 //   6  as 5 with half as many items in LDS
+//   7  as 1, x loaded and staged by the poller wave alone, right after its poll (before its own ring)
+//   8  as 7 with the LDS prefetch of 5
 // Every spin is bounded (abort flag).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -49,6 +51,10 @@ __device__ __forceinline__ int rsrc_flags() { return 0x00020000; }
 __device__ __forceinline__ unsigned ld_sc1_u32(const unsigned* p, int off) {
   return __builtin_amdgcn_raw_buffer_load_b32(
       __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(p), 0, 0x7fffffff, rsrc_flags()), off * 4, 0, 16);
+}
+__device__ __forceinline__ u32x4 ld_sc1_b128(const unsigned* p, int off16) {
+  return __builtin_amdgcn_raw_buffer_load_b128(
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned*>(p), 0, 0x7fffffff, rsrc_flags()), off16 * 16, 0, 16);
 }
 __device__ __forceinline__ void st_sc1_u32(unsigned* p, int off, unsigned v) {
   __builtin_amdgcn_raw_buffer_store_b32(v, __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7fffffff, rsrc_flags()), off * 4, 0, 16);
@@ -101,7 +107,7 @@ __device__ __forceinline__ void issue_ring(const u32x4* p, int ipw, u32x4 (&ring
 // ---- mode 0: one launch per phase
 __global__ __launch_bounds__(kThreads, 1) void phase_kernel(const u32x4* w, int ipw, int xw, const unsigned* xin,
                                                             unsigned* xout) {
-  __shared__ unsigned xs[kXMax];
+  __shared__ __attribute__((aligned(16))) unsigned xs[kXMax];
   __shared__ float red[8];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned xr[11];
@@ -130,7 +136,7 @@ constexpr int kPF = 12;
 template <int MODE>
 __global__ __launch_bounds__(kThreads, 1) void persist_kernel(Chain c, int layers, unsigned* xbuf, unsigned* ctr,
                                                               unsigned* abort_flag, unsigned long long* ts) {
-  __shared__ unsigned xs[kXMax];
+  __shared__ __attribute__((aligned(16))) unsigned xs[kXMax];
   __shared__ __attribute__((aligned(16))) u32x4 pfl[MODE >= 5 ? 8 * kPF * 64 : 1];   // [wave][item][lane]
   __shared__ float red[8];
   __shared__ unsigned dead;
@@ -138,7 +144,8 @@ __global__ __launch_bounds__(kThreads, 1) void persist_kernel(Chain c, int layer
   const int G = gridDim.x;
   constexpr int kPollWave = 0;
   const bool prefetch = MODE == 1 || MODE == 3 || MODE == 4 || MODE >= 5;
-  const int npf_max = MODE == 5 ? kPF : MODE == 6 ? kPF / 2 : 0;
+  const int npf_max = MODE == 5 || MODE == 8 ? kPF : MODE == 6 ? kPF / 2 : 0;
+  constexpr bool kX0 = MODE >= 7;   // x staged by the poller wave alone, before its own ring
   const bool self_pf = MODE == 4 || wave != kPollWave;
   if (tid == 0) dead = 0;
   if (tid == 0 && blockIdx.x == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
@@ -176,15 +183,27 @@ __global__ __launch_bounds__(kThreads, 1) void persist_kernel(Chain c, int layer
         }
         lds_barrier();
       }
-      if (prefetch && !self_pf) issue_ring(p, ipw, ring);
       const unsigned* xin = xbuf + (n & 1) * kXMax;
-      unsigned xr[11];
+      if (kX0) {
+        if (wave == kPollWave) {
+          u32x4 xq[22];
 #pragma unroll
-      for (int q = 0; q < 11; ++q) xr[q] = ld_sc1_u32(xin, (tid + q * kThreads) % xw);
-      if (!prefetch) issue_ring(p, ipw, ring);
+          for (int q = 0; q < 22; ++q) xq[q] = ld_sc1_b128(xin, (lane + q * 64) % (xw >> 2));
+          if (prefetch) issue_ring(p, ipw, ring);
 #pragma unroll
-      for (int q = 0; q < 11; ++q)
-        if (tid + q * kThreads < xw) xs[tid + q * kThreads] = xr[q];
+          for (int q = 0; q < 22; ++q)
+            if (lane + q * 64 < (xw >> 2)) *(u32x4*)(xs + 4 * (lane + q * 64)) = xq[q];
+        }
+      } else {
+        if (prefetch && !self_pf) issue_ring(p, ipw, ring);
+        unsigned xr[11];
+#pragma unroll
+        for (int q = 0; q < 11; ++q) xr[q] = ld_sc1_u32(xin, (tid + q * kThreads) % xw);
+        if (!prefetch) issue_ring(p, ipw, ring);
+#pragma unroll
+        for (int q = 0; q < 11; ++q)
+          if (tid + q * kThreads < xw) xs[tid + q * kThreads] = xr[q];
+      }
       if (npf_max > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the asm DMA (invisible to hipcc)
       lds_barrier();
       float acc = stream_phase(p, ipw, ring, xs, xw, npf, pfl + wave * kPF * 64 + lane);
@@ -269,7 +288,7 @@ int main(int argc, char** argv) {
     }
     printf("mode 0 (graph of %d launches): %.1f us, %.2f us per layer\n", layers * kPh, best * 1e3, best * 1e3 / layers);
   }
-  for (int mode : {1, 4, 5, 6}) {
+  for (int mode : {1, 7, 8}) {
     float best = 1e30f, span_best = 1e30f;
     for (int r = 0; r < 8; ++r) {
       CK(hipMemsetAsync(ctr, 0, 256 * 4, s));
@@ -281,6 +300,8 @@ int main(int argc, char** argv) {
       if (mode == 3) hipLaunchKernelGGL(persist_kernel<3>, dim3(G), dim3(kThreads), 0, s, c, layers, xbuf, ctr, abort_flag, ts);
       if (mode == 4) hipLaunchKernelGGL(persist_kernel<4>, dim3(G), dim3(kThreads), 0, s, c, layers, xbuf, ctr, abort_flag, ts);
       if (mode == 5) hipLaunchKernelGGL(persist_kernel<5>, dim3(G), dim3(kThreads), 0, s, c, layers, xbuf, ctr, abort_flag, ts);
+      if (mode == 7) hipLaunchKernelGGL(persist_kernel<7>, dim3(G), dim3(kThreads), 0, s, c, layers, xbuf, ctr, abort_flag, ts);
+      if (mode == 8) hipLaunchKernelGGL(persist_kernel<8>, dim3(G), dim3(kThreads), 0, s, c, layers, xbuf, ctr, abort_flag, ts);
       if (mode == 6) hipLaunchKernelGGL(persist_kernel<6>, dim3(G), dim3(kThreads), 0, s, c, layers, xbuf, ctr, abort_flag, ts);
       CK(hipEventRecord(e1, s));
       CK(hipEventSynchronize(e1));
