@@ -250,16 +250,13 @@ def main() -> int:
     # Dominant kernel.  Live timing on the engine stream (ti_engine_time_kernel): the launches of
     # one class as the step runs them (same kernel, x mode and epilogue), cycling through the
     # layers so the weights come from HBM, captured into a graph and replayed back to back for
-    # several ms between two HIP events.
-    #  * one stream with the persistent decode layers on (the 7B default): pds_kernel, one
-    #    launch per step holding every layer's weights + K/V (~97 % of the step's bytes);
-    #  * otherwise the decode GEMM family: layers x (qkv, o, gate/up, down) + lm_head launches,
-    #    achieved = sum(bytes) / sum(time), which is what profiles/*_kernel_stats.txt gives as
-    #    sum(calls x bytes) / total time over the same rows; each class names its kernel.
+    # several ms between two HIP events.  The decode GEMM family: layers x (qkv, o, gate/up,
+    # down) + lm_head launches, achieved = sum(bytes) / sum(time), which is what
+    # profiles/*_kernel_stats.txt gives as sum(calls x bytes) / total time over the same rows;
+    # each class names its kernel.
     names = ["qkv", "o", "gate_up", "down", "lm_head"]
     shapes = {"qkv": (nh * hd + 2 * nkv * hd, H), "o": (H, nh * hd), "gate_up": (2 * I, H), "down": (H, I),
               "lm_head": (V, H)}
-    pds_on = B == 1 and e.set_pds(None)
     fold_on = B == 1 and e.set_fold(None)
     lib = T.lib()
 
@@ -290,29 +287,18 @@ def main() -> int:
         kname = class_kernel(name)
         per[name] = {"avg_us": round(us, 3), "bytes": int(by), "GBps": round(by / us / 1e3, 1), "kernel": kname}
         kernels_used.setdefault(kname, []).append(name)
-        if pds_on and name != "lm_head":
-            per[name]["note"] = "per-layer launch of the graph path (not run by the step: pds_kernel replaces it)"
         gemv_bytes += by * cnt
         gemv_us += us * cnt
         n_launch += cnt
     att_us, att_bytes = e.time_kernel(5, B, L, args.kernel_reps)
     per["attention"] = {"avg_us": round(att_us, 3), "bytes": int(att_bytes), "GBps": round(att_bytes / att_us / 1e3, 1),
                         "kernel": "attn_split_kernel"}
-    if pds_on:
-        pds_us, pds_bytes = e.time_kernel(6, B, L, 2)
-        per["pds"] = {"avg_us": round(pds_us, 3), "bytes": int(pds_bytes), "GBps": round(pds_bytes / pds_us / 1e3, 1),
-                      "kernel": "pds_kernel"}
-        dom = {"kernel": f"pds_kernel (persistent decode layers: {layers} x (QKV, attention, O, gate/up, down) in one "
-                         f"launch per step)", "bytes_per_launch": int(pds_bytes), "avg_launch_us": round(pds_us, 3)}
-        achieved = pds_bytes / pds_us / 1e3
-    else:
-        dom = {"kernel": " + ".join(f"{k} ({', '.join(v)})" for k, v in kernels_used.items()),
-               "bytes_per_launch": int(gemv_bytes / n_launch), "avg_launch_us": round(gemv_us / n_launch, 3)}
-        achieved = gemv_bytes / gemv_us / 1e3   # GB/s
+    dom = {"kernel": " + ".join(f"{k} ({', '.join(v)})" for k, v in kernels_used.items()),
+           "bytes_per_launch": int(gemv_bytes / n_launch), "avg_launch_us": round(gemv_us / n_launch, 3)}
+    achieved = gemv_bytes / gemv_us / 1e3   # GB/s
     e.close()
 
-    traffic, traffic_src = pmc_traffic("pds_kernel" if pds_on else (f"gemv_wq_kernel<{bits}>" if B == 1 else "gemm_family"),
-                                       args.model, B)
+    traffic, traffic_src = pmc_traffic(f"gemv_wq_kernel<{bits}>" if B == 1 else "gemm_family", args.model, B)
     result = None
     if g.rank == 0:
         result = {

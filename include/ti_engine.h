@@ -140,15 +140,12 @@ int ti_engine_set_prefill(ti_engine* e, int rows);
  * on = 0/1 sets both, -1 leaves them; *active (nullable) receives whether 1-stream steps fold. */
 int ti_engine_set_fold(ti_engine* e, int on, int* active);
 
-/* Single-stream steps run every decode layer in ONE persistent launch (ti_pds_decode) when on
- * and the model qualifies (INT4, heads == kv_heads, head_dim 128, 8 splits, hidden = 128 *
- * heads, fold and split partials on); bit-identical to the per-layer launches.  -1 leaves the
- * setting; *active (nullable) receives whether single-stream steps use it.  Env TI_PDS. */
+/* Deprecated (round 5): the persistent decode launch was removed from the product (the per-layer
+ * launches beat it at every shape).  Kept for one release: on = 0 / -1 succeed with
+ * *active = 0, on = 1 returns TI_ERR_UNSUPPORTED; ti_engine_pds_error always reports 0 and
+ * ti_engine_pds_timestamps TI_ERR_UNSUPPORTED. */
 int ti_engine_set_pds(ti_engine* e, int on, int* active);
-/* Bit 0: a persistent launch's hand-off wait timed out (its results are undefined). */
 int ti_engine_pds_error(ti_engine* e, uint32_t* err);
-/* Diagnostic (engine created with env TI_PDS_TS=1): the last persistent launch's phase
- * timestamps, [256][layers][5][8] s_memrealtime ticks (100 MHz), n entries at most. */
 int ti_engine_pds_timestamps(ti_engine* e, unsigned long long* out, size_t n);
 
 /* One decode step: token[s] at position pos[s] for each stream; logits [n][vocab] to host
@@ -168,8 +165,7 @@ int ti_engine_sync(ti_engine* e);
 int ti_engine_last_tokens(ti_engine* e, int n_streams, int32_t* tokens);
 
 /* Live per-kernel timing: the step's launches of class `which` (0 qkv, 1 o, 2 gate/up,
- * 3 down, 4 lm_head, 5 attention, 6 the persistent decode layers -- one launch for all layers,
- * single stream, when persistent decode is on), `reps` of them cycling through the layers,
+ * 3 down, 4 lm_head, 5 attention), `reps` of them cycling through the layers,
  * captured into a graph that is replayed back to back (several ms) between two HIP events on
  * the engine stream.  avg_us = average per launch; bytes = algorithmic HBM bytes per launch. */
 int ti_engine_time_kernel(ti_engine* e, int which, int n_streams, int kv_len, int reps, double* avg_us,

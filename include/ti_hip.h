@@ -337,58 +337,9 @@ int ti_gemm_kernel_name(int bits, int x_kind, int M, int N, int K, char* buf, in
  * the box it ran on. */
 int ti_hbm_calibrate(size_t bytes, int reps, double* read_gbps, double* copy_gbps, ti_stream_t s);
 
-/* ----------------------------------------------------- persistent decode layers
- * All n_layers decode layers of ONE stream in one persistent launch (pds.hip): replaces the
- * per-layer QKV / attention / O / gate-up / down launches of forward_pass_incremental
- * (inference_engine.cpp:1493-1552, TransformerLayer::forward_incremental :203-279) for INT4 / INT8
- * group-128 weights, head_dim 64 / 128, MHA or GQA, grid = heads * 8 workgroups (<= the CU
- * count, one per CU; shapes: ti_pds_supported).  Input: h, fx / ss as ti_step_begin leaves them
- * with the layer-0 fold (n_ss0 partials); output: h and fx / ss folded with out_norm (n_ss =
- * grid partials) for the lm_head's TI_X_F16_FOLDED input.  Same arithmetic, bit for bit, as
- * the per-layer launches with the fold and split-partials hand-offs.  ctr (n_layers * 5 * 256
- * words) and launches (grid words) start zeroed and must not be touched between calls; *err
- * gets bit 0 when a hand-off wait exceeded ~50 ms (results then undefined). */
-typedef struct ti_pds_layer {
-  const void* tiles[4];              /* packed INT4 tiles: qkv, o, gate/up (interleaved), down */
-  const uint16_t* scales[4];
-  const float* attn_norm;
-  const float* ffn_norm;
-  uint16_t* k_cache;                 /* [kv_heads][max_seq][head_dim] fp16, stream 0 */
-  uint16_t* v_cache;
-} ti_pds_layer;
-typedef struct ti_pds_args {
-  const ti_pds_layer* layers;        /* device array [n_layers] */
-  int32_t n_layers, grid, H, I, qd, heads, kv_heads, head_dim, max_seq, n_ss0;
-  float eps;
-  const int32_t* pos;                /* [1] this step's position */
-  const float* rope_cs;              /* [max_seq][head_dim] (cos, sin) */
-  const float* out_norm;
-  float* h;
-  uint16_t* fx;
-  float* ss;                         /* [grid] */
-  float* q;
-  uint16_t* act;
-  uint16_t* part_o;                  /* [heads][8][head_dim] */
-  float* part_ml;                    /* [heads][8][2] */
-  uint32_t* ctr;
-  uint32_t* launches;
-  uint32_t* err;
-  const void* zero;                  /* >= 2 KiB of readable memory, never written */
-  unsigned long long* ts;            /* diagnostic phase timestamps [grid][n_layers][5][8], or NULL */
-  /* data-tagged hand-offs: 8-byte {payload, tag} granules, ti_pds_granule_words(...) of them,
-   * zero before the first launch */
-  unsigned long long* gran;
-  int32_t drop_wg;                   /* diagnostic: workgroup that withholds its first down-projection
-                                      * granules (a producer lost mid-launch); -1 = none */
-  int32_t bits;                      /* 4 or 8 (group-128 tiles) */
-} ti_pds_args;
-size_t ti_pds_granule_words(int H, int I, int qd, int heads, int grid);
-/* 1 if ti_pds_decode takes this shape: bits 4 / 8, head_dim 64 / 128, heads / kv_heads a power of
- * two, grid = 8 * heads <= 256 workgroups (one per CU), hidden / 16 <= grid, layers <= 64, at most 4
- * QKV and 8 gate/up tiles per workgroup. */
-int ti_pds_supported(int bits, int H, int I, int heads, int kv_heads, int head_dim, int grid, int layers);
-#define TI_PDS_CTR_WORDS_PER_LAYER (5 * 8 * 32)
-int ti_pds_decode(const ti_pds_args* a, ti_stream_t s);
+/* (Round 5: the persistent decode launch ti_pds_decode, its ti_pds_args / ti_pds_layer structs,
+ * ti_pds_supported and ti_pds_granule_words were removed -- the per-layer launches beat it at every
+ * shape, DESIGN 4.15.  ti_engine_set_pds stays as a stub for one release) */
 
 /* ------------------------------------------------------- step begin (device loop)
  * One block per stream: picks the token of this step (prompt token while step < n_in[m],

@@ -12,7 +12,7 @@ over every dispatch of the kernel family in the pass (the replayed decode steps 
 bench's per-shape timing launches, same mixture of shapes).
 
 Families: the decode GEMM (every launch of gemv_wq_kernel / gemm_rows_kernel / gemm_tile_kernel:
-one projection each), the attention (attn_split_kernel) and the persistent launch (pds_kernel).
+one projection each) and the attention (attn_split_kernel).
 The GEMM family's key is the one bench.py's roofline names: "gemv_wq_kernel<BITS>" for one stream
 (the fused kernel runs every projection), "gemm_family" for batched steps (rows / tile kernels)."""
 import argparse
@@ -60,7 +60,7 @@ def main():
     for r in rows:
         name = r["Kernel_Name"]
         key = gemm_key if any(g in name for g in GEMM) else (
-            "attn_split_kernel" if "attn_split_kernel" in name else ("pds_kernel" if "pds_kernel" in name else None))
+            "attn_split_kernel" if "attn_split_kernel" in name else None)
         if key:
             fam[key].append(float(r["Counter_Value"]) * 1024.0 * 2.0)
             names[key].add(name.split("(")[0][:80])

@@ -8,5 +8,5 @@ export TMPDIR=/tmp
 mkdir -p $O
 cd $R
 rm -f $O/deep_parity.jsonl
-TI_PARITY_LOG=$O/deep_parity.jsonl timeout -k 10 500 python3 -u -m pytest tests/test_gpu_deep.py tests/test_gpu_threads.py tests/test_gpu_pds.py tests/test_gpu_beam.py -v --timeout 200 --timeout-method thread > $O/deep_tests.log 2>&1 || true
+TI_PARITY_LOG=$O/deep_parity.jsonl timeout -k 10 500 python3 -u -m pytest tests/test_gpu_deep.py tests/test_gpu_threads.py tests/test_gpu_beam.py -v --timeout 200 --timeout-method thread > $O/deep_tests.log 2>&1 || true
 bash tools/side_configs.sh ${1:-r3start}

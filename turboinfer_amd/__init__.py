@@ -83,10 +83,10 @@ EXPORTED = [
     "ti_gemm_grid", "ti_engine_set_fold",
     "ti_attn_decode_partials", "ti_sample_device", "ti_sample_step", "ti_engine_generate_sampled",
     "ti_engine_beam_search", "ti_engine_serve", 
-    "ti_pds_decode", "ti_engine_set_pds", "ti_engine_pds_error", "ti_engine_pds_timestamps",
+    "ti_engine_set_pds", "ti_engine_pds_error", "ti_engine_pds_timestamps",
     "ti_wpack_q_host", "ti_engine_set_tensor_q", "ti_sample_workspace_bytes", "ti_sample_device_ws",
     "ti_wpack_q1_host", "ti_engine_set_tensor_q1", "ti_epilogue_bytes",
-    "ti_sample_step_ws", "ti_pds_granule_words", "ti_hbm_calibrate", "ti_gemm_kernel_name", "ti_pds_supported",
+    "ti_sample_step_ws", "ti_hbm_calibrate", "ti_gemm_kernel_name",
     "ti_gemm_fold_partials", "ti_engine_set_stop", "ti_engine_counters",
 ]
 
@@ -458,8 +458,8 @@ class Engine:
         return bool(act.value)
 
     def set_pds(self, on=None) -> bool:
-        """All decode layers of a single-stream step in one persistent launch on/off (None:
-        query); returns whether 1-stream steps use it (ti_engine_set_pds)."""
+        """Deprecated (round 5: the persistent launch was removed): on=True raises,
+        off / query return False (ti_engine_set_pds)."""
         act = C.c_int(0)
         check(lib().ti_engine_set_pds(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
         return bool(act.value)

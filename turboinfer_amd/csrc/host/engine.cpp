@@ -141,17 +141,6 @@ struct ti_engine {
   size_t weight_bytes = 0, kv_bytes = 0;
   std::map<std::pair<int, int>, hipGraphExec_t> graphs;  // (M, advance | sampled << 1)
   int replay_M = 0;
-  // all decode layers of a single-stream step in one persistent launch (ti_pds_decode,
-  // pds.hip): ti_engine_set_pds / TI_PDS; needs the fold and the split partials
-  bool pds_on = false;
-  ti_pds_layer* pds_layers = nullptr;   // device [layers]
-  uint32_t* pds_ctr = nullptr;          // [layers * TI_PDS_CTR_WORDS_PER_LAYER], monotonic
-  uint32_t* pds_launches = nullptr;     // [256]
-  uint32_t* pds_err = nullptr;
-  void* pds_zero = nullptr;             // 4 KiB of zeros, never written
-  unsigned long long* pds_gran = nullptr;   // granule hand-offs (ti_pds_granule_words)
-  unsigned long long* pds_ts = nullptr; // TI_PDS_TS=1: phase timestamps of the last launch
-  int pds_drop = -1;                    // diagnostic: workgroup that withholds a hand-off (TI_PDS_FORCE_ERR=2)
 
   int qd() const { return c.heads * c.head_dim; }
   int kvd() const { return c.kv_heads * c.head_dim; }
@@ -301,35 +290,6 @@ int gemm_rows(ti_engine* e, const DevLinear& W, int M, const void* x, int x_kind
   return TI_OK;
 }
 
-// After a synchronisation: fail (and re-arm) if a persistent launch's hand-off wait timed out.
-int handoff_check(ti_engine* e) {
-  // The persistent decode launch (pds.hip) bounds every hand-off wait: a wait that times out sets
-  // pds_err and the launch (and any later one) finishes without waiting, so its outputs are
-  // invalid.  Fatal here: the caller gets an error instead of tokens, the engine drops back to
-  // the per-layer graph (pds off, step graphs re-captured) and the hand-off state is reset.
-  if (e->pds_on && e->pds_err) {
-    uint32_t err = 0;
-    TI_TRY(ti_memcpy_d2h(&err, e->pds_err, 4, e->s));
-    if (err) {
-      e->pds_on = false;
-      e->pds_drop = -1;
-      for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
-      e->graphs.clear();
-      TI_TRY(ti_memset(e->pds_err, 0, 4, e->s));
-      TI_TRY(ti_memset(e->pds_ctr, 0, (size_t)e->c.layers * TI_PDS_CTR_WORDS_PER_LAYER * 4, e->s));
-      TI_TRY(ti_memset(e->pds_launches, 0, 256 * 4, e->s));
-      // launch epochs restart: stale granules would carry the new epochs' tags
-      TI_TRY(ti_memset(e->pds_gran, 0,
-                       ti_pds_granule_words(e->c.hidden, e->c.inter, e->qd(), e->c.heads, e->c.kv_heads * 8) * 8, e->s));
-      TI_TRY(ti_stream_sync(e->s));
-      return ti_set_error(TI_ERR_HIP,
-                          "engine: a persistent decode hand-off wait timed out (err 0x%x); results of this call are "
-                          "invalid, persistent decode is now off for this engine",
-                          err);
-    }
-  }
-  return TI_OK;
-}
 
 int get_graph(ti_engine* e, int M, int advance, hipGraphExec_t* out);
 
@@ -372,62 +332,6 @@ bool part_usable(ti_engine* e, int M) {
          e->qd() <= 4096;
 }
 
-// Persistent decode layers (ti_pds_decode): one stream with the fold and the split partials (8
-// splits, so the persistent launch forms every partial as the per-layer launches do), INT4 / INT8,
-// the shapes ti_pds_supported takes (Llama-2-7B, TinyLlama-1.1B), grid = 8 heads <= the CU count.
-std::atomic<int> g_pds_cus{0};   // CU count of the first device asked (engines may run on several threads)
-bool pds_usable(ti_engine* e, int M) {
-  const ti_engine_config& c = e->c;
-  if (!e->pds_on || !e->pds_layers || M != 1 || (c.bits != 4 && c.bits != 8) || c.compat) return false;
-  if (!fold_usable(e, M) || !part_usable(e, M) || e->splits_for(M) != 8) return false;
-  if (!ti_pds_supported(c.bits, c.hidden, c.inter, c.heads, c.kv_heads, c.head_dim, c.heads * 8, c.layers)) return false;
-  int cus = g_pds_cus.load(std::memory_order_relaxed);
-  if (cus == 0) {
-    int dev = 0, n = 0;
-    cus = (hipGetDevice(&dev) == hipSuccess &&
-           hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess) ? n : -1;
-    g_pds_cus.store(cus, std::memory_order_relaxed);   // (a racing first call stores the same value)
-  }
-  return cus >= c.heads * 8;
-}
-
-// The persistent decode-layers launch (ti_pds_decode) of a single-stream step: input h / fx / ss
-// with the layer-0 fold of n_ss0 partials, output h and fx / ss folded with out_norm.
-int pds_launch(ti_engine* e, int n_ss0) {
-  const ti_engine_config& c = e->c;
-  ti_pds_args pa{};
-  pa.layers = e->pds_layers;
-  pa.n_layers = c.layers;
-  pa.grid = c.heads * 8;
-  pa.H = c.hidden;
-  pa.I = c.inter;
-  pa.qd = e->qd();
-  pa.heads = c.heads;
-  pa.kv_heads = c.kv_heads;
-  pa.head_dim = c.head_dim;
-  pa.max_seq = c.max_seq;
-  pa.n_ss0 = n_ss0;
-  pa.eps = c.eps;
-  pa.pos = e->pos;
-  pa.rope_cs = e->rope_cs;
-  pa.out_norm = e->out_norm;
-  pa.h = e->h;
-  pa.fx = e->fx;
-  pa.ss = e->ss;
-  pa.q = e->q;
-  pa.act = e->act;
-  pa.part_o = e->part_o;
-  pa.part_ml = e->part_ml;
-  pa.ctr = e->pds_ctr;
-  pa.launches = e->pds_launches;
-  pa.err = e->pds_err;
-  pa.zero = e->pds_zero;
-  pa.gran = e->pds_gran;
-  pa.ts = e->pds_ts;
-  pa.drop_wg = e->pds_drop;
-  pa.bits = c.bits;
-  return ti_pds_decode(&pa, e->s);
-}
 
 // One decode step for streams [0, M) on e->s.  Graph-capturable (no host sync / alloc).
 int enqueue_step(ti_engine* e, int M, int advance) {
@@ -504,12 +408,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     return TI_OK;
   };
 
-  const bool pds = pds_usable(e, M);
-  if (pds) {   // every layer in one persistent launch; the lm_head stages its fold (grid partials)
-    TI_TRY(pds_launch(e, n_ss));
-    n_ss = c.hidden / 16;   // one sum of h^2 per down tile (ti_pds_decode)
-  }
-  for (int l = 0; l < (pds ? 0 : c.layers); ++l) {
+  for (int l = 0; l < c.layers; ++l) {
     DevLayer& L = e->layer[l];
     ti_epilogue ep{};
     ep.kind = TI_EPI_QKV_ROPE_KV;
@@ -803,31 +702,6 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
     for (auto& L : e->layer) tab.push_back(L.vc);
     if ((rc = e->alloc_t(&e->kv_tab, tab.size())) || (rc = ti_memcpy_h2d(e->kv_tab, tab.data(), tab.size() * sizeof(void*), e->s)))
       return fail(rc);
-    if (c.bits == 4 || c.bits == 8) {   // persistent decode layers (pds_usable decides per step)
-      std::vector<ti_pds_layer> pl((size_t)c.layers);
-      for (int l = 0; l < c.layers; ++l) {
-        DevLayer& L = e->layer[l];
-        const DevLinear* lin[4] = {&L.qkv, &L.o, &L.gu, &L.down};
-        for (int i = 0; i < 4; ++i) {
-          pl[l].tiles[i] = lin[i]->tiles;
-          pl[l].scales[i] = lin[i]->scales;
-        }
-        pl[l].attn_norm = L.attn_norm;
-        pl[l].ffn_norm = L.ffn_norm;
-        pl[l].k_cache = L.kc;
-        pl[l].v_cache = L.vc;
-      }
-      if ((rc = e->alloc(reinterpret_cast<void**>(&e->pds_layers), pl.size() * sizeof(ti_pds_layer))) ||
-          (rc = ti_memcpy_h2d(e->pds_layers, pl.data(), pl.size() * sizeof(ti_pds_layer), e->s)) ||
-          (rc = e->alloc_t(&e->pds_ctr, (size_t)c.layers * TI_PDS_CTR_WORDS_PER_LAYER)) ||
-          (rc = e->alloc_t(&e->pds_launches, (size_t)256)) || (rc = e->alloc_t(&e->pds_err, (size_t)1)) ||
-          (rc = e->alloc(&e->pds_zero, 4096)) ||
-          (rc = e->alloc_t(&e->pds_gran, ti_pds_granule_words(H, I, e->qd(), c.heads, c.kv_heads * 8))))
-        return fail(rc);
-      if (const char* env = getenv("TI_PDS")) e->pds_on = atoi(env) != 0;
-      if (const char* env = getenv("TI_PDS_TS"))
-        if (atoi(env) != 0 && (rc = e->alloc_t(&e->pds_ts, (size_t)256 * c.layers * 5 * 8))) return fail(rc);
-    }
   }
   const int R = std::max(B, e->rows_cap);
   if ((rc = e->alloc_t(&e->h, (size_t)R * H)) || (rc = e->alloc_t(&e->logits, (size_t)B * V)) ||
@@ -1062,7 +936,6 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
   if (e->stop_token < 0) {
     TI_TRY(run_steps(e, n, 1, steps - s0));
     TI_TRY(ti_stream_sync(e->s));
-    TI_TRY(handoff_check(e));
     TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
     TI_TRY(read_argmax(e, n, am));
   } else {
@@ -1075,7 +948,6 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
       ran += S;
       TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
       TI_TRY(read_argmax(e, n, am));   // (synchronises the stream)
-      TI_TRY(handoff_check(e));
       bool all = true;
       for (int m = 0; m < n && all; ++m) {
         bool hit = false;
@@ -1437,7 +1309,6 @@ int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32
     TI_TRY(run_steps(e, B, 1, S));
     TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
     TI_TRY(read_argmax(e, B, am));   // synchronises the stream
-    TI_TRY(handoff_check(e));          // before any token of the chunk is handed out
     for (int m = 0; m < B; ++m) {
       const int r = slot_req[m];
       if (r < 0) continue;
@@ -1497,7 +1368,6 @@ int ti_engine_step(ti_engine* e, int n, const int32_t* tokens, const int32_t* po
   TI_TRY(ti_memset(e->step_ctr, 0, 4, e->s));
   TI_TRY(run_steps(e, n, 1, 1));
   TI_TRY(ti_stream_sync(e->s));
-  TI_TRY(handoff_check(e));
   if (logits) TI_TRY(ti_memcpy_d2h(logits, e->logits, (size_t)n * c.vocab * 4, e->s));
   return TI_OK;
 }
@@ -1564,7 +1434,7 @@ int ti_engine_sync(ti_engine* e) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_sync: null");
   DeviceScope bind_(e);
   TI_TRY(ti_stream_sync(e->s));
-  return handoff_check(e);
+  return TI_OK;
 }
 
 
@@ -1582,49 +1452,24 @@ int ti_engine_set_fold(ti_engine* e, int on, int* active) {
 }
 
 
+// The persistent decode launch (round 4, pds.hip) was removed from the product in round 5: it
+// lost to the per-layer graph at every shape.  The entry points stay for one release:
+// off is accepted, on reports TI_ERR_UNSUPPORTED.
 int ti_engine_set_pds(ti_engine* e, int on, int* active) {
   if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_pds: null");
-  DeviceScope bind_(e);
-  if (on >= 0 && (on != 0) != e->pds_on) {
-    TI_TRY(ti_stream_sync(e->s));   // captured step graphs bake the setting in
-    for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
-    e->graphs.clear();
-    e->pds_on = on != 0;
-  }
-  // diagnostic (tests/test_gpu_pds.py): TI_PDS_FORCE_ERR=1 pre-sets the hand-off error word, so
-  // the next persistent launch runs without waits and the engine must report it as fatal;
-  // TI_PDS_FORCE_ERR=2 makes workgroup 0 withhold its first down-projection granules in every
-  // launch (a producer lost mid-launch: every other workgroup's wait must end in one timeout)
-  if (on > 0 && e->pds_err)
-    if (const char* env = getenv("TI_PDS_FORCE_ERR")) {
-      if (atoi(env) == 1) TI_TRY(ti_memset(e->pds_err, 0xff, 4, e->s));
-      if (atoi(env) == 2) {
-        e->pds_drop = 0;
-        for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
-        e->graphs.clear();
-      }
-    }
-  if (active) *active = pds_usable(e, 1) ? 1 : 0;
+  if (active) *active = 0;
+  if (on > 0) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_set_pds: persistent decode was removed (DESIGN 4.15)");
   return TI_OK;
 }
 
-int ti_engine_pds_timestamps(ti_engine* e, unsigned long long* out, size_t n) {
+int ti_engine_pds_timestamps(ti_engine* e, unsigned long long* out, size_t) {
   if (!e || !out) return ti_set_error(TI_ERR_ARG, "ti_engine_pds_timestamps: null");
-  DeviceScope bind_(e);
-  if (!e->pds_ts) return ti_set_error(TI_ERR_ARG, "ti_engine_pds_timestamps: engine built without TI_PDS_TS=1");
-  const size_t have = (size_t)256 * e->c.layers * 5 * 8;
-  TI_TRY(ti_stream_sync(e->s));
-  E_CHECK(hipMemcpy(out, e->pds_ts, std::min(n, have) * 8, hipMemcpyDeviceToHost), "hipMemcpy(pds_ts)");
-  return TI_OK;
+  return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_pds_timestamps: persistent decode was removed (DESIGN 4.15)");
 }
 
 int ti_engine_pds_error(ti_engine* e, uint32_t* err) {
   if (!e || !err) return ti_set_error(TI_ERR_ARG, "ti_engine_pds_error: null");
-  DeviceScope bind_(e);
   *err = 0;
-  if (!e->pds_err) return TI_OK;
-  TI_TRY(ti_stream_sync(e->s));
-  E_CHECK(hipMemcpy(err, e->pds_err, 4, hipMemcpyDeviceToHost), "hipMemcpy(pds_err)");
   return TI_OK;
 }
 
@@ -1662,9 +1507,6 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
       case 4: W = &e->lm; x = e->h; xk = TI_X_F32_RMSNORM; ldx = H; nw = e->out_norm;
         ep.kind = TI_EPI_LOGITS_ARGMAX; ep.ldo = c.vocab; ep.out = e->logits; ep.argmax = e->argmax; break;
       case 5: break;
-      case 6:   // the persistent decode layers (one launch per step)
-        if (!pds_usable(e, n)) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_time_kernel: persistent decode off");
-        break;
       default: return ti_set_error(TI_ERR_ARG, "ti_engine_time_kernel: which=%d", which);
     }
     if (which == 1 || which == 3) {
@@ -1725,7 +1567,6 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
     cur = (cur + 1) % c.layers;
     TI_TRY(setup(L, W, x, xk, ldx, nw, ep));
     // (the one lm_head, 68 MB at 7B, fits the Infinity Cache: back-to-back it runs warm)
-    if (which == 6) return pds_launch(e, 1);
     if (which == 5 && part)
       return ti_attn_decode_partials(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, n, c.heads, c.kv_heads,
                                      c.head_dim, e->splits_for(n), e->part_o, e->part_ml, e->s);
