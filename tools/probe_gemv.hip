@@ -9,6 +9,7 @@
 //   +8 no x / scale dependency (constants), +16 non-temporal weight loads.
 // Weights are random bytes (timing does not depend on values); x is fp16 or f32+rmsnorm.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -129,6 +130,13 @@ int main(int argc, char** argv) {
           post += (double)(ts[b * 8 + 4] - ts[b * 8 + 5]) * 0.01 / grid;
         }
         printf("   waves: end skew %.2f us, wave0 after first %.2f us | barrier->end %.2f us\n", skew, w0late, post);
+        {   // workgroup end times after the first start: how unbalanced the grid finishes
+          static double ends[4096];
+          for (int b = 0; b < grid; ++b) ends[b] = (ts[b * 8 + 4] - t0) * 0.01;
+          std::sort(ends, ends + grid);
+          printf("   workgroup end (us after first start): min %.2f p10 %.2f p50 %.2f p90 %.2f max %.2f\n", ends[0],
+                 ends[grid / 10], ends[grid / 2], ends[grid * 9 / 10], ends[grid - 1]);
+        }
         printf("   span %.2f us | start skew avg %.2f max %.2f | issue %.2f/%.2f/%.2f | stage %.2f/%.2f/%.2f | "
                "stream %.2f/%.2f/%.2f | epi %.2f/%.2f/%.2f (min/avg/max)\n",
                (tend - t0) * 0.01, start[1], start[2], ph[0][0], ph[0][1], ph[0][2], ph[1][0], ph[1][1], ph[1][2],
