@@ -299,6 +299,7 @@ def main() -> int:
     e.close()
 
     traffic, traffic_src = pmc_traffic(f"gemv_wq_kernel<{bits}>" if B == 1 else "gemm_family", args.model, B)
+    att_traffic, _ = pmc_traffic("attn_split_kernel", args.model, B)
     result = None
     if g.rank == 0:
         result = {
@@ -323,7 +324,7 @@ def main() -> int:
                               "traffic_source": traffic_src}, **dom),
             "attention_roofline": {"bound": "hbm", "kernel": "attn_split_kernel", "achieved": per["attention"]["GBps"],
                                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": round(per["attention"]["GBps"] / HBM_PEAK_GBS, 4),
+                                   "frac": round(per["attention"]["GBps"] / HBM_PEAK_GBS, 4), "traffic": att_traffic,
                                    "share_of_step_bytes": round(layers * att_bytes / sb, 4)},
             "calibration": {"hbm_read_GBps": round(hbm_read, 1), "hbm_copy_GBps": round(hbm_copy, 1),
                             "note": "same run, this GPU: 1 GiB streamed once by 2 workgroups per CU (read) and "

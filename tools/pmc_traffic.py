@@ -74,9 +74,30 @@ def main():
     # class whose algorithmic bytes are nearest, the per-class means are weighted by the step's own
     # mixture (layers x QKV, O, gate/up, down + 1 lm_head), comparable to the bench line's
     # bytes_per_launch.
+    # Classes by position in each decode step: after a step_begin dispatch the step issues, per layer,
+    # the QKV, O, gate/up and down GEMMs in that order and then the lm_head (layers x 4 + 1 GEMM
+    # dispatches); the bench's per-class timing launches outside the steps are not labelled.  Fall
+    # back to the nearest algorithmic bytes when no complete step is found.
     per = defaultdict(list)
-    for b in fam.get(gemm_key, []):
-        per[min(algo, key=lambda c: abs(algo[c] - b))].append(b)
+    layers = n["qkv"]
+    order = ["qkv", "o", "gate_up", "down"]
+    pos = None
+    for r in sorted(rows, key=lambda r: int(r["Dispatch_Id"])):
+        name = r["Kernel_Name"]
+        if "step_begin_kernel" in name:
+            pos = 0
+            continue
+        if pos is None or not any(g in name for g in GEMM):
+            continue
+        cls = order[pos % 4] if pos < 4 * layers else "lm_head"
+        per[cls].append(float(r["Counter_Value"]) * 1024.0 * 2.0)
+        pos = pos + 1 if pos < 4 * layers else None
+    out["class_labels"] = "step position"
+    if len(per) != len(algo):
+        out["class_labels"] = "nearest algorithmic bytes"
+        per = defaultdict(list)
+        for b in fam.get(gemm_key, []):
+            per[min(algo, key=lambda c: abs(algo[c] - b))].append(b)
     if len(per) == len(algo):
         cls = {c: {"dispatches": len(per[c]), "traffic_bytes": round(sum(per[c]) / len(per[c])), "algorithmic_bytes": algo[c],
                    "ratio": round(sum(per[c]) / len(per[c]) / algo[c], 4)} for c in algo}
