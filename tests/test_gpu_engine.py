@@ -287,3 +287,32 @@ def test_engine_batch_beyond_one_gemm_chunk(ti, oracle):
     for b in (0, 7, 16, 19):
         ref, ref_logits = _oracle_tokens(oracle, MID, seed, jit, prompts[b], 3)
         assert_greedy(got[b].tolist(), ref, ref_logits, f"stream {b}")
+
+
+def test_generate_stop_token_per_stream(ti):
+    """ti_engine_set_stop (generate()'s EOS break, inference_engine.cpp:760-764) on two streams of one
+    engine: stream 0 (prompt 1 17 42, seed 78) emits token 2 as its third token, stream 1 (prompt 7)
+    not within 30.  With the stop set, stream 0's tokens end at its stop token (-1 after) and stream 1's
+    are the tokens of the run without a stop; the loop runs every step (stream 1 never stops).  Stream
+    0 alone stops after the first chunk of 4 steps (ti_engine_counters), not after 30."""
+    cfg = dict(vocab=128, hidden=256, layers=2, heads=4, kv_heads=2, head_dim=64, inter=512, bits=4,
+               max_seq=256, rope_theta=10000.0, eps=1e-5)
+    e = engine_for(ti, cfg, max_batch=2)
+    e.synth(78, 0.1)
+    a, b, n = [1, 17, 42], [7], 30
+    full = e.generate([a, b], n)
+    full1 = e.generate([a], n)                           # (one stream: the M = 1 path)
+    assert full[0][:3].tolist()[-1] == 2 and 2 not in full[0][:2].tolist(), full[0][:3]
+    assert 2 not in full[1].tolist()
+    d0, _ = e.counters()
+    e.set_stop(2)
+    got = e.generate([a, b], n)
+    d1, _ = e.counters()
+    assert got[0].tolist() == full[0][:3].tolist() + [-1] * (n - 3)
+    assert got[1].tolist() == full[1].tolist()
+    assert d1 - d0 == len(a) + n - 1 - (len(b) - 1)   # every step of the loop (prefill took len(b) - 1 = 0)
+    one = e.generate([a], n)
+    d2, _ = e.counters()
+    e.close()
+    assert one[0].tolist() == full1[0][:3].tolist() + [-1] * (n - 3)
+    assert d2 - d1 == 4                                  # the first chunk covers the stop (3 tokens)
