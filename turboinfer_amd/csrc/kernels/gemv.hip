@@ -1581,6 +1581,12 @@ __device__ __forceinline__ bool splitk_merge(const GemvArgs& a, f32x4 (&acc)[TPW
 #ifndef TI_TILE_EPI_LDS
 #define TI_TILE_EPI_LDS 1   // 0: every epilogue per element from the MFMA layout (A/B knob)
 #endif
+#ifndef TI_TILE_HALVES
+// 1: the asm loops compute each group as two halves (compute_half: k-steps 0-1, then 2-3, half the A
+// fragments live at a time); 3-5 % less time than the whole group at once (compute) on TPW 2-4 at
+// 256-1024 rows (profiles/r5_tile_halves_ab.txt).  0: compute (A/B knob)
+#define TI_TILE_HALVES 1
+#endif
 constexpr int kTileEpiStride = 20;   // floats per row of a wave's 64 x 16 staging block (padded: no bank conflicts)
 __host__ __device__ constexpr int tile_epi_lds_bytes() { return kGemvWaves * 64 * kTileEpiStride * 4; }
 
@@ -1778,6 +1784,35 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
       for (int b = 0; b < RB; ++b) acc[t][b] = fma_scale4(sc, tmp[b], acc[t][b]);
     }
   };
+  // The same group in two halves (k-steps 0-1 / 2-3; the MFMA partials tmpS carried between them):
+  // the same products and sums in the same order as compute.
+  f32x4 tmpS[TPW][RB];
+  auto compute_half = [&](const u32x4 (&w)[TPW], int kg, auto hc) __attribute__((always_inline)) {
+    constexpr int H = decltype(hc)::value;
+    const f16* xr = xb + (kg & (XB - 1)) * BM * 128 + (wm * 16 * RB + r) * 128;
+    f16x8 xf[RB][2];
+#pragma unroll
+    for (int b = 0; b < RB; ++b)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) xf[b][j] = *(const f16x8*)(xr + b * 16 * 128 + (((kq * 4 + 2 * H + j) ^ r) * 8));
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if constexpr (H == 0)
+#pragma unroll
+        for (int b = 0; b < RB; ++b) tmpS[t][b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f16x8 bf = deq_int4_signed(w[t][2 * H + j], magic);
+#pragma unroll
+        for (int b = 0; b < RB; ++b) tmpS[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xf[b][j], bf, tmpS[t][b], 0, 0, 0);
+      }
+      if constexpr (H == 1) {
+        const float sc = h2f(sl[((wn * TPW + t) * KT + kg) * 16 + r]);
+#pragma unroll
+        for (int b = 0; b < RB; ++b) acc[t][b] = fma_scale4(sc, tmpS[t][b], acc[t][b]);
+      }
+    }
+  };
   // Per group kg: x(kg) and W(kg) were issued earlier; issue x(kg + 1) and W(kg + WR - 1),
   // wait until only those weight loads are younger than x(kg + 1)... (see below), compute kg.
   const int KTP = (nk + kTileWR - 1) / kTileWR * kTileWR;
@@ -1824,7 +1859,14 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #pragma unroll
           for (int t = 0; t < TPW; ++t) asm volatile("" : "+v"(W[su][t]));
           TILE_CY(3);
-          if (kg >= 0 && kg < nk) compute(W[su], kb + kg);
+          if (kg >= 0 && kg < nk) {
+            if constexpr (TI_TILE_HALVES && !G32) {
+              compute_half(W[su], kb + kg, std::integral_constant<int, 0>());
+              compute_half(W[su], kb + kg, std::integral_constant<int, 1>());
+            } else {
+              compute(W[su], kb + kg);
+            }
+          }
           TILE_CY(4);
         }
       }
@@ -1857,7 +1899,14 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvAr
 #if TI_GEMV_EXP & 2048   // diagnostic (tools/tile_diag.sh): operand streams only, no dequant / MFMA
         if (kg >= 0 && kg < nk && lane == 64) compute(W[u], kb + kg);
 #else
-        if (kg >= 0 && kg < nk) compute(W[u], kb + kg);
+        if (kg >= 0 && kg < nk) {
+          if constexpr (TI_TILE_HALVES && !G32) {
+            compute_half(W[u], kb + kg, std::integral_constant<int, 0>());
+            compute_half(W[u], kb + kg, std::integral_constant<int, 1>());
+          } else {
+            compute(W[u], kb + kg);
+          }
+        }
 #endif
         TILE_CY(4);
       }
