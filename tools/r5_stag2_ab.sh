@@ -1,4 +1,7 @@
 #!/bin/bash
+# RECORD ONLY: TI_TILE_STAG was removed after these A/Bs (profiles/r5_tile_stagger_ab.txt, r5_tile_halves_ab.txt);
+# the halves they isolated are the default now (TI_TILE_HALVES).  The script stops here.
+echo "TI_TILE_STAG was removed (profiles/r5_tile_stagger_ab.txt)"; exit 2
 # Decomposes the stagger A/B (profiles/r5_tile_stagger_ab.txt): TI_TILE_STAG=2 runs the staggered
 # loop's issue order (activations 2 groups ahead, halves back to back) with no wave late; TI_TILE_HALVES=1
 # the halves in the product loops (activations 3 groups ahead).

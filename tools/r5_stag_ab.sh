@@ -1,4 +1,7 @@
 #!/bin/bash
+# RECORD ONLY: TI_TILE_STAG was removed after these A/Bs (profiles/r5_tile_stagger_ab.txt, r5_tile_halves_ab.txt);
+# the halves they isolated are the default now (TI_TILE_HALVES).  The script stops here.
+echo "TI_TILE_STAG was removed (profiles/r5_tile_stagger_ab.txt)"; exit 2
 # Staggered tile GEMM (TI_TILE_STAG=1 build in tools/bin/stag/): parity (tile / prefill tests with
 # the variant library), then tools/rows_bench.py at 256 / 512 / 1024 rows and the 512-token
 # prefill, interleaved per arm.
