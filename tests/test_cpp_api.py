@@ -347,13 +347,15 @@ def test_generate_stops_the_device_loop_at_eos(api_check, oracle, tmp_path, seed
     assert got == prompt + want
     out = outp.splitlines()
     assert out[0] == "eos_token"
+    # the prompt's prefill chunk (its last row gives token 1), then the chunk schedule until the
+    # EOS step (token k) is covered
     steps = 0
-    for chunk in (4, 8, 16, 32):      # the chunk schedule until the EOS step is covered
+    for chunk in (4, 8, 16, 32):
         steps += chunk
-        if steps >= k:
+        if steps >= k - 1:
             break
     passes = [ln for ln in out if "Forward Passes:" in ln]
-    assert passes and int(passes[0].split(":")[1]) == steps + 1, (passes, steps)   # + the prompt's prefill chunk
+    assert passes and int(passes[0].split(":")[1]) == steps + 1, (passes, steps)
 
 
 @pytest.mark.gpu

@@ -316,3 +316,30 @@ def test_generate_stop_token_per_stream(ti):
     e.close()
     assert one[0].tolist() == full1[0][:3].tolist() + [-1] * (n - 3)
     assert d2 - d1 == 4                                  # the first chunk covers the stop (3 tokens)
+
+
+def test_generate_last_prompt_row_gives_first_token(ti):
+    """One greedy stream: the last prompt token is a prefill row and the first token comes from the
+    final rms_norm + lm_head on its hidden row (as the reference's forward_pass computes the last
+    position's logits), not from a decode step.  Against the same prompt as two streams (which
+    takes the decode step for it): the same tokens, logits within the deep bar (5e-3 x max|logit|),
+    and one decode step fewer per stream (ti_engine_counters)."""
+    cfg = dict(vocab=512, hidden=512, layers=4, heads=8, kv_heads=2, head_dim=64, inter=1024, bits=4,
+               max_seq=512, rope_theta=10000.0, eps=1e-5)
+    e = engine_for(ti, cfg, max_batch=2)
+    e.synth(31, 0.1)
+    e.set_prefill(64)                                     # 100-token prompt: chunks of 64 + 36 rows
+    prompt = [int(t) for t in np.random.RandomState(5).randint(0, cfg["vocab"], size=100)]
+    for max_new in (1, 6):
+        d0, p0 = e.counters()
+        one, lg1 = e.generate([prompt], max_new, want_logits=True)
+        d1, p1 = e.counters()
+        two, lg2 = e.generate([prompt, prompt], max_new, want_logits=True)
+        d2, p2 = e.counters()
+        assert (d1 - d0, p1 - p0) == (max_new - 1, 2)
+        assert (d2 - d1, p2 - p1) == (max_new, 4)
+        assert one[0].tolist() == two[0].tolist() == two[1].tolist()
+        if max_new == 1:   # both logits rows are the last prompt position's
+            bar = 5e-3 * float(np.max(np.abs(lg2[0])))
+            assert float(np.max(np.abs(lg1[0] - lg2[0]))) <= bar
+    e.close()

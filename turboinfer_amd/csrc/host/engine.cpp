@@ -491,6 +491,15 @@ size_t ws_bytes(const ti_engine* e) {
   return b;
 }
 
+// TI_PREFILL_LOGITS=0: the last prompt token through a decode step instead (A/B knob, ti_engine_generate)
+static bool prefill_logits_on() {
+  static const int on = [] {
+    const char* v = getenv("TI_PREFILL_LOGITS");
+    return v ? atoi(v) != 0 : 1;
+  }();
+  return on != 0;
+}
+
 static bool prefill_attn_on() {
   static const int on = [] {
     const char* v = getenv("TI_ATTN_PREFILL");
@@ -913,13 +922,33 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
   TI_TRY(ti_memcpy_h2d(e->in_tokens, in.data(), in.size() * 4, e->s));
   TI_TRY(ti_memcpy_h2d(e->n_in, nin.data(), (size_t)n * 4, e->s));
   TI_TRY(ti_memcpy_h2d(e->base_pos, base.data(), (size_t)n * 4, e->s));
-  // all but the last prompt token of the shortest prompt go through prefill; the decode loop
-  // then starts at that step (same positions, same token feed, same outputs)
+  // All but the last prompt token of the shortest prompt go through prefill; the decode loop
+  // then starts at that step (same positions, same token feed, same outputs).  One greedy stream:
+  // the last prompt token is a prefill row too, and the final rms_norm + lm_head + argmax run on
+  // its hidden row (the reference's forward_pass computes the last position's logits the same
+  // way, inference_engine.cpp:1429-1491), so the first generated token costs one GEMV, not a
+  // decode step over every layer; the decode loop starts at the step that feeds it.
   int s0 = 0;
   if (e->pf_rows > 0) {
-    s0 = *std::min_element(nin.begin(), nin.end()) - 1;
+    const int lmin = *std::min_element(nin.begin(), nin.end());
+    const bool last_in_prefill = n == 1 && !e->samp_on && lmin >= 2 && prefill_logits_on();
+    s0 = last_in_prefill ? lmin : lmin - 1;
+    int last_rows = 0;
     for (int m = 0; m < n; ++m)
-      for (int t0 = 0; t0 < s0; t0 += e->pf_rows) TI_TRY(enqueue_prefill(e, m, t0, std::min(e->pf_rows, s0 - t0), base[m]));
+      for (int t0 = 0; t0 < s0; t0 += e->pf_rows) {
+        last_rows = std::min(e->pf_rows, s0 - t0);
+        TI_TRY(enqueue_prefill(e, m, t0, last_rows, base[m]));
+      }
+    if (last_in_prefill) {
+      // argmax slots of row 0: zeroed by the chunk's step_begin
+      ti_epilogue el{};
+      el.kind = TI_EPI_LOGITS_ARGMAX;
+      el.ldo = c.vocab;
+      el.out = e->logits;
+      el.argmax = e->argmax;
+      TI_TRY(gemm_rows(e, e->lm, 1, e->h + (size_t)(last_rows - 1) * c.hidden, TI_X_F32_RMSNORM, c.hidden, e->out_norm,
+                       el, 4, false));
+    }
   }
   TI_TRY(ti_memcpy_h2d(e->step_ctr, &s0, 4, e->s));
   std::vector<int32_t> outd((size_t)n * e->out_cap);
