@@ -147,10 +147,11 @@ def test_deep_bench_replay(ti, golden, name):
 @pytest.mark.parametrize("name", ["llama2_7b", "llama3_8b"])
 def test_deep_prefill_then_decode(ti, golden, name):
     """prefill at full width and depth.  A 120-token prompt from an empty cache
-    (tests/golden/gen_deep_prefill.py): the engine runs its first 119 tokens as ONE prefill chunk --
-    the tile GEMM at 119 rows and the MFMA causal attention, at every one of the 32 layers, the KV they
-    write then read by the decode steps -- and decodes 3 greedy tokens from the last prompt token
-    (reference forward_pass + forward_pass_incremental, inference_engine.cpp:1429-1552).  Every
+    (tests/golden/gen_deep_prefill.py): the engine runs the 120 tokens as ONE prefill chunk -- the
+    tile GEMM at 120 rows and the MFMA causal attention, at every one of the 32 layers; the first
+    token's logits from the last row's lm_head, the KV they write then read by the decode steps --
+    and decodes 2 more greedy tokens (reference forward_pass + forward_pass_incremental,
+    inference_engine.cpp:1429-1552).  Every
     generated step's logits within TOL_DEEP * max|logit| of the full-depth oracle (which feeds the
     prompt token by token), and every token equal."""
     d = golden(f"deep_prefill_{name}")
@@ -173,9 +174,9 @@ def test_deep_prefill_then_decode(ti, golden, name):
 def test_deep_prefill_512_row_chunks(ti, golden, name):
     """prefill at the chunk size it is timed at.  A 640-token prompt
     (tests/golden/gen_deep_prefill.py, TI_PF_PROMPT=640) with the engine's chunk limit at 512 rows:
-    the first 639 tokens run as a 512-row chunk (the 7B / Llama-3 tile plans at 512 rows) and then a
-    127-row chunk whose causal attention reads the first chunk's K/V, at all 32 layers; then 3 greedy
-    decode steps.  Logits within TOL_DEEP * max|logit| of the oracle at every generated step, every
+    the prompt runs as a 512-row chunk (the 7B / Llama-3 tile plans at 512 rows) and then a 128-row
+    chunk whose causal attention reads the first chunk's K/V, at all 32 layers, and whose last row
+    gives the first token; then 2 greedy decode steps.  Logits within TOL_DEEP * max|logit| of the oracle at every generated step, every
     token equal, and the engine's counters show the two prompt chunks per call."""
     d = golden(f"deep_prefill640_{name}")
     cfg = json.loads(str(d["cfg"]))
@@ -188,7 +189,7 @@ def test_deep_prefill_512_row_chunks(ti, golden, name):
     for n in range(1, len(ref) + 1):
         _, c0 = e.counters()
         got, lg = e.generate([prompt], n, want_logits=True)
-        assert e.counters()[1] - c0 == 2          # 512 + 127 prompt rows
+        assert e.counters()[1] - c0 == 2          # 512 + 128 prompt rows
         r = ref_lg[n - 1].astype(np.float64)
         worst = max(worst, float(np.max(np.abs(lg[0].astype(np.float64) - r))) / float(np.max(np.abs(r))))
     e.close()

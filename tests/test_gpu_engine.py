@@ -319,27 +319,38 @@ def test_generate_stop_token_per_stream(ti):
 
 
 def test_generate_last_prompt_row_gives_first_token(ti):
-    """One greedy stream: the last prompt token is a prefill row and the first token comes from the
-    final rms_norm + lm_head on its hidden row (as the reference's forward_pass computes the last
-    position's logits), not from a decode step.  Against the same prompt as two streams (which
-    takes the decode step for it): the same tokens, logits within the deep bar (5e-3 x max|logit|),
-    and one decode step fewer per stream (ti_engine_counters)."""
+    """Greedy streams whose prompts have one length: the last prompt token is a prefill row and the
+    first token comes from the final rms_norm + lm_head on its hidden row (as the reference's
+    forward_pass computes the last position's logits), not from a decode step.  Against the same
+    prompt beside a shorter one (unequal lengths take the decode step for it): the same tokens,
+    logits within the deep bar (5e-3 x max|logit|), and the step counts of ti_engine_counters."""
     cfg = dict(vocab=512, hidden=512, layers=4, heads=8, kv_heads=2, head_dim=64, inter=1024, bits=4,
                max_seq=512, rope_theta=10000.0, eps=1e-5)
     e = engine_for(ti, cfg, max_batch=2)
     e.synth(31, 0.1)
-    e.set_prefill(64)                                     # 100-token prompt: chunks of 64 + 36 rows
-    prompt = [int(t) for t in np.random.RandomState(5).randint(0, cfg["vocab"], size=100)]
-    for max_new in (1, 6):
-        d0, p0 = e.counters()
-        one, lg1 = e.generate([prompt], max_new, want_logits=True)
-        d1, p1 = e.counters()
-        two, lg2 = e.generate([prompt, prompt], max_new, want_logits=True)
-        d2, p2 = e.counters()
-        assert (d1 - d0, p1 - p0) == (max_new - 1, 2)
-        assert (d2 - d1, p2 - p1) == (max_new, 4)
-        assert one[0].tolist() == two[0].tolist() == two[1].tolist()
-        if max_new == 1:   # both logits rows are the last prompt position's
-            bar = 5e-3 * float(np.max(np.abs(lg2[0])))
-            assert float(np.max(np.abs(lg1[0] - lg2[0]))) <= bar
+    e.set_prefill(64)                                     # 100-token prompts: chunks of 64 + 36 rows
+    rng = np.random.RandomState(5)
+    p1, p2 = ([int(t) for t in rng.randint(0, cfg["vocab"], size=100)] for _ in range(2))
+
+    def run(prompts, k):
+        d0, c0 = e.counters()
+        out, lg = e.generate(prompts, k, want_logits=True)
+        d1, c1 = e.counters()
+        return out, lg, d1 - d0, c1 - c0
+
+    for k in (1, 6):
+        one, lg1, d, c = run([p1], k)
+        assert (d, c) == (k - 1, 2)
+        two, lg2, d, c = run([p1, p2], k)
+        assert (d, c) == (k - 1, 4)
+        # unequal lengths: stream 0 (the longer) through the decode step, which runs from the
+        # shorter prompt's last token; its last step is stream 0's last prompt position
+        ref1, rl1, d, c = run([p1, p2[:-1]], k)
+        assert (d, c) == (k + 1, 4)
+        ref2, rl2, _, _ = run([p2, p1[:-1]], k)
+        assert one[0].tolist() == two[0].tolist() == ref1[0].tolist()
+        assert two[1].tolist() == ref2[0].tolist()
+        if k == 1:   # the last prompt position's logits, both ways
+            for got, ref in ((lg1[0], rl1[0]), (lg2[0], rl1[0]), (lg2[1], rl2[0])):
+                assert float(np.max(np.abs(got - ref))) <= 5e-3 * float(np.max(np.abs(ref)))
     e.close()

@@ -83,6 +83,7 @@ struct ti_engine {
   float* rope_cs = nullptr;
   // step buffers
   float* h = nullptr;
+  float* h_last = nullptr;   // [max_batch][hidden]: each stream's last prompt row (ti_engine_generate)
   float* q = nullptr;
   float* tmp = nullptr;        // compat FFN activations (fp32)
   float* logits = nullptr;
@@ -713,7 +714,8 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
       return fail(rc);
   }
   const int R = std::max(B, e->rows_cap);
-  if ((rc = e->alloc_t(&e->h, (size_t)R * H)) || (rc = e->alloc_t(&e->logits, (size_t)B * V)) ||
+  if ((rc = e->alloc_t(&e->h, (size_t)R * H)) || (rc = e->alloc_t(&e->h_last, (size_t)B * H)) ||
+      (rc = e->alloc_t(&e->logits, (size_t)B * V)) ||
       (rc = e->alloc_t(&e->argmax, (size_t)R * TI_ARGMAX_SLOTS)) || (rc = e->alloc_t(&e->pos, (size_t)R)) ||
       (rc = e->alloc_t(&e->base_pos, (size_t)B)) || (rc = e->alloc_t(&e->step_ctr, (size_t)1)) ||
       (rc = e->alloc_t(&e->n_in, (size_t)B)) || (rc = ensure_io(e, 8, 8)))
@@ -923,31 +925,38 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
   TI_TRY(ti_memcpy_h2d(e->n_in, nin.data(), (size_t)n * 4, e->s));
   TI_TRY(ti_memcpy_h2d(e->base_pos, base.data(), (size_t)n * 4, e->s));
   // All but the last prompt token of the shortest prompt go through prefill; the decode loop
-  // then starts at that step (same positions, same token feed, same outputs).  One greedy stream:
-  // the last prompt token is a prefill row too, and the final rms_norm + lm_head + argmax run on
-  // its hidden row (the reference's forward_pass computes the last position's logits the same
-  // way, inference_engine.cpp:1429-1491), so the first generated token costs one GEMV, not a
-  // decode step over every layer; the decode loop starts at the step that feeds it.
+  // then starts at that step (same positions, same token feed, same outputs).  Greedy streams
+  // whose prompts have one length: the last prompt token is a prefill row too, and the final
+  // rms_norm + lm_head + argmax run on each stream's last hidden row (the reference's forward_pass
+  // computes the last position's logits the same way, inference_engine.cpp:1429-1491), so the
+  // first generated token costs one lm_head GEMM, not a decode step over every layer; the decode
+  // loop starts at the step that feeds it.
   int s0 = 0;
   if (e->pf_rows > 0) {
     const int lmin = *std::min_element(nin.begin(), nin.end());
-    const bool last_in_prefill = n == 1 && !e->samp_on && lmin >= 2 && prefill_logits_on();
+    const bool one_len = *std::max_element(nin.begin(), nin.end()) == lmin;
+    const bool last_in_prefill = one_len && !e->samp_on && lmin >= 2 && prefill_logits_on();
     s0 = last_in_prefill ? lmin : lmin - 1;
     int last_rows = 0;
-    for (int m = 0; m < n; ++m)
+    for (int m = 0; m < n; ++m) {
       for (int t0 = 0; t0 < s0; t0 += e->pf_rows) {
         last_rows = std::min(e->pf_rows, s0 - t0);
         TI_TRY(enqueue_prefill(e, m, t0, last_rows, base[m]));
       }
+      if (last_in_prefill && n > 1)   // (the next stream's chunks reuse h)
+        TI_TRY(ti_memcpy_d2d(e->h_last + (size_t)m * c.hidden, e->h + (size_t)(last_rows - 1) * c.hidden,
+                             (size_t)c.hidden * 4, e->s));
+    }
     if (last_in_prefill) {
-      // argmax slots of row 0: zeroed by the chunk's step_begin
+      // one stream: its row in place, argmax slots cleared by the chunk's step_begin
+      if (n > 1) TI_TRY(ti_memset(e->argmax, 0, (size_t)n * TI_ARGMAX_SLOTS * 8, e->s));
       ti_epilogue el{};
       el.kind = TI_EPI_LOGITS_ARGMAX;
       el.ldo = c.vocab;
       el.out = e->logits;
       el.argmax = e->argmax;
-      TI_TRY(gemm_rows(e, e->lm, 1, e->h + (size_t)(last_rows - 1) * c.hidden, TI_X_F32_RMSNORM, c.hidden, e->out_norm,
-                       el, 4, false));
+      const float* x = n > 1 ? e->h_last : e->h + (size_t)(last_rows - 1) * c.hidden;
+      TI_TRY(gemm_rows(e, e->lm, n, x, TI_X_F32_RMSNORM, c.hidden, e->out_norm, el, 4, false));
     }
   }
   TI_TRY(ti_memcpy_h2d(e->step_ctr, &s0, 4, e->s));
