@@ -128,7 +128,10 @@ int ti_engine_serve(ti_engine* e, int n_req, const int32_t* prompts, const int32
 /* Prefill of ti_engine_generate's prompts (reference forward_pass, inference_engine.cpp:
  * 1429-1491): all but the last token of the shortest prompt are processed `rows` tokens at a
  * time as rows of the batched GEMMs and causal attention over the stream's own KV cache,
- * instead of one token per decode step.  Default: TI_GEMM_MAX_ROWS (int4) or 16; 0 = off. */
+ * instead of one token per decode step.  Greedy streams whose prompts have one length (at least
+ * 2 tokens) run the last token as a prefill row too, and their first token comes from the final
+ * rms_norm + lm_head on that row (env TI_PREFILL_LOGITS=0: a decode step instead).
+ * Default: TI_GEMM_MAX_ROWS (int4) or 16; 0 = off. */
 int ti_engine_set_prefill(ti_engine* e, int rows);
 
 /* Fused hand-offs of single-stream steps: (1) the folded rms_norm (ti_hip.h TI_X_F16_FOLDED):

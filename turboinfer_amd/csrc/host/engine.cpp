@@ -476,8 +476,9 @@ int enqueue_step(ti_engine* e, int M, int advance) {
 // Prefill (reference forward_pass, inference_engine.cpp:1429-1491, with the KV kept): prompt
 // tokens [t0, t0 + rows) of stream m at positions base + t0 + j, as `rows` rows of the
 // batched path that share stream m's KV cache (epilogue / attention stream stride 0: row j
-// appends at its own position and attends to [0, base + t0 + j], causal).  No lm_head: the
-// decode loop takes over at the last prompt token.  Not graph-captured (host position upload).
+// appends at its own position and attends to [0, base + t0 + j], causal).  No lm_head here: the
+// decode loop takes over at the last prompt token, or ti_engine_generate runs the lm_head on the
+// chunk's last row.  Not graph-captured (host position upload).
 // TI_ATTN_PREFILL=0: prefill chunks through the decode attention kernel (A/B knob)
 static bool prefill_attn_on();
 
