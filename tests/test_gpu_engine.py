@@ -354,3 +354,26 @@ def test_generate_last_prompt_row_gives_first_token(ti):
             for got, ref in ((lg1[0], rl1[0]), (lg2[0], rl1[0]), (lg2[1], rl2[0])):
                 assert float(np.max(np.abs(got - ref))) <= 5e-3 * float(np.max(np.abs(ref)))
     e.close()
+
+
+def test_generate_stop_at_the_prefill_token(ti):
+    """The stop token as the first generated token, which the prefill's last row gives: the device
+    loop runs no step at all (the reference breaks before its next forward pass), for max_new 1 and
+    6, and the stop set with max_new 1 returns that token (ti_engine_counters)."""
+    cfg = dict(vocab=512, hidden=512, layers=4, heads=8, kv_heads=2, head_dim=64, inter=1024, bits=4,
+               max_seq=512, rope_theta=10000.0, eps=1e-5)
+    e = engine_for(ti, cfg)
+    e.synth(47, 0.1)
+    e.set_prefill(64)
+    p = [int(t) for t in np.random.RandomState(9).randint(0, cfg["vocab"], size=80)]
+    ref = e.generate([p], 6)[0].tolist()
+    e.set_stop(ref[1] if ref[1] != ref[0] else -1)         # a stop that is not the first token
+    if ref[1] != ref[0]:
+        assert e.generate([p], 6)[0].tolist() == ref[:2] + [-1] * 4
+    e.set_stop(ref[0])
+    for k in (1, 6):
+        d0, _ = e.counters()
+        got = e.generate([p], k)[0].tolist()
+        d1, _ = e.counters()
+        assert got == [ref[0]] + [-1] * (k - 1) and d1 == d0, (got, d1 - d0)
+    e.close()

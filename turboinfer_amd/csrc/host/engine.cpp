@@ -981,20 +981,26 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
     // chunks of 4, 8, 16, 32, then 64 steps; after each, every stream's new tokens are read back
     // (one small copy) and the loop ends once each has emitted the stop token
     ran = s0;
-    for (int chunk = 4; ran < steps; chunk = std::min(chunk * 2, 64)) {
-      const int S = std::min(chunk, steps - ran);
-      TI_TRY(run_steps(e, n, 1, S));
-      ran += S;
+    bool all = false;
+    auto read_back = [&]() -> int {   // every stream's tokens so far; all = each stopped or complete
       TI_TRY(ti_memcpy_d2h(outd.data(), e->out_tokens, outd.size() * 4, e->s));
       TI_TRY(read_argmax(e, n, am));   // (synchronises the stream)
-      bool all = true;
+      all = true;
       for (int m = 0; m < n && all; ++m) {
         bool hit = false;
         const int produced = ran - nin[m] + 1;
         for (int t = 0; t < std::min(produced, max_new) && !hit; ++t) hit = token_at(m, t, ran) == e->stop_token;
         all = hit || produced >= max_new;
       }
-      if (all) break;
+      return TI_OK;
+    };
+    // the prefill's last rows gave every stream its first token: it may already be the stop
+    if (ran >= nin_max) TI_TRY(read_back());
+    for (int chunk = 4; ran < steps && !all; chunk = std::min(chunk * 2, 64)) {
+      const int S = std::min(chunk, steps - ran);
+      TI_TRY(run_steps(e, n, 1, S));
+      ran += S;
+      TI_TRY(read_back());
     }
   }
   for (int m = 0; m < n; ++m) {
