@@ -170,30 +170,32 @@ def test_deep_prefill_then_decode(ti, golden, name):
     assert_greedy(got[0].tolist(), ref, ref_lg, f"{name} prefill")
 
 
+@pytest.mark.parametrize("rows", [512, 1024])
 @pytest.mark.parametrize("name", ["llama2_7b", "llama3_8b"])
-def test_deep_prefill_512_row_chunks(ti, golden, name):
+def test_deep_prefill_512_row_chunks(ti, golden, name, rows):
     """prefill at the chunk size it is timed at.  A 640-token prompt
     (tests/golden/gen_deep_prefill.py, TI_PF_PROMPT=640) with the engine's chunk limit at 512 rows:
     the prompt runs as a 512-row chunk (the 7B / Llama-3 tile plans at 512 rows) and then a 128-row
     chunk whose causal attention reads the first chunk's K/V, at all 32 layers, and whose last row
     gives the first token; then 2 greedy decode steps.  Logits within TOL_DEEP * max|logit| of the oracle at every generated step, every
-    token equal, and the engine's counters show the two prompt chunks per call."""
+    token equal, and the engine's counters show the two prompt chunks per call.  With the int4
+    default limit (1024 rows) the whole prompt is one 640-row chunk."""
     d = golden(f"deep_prefill640_{name}")
     cfg = json.loads(str(d["cfg"]))
     prompt, ref, ref_lg = d["prompt"].tolist(), d["tokens"].tolist(), d["logits"]
     assert len(prompt) == 640
     e = engine_for(ti, cfg, max_batch=1)
     e.synth(int(d["seed"][0]), 0.0)
-    e.set_prefill(512)
+    e.set_prefill(rows)
     worst = 0.0
     for n in range(1, len(ref) + 1):
         _, c0 = e.counters()
         got, lg = e.generate([prompt], n, want_logits=True)
-        assert e.counters()[1] - c0 == 2          # 512 + 128 prompt rows
+        assert e.counters()[1] - c0 == (2 if rows == 512 else 1)   # 512 + 128 prompt rows, or 640
         r = ref_lg[n - 1].astype(np.float64)
         worst = max(worst, float(np.max(np.abs(lg[0].astype(np.float64) - r))) / float(np.max(np.abs(r))))
     e.close()
-    _log(dict(config=name, case="prefill640(512+127)+decode3", layers=cfg["layers"], max_rel_err=worst, tol=TOL))
+    _log(dict(config=name, case=f"prefill640(chunks of {rows})+decode3", layers=cfg["layers"], max_rel_err=worst, tol=TOL))
     assert worst <= TOL, f"{name}: logit error {worst:.4g} * max|logit| > {TOL}"
     assert_greedy(got[0].tolist(), ref, ref_lg, f"{name} prefill 512-row chunks")
 
