@@ -1,4 +1,6 @@
 #!/bin/bash
+# RECORD ONLY: TI_TILE_PRIO is no longer read by the library (profiles/r4_tile_prio_ab.txt); the script stops here.
+echo "TI_TILE_PRIO is gone (profiles/r4_tile_prio_ab.txt)"; exit 2
 # Tile GEMM: waves 4-7 at s_setprio 1 (abx/prio, -DTI_TILE_PRIO=1) vs the product build, one box,
 # interleaved: per-kernel times (rocprofv3 over tools/tile_one.py, 7B shapes at 512 rows) and
 # 512-token prefill; then the prefill tests under the variant.

@@ -1,4 +1,6 @@
 #!/bin/bash
+# RECORD ONLY: TI_GEMV_WG_PER_CU is no longer read by the library (DESIGN 4.1 (a second workgroup per CU measured slower)); the script stops here.
+echo "TI_GEMV_WG_PER_CU is gone (DESIGN 4.1 (a second workgroup per CU measured slower))"; exit 2
 # Fused-GEMV ring depth (TI_GEMV_RING_VGPRS 20 = product, exp/r24, exp/r32 builds) and two
 # workgroups per CU (TI_GEMV_WG_PER_CU=2) on the one-stream 7B and TinyLlama benches.
 # Variant builds: make BUILD=/tmp/build_rNN LIB=exp/rNN/libturboinfer_amd.so EXTRA=-DTI_GEMV_RING_VGPRS=NN
