@@ -113,6 +113,14 @@ __device__ __forceinline__ float groups_sum(float v) {
   else return v;
 }
 
+// Slot order in the K/V ring: the slot's registers pass through an empty asm issued after the
+// previous slot's softmax (tied to its running sum), so the scores of later slots cannot be
+// hoisted to the top of the pass -- where they would wait for the loads issued last and drain the
+// ring once per pass -- and each slot waits only for its own loads.
+__device__ __forceinline__ void ring_pin(u32x4& k, u32x4& v, float& prev) {
+  asm volatile("" : "+v"(k), "+v"(v), "+v"(prev));
+}
+
 template <int HD, int G, int R, bool HP, int NW = kAttnWaves, bool ROT = false>   // HP: head-parallel lanes (G >= 4, HD / (64 / G) == 8; see below)
 __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, int kvh, int m) {
   static_assert(!HP || (G >= 4 && HD / (64 / G) == 8), "head-parallel layout: 8 dims per lane");
@@ -162,15 +170,15 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
       kr[s] = ld_k((int64_t)key * HD + dh * 8);
       vr[s] = ld_v((int64_t)key * HD + dh * 8);
     };
+    // q first, then the ring, all issued before any wait: the loop head then sees the ring's loads
+    // youngest and in slot order, as its own back edge does, and waits for one slot at a time
+    const size_t qe = (size_t)m * a.heads * HD + (size_t)(kvh * G + hg) * HD + dh * 8;
+    const float4 q0 = ld_q4(qe), q1 = ld_q4(qe + 4);
 #pragma unroll
     for (int s = 0; s < R; ++s) refill(s);
     float qh[8];
-    {
-      const size_t qe = (size_t)m * a.heads * HD + (size_t)(kvh * G + hg) * HD + dh * 8;
-      const float4 q0 = ld_q4(qe), q1 = ld_q4(qe + 4);
-      qh[0] = q0.x * a.scale; qh[1] = q0.y * a.scale; qh[2] = q0.z * a.scale; qh[3] = q0.w * a.scale;
-      qh[4] = q1.x * a.scale; qh[5] = q1.y * a.scale; qh[6] = q1.z * a.scale; qh[7] = q1.w * a.scale;
-    }
+    qh[0] = q0.x * a.scale; qh[1] = q0.y * a.scale; qh[2] = q0.z * a.scale; qh[3] = q0.w * a.scale;
+    qh[4] = q1.x * a.scale; qh[5] = q1.y * a.scale; qh[6] = q1.z * a.scale; qh[7] = q1.w * a.scale;
     float m1 = -INFINITY, l1 = 0.0f, acc1[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc1[e] = 0.0f;
@@ -198,6 +206,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
     for (; j0 + R <= total; j0 += R) {
 #pragma unroll
       for (int s = 0; s < R; ++s) {
+        ring_pin(kr[s], vr[s], l1);
         consume(kr[s], vr[s]);
         refill(s);
       }
@@ -214,7 +223,8 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
     }
     __syncthreads();
   } else {
-    // the K/V ring first (nothing else to wait for), then q
+    // q first, then the K/V ring, all issued before any wait: the loop head then sees the ring's
+    // loads youngest and in slot order, as its own back edge does, and waits for one slot at a time
     int rj = 0;
     // ROT: each workgroup starts its sweep at its own slot (wrapping), so the workgroups of a
     // launch do not walk their equally aligned K/V ranges in lockstep
@@ -231,14 +241,20 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
       kr[s] = ld_k((int64_t)key * HD + dl * 8);
       vr[s] = ld_v((int64_t)key * HD + dl * 8);
     };
+    float4 qr[G][2];
+  #pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const size_t qe = (size_t)m * a.heads * HD + (size_t)(kvh * G + g) * HD + dl * 8;
+      qr[g][0] = ld_q4(qe);
+      qr[g][1] = ld_q4(qe + 4);
+    }
   #pragma unroll
     for (int s = 0; s < R; ++s) refill(s);
 
     float q[G][8];
   #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const size_t qe = (size_t)m * a.heads * HD + (size_t)(kvh * G + g) * HD + dl * 8;
-      const float4 q0 = ld_q4(qe), q1 = ld_q4(qe + 4);
+      const float4 q0 = qr[g][0], q1 = qr[g][1];
       q[g][0] = q0.x * a.scale; q[g][1] = q0.y * a.scale; q[g][2] = q0.z * a.scale; q[g][3] = q0.w * a.scale;
       q[g][4] = q1.x * a.scale; q[g][5] = q1.y * a.scale; q[g][6] = q1.z * a.scale; q[g][7] = q1.w * a.scale;
     }
@@ -278,6 +294,7 @@ __device__ __forceinline__ void attn_split_body(const AttnArgs& a, int split, in
     for (; j0 + R <= total; j0 += R) {
   #pragma unroll
       for (int s = 0; s < R; ++s) {
+        ring_pin(kr[s], vr[s], lrun[G - 1]);
         consume(kr[s], vr[s]);
         refill(s);
       }

@@ -112,9 +112,11 @@ __device__ __forceinline__ float group_sum(float v) {
 // (persistent decode hand-offs, split merges: MI355X_MICROARCH.md "Hand-offs measured with sc1 loads")
 constexpr int kAuxSc1Load = 16;   // buffer aux bit 4 = sc1 on gfx950
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sc1_rsrc(const void* base) {
+// a raw buffer resource over [base, base + 2 GiB): the cache policy is the access's aux bits
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sc1_rsrc(const void* base) { return buffer_rsrc(base); }
 __device__ __forceinline__ uint32_t ld_sc1_u32(const void* p) {
   return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

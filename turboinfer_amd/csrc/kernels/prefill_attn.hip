@@ -76,9 +76,12 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
   const int qb = gridDim.x - 1 - blockIdx.x, kvh = blockIdx.y;
   const int q0 = qb * qpw, qi = min(q0 + (r >> gsh), M - 1), h = kvh * G + (r & (G - 1));
   const int p = pos[qi];
-  int kmax = p;
+  int kmax = p, kmin = p;
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) kmax = max(kmax, __shfl_xor(kmax, o, 64));
+  for (int o = 1; o < 16; o <<= 1) {
+    kmax = max(kmax, __shfl_xor(kmax, o, 64));
+    kmin = min(kmin, __shfl_xor(kmin, o, 64));
+  }
   // B operand of step c: dims 32c + 8g + e of this lane's column, split into fp16 hi + lo
   f16x8 qh[KW], ql[KW];
   {
@@ -96,17 +99,25 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
       }
     }
   }
-  const uint16_t* kb0 = kc + (size_t)kvh * max_seq * HD + 8 * g;
-  const uint16_t* vb0 = vc + (size_t)kvh * max_seq * HD + r * DV;
+  // K / V through buffer loads (the kv-head's cache is the resource, byte offsets per lane): a
+  // plain load whose value feeds the ring's loop phi is sunk below the phi by the compiler (one
+  // load at the use, nothing in flight); the buffer intrinsic keeps each refill where it is issued
+  const auto krs = buffer_rsrc(kc + (size_t)kvh * max_seq * HD), vrs = buffer_rsrc(vc + (size_t)kvh * max_seq * HD);
+  // keys past every column's prefix (kmax) may be unwritten (NaN): they read row kmax instead,
+  // finite, which their p = 0 then multiplies away exactly (no branch per load); a block past the
+  // last (a refill that is never consumed) reads row kmax too, a cache hit
+  const int kl = min(kmax, max_seq - 1);
   auto load = [&](int kb, KRaw& k, VRaw (&v)[4]) {
-    const int kk = min(kb * 16 + r, max_seq - 1);
+    const int kk = min(kb * 16 + r, kl);
 #pragma unroll
-    for (int c = 0; c < KW; ++c) k[c] = *(const u32x4*)(kb0 + (uint32_t)(kk * HD + 32 * c));
-    // keys past every column's prefix (kmax) may be unwritten (NaN): they read row kmax instead,
-    // finite, which their p = 0 then multiplies away exactly (no branch per load)
-    const int kl = min(kmax, max_seq - 1);
+    for (int c = 0; c < KW; ++c)
+      k[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, (kk * HD + 8 * g + 32 * c) * 2, 0, 0));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = *(const VRaw*)(vb0 + (uint32_t)(min(kb * 16 + 4 * g + j, kl) * HD));
+    for (int j = 0; j < 4; ++j) {
+      const int off = (min(kb * 16 + 4 * g + j, kl) * HD + r * DV) * 2;
+      if constexpr (HD == 128) v[j] = __builtin_bit_cast(VRaw, __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0));
+      else v[j] = __builtin_bit_cast(VRaw, __builtin_amdgcn_raw_buffer_load_b64(vrs, off, 0, 0));
+    }
   };
   f32x4 acc[DV];
 #pragma unroll
@@ -120,15 +131,31 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
   VRaw vr[kPfRing][4];
 #pragma unroll
   for (int u = 0; u < kPfRing; ++u) load(u, kr[u], vr[u]);   // past nkb: clamped rows, zero V
+  // let the first blocks land before the loop: with loads of the prologue still in flight at the
+  // loop head the compiler merges their (different) issue order with the loop's own and waits for
+  // every load at the top of each pass; with none, the loop's count alone sets the waits
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
   // NB blocks (16 NB keys) per online-softmax step: one column max across the four lanes, one
   // alpha and one rescale of O per step (2 when the ring divides into pairs); the wave's time is
   // this chain, not the K / V stream
-  constexpr int NB = kPfRing % 2 == 0 ? 2 : 1;
+#ifndef TI_PF_NB
+#define TI_PF_NB 2   // blocks per softmax step (at most; a divisor of the ring)
+#endif
+  constexpr int NB = kPfRing % TI_PF_NB == 0 ? TI_PF_NB : kPfRing % 2 == 0 ? 2 : 1;
   for (int kb0 = 0; kb0 < nkb; kb0 += kPfRing) {
 #pragma unroll
     for (int u = 0; u < kPfRing; u += NB) {
+      // no exit inside the pass: blocks past nkb hold only keys past every column's position, so
+      // they score -inf, leave m and l alone (alpha 1) and add p = 0 times finite V -- exactly
+      // nothing; a straight-line pass keeps the loads in flight across the back edge countable
       const int kb = kb0 + u;
-      if (kb >= nkb) break;
+      // order the steps: this step's K enters through an empty asm issued after the previous step's
+      // softmax, so its S = K Q^T cannot be hoisted into earlier steps, where it would wait for the
+      // blocks loaded last and drain the ring once per pass
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int c = 0; c < KW; ++c) asm volatile("" : "+v"(kr[u + b][c]));
       f32x4 s[NB];
 #pragma unroll
       for (int b = 0; b < NB; ++b) s[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
@@ -140,34 +167,52 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
           s[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[c], s[b], 0, 0, 0);
           s[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[c], s[b], 0, 0, 0);
         }
-      // keys past the column's position (and a second block past nkb: its keys are past kmax)
+      // keys past the column's position (and a second block past nkb: its keys are past kmax) score
+      // -inf; only the steps that reach past the shortest column's position (kmin) test them
       float pv[NB][4], bm = -INFINITY;
 #pragma unroll
       for (int b = 0; b < NB; ++b)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bool ok = (kb + b) * 16 + 4 * g + i <= p;
-          pv[b][i] = ok ? s[b][i] : -INFINITY;
-          bm = fmaxf(bm, pv[b][i]);
-        }
+        for (int i = 0; i < 4; ++i) pv[b][i] = s[b][i];
+      if ((kb + NB) * 16 - 1 > kmin) {   // wave-uniform
+        const int lim = p - kb * 16 - 4 * g;
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (16 * b + i > lim) pv[b][i] = -INFINITY;
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bm = fmaxf(bm, pv[b][i]);
       bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
       bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+      // The running max moves only when a column's block max exceeds it by more than kPfSlack
+      // (e^8: p stays below 2981, exact enough in the fp16 hi + lo split, and l, O in fp32): the
+      // O rescale -- 32 accumulators read, scaled and written back per lane -- then runs in the
+      // first steps and rarely after.  softmax(s) = exp(s - m) / sum exp(s - m) for any m.
+      constexpr float kPfSlack = 8.0f;
       const float mn = fmaxf(m_run, bm);   // finite: key 0 is in every row's prefix
-      const float alpha = m_run == mn ? 1.0f : __expf(m_run - mn);
+      if (__builtin_amdgcn_ballot_w64(mn > m_run + kPfSlack) != 0) {   // wave-uniform; the first step
+        const float alpha = m_run == mn ? 1.0f : __expf(m_run - mn);
+        l_run *= alpha;
+        m_run = mn;
+#pragma unroll
+        for (int t = 0; t < DV; ++t)   // O^T: every row of the lane's accumulators is its own column's
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[t][i] *= alpha;
+      }
       float ps = 0.0f;
 #pragma unroll
       for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          pv[b][i] = pv[b][i] == -INFINITY ? 0.0f : __expf(pv[b][i] - mn);
+          pv[b][i] = __expf(pv[b][i] - m_run);   // a masked key: exp2(-inf) = 0 exactly
           ps += pv[b][i];
         }
-      l_run = l_run * alpha + ps;
-      m_run = mn;
-#pragma unroll
-      for (int t = 0; t < DV; ++t)   // O^T: every row of the lane's accumulators is its own column's
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[t][i] *= alpha;
+      l_run += ps;
+      asm volatile("" : "+v"(l_run));
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
         f16x4 ph, pl;
@@ -196,7 +241,9 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(bf, ph, acc[t], 0, 0, 0);
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(bf, pl, acc[t], 0, 0, 0);
         }
-        if (kb + b + kPfRing < nkb) load(kb + b + kPfRing, kr[u + b], vr[u + b]);
+        // unconditional refill: a branch here leaves the loop's back edge with a variable count of
+        // loads in flight, and the compiler then waits for all of them at the top of every pass
+        load(kb + b + kPfRing, kr[u + b], vr[u + b]);
       }
     }
   }
