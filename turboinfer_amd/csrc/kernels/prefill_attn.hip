@@ -54,15 +54,19 @@ __device__ __forceinline__ void pf_split(float x, _Float16& hi, _Float16& lo) {
   lo = (_Float16)(x - (float)hi);
 }
 
+#ifndef TI_PF_DIAG
+#define TI_PF_DIAG 0   // diagnostics only (tools/r5_pfdiag.sh): 1 cache-resident K / V, 2 no math
+#endif
 #ifndef TI_PF_RING
-#define TI_PF_RING 3   // K / V blocks in flight per wave (3: 246 registers at hd 128, two waves per SIMD)
+#define TI_PF_RING 3   // K / V blocks in flight per wave (3: two waves per SIMD, held to 256 registers)
 #endif
 #ifndef TI_PF_RING_DEEP
 #define TI_PF_RING_DEEP 4   // the ring when every wave of the launch has a SIMD to itself (4 and 6 measured equal)
 #endif
 
-template <int HD, int RING = TI_PF_RING>
-__global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restrict__ q, const uint16_t* __restrict__ kc,
+// WPE: waves per SIMD the shallow-ring build must fit (2: at most 256 registers with the AGPRs)
+template <int HD, int RING = TI_PF_RING, int WPE = 1>
+__global__ __launch_bounds__(64, WPE) void attn_prefill_kernel(const float* __restrict__ q, const uint16_t* __restrict__ kc,
                                                           const uint16_t* __restrict__ vc, int max_seq,
                                                           const int32_t* __restrict__ pos, int M, int heads, int gsh,
                                                           float scale, uint16_t* __restrict__ out) {
@@ -108,6 +112,9 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
   // last (a refill that is never consumed) reads row kmax too, a cache hit
   const int kl = min(kmax, max_seq - 1);
   auto load = [&](int kb, KRaw& k, VRaw (&v)[4]) {
+#if TI_PF_DIAG & 1   // diagnostic: every block re-reads block 0 (cache-resident K / V)
+    kb = 0;
+#endif
     const int kk = min(kb * 16 + r, kl);
 #pragma unroll
     for (int c = 0; c < KW; ++c)
@@ -156,6 +163,17 @@ __global__ __launch_bounds__(64) void attn_prefill_kernel(const float* __restric
       for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int c = 0; c < KW; ++c) asm volatile("" : "+v"(kr[u + b][c]));
+#if TI_PF_DIAG & 2   // diagnostic: the K / V stream alone (each slot waited for and refilled, no math)
+      if constexpr (HD == 128) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(vr[u + b][j]));
+          load(kb + b + kPfRing, kr[u + b], vr[u + b]);
+        }
+        continue;
+      }
+#endif
       f32x4 s[NB];
 #pragma unroll
       for (int b = 0; b < NB; ++b) s[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
@@ -306,14 +324,14 @@ extern "C" int ti_attn_prefill(const float* q, const uint16_t* k_cache, const ui
       hipLaunchKernelGGL((ti::attn_prefill_kernel<128, TI_PF_RING_DEEP>), grid, dim3(64), 0, s, q, k_cache, v_cache,
                          max_seq, pos, M, heads, gsh, scale, out);
     else
-      hipLaunchKernelGGL((ti::attn_prefill_kernel<128, TI_PF_RING>), grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq,
+      hipLaunchKernelGGL((ti::attn_prefill_kernel<128, TI_PF_RING, 2>), grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq,
                          pos, M, heads, gsh, scale, out);
   } else {
     if (deep)
       hipLaunchKernelGGL((ti::attn_prefill_kernel<64, TI_PF_RING_DEEP>), grid, dim3(64), 0, s, q, k_cache, v_cache,
                          max_seq, pos, M, heads, gsh, scale, out);
     else
-      hipLaunchKernelGGL((ti::attn_prefill_kernel<64, TI_PF_RING>), grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq,
+      hipLaunchKernelGGL((ti::attn_prefill_kernel<64, TI_PF_RING, 2>), grid, dim3(64), 0, s, q, k_cache, v_cache, max_seq,
                          pos, M, heads, gsh, scale, out);
   }
   TI_LAUNCH_CHECK("attn_prefill_kernel");
