@@ -112,6 +112,17 @@ __device__ __forceinline__ float group_sum(float v) {
 // (persistent decode hand-offs, split merges: MI355X_MICROARCH.md "Hand-offs measured with sc1 loads")
 constexpr int kAuxSc1Load = 16;   // buffer aux bit 4 = sc1 on gfx950
 
+// 64 lanes x 16 B -> LDS at the wave-uniform byte address lds (M0 set and restored in the
+// statement).  Issued from asm, so hipcc does not count it: the caller waits with a counted
+// s_waitcnt vmcnt and a barrier before the LDS is read.
+__device__ __forceinline__ void dma_1k_asm(const void* src_lane, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src_lane), "s"(lds)
+               : "memory");
+}
+
 // a raw buffer resource over [base, base + 2 GiB): the cache policy is the access's aux bits
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);

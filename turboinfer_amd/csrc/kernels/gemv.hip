@@ -1468,14 +1468,6 @@ __host__ __device__ inline int tile_lds_bytes(int K, int tpw, bool g32 = false, 
 #ifndef TI_TILE_WNT
 #define TI_TILE_WNT 0   // weight tiles are re-read by the row blocks of a column block (L2): default policy
 #endif
-// 64 lanes x 16 B -> LDS at the wave-uniform byte address lds (M0 set and restored in the statement)
-__device__ __forceinline__ void dma_1k_asm(const void* src_lane, uint32_t lds) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src_lane), "s"(lds)
-               : "memory");
-}
 // A 16-byte VGPR load hipcc does not count (beside the asm DMA it could not count its own loads
 // exactly either): the caller waits with a counted s_waitcnt and ties the destination ("+v")
 // before any use (cdna_hip_programming.md 5.7, item 1, form ii).

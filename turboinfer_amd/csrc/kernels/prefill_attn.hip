@@ -24,6 +24,7 @@
 // it in place, and the lane writes hd/4 contiguous outputs of its column at the end.
 // Queries are dealt longest-prefix first; a 4-block K / V ring per wave hides the loads.
 #include <math.h>
+#include <stdlib.h>
 
 #include <atomic>
 
@@ -288,6 +289,200 @@ __global__ __launch_bounds__(64, WPE) void attn_prefill_kernel(const float* __re
   }
 }
 
+// ---------------------------------------------------------------- shared K / V blocks (hd 128)
+// The kernel above gives every wave its own K / V stream from L2, and that stream bounds it
+// (profiles/r5_prefill_attn_diag.txt: 21.5 of 24 us at 512 rows; half-line K reads, ~80 block loads
+// per CU).  Here a workgroup of 4 waves (one per SIMD) takes 4 query blocks of one kv-head -- wave w
+// block j + w QG, so every workgroup holds one long and one short chain -- and copies each K / V
+// block of their union once into an LDS ring (LDS-DMA, full 128-byte lines), which all 4 waves read.
+// The per-wave math is the kernel above's: S^T = K Q^T and O^T += V^T P^T on fp16 MFMA with the fp32
+// operand in hi + lo, online softmax per column, two blocks per step.
+//   K block in LDS: [16 keys][16 chunks of 16 B], the logical chunk c of key row r at physical c ^ r
+//   (an A-fragment read, lane (r, g) chunk 4c + g, is conflict-free in every ds_read_b128 lane group);
+//   V block: [16 keys][16 chunks], unswizzled (lane (r, g) reads chunk r of rows 4g + j).
+// Per iteration (blocks kb, kb + 1): wait for this wave's DMAs of kb, kb + 1; barrier (everyone's
+// landed, and everyone is done with kb - 2, kb - 1); DMA kb + R - 2, kb + R - 1 into their slots;
+// compute.  Waves past their own chain keep copying until the workgroup's longest is done.
+#ifndef TI_PF_WG_RING
+#define TI_PF_WG_RING 6   // K / V blocks in the LDS ring (8 KiB each)
+#endif
+__global__ __launch_bounds__(256, 1) void attn_prefill_wg_kernel(const float* __restrict__ q, const uint16_t* __restrict__ kc,
+                                                                 const uint16_t* __restrict__ vc, int max_seq,
+                                                                 const int32_t* __restrict__ pos, int M, int heads, int gsh,
+                                                                 float scale, uint16_t* __restrict__ out) {
+  constexpr int HD = 128, DV = HD / 16, KW = HD / 32, R = TI_PF_WG_RING, NB = 2;
+  static_assert(R % NB == 0 && R >= 2 * NB, "ring: whole steps, one in flight beside the one computed");
+  __shared__ __attribute__((aligned(16))) uint16_t sk[R][16 * HD];
+  __shared__ __attribute__((aligned(16))) uint16_t sv[R][16 * HD];
+  __shared__ int s_kmax[4];
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int G = 1 << gsh, qpw = 16 >> gsh;
+  const int kvh = blockIdx.y, QG = gridDim.x, nq = (M + qpw - 1) / qpw;
+  const int qb = (QG - 1 - blockIdx.x) + wave * QG;   // longest chains first
+  const bool live = qb < nq;                          // (a wave past the chunk only copies)
+  const int q0 = qb * qpw, qi = min(q0 + (r >> gsh), M - 1), h = kvh * G + (r & (G - 1));
+  const int p = pos[qi];
+  int kmax = p, kmin = p;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    kmax = max(kmax, __shfl_xor(kmax, o, 64));
+    kmin = min(kmin, __shfl_xor(kmin, o, 64));
+  }
+  if (lane == 0) s_kmax[wave] = live ? kmax : 0;
+  f16x8 qh[KW], ql[KW];
+  {
+    const float* qr = q + ((size_t)qi * heads + h) * HD + 8 * g;
+#pragma unroll
+    for (int c = 0; c < KW; ++c) {
+      const float4 t0 = *(const float4*)(qr + 32 * c), t1 = *(const float4*)(qr + 32 * c + 4);
+      const float v[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 hi, lo;
+        pf_split(v[e] * scale, hi, lo);
+        qh[c][e] = hi;
+        ql[c][e] = lo;
+      }
+    }
+  }
+  __syncthreads();
+  const int kmax_wg = max(max(s_kmax[0], s_kmax[1]), max(s_kmax[2], s_kmax[3]));
+  const int kl = min(kmax_wg, max_seq - 1);   // rows past it may be unwritten: read row kl instead
+  const int nkb = kmax_wg / 16 + 1, nkb_w = live ? kmax / 16 + 1 : 0;
+  const uint16_t* kbase = kc + (size_t)kvh * max_seq * HD;
+  const uint16_t* vbase = vc + (size_t)kvh * max_seq * HD;
+  const uint32_t sk_lds = (uint32_t)(uintptr_t)&sk[0][0], sv_lds = (uint32_t)(uintptr_t)&sv[0][0];
+  // this wave's quarter of block kb: key rows 4 wave .. 4 wave + 3 of K and of V, 1 KiB each
+  const int drow = 4 * wave + (lane >> 4), dch = lane & 15;
+  auto issue = [&](int kb) {
+    const int key = min(kb * 16 + drow, kl), slot = kb % R;
+    dma_1k_asm(kbase + (size_t)key * HD + ((dch ^ drow) * 8),
+               __builtin_amdgcn_readfirstlane(sk_lds + (uint32_t)((slot * 16 * HD + wave * 4 * HD) * 2)));
+    dma_1k_asm(vbase + (size_t)key * HD + dch * 8,
+               __builtin_amdgcn_readfirstlane(sv_lds + (uint32_t)((slot * 16 * HD + wave * 4 * HD) * 2)));
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // q and pos in: only the DMAs are counted below
+#pragma unroll
+  for (int kb = 0; kb < R - NB; ++kb) issue(kb);
+  f32x4 acc[DV];
+#pragma unroll
+  for (int t = 0; t < DV; ++t) acc[t] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+  float m_run = -INFINITY, l_run = 0.0f;
+  constexpr float kPfSlack = 8.0f;   // as above: O rescaled only when a column max moves by > 8
+  for (int kb = 0; kb < nkb; kb += NB) {
+    // this wave's DMAs of kb, kb + 1 are the oldest 2 NB of the 2 (R - NB) in flight
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (R - 2 * NB)) : "memory");
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) issue(kb + R - NB + b);
+    if (kb < nkb_w) {   // wave-uniform
+      f32x4 sacc[NB];
+      u32x4 vraw[NB][4];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const uint16_t* kr = &sk[(kb + b) % R][r * HD];
+        sacc[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int c = 0; c < KW; ++c) {
+          const f16x8 kf = __builtin_bit_cast(f16x8, *(const u32x4*)(kr + (((4 * c + g) ^ r) * 8)));
+          sacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[c], sacc[b], 0, 0, 0);
+          sacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[c], sacc[b], 0, 0, 0);
+        }
+        const uint16_t* vb = &sv[(kb + b) % R][0];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) vraw[b][j] = *(const u32x4*)(vb + (4 * g + j) * HD + r * DV);
+      }
+      float pv[NB][4], bm = -INFINITY;
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pv[b][i] = sacc[b][i];
+      if ((kb + NB) * 16 - 1 > kmin) {   // wave-uniform: a step past the shortest column's position
+        const int lim = p - kb * 16 - 4 * g;
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (16 * b + i > lim) pv[b][i] = -INFINITY;
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bm = fmaxf(bm, pv[b][i]);
+      bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+      const float mn = fmaxf(m_run, bm);
+      if (__builtin_amdgcn_ballot_w64(mn > m_run + kPfSlack) != 0) {
+        const float alpha = m_run == mn ? 1.0f : __expf(m_run - mn);
+        l_run *= alpha;
+        m_run = mn;
+#pragma unroll
+        for (int t = 0; t < DV; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[t][i] *= alpha;
+      }
+      float ps = 0.0f;
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pv[b][i] = __expf(pv[b][i] - m_run);
+          ps += pv[b][i];
+        }
+      l_run += ps;
+      // O^T += V^T P^T over both blocks in one 32-key product (16x16x32, the full-rate form): k index
+      // 8 g + e is key 4 g + e of the first block for e < 4 and of the second for e >= 4, in the
+      // A fragment (V, lane (dim r DV + t, k)) and the B fragment (P, lane (column r, k)) alike
+      f16x8 ph, pl;
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          _Float16 hi, lo;
+          pf_split(pv[b][e], hi, lo);
+          ph[4 * b + e] = hi;
+          pl[4 * b + e] = lo;
+        }
+#pragma unroll
+      for (int t = 0; t < DV; ++t) {
+        const uint32_t sel = (t & 1) ? 0x07060302u : 0x05040100u;
+        uint32_t w[4];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          w[2 * b] = __builtin_amdgcn_perm(vraw[b][1][t >> 1], vraw[b][0][t >> 1], sel);
+          w[2 * b + 1] = __builtin_amdgcn_perm(vraw[b][3][t >> 1], vraw[b][2][t >> 1], sel);
+        }
+        const f16x8 bf = __builtin_bit_cast(f16x8, (u32x4){w[0], w[1], w[2], w[3]});
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf, ph, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf, pl, acc[t], 0, 0, 0);
+      }
+    }
+  }
+  // the ring's last copies (clamped rows past the end) land before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!live) return;
+  float lt = l_run + __shfl_xor(l_run, 16, 64);
+  lt += __shfl_xor(lt, 32, 64);
+  const float inv = 1.0f / lt;
+  const int row = q0 + (r >> gsh), hh = kvh * G + (r & (G - 1));
+  if (row < M) {
+    uint16_t* dst = out + ((size_t)row * heads + hh) * HD + 4 * g * DV;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t o[DV / 2];
+#pragma unroll
+      for (int t = 0; t < DV / 2; ++t) {
+        const uint16_t lo = __builtin_bit_cast(uint16_t, (_Float16)(acc[2 * t][i] * inv));
+        const uint16_t hi = __builtin_bit_cast(uint16_t, (_Float16)(acc[2 * t + 1][i] * inv));
+        o[t] = lo | ((uint32_t)hi << 16);
+      }
+      *(ti::u32x4*)(dst + i * DV) = (ti::u32x4){o[0], o[1], o[2], o[3]};
+    }
+  }
+}
+
 }  // namespace ti
 
 extern "C" int ti_attn_prefill(const float* q, const uint16_t* k_cache, const uint16_t* v_cache, int max_seq,
@@ -319,7 +514,17 @@ extern "C" int ti_attn_prefill(const float* q, const uint16_t* k_cache, const ui
     simds.store(ns, std::memory_order_relaxed);   // (a racing first call stores the same value)
   }
   const bool deep = (long)grid.x * grid.y <= ns;
-  if (head_dim == 128) {
+  static const bool wg = [] {
+    const char* e = getenv("TI_PF_WG");
+    return !(e && e[0] == '0');
+  }();
+  const dim3 gw((grid.x + 3) / 4, kv_heads);
+  // 4 query blocks of a kv-head per workgroup, K / V shared in LDS -- when that still gives every CU
+  // a workgroup (256 rows of 7B: 128 workgroups, the per-wave kernel's 512 waves are faster)
+  if (head_dim == 128 && wg && (long)gw.x * gw.y * 4 >= ns) {
+    hipLaunchKernelGGL(ti::attn_prefill_wg_kernel, gw, dim3(256), 0, s, q, k_cache, v_cache, max_seq, pos, M, heads, gsh,
+                       scale, out);
+  } else if (head_dim == 128) {
     if (deep)
       hipLaunchKernelGGL((ti::attn_prefill_kernel<128, TI_PF_RING_DEEP>), grid, dim3(64), 0, s, q, k_cache, v_cache,
                          max_seq, pos, M, heads, gsh, scale, out);
