@@ -304,23 +304,30 @@ __global__ __launch_bounds__(64, WPE) void attn_prefill_kernel(const float* __re
 // landed, and everyone is done with kb - 2, kb - 1); DMA kb + R - 2, kb + R - 1 into their slots;
 // compute.  Waves past their own chain keep copying until the workgroup's longest is done.
 #ifndef TI_PF_WG_RING
-#define TI_PF_WG_RING 6   // K / V blocks in the LDS ring (8 KiB each)
+#define TI_PF_WG_RING 6    // K / V blocks in the LDS ring (8 KiB each), 4-wave workgroups
 #endif
-__global__ __launch_bounds__(256, 1) void attn_prefill_wg_kernel(const float* __restrict__ q, const uint16_t* __restrict__ kc,
+#ifndef TI_PF_WG_RING2
+#define TI_PF_WG_RING2 12  // the same, 8-wave workgroups (4 blocks per iteration)
+#endif
+// HALVES 2: 8 waves, two per SIMD -- waves w and w + 4 share query block w & 3 and take alternate
+// pairs of its key blocks (iteration = 4 blocks, half h computes blocks 2 h, 2 h + 1 of it), merging
+// their (max, sum, O) through LDS at the end: two chains per SIMD hide each other's latencies.
+template <int HALVES, int R>
+__global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const float* __restrict__ q, const uint16_t* __restrict__ kc,
                                                                  const uint16_t* __restrict__ vc, int max_seq,
                                                                  const int32_t* __restrict__ pos, int M, int heads, int gsh,
                                                                  float scale, uint16_t* __restrict__ out) {
-  constexpr int HD = 128, DV = HD / 16, KW = HD / 32, R = TI_PF_WG_RING, NB = 2;
-  static_assert(R % NB == 0 && R >= 2 * NB, "ring: whole steps, one in flight beside the one computed");
+  constexpr int HD = 128, DV = HD / 16, KW = HD / 32, NB = 2, BI = NB * HALVES;   // BI: blocks per iteration
+  static_assert(R % BI == 0 && R >= 2 * BI, "ring: whole iterations, one in flight beside the one computed");
   __shared__ __attribute__((aligned(16))) uint16_t sk[R][16 * HD];
   __shared__ __attribute__((aligned(16))) uint16_t sv[R][16 * HD];
   __shared__ int s_kmax[4];
   const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qw = wave & 3, half = wave >> 2;
   const int G = 1 << gsh, qpw = 16 >> gsh;
   const int kvh = blockIdx.y, QG = gridDim.x, nq = (M + qpw - 1) / qpw;
-  const int qb = (QG - 1 - blockIdx.x) + wave * QG;   // longest chains first
-  const bool live = qb < nq;                          // (a wave past the chunk only copies)
+  const int qb = (QG - 1 - blockIdx.x) + qw * QG;   // longest chains first
+  const bool live = qb < nq;                        // (a wave past the chunk only copies)
   const int q0 = qb * qpw, qi = min(q0 + (r >> gsh), M - 1), h = kvh * G + (r & (G - 1));
   const int p = pos[qi];
   int kmax = p, kmin = p;
@@ -329,7 +336,7 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_wg_kernel(const float* __
     kmax = max(kmax, __shfl_xor(kmax, o, 64));
     kmin = min(kmin, __shfl_xor(kmin, o, 64));
   }
-  if (lane == 0) s_kmax[wave] = live ? kmax : 0;
+  if (lane == 0 && half == 0) s_kmax[qw] = live ? kmax : 0;
   f16x8 qh[KW], ql[KW];
   {
     const float* qr = q + ((size_t)qi * heads + h) * HD + 8 * g;
@@ -353,29 +360,33 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_wg_kernel(const float* __
   const uint16_t* kbase = kc + (size_t)kvh * max_seq * HD;
   const uint16_t* vbase = vc + (size_t)kvh * max_seq * HD;
   const uint32_t sk_lds = (uint32_t)(uintptr_t)&sk[0][0], sv_lds = (uint32_t)(uintptr_t)&sv[0][0];
-  // this wave's quarter of block kb: key rows 4 wave .. 4 wave + 3 of K and of V, 1 KiB each
-  const int drow = 4 * wave + (lane >> 4), dch = lane & 15;
-  auto issue = [&](int kb) {
-    const int key = min(kb * 16 + drow, kl), slot = kb % R;
-    dma_1k_asm(kbase + (size_t)key * HD + ((dch ^ drow) * 8),
-               __builtin_amdgcn_readfirstlane(sk_lds + (uint32_t)((slot * 16 * HD + wave * 4 * HD) * 2)));
-    dma_1k_asm(vbase + (size_t)key * HD + dch * 8,
-               __builtin_amdgcn_readfirstlane(sv_lds + (uint32_t)((slot * 16 * HD + wave * 4 * HD) * 2)));
+  // An iteration's BI blocks are 8 BI DMA instructions of 1 KiB (a block: K rows 0-3, 4-7, 8-11, 12-15,
+  // then V's); wave w issues instructions 4 w .. 4 w + 3: all of K or all of V of block w / 2.
+  const int dblk = wave >> 1, dv = wave & 1, dch = lane & 15;
+  auto issue = [&](int kb0) {   // the iteration starting at block kb0
+    const int kb = kb0 + dblk, slot = kb % R;
+    const uint32_t base = (dv ? sv_lds : sk_lds) + (uint32_t)(slot * 16 * HD * 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 4 * i + (lane >> 4), key = min(kb * 16 + row, kl);
+      const uint16_t* src = dv ? vbase + (size_t)key * HD + dch * 8 : kbase + (size_t)key * HD + ((dch ^ row) * 8);
+      dma_1k_asm(src, __builtin_amdgcn_readfirstlane(base + (uint32_t)(i * 4 * HD * 2)));
+    }
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // q and pos in: only the DMAs are counted below
 #pragma unroll
-  for (int kb = 0; kb < R - NB; ++kb) issue(kb);
+  for (int kb = 0; kb < R - BI; kb += BI) issue(kb);
   f32x4 acc[DV];
 #pragma unroll
   for (int t = 0; t < DV; ++t) acc[t] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
   float m_run = -INFINITY, l_run = 0.0f;
   constexpr float kPfSlack = 8.0f;   // as above: O rescaled only when a column max moves by > 8
-  for (int kb = 0; kb < nkb; kb += NB) {
-    // this wave's DMAs of kb, kb + 1 are the oldest 2 NB of the 2 (R - NB) in flight
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (R - 2 * NB)) : "memory");
+  for (int kbi = 0; kbi < nkb; kbi += BI) {
+    // this wave's 4 DMAs of iteration kbi are the oldest of the 4 (R / BI - 1) in flight
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R / BI - 2)) : "memory");
     __syncthreads();
-#pragma unroll
-    for (int b = 0; b < NB; ++b) issue(kb + R - NB + b);
+    issue(kbi + R - BI);
+    const int kb = kbi + NB * half;   // this half's pair
     if (kb < nkb_w) {   // wave-uniform
       f32x4 sacc[NB];
       u32x4 vraw[NB][4];
@@ -459,9 +470,30 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_wg_kernel(const float* __
       }
     }
   }
-  // the ring's last copies (clamped rows past the end) land before the workgroup's LDS is released
+  // the ring's last copies (clamped rows past the end) land before the ring is reused / released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (HALVES == 2) {   // half 1 hands (m, l, O) to half 0 through the ring's LDS
+    float* xs = (float*)&sk[0][0] + (size_t)qw * 64 * (4 * DV + 2);
+    if (half == 1) {
+#pragma unroll
+      for (int t = 0; t < DV; ++t) *(f32x4*)(xs + (4 * t) * 64 + 4 * lane) = acc[t];
+      xs[4 * DV * 64 + lane] = m_run;
+      xs[4 * DV * 64 + 64 + lane] = l_run;
+    }
+    __syncthreads();
+    if (half == 1) return;
+    const float m1 = xs[4 * DV * 64 + lane], l1 = xs[4 * DV * 64 + 64 + lane];
+    const float mx = fmaxf(m_run, m1);
+    const float f0 = m_run == -INFINITY ? 0.0f : __expf(m_run - mx), f1 = m1 == -INFINITY ? 0.0f : __expf(m1 - mx);
+    l_run = l_run * f0 + l1 * f1;
+#pragma unroll
+    for (int t = 0; t < DV; ++t) {
+      const f32x4 o1 = *(const f32x4*)(xs + (4 * t) * 64 + 4 * lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[t][i] = acc[t][i] * f0 + o1[i] * f1;
+    }
+  }
   if (!live) return;
   float lt = l_run + __shfl_xor(l_run, 16, 64);
   lt += __shfl_xor(lt, 32, 64);
@@ -514,16 +546,21 @@ extern "C" int ti_attn_prefill(const float* q, const uint16_t* k_cache, const ui
     simds.store(ns, std::memory_order_relaxed);   // (a racing first call stores the same value)
   }
   const bool deep = (long)grid.x * grid.y <= ns;
-  static const bool wg = [] {
+  static const int wgk = [] {   // 0: per-wave kernel, 1: workgroup of 4 waves, 2: of 8 (key-split halves)
     const char* e = getenv("TI_PF_WG");
-    return !(e && e[0] == '0');
+    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
   }();
+  const bool wg = wgk > 0, wg2 = wgk == 2;
   const dim3 gw((grid.x + 3) / 4, kv_heads);
   // 4 query blocks of a kv-head per workgroup, K / V shared in LDS -- when that still gives every CU
   // a workgroup (256 rows of 7B: 128 workgroups, the per-wave kernel's 512 waves are faster)
   if (head_dim == 128 && wg && (long)gw.x * gw.y * 4 >= ns) {
-    hipLaunchKernelGGL(ti::attn_prefill_wg_kernel, gw, dim3(256), 0, s, q, k_cache, v_cache, max_seq, pos, M, heads, gsh,
-                       scale, out);
+    if (wg2)
+      hipLaunchKernelGGL((ti::attn_prefill_wg_kernel<2, TI_PF_WG_RING2>), gw, dim3(512), 0, s, q, k_cache, v_cache, max_seq,
+                         pos, M, heads, gsh, scale, out);
+    else
+      hipLaunchKernelGGL((ti::attn_prefill_wg_kernel<1, TI_PF_WG_RING>), gw, dim3(256), 0, s, q, k_cache, v_cache, max_seq,
+                         pos, M, heads, gsh, scale, out);
   } else if (head_dim == 128) {
     if (deep)
       hipLaunchKernelGGL((ti::attn_prefill_kernel<128, TI_PF_RING_DEEP>), grid, dim3(64), 0, s, q, k_cache, v_cache,
