@@ -17,7 +17,7 @@ T.check(L.ti_event_create(C.byref(a)))
 T.check(L.ti_event_create(C.byref(b)))
 heads, hd, max_seq = 32, 128, 2048
 rng = np.random.RandomState(0)
-for kvh, M in [(32, 256), (32, 512), (32, 1024), (8, 512)]:   # 7B MHA; Llama-3-8B GQA 4
+for kvh, M in [(32, 128), (32, 256), (32, 512), (32, 1024), (8, 512)]:   # 7B MHA; Llama-3-8B GQA 4
     kc = T.DeviceBuffer.from_array(rng.standard_normal((kvh, max_seq, hd)).astype(np.float16))
     vc = T.DeviceBuffer.from_array(rng.standard_normal((kvh, max_seq, hd)).astype(np.float16))
     q = T.DeviceBuffer.from_array(rng.standard_normal((M, heads * hd)).astype(np.float32))
