@@ -321,10 +321,18 @@ int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, const uint1
  * out [M][heads*head_dim] fp16.  One wave per 16 (row, q-head) columns streams each key once for
  * them on fp16 MFMA with the fp32 operands split into fp16 hi + lo parts (fp32-accurate products;
  * ti_attn_decode reads the prefix once per row).  head_dim 64 or 128;
- * heads % kv_heads == 0.  Replaces ti_attn_decode(kv_stream_stride = 0) for row-major chunks. */
+ * heads % kv_heads == 0.  Replaces ti_attn_decode(kv_stream_stride = 0) for row-major chunks.
+ * At head_dim 128, chunks whose grid fills the chip run the shared-K/V kernel: a workgroup per
+ * (kv-head, 4 query blocks) copies each K / V block once into LDS for all its waves. */
 int ti_attn_prefill(const float* q, const uint16_t* k_cache, const uint16_t* v_cache, int max_seq,
                     const int32_t* pos, int M, int heads, int kv_heads, int head_dim, uint16_t* out,
                     ti_stream_t s);
+/* Kernel choice of later ti_attn_prefill calls in this process (parity tests and A/Bs; not a
+ * reference interface): 0 automatic (the default, TI_PF_WG applies), 1 the per-wave kernel,
+ * 2 the shared-K/V kernel with 4-wave workgroups, 3 with 8-wave workgroups (key-split halves).
+ * Modes 2 and 3 apply at head_dim 128 at any grid size; other head_dims take the per-wave kernel.
+ * Returns the previous mode, or -1 for a mode outside 0..3 (nothing changed). */
+int ti_attn_prefill_set_kernel(int mode);
 
 /* The kernel ti_gemm_wq_a16 launches for plain (not group-32) weights of this shape, e.g.
  * "gemv_wq_kernel<4,4>", "gemm_rows_kernel", "gemm_tile_kernel" (bench / profile labels). */

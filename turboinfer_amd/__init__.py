@@ -73,7 +73,7 @@ EXPORTED = [
     "ti_device_sync", "ti_event_create", "ti_event_destroy", "ti_event_record", "ti_event_elapsed_ms",
     "ti_wpack_tile_bytes", "ti_wpack_scale_bytes", "ti_wpack_host", "ti_wsynth_device", "ti_fill_uniform_f16",
     "ti_fill_uniform_f32", "ti_fill_kv_uniform", "ti_kv_copy_slots", "ti_gemm_wq_a16", "ti_gemm_lds_bytes", "ti_gemm_prepare",
-    "ti_gemm_max_rows", "ti_gemm_packed_rows", "ti_gemm_packed_rows_for", "ti_gemm_tile_plan", "ti_rmsnorm_f16", "ti_rmsnorm_f16_packed", "ti_attn_decode_packed", "ti_attn_prefill",
+    "ti_gemm_max_rows", "ti_gemm_packed_rows", "ti_gemm_packed_rows_for", "ti_gemm_tile_plan", "ti_rmsnorm_f16", "ti_rmsnorm_f16_packed", "ti_attn_decode_packed", "ti_attn_prefill", "ti_attn_prefill_set_kernel",
     "ti_attn_workspace_bytes", "ti_attn_decode", "ti_step_begin", "ti_matmul_f32", "ti_rms_norm_f32",
     "ti_rope_f32", "ti_silu_f32", "ti_relu_f32", "ti_add_f32", "ti_mul_f32", "ti_softmax_f32", "ti_attention_f32",
     "ti_argmax_f32", "ti_engine_create", "ti_engine_destroy", "ti_engine_get_stream", "ti_engine_memory", "ti_engine_set_tensor",
@@ -139,6 +139,7 @@ def lib() -> C.CDLL:
         L.ti_attn_decode.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
         L.ti_attn_decode_packed.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
         L.ti_attn_prefill.argtypes = [vp, vp, vp, i32, vp, i32, i32, i32, i32, vp, vp]
+        L.ti_attn_prefill_set_kernel.argtypes = [i32]
         if hasattr(L, "ti_sample_device"):
             L.ti_sample_device.argtypes = [vp, i32, i32, i32, f32, i32, f32, vp, vp, vp, vp]
         if hasattr(L, "ti_sample_device_ws"):

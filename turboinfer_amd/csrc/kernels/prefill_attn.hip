@@ -438,7 +438,8 @@ __global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const 
       for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          pv[b][i] = __expf(pv[b][i] - m_run);
+          // (half 1 may meet a column whose keys so far are all masked: m_run -inf, p 0)
+          pv[b][i] = HALVES == 2 && m_run == -INFINITY ? 0.0f : __expf(pv[b][i] - m_run);
           ps += pv[b][i];
         }
       l_run += ps;
@@ -517,6 +518,13 @@ __global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const 
 
 }  // namespace ti
 
+static std::atomic<int> g_pf_kernel{0};
+
+extern "C" int ti_attn_prefill_set_kernel(int mode) {
+  if (mode < 0 || mode > 3) return -1;
+  return g_pf_kernel.exchange(mode);
+}
+
 extern "C" int ti_attn_prefill(const float* q, const uint16_t* k_cache, const uint16_t* v_cache, int max_seq,
                                const int32_t* pos, int M, int heads, int kv_heads, int head_dim, uint16_t* out,
                                ti_stream_t stream) {
@@ -550,11 +558,13 @@ extern "C" int ti_attn_prefill(const float* q, const uint16_t* k_cache, const ui
     const char* e = getenv("TI_PF_WG");
     return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
   }();
-  const bool wg = wgk > 0, wg2 = wgk == 2;
+  const int forced = g_pf_kernel.load(std::memory_order_relaxed);   // ti_attn_prefill_set_kernel
+  const int k = forced == 0 ? wgk : forced - 1;
+  const bool wg = k > 0, wg2 = k == 2;
   const dim3 gw((grid.x + 3) / 4, kv_heads);
   // 4 query blocks of a kv-head per workgroup, K / V shared in LDS -- when that still gives every CU
   // a workgroup (256 rows of 7B: 128 workgroups, the per-wave kernel's 512 waves are faster)
-  if (head_dim == 128 && wg && (long)gw.x * gw.y * 4 >= ns) {
+  if (head_dim == 128 && wg && (forced > 1 || (long)gw.x * gw.y * 4 >= ns)) {
     if (wg2)
       hipLaunchKernelGGL((ti::attn_prefill_wg_kernel<2, TI_PF_WG_RING2>), gw, dim3(512), 0, s, q, k_cache, v_cache, max_seq,
                          pos, M, heads, gsh, scale, out);
