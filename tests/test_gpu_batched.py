@@ -280,9 +280,26 @@ def test_batched_qkv_rope_kv_append(ti, oracle, splitk_ws, hd, nh, nkv, splitk):
         np.testing.assert_allclose(vcache[m, :, pos[m]], v[m].reshape(nkv, hd), rtol=2e-3, atol=2e-3)
 
 
-def test_rmsnorm_f16_matches_fused_prologue(ti, oracle):
+@pytest.mark.parametrize("K", [2048, 11008, 16384, 20480])
+def test_rmsnorm_f16_row_lengths(ti, oracle, K):
+    """ti_rmsnorm_f16 holds a row in registers in 1-4 pieces per thread (K <= 16384) and re-reads
+    it beyond that: every form against the oracle's rms_norm."""
+    M = 3
+    rng = np.random.RandomState(K)
+    x = (rng.standard_normal((M, K)) * 2).astype(f32)
+    nw = (1 + 0.1 * rng.standard_normal(K)).astype(f32)
+    xd, nwd = dev(ti, x), dev(ti, nw)
+    yd = ti.DeviceBuffer(M * K * 2)
+    ti.check(ti.lib().ti_rmsnorm_f16(xd.ptr, K, nwd.ptr, 1e-5, yd.ptr, K, M, K, None))
+    ti.sync()
+    ref = oracle.rms_norm(x, nw)
+    np.testing.assert_allclose(yd.download(f16, (M, K)).astype(f32), ref.astype(f16).astype(f32), rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("K", [4096, 8192])
+def test_rmsnorm_f16_matches_fused_prologue(ti, oracle, K):
     """ti_rmsnorm_f16 rows fed to the fused kernel == its own rms_norm prologue (same arithmetic)."""
-    M, K, N = 2, 4096, 256
+    M, N = 2, 256
     rng = np.random.RandomState(9)
     x = (rng.standard_normal((M, K)) * 2).astype(f32)
     nw = (1 + 0.1 * rng.standard_normal(K)).astype(f32)
