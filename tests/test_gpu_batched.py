@@ -282,8 +282,8 @@ def test_batched_qkv_rope_kv_append(ti, oracle, splitk_ws, hd, nh, nkv, splitk):
 
 @pytest.mark.parametrize("K", [2048, 11008, 16384, 20480])
 def test_rmsnorm_f16_row_lengths(ti, oracle, K):
-    """ti_rmsnorm_f16 holds a row in registers in 1-4 pieces per thread (K <= 16384) and re-reads
-    it beyond that: every form against the oracle's rms_norm."""
+    """ti_rmsnorm_f16 at row lengths of 1 to 5 pieces of 8 floats per thread (the hidden sizes of
+    the served models and past them) against the oracle's rms_norm."""
     M = 3
     rng = np.random.RandomState(K)
     x = (rng.standard_normal((M, K)) * 2).astype(f32)
