@@ -307,7 +307,7 @@ __global__ __launch_bounds__(64, WPE) void attn_prefill_kernel(const float* __re
 #define TI_PF_WG_RING 6    // K / V blocks in the LDS ring (8 KiB each), 4-wave workgroups
 #endif
 #ifndef TI_PF_WG_RING2
-#define TI_PF_WG_RING2 12  // the same, 8-wave workgroups (4 blocks per iteration)
+#define TI_PF_WG_RING2 8   // the same, 8-wave workgroups (4 blocks per iteration; 8 beat 12 and 16, profiles/r5_prefill_wg_ring_ab.txt)
 #endif
 // HALVES 2: 8 waves, two per SIMD -- waves w and w + 4 share query block w & 3 and take alternate
 // pairs of its key blocks (iteration = 4 blocks, half h computes blocks 2 h, 2 h + 1 of it), merging
