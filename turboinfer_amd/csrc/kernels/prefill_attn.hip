@@ -306,6 +306,9 @@ __global__ __launch_bounds__(64, WPE) void attn_prefill_kernel(const float* __re
 #ifndef TI_PF_WG_RING
 #define TI_PF_WG_RING 6    // K / V blocks in the LDS ring (8 KiB each), 4-wave workgroups
 #endif
+#ifndef TI_PF_WG_LATE_DMA
+#define TI_PF_WG_LATE_DMA 0
+#endif
 #ifndef TI_PF_WG_RING2
 #define TI_PF_WG_RING2 8   // the same, 8-wave workgroups (4 blocks per iteration; 8 beat 12 and 16, profiles/r5_prefill_wg_ring_ab.txt)
 #endif
@@ -385,11 +388,14 @@ __global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const 
     // this wave's 4 DMAs of iteration kbi are the oldest of the 4 (R / BI - 1) in flight
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (R / BI - 2)) : "memory");
     __syncthreads();
+#if !TI_PF_WG_LATE_DMA
     issue(kbi + R - BI);
+#endif
     const int kb = kbi + NB * half;   // this half's pair
-    if (kb < nkb_w) {   // wave-uniform
-      f32x4 sacc[NB];
-      u32x4 vraw[NB][4];
+    const bool act = kb < nkb_w;      // wave-uniform
+    f32x4 sacc[NB];
+    u32x4 vraw[NB][4];
+    if (act) {
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
         const uint16_t* kr = &sk[(kb + b) % R][r * HD];
@@ -404,6 +410,11 @@ __global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const 
 #pragma unroll
         for (int j = 0; j < 4; ++j) vraw[b][j] = *(const u32x4*)(vb + (4 * g + j) * HD + r * DV);
       }
+    }
+#if TI_PF_WG_LATE_DMA   // the next DMAs issued under this step's S = K Q^T rather than before it
+    issue(kbi + R - BI);
+#endif
+    if (act) {
       float pv[NB][4], bm = -INFINITY;
 #pragma unroll
       for (int b = 0; b < NB; ++b)
