@@ -1,5 +1,6 @@
 #!/bin/bash
 # RECORD ONLY: the half-grid criterion was not kept (profiles/r5_prefill_wg256_ab.txt).
+echo "the half-grid criterion was not kept (profiles/r5_prefill_wg256_ab.txt)"; exit 2
 # 8-wave prefill attention also when its grid covers half the CUs (7B 256-row chunks): prefill-attention parity,
 # then the attention alone, the previous commit's build (ablib/prev.so) against the new one, interleaved.
 export TMPDIR=/tmp
