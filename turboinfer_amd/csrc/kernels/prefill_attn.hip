@@ -292,22 +292,23 @@ __global__ __launch_bounds__(64, WPE) void attn_prefill_kernel(const float* __re
 // ---------------------------------------------------------------- shared K / V blocks (hd 128)
 // The kernel above gives every wave its own K / V stream from L2, and that stream bounds it
 // (profiles/r5_prefill_attn_diag.txt: 21.5 of 24 us at 512 rows; half-line K reads, ~80 block loads
-// per CU).  Here a workgroup of 4 waves (one per SIMD) takes 4 query blocks of one kv-head -- wave w
-// block j + w QG, so every workgroup holds one long and one short chain -- and copies each K / V
-// block of their union once into an LDS ring (LDS-DMA, full 128-byte lines), which all 4 waves read.
-// The per-wave math is the kernel above's: S^T = K Q^T and O^T += V^T P^T on fp16 MFMA with the fp32
-// operand in hi + lo, online softmax per column, two blocks per step.
+// per CU).  Here a workgroup takes 4 query blocks of one kv-head -- query wave q block j + q QG, so
+// every workgroup holds long and short chains -- and copies each K / V block of their union once
+// into an LDS ring (LDS-DMA, full 128-byte lines), which all its waves read.
+// The per-wave math is the kernel above's: S^T = K Q^T on fp16 MFMA with the fp32 operand in hi + lo,
+// online softmax per column, two blocks per step, and O^T += V^T P^T as one 32-key 16x16x32 product.
 //   K block in LDS: [16 keys][16 chunks of 16 B], the logical chunk c of key row r at physical c ^ r
 //   (an A-fragment read, lane (r, g) chunk 4c + g, is conflict-free in every ds_read_b128 lane group);
 //   V block: [16 keys][16 chunks], unswizzled (lane (r, g) reads chunk r of rows 4g + j).
-// Per iteration (blocks kb, kb + 1): wait for this wave's DMAs of kb, kb + 1; barrier (everyone's
-// landed, and everyone is done with kb - 2, kb - 1); DMA kb + R - 2, kb + R - 1 into their slots;
-// compute.  Waves past their own chain keep copying until the workgroup's longest is done.
+// Per iteration of BI blocks (2 per half): wait for this wave's 4 DMAs of the iteration; barrier
+// (everyone's landed, and everyone is done with the previous iteration's blocks); DMA the iteration
+// R / BI - 1 ahead into the slots just freed; compute.  Waves past their own chain keep copying until
+// the workgroup's longest is done; the last DMAs drain before the ring's LDS is reused or released.
 #ifndef TI_PF_WG_RING
 #define TI_PF_WG_RING 6    // K / V blocks in the LDS ring (8 KiB each), 4-wave workgroups
 #endif
 #ifndef TI_PF_WG_LATE_DMA
-#define TI_PF_WG_LATE_DMA 0
+#define TI_PF_WG_LATE_DMA 0   // 1: DMAs issued after the step's S = K Q^T (even, profiles/r5_prefill_wg_latedma_ab.txt)
 #endif
 #ifndef TI_PF_WG_RING2
 #define TI_PF_WG_RING2 8   // the same, 8-wave workgroups (4 blocks per iteration; 8 beat 12 and 16, profiles/r5_prefill_wg_ring_ab.txt)
