@@ -123,6 +123,19 @@ __device__ __forceinline__ void dma_1k_asm(const void* src_lane, uint32_t lds) {
                : "memory");
 }
 
+// max / sum with the lane 16 or 32 apart (l ^ 16, l ^ 32) through gfx950's v_permlane16/32_swap,
+// VALU only (a __shfl_xor across rows is an LDS round trip): after a swap of x with itself, lane l
+// holds x[l] in one result and x[l ^ 16] (x[l ^ 32]) in the other, in some order -- max and + of
+// the two are exact and order-free.
+__device__ __forceinline__ float xor16_max(float x) {
+  const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(t[0]), __uint_as_float(t[1]));
+}
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(t[0]), __uint_as_float(t[1]));
+}
+
 // a raw buffer resource over [base, base + 2 GiB): the cache policy is the access's aux bits
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);

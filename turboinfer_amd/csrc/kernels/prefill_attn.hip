@@ -56,7 +56,8 @@ __device__ __forceinline__ void pf_split(float x, _Float16& hi, _Float16& lo) {
 }
 
 #ifndef TI_PF_DIAG
-#define TI_PF_DIAG 0   // diagnostics only (tools/r5_pfdiag.sh): 1 cache-resident K / V, 2 no math
+#define TI_PF_DIAG 0   // diagnostics only (tools/r5_pfdiag.sh, r5_pfwgdiag.sh): 1 cache-resident K / V, 2 no math;
+                       // shared-K/V kernel: 4 ring and barriers only, 8 no copies past the prologue
 #endif
 #ifndef TI_PF_RING
 #define TI_PF_RING 3   // K / V blocks in flight per wave (3: two waves per SIMD, held to 256 registers)
@@ -307,6 +308,9 @@ __global__ __launch_bounds__(64, WPE) void attn_prefill_kernel(const float* __re
 #ifndef TI_PF_WG_RING
 #define TI_PF_WG_RING 6    // K / V blocks in the LDS ring (8 KiB each), 4-wave workgroups
 #endif
+#ifndef TI_PF_PERMLANE
+#define TI_PF_PERMLANE 1   // the softmax's cross-row max by v_permlane16/32_swap instead of ds_bpermute
+#endif
 #ifndef TI_PF_WG_LATE_DMA
 #define TI_PF_WG_LATE_DMA 0   // 1: DMAs issued after the step's S = K Q^T (even, profiles/r5_prefill_wg_latedma_ab.txt)
 #endif
@@ -368,6 +372,9 @@ __global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const 
   // then V's); wave w issues instructions 4 w .. 4 w + 3: all of K or all of V of block w / 2.
   const int dblk = wave >> 1, dv = wave & 1, dch = lane & 15;
   auto issue = [&](int kb0) {   // the iteration starting at block kb0
+#if TI_PF_DIAG & 8   // diagnostic: no copies past the prologue (the math on stale blocks)
+    if (kb0 >= R - BI) return;
+#endif
     const int kb = kb0 + dblk, slot = kb % R;
     const uint32_t base = (dv ? sv_lds : sk_lds) + (uint32_t)(slot * 16 * HD * 2);
 #pragma unroll
@@ -393,7 +400,11 @@ __global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const 
     issue(kbi + R - BI);
 #endif
     const int kb = kbi + NB * half;   // this half's pair
+#if TI_PF_DIAG & 4   // diagnostic: the ring and its barriers alone, no math
+    const bool act = false;
+#else
     const bool act = kb < nkb_w;      // wave-uniform
+#endif
     f32x4 sacc[NB];
     u32x4 vraw[NB][4];
     if (act) {
@@ -433,8 +444,12 @@ __global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const 
       for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int i = 0; i < 4; ++i) bm = fmaxf(bm, pv[b][i]);
+#if TI_PF_PERMLANE
+      bm = xor32_max(xor16_max(bm));   // the column's max over its 4 lane groups, VALU only
+#else
       bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
       bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+#endif
       const float mn = fmaxf(m_run, bm);
       if (__builtin_amdgcn_ballot_w64(mn > m_run + kPfSlack) != 0) {
         const float alpha = m_run == mn ? 1.0f : __expf(m_run - mn);
