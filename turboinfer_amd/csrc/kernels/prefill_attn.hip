@@ -308,6 +308,9 @@ __global__ __launch_bounds__(64, WPE) void attn_prefill_kernel(const float* __re
 #ifndef TI_PF_WG_RING
 #define TI_PF_WG_RING 6    // K / V blocks in the LDS ring (8 KiB each), 4-wave workgroups
 #endif
+#ifndef TI_PF_QK_SPLIT
+#define TI_PF_QK_SPLIT 0   // shared-K/V kernel: S = K Q^T's hi and lo products in separate chains
+#endif
 #ifndef TI_PF_PERMLANE
 #define TI_PF_PERMLANE 1   // the softmax's cross-row max by v_permlane16/32_swap instead of ds_bpermute
 #endif
@@ -411,6 +414,16 @@ __global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const 
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
         const uint16_t* kr = &sk[(kb + b) % R][r * HD];
+#if TI_PF_QK_SPLIT   // the hi and lo products in two chains (four independent per step), summed after
+        f32x4 sh = (f32x4){0.0f, 0.0f, 0.0f, 0.0f}, sl = sh;
+#pragma unroll
+        for (int c = 0; c < KW; ++c) {
+          const f16x8 kf = __builtin_bit_cast(f16x8, *(const u32x4*)(kr + (((4 * c + g) ^ r) * 8)));
+          sh = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[c], sh, 0, 0, 0);
+          sl = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[c], sl, 0, 0, 0);
+        }
+        sacc[b] = sh + sl;
+#else
         sacc[b] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int c = 0; c < KW; ++c) {
@@ -418,6 +431,7 @@ __global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const 
           sacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[c], sacc[b], 0, 0, 0);
           sacc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[c], sacc[b], 0, 0, 0);
         }
+#endif
         const uint16_t* vb = &sv[(kb + b) % R][0];
 #pragma unroll
         for (int j = 0; j < 4; ++j) vraw[b][j] = *(const u32x4*)(vb + (4 * g + j) * HD + r * DV);
