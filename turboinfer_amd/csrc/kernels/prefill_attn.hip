@@ -59,6 +59,9 @@ __device__ __forceinline__ void pf_split(float x, _Float16& hi, _Float16& lo) {
 #define TI_PF_DIAG 0   // diagnostics only (tools/r5_pfdiag.sh, r5_pfwgdiag.sh): 1 cache-resident K / V, 2 no math;
                        // shared-K/V kernel: 4 ring and barriers only, 8 no copies past the prologue
 #endif
+#ifndef TI_PF_PERMLANE
+#define TI_PF_PERMLANE 1   // the softmax's cross-row max by v_permlane16/32_swap instead of ds_bpermute
+#endif
 #ifndef TI_PF_RING
 #define TI_PF_RING 3   // K / V blocks in flight per wave (3: two waves per SIMD, held to 256 registers)
 #endif
@@ -206,8 +209,12 @@ __global__ __launch_bounds__(64, WPE) void attn_prefill_kernel(const float* __re
       for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int i = 0; i < 4; ++i) bm = fmaxf(bm, pv[b][i]);
+#if TI_PF_PERMLANE
+      bm = xor32_max(xor16_max(bm));   // the column's max over its 4 lane groups, VALU only
+#else
       bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
       bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+#endif
       // The running max moves only when a column's block max exceeds it by more than kPfSlack
       // (e^8: p stays below 2981, exact enough in the fp16 hi + lo split, and l, O in fp32): the
       // O rescale -- 32 accumulators read, scaled and written back per lane -- then runs in the
@@ -310,9 +317,6 @@ __global__ __launch_bounds__(64, WPE) void attn_prefill_kernel(const float* __re
 #endif
 #ifndef TI_PF_QK_SPLIT
 #define TI_PF_QK_SPLIT 0   // shared-K/V kernel: S = K Q^T's hi and lo products in separate chains
-#endif
-#ifndef TI_PF_PERMLANE
-#define TI_PF_PERMLANE 1   // the softmax's cross-row max by v_permlane16/32_swap instead of ds_bpermute
 #endif
 #ifndef TI_PF_WG_LATE_DMA
 #define TI_PF_WG_LATE_DMA 0   // 1: DMAs issued after the step's S = K Q^T (even, profiles/r5_prefill_wg_latedma_ab.txt)
