@@ -132,16 +132,35 @@ def pmc_traffic(kernel: str, model: str, batch: int):
     return (best[1], best[2]) if best else (None, None)
 
 
+def rank_plan(args, rank: int, vocab: int) -> dict:
+    """What rank `rank` of a replica job runs: its own B = --batch streams (the request shard:
+    global_batch = B x world), its weight seed, each stream's KV seed and the replay's first
+    token.  Distinct per rank, so no two replicas decode the same requests."""
+    B = args.batch
+    return {"streams": B, "weight_seed": args.seed + rank,
+            "kv_seeds": [args.seed + 1000 * rank + s for s in range(B)],
+            "first_token": (args.seed + rank) % vocab}
+
+
 def dry_run(g: "Group", args) -> int:
     """The replica path without a GPU: every rank takes part in the same two barriers and the
-    max over ranks as a real run, with a fixed per-rank duration in place of the timed steps."""
+    max over ranks as a real run, with a fixed per-rank duration in place of the timed steps,
+    and rank 0 gathers every rank's shard plan (rank_plan) to report it."""
     g.barrier()
     dt = g.max(0.001 * (g.rank + 1))
+    plan = rank_plan(args, g.rank, MODELS[args.model][0])
+    plans = [plan]
+    if g.dist:
+        plans = [None] * g.world
+        g.dist.all_gather_object(plans, plan)
     g.barrier()
     if g.rank == 0:
         print(json.dumps({"metric": "decode tokens/s/GPU, Llama-7B-shape INT4 @2048 ctx; % HBM-read roofline",
                           "value": None, "dry_run": True, "n_gpus": g.world, "max_rank_s": dt,
-                          "config": {"global_batch": args.batch * g.world, "parallelism": f"replicas{g.world}"}}))
+                          "config": {"global_batch": args.batch * g.world, "parallelism": f"replicas{g.world}"},
+                          "rank_plans": [{"rank": r, "streams": p["streams"], "weight_seed": p["weight_seed"],
+                                          "first_token": p["first_token"], "kv_seed_first": p["kv_seeds"][0],
+                                          "kv_seed_last": p["kv_seeds"][-1]} for r, p in enumerate(plans)]}))
     g.close()
     return 0
 
@@ -226,10 +245,11 @@ def main() -> int:
     B, L = args.batch, args.kv
     e = T.Engine(V, H, layers, nh, nkv, hd, I, bits=bits, max_seq=L, max_batch=B, rope_theta=theta,
                  device=g.local_rank, attn_splits=args.attn_splits)
-    e.synth(args.seed + g.rank, 0.0)
+    plan = rank_plan(args, g.rank, V)
+    e.synth(plan["weight_seed"], 0.0)
     for s in range(B):
-        e.fill_kv(s, L - 1, args.seed + 1000 * g.rank + s)
-    e.replay_prepare(B, L, (args.seed + g.rank) % V)
+        e.fill_kv(s, L - 1, plan["kv_seeds"][s])
+    e.replay_prepare(B, L, plan["first_token"])
 
     e.replay_run(args.warmup)
     e.sync()

@@ -143,14 +143,6 @@ int ti_engine_set_prefill(ti_engine* e, int rows);
  * on = 0/1 sets both, -1 leaves them; *active (nullable) receives whether 1-stream steps fold. */
 int ti_engine_set_fold(ti_engine* e, int on, int* active);
 
-/* Deprecated (round 5): the persistent decode launch was removed from the product (the per-layer
- * launches beat it at every shape).  Kept for one release: on = 0 / -1 succeed with
- * *active = 0, on = 1 returns TI_ERR_UNSUPPORTED; ti_engine_pds_error always reports 0 and
- * ti_engine_pds_timestamps TI_ERR_UNSUPPORTED. */
-int ti_engine_set_pds(ti_engine* e, int on, int* active);
-int ti_engine_pds_error(ti_engine* e, uint32_t* err);
-int ti_engine_pds_timestamps(ti_engine* e, unsigned long long* out, size_t n);
-
 /* One decode step: token[s] at position pos[s] for each stream; logits [n][vocab] to host
  * (used for non-greedy sampling and per-step parity). */
 int ti_engine_step(ti_engine* e, int n_streams, const int32_t* tokens, const int32_t* pos, float* logits);
@@ -166,6 +158,28 @@ int ti_engine_replay_run(ti_engine* e, int steps);
 int ti_engine_sync(ti_engine* e);
 /* tokens decided by the last replay step, [n_streams] */
 int ti_engine_last_tokens(ti_engine* e, int n_streams, int32_t* tokens);
+
+/* In-step launch timing (bench.py's roofline; not a reference interface -- the reference
+ * times wall clock only, benchmarks/benchmark_inference.cpp:309-384).  The replay step graph
+ * (ti_engine_replay_prepare) is captured again with every decode kernel writing, per workgroup,
+ * s_memrealtime stamps (100 MHz) of wave 0's entry and of each wave's end into an engine-owned
+ * device buffer; the graph is replayed once untimed, then `steps` times, each replay alone on the
+ * stream.  Per launch i < min(*n_launch, cap): info[3 i ..] = {kind, tag, workgroups} (workgroups 0:
+ * the launch writes no stamps) and t[TI_STAMP_FIELDS i ..] the means over the steps, in us, of
+ *   [0] span    first workgroup entry -> last wave end
+ *   [1] period  first entry -> the next launch's first entry (the last launch: its span)
+ *   [2] entry skew  first -> last workgroup entry
+ *   [3] wave skew   per workgroup, first -> last wave end, averaged over the workgroups
+ *   [4] tail        median workgroup end -> last wave end
+ *   [5] gap         last wave end -> the next launch's first entry (the boundary)
+ *   [6] workgroups that ran on a CU another workgroup of the launch also ran on (a count)
+ * *n_launch receives the launches per step. */
+#define TI_STAMP_FIELDS 7
+enum { TI_STAMP_KIND_OTHER = 0, TI_STAMP_KIND_GEMV = 1, TI_STAMP_KIND_ATTN = 2, TI_STAMP_KIND_BEGIN = 3,
+       TI_STAMP_KIND_ROWS = 4, TI_STAMP_KIND_TILE = 5, TI_STAMP_KIND_RMSNORM = 6, TI_STAMP_KIND_MB = 7 };
+enum { TI_STAMP_TAG_BEGIN = 0, TI_STAMP_TAG_QKV = 1, TI_STAMP_TAG_ATTN = 2, TI_STAMP_TAG_O = 3,
+       TI_STAMP_TAG_GATE_UP = 4, TI_STAMP_TAG_DOWN = 5, TI_STAMP_TAG_LM_HEAD = 6, TI_STAMP_TAG_OTHER = 7 };
+int ti_engine_stamp_steps(ti_engine* e, int steps, int cap, int32_t* info, double* t, int* n_launch);
 
 /* Live per-kernel timing: the step's launches of class `which` (0 qkv, 1 o, 2 gate/up,
  * 3 down, 4 lm_head, 5 attention), `reps` of them cycling through the layers,

@@ -347,7 +347,8 @@ int ti_hbm_calibrate(size_t bytes, int reps, double* read_gbps, double* copy_gbp
 
 /* (Round 5: the persistent decode launch ti_pds_decode, its ti_pds_args / ti_pds_layer structs,
  * ti_pds_supported and ti_pds_granule_words were removed -- the per-layer launches beat it at every
- * shape, DESIGN 4.15.  ti_engine_set_pds stays as a stub for one release) */
+ * shape; the ti_engine_set_pds / _pds_error / _pds_timestamps stubs left in round 6,
+ * INTEGRATION.md 3.) */
 
 /* ------------------------------------------------------- step begin (device loop)
  * One block per stream: picks the token of this step (prompt token while step < n_in[m],

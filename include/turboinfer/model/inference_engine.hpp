@@ -23,9 +23,11 @@
 // model's metadata or the environment (ModelMetadata::extra_params first, then the variable):
 //   * "turboinfer.weight_bits" / TI_WEIGHT_BITS: the weight format below (default 0 = auto);
 //   * "turboinfer.gpu_index" / TI_GPU_INDEX: the HIP device the engine binds (default 0).
-// A ModelData with metadata but no tensors (the reference's test programs) builds the engine's
-// synthetic INT4 model of that shape (ti_engine_synth): the reference runs such a model on its
-// placeholder fallbacks instead.
+//   * "turboinfer.synthetic" / TI_SYNTHETIC: "1" lets a ModelData with metadata but no tensors (the
+//     reference's test programs) build the engine's seeded synthetic INT4 model of that shape
+//     (ti_engine_synth; the reference runs such a model on its placeholder fallbacks); without it
+//     such a ModelData throws std::runtime_error.
+// TensorEngine binds the device TI_GPU_INDEX names (default 0).
 //
 // Model forms accepted (reference weight names, inference_engine.cpp:483-563):
 //   * llama: token_embeddings / embed_tokens, per-layer q/k/v/o, gate/up/down, both norms,

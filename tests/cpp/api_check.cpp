@@ -299,11 +299,49 @@ static int tinq_load(const std::string& in, const std::string& dir) {
   return 0;
 }
 
+// A ModelData with metadata and no tensors: the engine's synthetic model only when asked
+// ("turboinfer.synthetic" in extra_params or TI_SYNTHETIC=1), otherwise InferenceEngine throws.
+static int tensorless(int ask) {
+  model::ModelData md;
+  auto& m = md.metadata();
+  m.name = "tensorless";
+  m.architecture = "llama";
+  m.vocab_size = 512;
+  m.hidden_size = 256;
+  m.num_layers = 2;
+  m.num_heads = 4;
+  m.intermediate_size = 512;
+  if (ask) m.extra_params["turboinfer.synthetic"] = "1";
+  model::InferenceConfig cfg;
+  cfg.max_sequence_length = 64;
+  try {
+    model::InferenceEngine eng(md, cfg);
+    const auto r = eng.generate(std::vector<int>{1, 2, 3}, 4);
+    std::cout << "built " << r.tokens.size() << "\n";
+  } catch (const std::runtime_error& e) {
+    std::cout << "threw " << e.what() << "\n";
+  }
+  return 0;
+}
+
+// TensorEngine's device (TI_GPU_INDEX) and one op on it
+static int tensor_engine_device() {
+  core::TensorEngine te(core::ComputeDevice::kGPU);
+  std::cout << te.device_info() << "\n";
+  Tensor a(TensorShape({4}), DataType::kFloat32), b(TensorShape({4}), DataType::kFloat32);
+  for (int i = 0; i < 4; ++i) a.data_ptr<float>()[i] = b.data_ptr<float>()[i] = (float)i;
+  const Tensor c = te.add(a, b);
+  std::cout << "add " << c.data_ptr<float>()[3] << "\n";
+  return 0;
+}
+
 int main(int argc, char** argv) {
   try {
     if (argc < 2) throw std::runtime_error("usage: api_check tensor|quant|op|generate ...");
     const std::string mode = argv[1];
     if (mode == "tensor") return tensor_checks();
+    if (mode == "tensorless" && argc == 3) return tensorless(std::atoi(argv[2]));
+    if (mode == "tensor_engine_device") return tensor_engine_device();
     if (mode == "quant" && argc == 6) return quant(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argv[5]);
     if (mode == "op" && argc >= 5) return op(argc, argv);
     if (mode == "tinq_save" && argc == 6) return tinq_save(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argv[5]);

@@ -14,6 +14,11 @@ TOL_DEEP = 5e-3 (north_star: 1e-2 relative).  The engine computes in fp16 activa
 KV cache with fp32 accumulation; the error grows with depth: 5.6-8.4e-4 * max|logit| at 2 layers
 (test_gpu_engine.py, TOL 2e-3), 2.6e-3 at 32 layers of 7B (round 3, first run).
 
+north_star's literal bound, "fp16 logits within 1e-2 relative", is also asserted per element on
+the logits that decide the token: at every checked step the oracle's 16 largest logits, each
+|y_i - r_i| / |r_i| <= TOL_ELEM = 1e-2 (the max-norm bound above covers the
+rest of the vector, whose entries near zero make a per-element ratio meaningless).
+
 Set TI_PARITY_LOG=<file> to append each checked stream's measured error (JSON lines)."""
 from __future__ import annotations
 
@@ -28,6 +33,14 @@ from test_gpu_engine import engine_for, margin
 pytestmark = pytest.mark.gpu
 
 TOL = TOL_DEEP = 5e-3
+TOL_ELEM = 1e-2   # north_star: per element, relative, on the oracle's top-16 logits of each step
+
+
+def top16_rel(got, ref):
+    """max over the oracle's 16 largest logits of |got_i - ref_i| / |ref_i|."""
+    ref = np.asarray(ref, np.float64)
+    idx = np.argpartition(ref, -16)[-16:]
+    return float(np.max(np.abs(np.asarray(got, np.float64)[idx] - ref[idx]) / np.abs(ref[idx])))
 
 
 def assert_greedy(got, ref, ref_logits, what=""):
@@ -71,7 +84,7 @@ def _run(ti, golden, name, B, slots, which=None):
         e.fill_kv(s, fill, params[s][1])
     n = len(ref[0][0])
     feed = [p[0] for p in params]
-    worst = {}
+    worst, worst16 = {}, {}
     for step in range(n):
         lg = e.step(feed, [fill + step] * B)
         feed = [int(t) for t in np.argmax(lg, axis=1)]
@@ -80,10 +93,13 @@ def _run(ti, golden, name, B, slots, which=None):
             mx = float(np.max(np.abs(r)))
             err = float(np.max(np.abs(lg[s].astype(np.float64) - r)))
             worst[i] = max(worst.get(i, 0.0), err / mx)
+            worst16[i] = max(worst16.get(i, 0.0), top16_rel(lg[s], r))
             feed[s] = ref[i][0][step]
     for i, s in enumerate(slots):
-        _log(dict(config=name, streams=B, slot=s, layers=cfg["layers"], max_rel_err=worst[i], tol=TOL))
+        _log(dict(config=name, streams=B, slot=s, layers=cfg["layers"], max_rel_err=worst[i], tol=TOL,
+                  top16_max_rel_err=worst16[i], tol_elem=TOL_ELEM))
         assert worst[i] <= TOL, f"{name} stream {i}: logit error {worst[i]:.4g} * max|logit| > {TOL}"
+        assert worst16[i] <= TOL_ELEM, f"{name} stream {i}: top-16 logit relative error {worst16[i]:.4g} > {TOL_ELEM}"
     for s in range(B):
         e.fill_kv(s, fill, params[s][1])
     got = e.generate([[p[0]] for p in params], n, start_pos=[fill] * B)
@@ -159,14 +175,17 @@ def test_deep_prefill_then_decode(ti, golden, name):
     prompt, ref, ref_lg = d["prompt"].tolist(), d["tokens"].tolist(), d["logits"]
     e = engine_for(ti, cfg, max_batch=1)
     e.synth(int(d["seed"][0]), 0.0)
-    worst = 0.0
+    worst = worst16 = 0.0
     for n in range(1, len(ref) + 1):   # logits of generated step n - 1 (each call prefills again)
         got, lg = e.generate([prompt], n, want_logits=True)
         r = ref_lg[n - 1].astype(np.float64)
         worst = max(worst, float(np.max(np.abs(lg[0].astype(np.float64) - r))) / float(np.max(np.abs(r))))
+        worst16 = max(worst16, top16_rel(lg[0], r))
     e.close()
-    _log(dict(config=name, case="prefill120+decode3", layers=cfg["layers"], max_rel_err=worst, tol=TOL))
+    _log(dict(config=name, case="prefill120+decode3", layers=cfg["layers"], max_rel_err=worst, tol=TOL,
+              top16_max_rel_err=worst16, tol_elem=TOL_ELEM))
     assert worst <= TOL, f"{name}: logit error {worst:.4g} * max|logit| > {TOL}"
+    assert worst16 <= TOL_ELEM, f"{name}: top-16 logit relative error {worst16:.4g} > {TOL_ELEM}"
     assert_greedy(got[0].tolist(), ref, ref_lg, f"{name} prefill")
 
 
@@ -187,16 +206,19 @@ def test_deep_prefill_512_row_chunks(ti, golden, name, rows):
     e = engine_for(ti, cfg, max_batch=1)
     e.synth(int(d["seed"][0]), 0.0)
     e.set_prefill(rows)
-    worst = 0.0
+    worst = worst16 = 0.0
     for n in range(1, len(ref) + 1):
         _, c0 = e.counters()
         got, lg = e.generate([prompt], n, want_logits=True)
         assert e.counters()[1] - c0 == (2 if rows == 512 else 1)   # 512 + 128 prompt rows, or 640
         r = ref_lg[n - 1].astype(np.float64)
         worst = max(worst, float(np.max(np.abs(lg[0].astype(np.float64) - r))) / float(np.max(np.abs(r))))
+        worst16 = max(worst16, top16_rel(lg[0], r))
     e.close()
-    _log(dict(config=name, case=f"prefill640(chunks of {rows})+decode3", layers=cfg["layers"], max_rel_err=worst, tol=TOL))
+    _log(dict(config=name, case=f"prefill640(chunks of {rows})+decode3", layers=cfg["layers"], max_rel_err=worst, tol=TOL,
+              top16_max_rel_err=worst16, tol_elem=TOL_ELEM))
     assert worst <= TOL, f"{name}: logit error {worst:.4g} * max|logit| > {TOL}"
+    assert worst16 <= TOL_ELEM, f"{name}: top-16 logit relative error {worst16:.4g} > {TOL_ELEM}"
     assert_greedy(got[0].tolist(), ref, ref_lg, f"{name} prefill 512-row chunks")
 
 
@@ -226,12 +248,15 @@ def _long_run(ti, golden, name, B, slot):
     for s in range(B):
         e.fill_kv(s, fill, params[s][1])
     feed = [p[0] for p in params]
-    curve, bad = [], []
+    curve, curve16, bad = [], [], []
     for step in range(n):
         lg = e.step(feed, [fill + step] * B)
         feed = [int(t) for t in np.argmax(lg, axis=1)]
         g = lg[slot].astype(np.float64)
         err = float(np.max(np.abs(g[top_i[step]] - top_v[step])))
+        curve16.append(float(np.max(np.abs(g[top_i[step]] - top_v[step]) / np.abs(top_v[step]))))
+        if curve16[-1] > TOL_ELEM:
+            bad.append(f"step {step}: top-16 logit relative error {curve16[-1]:.4g} > {TOL_ELEM}")
         if step in full:
             err = max(err, float(np.max(np.abs(g - full[step]))))
         curve.append(err / mx[step])
@@ -254,7 +279,8 @@ def _long_run(ti, golden, name, B, slot):
     c = np.array(curve)
     _log(dict(config=name, case=f"long{n}", streams=B, slot=slot, layers=cfg["layers"], max_rel_err=float(c.max()),
               err_by_16_steps=[round(float(c[i:i + 16].max()), 6) for i in range(0, n, 16)],
-              generate_matched=matched, first_near_tie=int(np.argmax(marg <= 3 * TOL * mx)), tol=TOL))
+              generate_matched=matched, first_near_tie=int(np.argmax(marg <= 3 * TOL * mx)), tol=TOL,
+              top16_max_rel_err=float(max(curve16)), tol_elem=TOL_ELEM))
     assert not bad, f"{name} long run: " + "; ".join(bad)
 
 

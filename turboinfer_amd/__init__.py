@@ -79,11 +79,10 @@ EXPORTED = [
     "ti_argmax_f32", "ti_engine_create", "ti_engine_destroy", "ti_engine_get_stream", "ti_engine_memory", "ti_engine_set_tensor",
     "ti_engine_synth", "ti_engine_fill_kv", "ti_engine_generate", "ti_engine_step", "ti_engine_compat_step",
     "ti_engine_replay_prepare", "ti_engine_set_prefill", "ti_engine_replay_run", "ti_engine_sync", "ti_engine_last_tokens",
-    "ti_engine_time_kernel", "ti_rope_table", "ti_sample_token", 
+    "ti_engine_time_kernel", "ti_engine_stamp_steps", "ti_rope_table", "ti_sample_token", 
     "ti_gemm_grid", "ti_engine_set_fold",
     "ti_attn_decode_partials", "ti_sample_device", "ti_sample_step", "ti_engine_generate_sampled",
     "ti_engine_beam_search", "ti_engine_serve", 
-    "ti_engine_set_pds", "ti_engine_pds_error", "ti_engine_pds_timestamps",
     "ti_wpack_q_host", "ti_engine_set_tensor_q", "ti_sample_workspace_bytes", "ti_sample_device_ws",
     "ti_wpack_q1_host", "ti_engine_set_tensor_q1", "ti_epilogue_bytes",
     "ti_sample_step_ws", "ti_hbm_calibrate", "ti_gemm_kernel_name",
@@ -154,10 +153,6 @@ def lib() -> C.CDLL:
                                                 C.POINTER(C.c_int)]
         if hasattr(L, "ti_attn_decode_partials"):
             L.ti_attn_decode_partials.argtypes = [vp, vp, vp, i64, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp]
-        if hasattr(L, "ti_engine_set_pds"):
-            L.ti_engine_set_pds.argtypes = [vp, i32, C.POINTER(C.c_int)]
-            L.ti_engine_pds_error.argtypes = [vp, C.POINTER(C.c_uint32)]
-            L.ti_engine_pds_timestamps.argtypes = [vp, vp, C.c_size_t]
         L.ti_step_begin.argtypes = [C.POINTER(StepArgs), vp]
         L.ti_matmul_f32.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, vp]
         L.ti_rms_norm_f32.argtypes = [vp, vp, vp, i32, i32, f32, vp]
@@ -197,6 +192,7 @@ def lib() -> C.CDLL:
         L.ti_engine_sync.argtypes = [vp]
         L.ti_engine_last_tokens.argtypes = [vp, i32, vp]
         L.ti_engine_time_kernel.argtypes = [vp, i32, i32, i32, i32, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.ti_engine_stamp_steps.argtypes = [vp, i32, i32, vp, vp, C.POINTER(C.c_int)]
         L.ti_hbm_calibrate.argtypes = [sz, i32, C.POINTER(C.c_double), C.POINTER(C.c_double), vp]
         L.ti_gemm_kernel_name.argtypes = [i32, i32, i32, i32, i32, C.c_char_p, i32]
         L.ti_rope_table.argtypes = [vp, i32, i32, f32, vp]
@@ -458,19 +454,6 @@ class Engine:
         check(lib().ti_engine_set_fold(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
         return bool(act.value)
 
-    def set_pds(self, on=None) -> bool:
-        """Deprecated (round 5: the persistent launch was removed): on=True raises,
-        off / query return False (ti_engine_set_pds)."""
-        act = C.c_int(0)
-        check(lib().ti_engine_set_pds(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
-        return bool(act.value)
-
-    def pds_error(self) -> int:
-        """Bit 0: a persistent launch's hand-off wait timed out."""
-        err = C.c_uint32(0)
-        check(lib().ti_engine_pds_error(self.h, C.byref(err)))
-        return int(err.value)
-
     def step(self, tokens, pos):
         t = np.ascontiguousarray(tokens, np.int32)
         p = np.ascontiguousarray(pos, np.int32)
@@ -501,6 +484,24 @@ class Engine:
         us, by = C.c_double(), C.c_double()
         check(lib().ti_engine_time_kernel(self.h, which, n_streams, kv_len, reps, C.byref(us), C.byref(by)))
         return us.value, by.value
+
+    STAMP_FIELDS = ("span_us", "period_us", "entry_skew_us", "wave_skew_us", "tail_us", "gap_us", "cu_shared_wgs")
+    STAMP_TAGS = ("begin", "qkv", "attention", "o", "gate_up", "down", "lm_head", "other")
+    STAMP_KINDS = ("other", "gemv", "attn", "step_begin", "rows", "tile", "rmsnorm", "mb")
+
+    def stamp_steps(self, steps=20, cap=4096):
+        """In-step launch timing of the replay step (ti_engine_stamp_steps): one dict per launch with
+        kind, tag, workgroups and the per-launch means of STAMP_FIELDS in us."""
+        info = np.zeros((cap, 3), np.int32)
+        t = np.zeros((cap, len(self.STAMP_FIELDS)), np.float64)
+        n = C.c_int(0)
+        check(lib().ti_engine_stamp_steps(self.h, steps, cap, _ptr(info), _ptr(t), C.byref(n)))
+        out = []
+        for i in range(min(n.value, cap)):
+            d = {"kind": self.STAMP_KINDS[info[i, 0]], "tag": self.STAMP_TAGS[info[i, 1]], "workgroups": int(info[i, 2])}
+            d.update({k: float(t[i, j]) for j, k in enumerate(self.STAMP_FIELDS)})
+            out.append(d)
+        return out
 
     def memory(self):
         w, k = C.c_size_t(), C.c_size_t()

@@ -374,7 +374,16 @@ class InferenceEngineImpl {
     if (!H || !L || !nh || !V || H % nh) throw std::runtime_error("InferenceEngine: incomplete model metadata");
     const size_t hd = H / nh;
     const int gpu = engine_option(md, "turboinfer.gpu_index", "TI_GPU_INDEX", 0);
-    if (m.num_tensors() == 0) return build_synthetic(md, c, gpu);
+    if (m.num_tensors() == 0) {
+      // a tensorless ModelData (what the reference's test programs build) runs the seeded synthetic
+      // model of that shape only when asked: otherwise a checkpoint that failed to load would decode
+      // plausible-looking tokens from random weights
+      if (engine_option(md, "turboinfer.synthetic", "TI_SYNTHETIC", 0) != 1)
+        throw std::runtime_error("InferenceEngine: the model has metadata but no tensors (set "
+                                 "extra_params[\"turboinfer.synthetic\"] = \"1\" or TI_SYNTHETIC=1 for the "
+                                 "seeded synthetic model of this shape)");
+      return build_synthetic(md, c, gpu);
+    }
     const core::Tensor* q0 = layer_tensor(m, 0, "self_attn.q_proj.weight", "attention.q_proj.weight");
     const core::Tensor* k0 = layer_tensor(m, 0, "self_attn.k_proj.weight", "attention.k_proj.weight");
     const core::Tensor* up0 = layer_tensor(m, 0, "mlp.up_proj.weight", "feed_forward.w1.weight");

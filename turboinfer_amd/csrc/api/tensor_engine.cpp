@@ -6,6 +6,7 @@
 // the engine stream, download.  No CPU arithmetic path exists.
 #include "turboinfer/core/tensor_engine.hpp"
 
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <sstream>
@@ -26,8 +27,9 @@ using api::DeviceBuffer;
 class TensorEngineImpl {
  public:
   ti_stream_t stream = nullptr;
-  explicit TensorEngineImpl(int device) {
-    check(ti_init(device), "ti_init");
+  int device = 0;
+  explicit TensorEngineImpl(int dev) : device(dev) {
+    check(ti_init(dev), "ti_init");
     check(ti_stream_create(&stream), "ti_stream_create");
   }
   ~TensorEngineImpl() {
@@ -72,7 +74,14 @@ TensorEngine::TensorEngine(ComputeDevice device) : device_(device) {
   if (ti_device_count(&count) != TI_OK || count < 1)
     throw std::runtime_error("GPU device requested but not available: no gfx950 (MI355X) device is visible");
   device_ = ComputeDevice::kGPU;
-  impl_ = std::make_unique<TensorEngineImpl>(0);
+  // the device ordinal: TI_GPU_INDEX, as InferenceEngine reads it when its model's extra_params do
+  // not name one (the reference binds device 0, tensor_engine.cpp:425-487)
+  int gpu = 0;
+  if (const char* v = std::getenv("TI_GPU_INDEX")) gpu = std::atoi(v);
+  if (gpu < 0 || gpu >= count)
+    throw std::runtime_error("TensorEngine: TI_GPU_INDEX=" + std::to_string(gpu) + " but " + std::to_string(count) +
+                             " device(s) are visible");
+  impl_ = std::make_unique<TensorEngineImpl>(gpu);
 }
 
 TensorEngine::~TensorEngine() = default;
@@ -92,7 +101,8 @@ std::string TensorEngine::device_info() const {
     ti_device_name(d, name, sizeof(name));
     os << "  GPU " << d << ": " << name << "\n";
   }
-  os << "  Active Device: " << device_to_string(device_) << " (HIP, gfx950 kernels)";
+  os << "  Active Device: " << device_to_string(device_) << " (HIP device " << (impl_ ? impl_->device : 0)
+     << ", gfx950 kernels)";
   return os.str();
 }
 

@@ -226,6 +226,20 @@ struct DeviceScope {
   DeviceScope& operator=(const DeviceScope&) = delete;
 };
 
+// In-step launch stamps (ti_engine_stamp_steps): while a stamped step graph is being captured on this
+// thread, every decode launcher asks ti_stamp_next for its workgroups' slot (kernels/common.hpp
+// stamp_end: kStampWords = 16 words per workgroup) and the launch's kind / tag / grid are recorded.
+constexpr int kStampWords = 16;
+struct StampCtx {
+  bool on = false;
+  unsigned long long* base = nullptr;   // NULL: the sizing pass (record only)
+  int tag = TI_STAMP_TAG_OTHER;
+  std::vector<int32_t> info;            // [launch][3] kind, tag, workgroups (0 = unstamped)
+  std::vector<size_t> offs;             // word offset of each launch's slot (second pass)
+};
+thread_local StampCtx g_stamp;
+inline void stamp_tag(int t) { g_stamp.tag = t; }
+
 int validate(const ti_engine_config& c) {
   if (c.vocab < 1 || c.hidden < 1 || c.layers < 0 || c.inter < 1 || c.max_seq < 1 || c.max_batch < 1)
     return ti_set_error(TI_ERR_ARG, "ti_engine_create: non-positive size in config");
@@ -367,6 +381,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     sa.fold_x = e->fx;
     sa.fold_ss = e->ss;
   }
+  stamp_tag(TI_STAMP_TAG_BEGIN);
   TI_TRY(ti_step_begin(&sa, e->s));
   int n_ss = 1;   // partials the last producer wrote (step_begin: one)
   // producer side (RESID epilogue); n_next: output width of the call that consumes the fold
@@ -430,18 +445,24 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     eo.out = e->h;
     fold_into(eo, L.ffn_norm, L.gu.N);
     if (part) {   // the O projection merges the attention's splits while staging its input
+      stamp_tag(TI_STAMP_TAG_QKV);
       TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));
+      stamp_tag(TI_STAMP_TAG_ATTN);
       TI_TRY(ti_attn_decode_partials(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M, c.heads, c.kv_heads,
                                      c.head_dim, e->splits_for(M), e->part_o, e->part_ml, e->s));
       eo.ss_in = e->part_ml;
       eo.n_ss = e->splits_for(M);
       eo.head_dim = c.head_dim;
+      stamp_tag(TI_STAMP_TAG_O);
       TI_TRY(gemm(L.o, e->part_o, TI_X_ATTN_SPLITS, qd, 2, nullptr, eo, 4, false));
     } else {
+      stamp_tag(TI_STAMP_TAG_QKV);
       TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));
+      stamp_tag(TI_STAMP_TAG_ATTN);
       TI_TRY((pk ? ti_attn_decode_packed : ti_attn_decode)(e->q, L.kc, L.vc, e->kv_stride, c.max_seq, e->pos, M,
                                                            c.heads, c.kv_heads, c.head_dim, e->splits_for(M), e->ws,
                                                            e->attn, e->s));
+      stamp_tag(TI_STAMP_TAG_O);
       TI_TRY(gemm(L.o, e->attn, pk ? TI_X_F16_PACKED : TI_X_F16, qd, 2, nullptr, eo, 4, false));
     }
 
@@ -450,6 +471,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     eg.ldo = I;
     eg.out = e->act;
     eg.out_packed = pk;
+    stamp_tag(TI_STAMP_TAG_GATE_UP);
     TI_TRY(gemm(L.gu, e->h, TI_X_F32_RMSNORM, H, 4, L.ffn_norm, eg, 2, false));
 
     ti_epilogue ed{};
@@ -457,6 +479,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     ed.ldo = H;
     ed.out = e->h;
     fold_into(ed, next_norm(l + 1), next_n(l + 1));
+    stamp_tag(TI_STAMP_TAG_DOWN);
     TI_TRY(gemm(L.down, e->act, pk ? TI_X_F16_PACKED : TI_X_F16, I, 2, nullptr, ed, 4, false));
   }
   ti_epilogue el{};
@@ -466,7 +489,9 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   el.argmax = e->argmax;
   el.step_ctr = e->step_ctr;
   el.advance = advance;
+  stamp_tag(TI_STAMP_TAG_LM_HEAD);
   TI_TRY(gemm(e->lm, e->h, TI_X_F32_RMSNORM, H, 4, e->out_norm, el, 4, true));
+  stamp_tag(TI_STAMP_TAG_OTHER);
   if (e->samp_on)   // sample_next_token on the device; its key feeds the token back (ti_hip.h)
     TI_TRY(ti_sample_step_ws(e->logits, V, M, V, e->samp_t, e->samp_k, e->samp_p, e->draws, e->draw_cap, e->step_ctr,
                              advance, e->n_in, e->argmax, e->lps, e->samp_ws, e->s));
@@ -1496,28 +1521,6 @@ int ti_engine_set_fold(ti_engine* e, int on, int* active) {
   return TI_OK;
 }
 
-
-// The persistent decode launch (round 4, pds.hip) was removed from the product in round 5: it
-// lost to the per-layer graph at every shape.  The entry points stay for one release:
-// off is accepted, on reports TI_ERR_UNSUPPORTED.
-int ti_engine_set_pds(ti_engine* e, int on, int* active) {
-  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_pds: null");
-  if (active) *active = 0;
-  if (on > 0) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_set_pds: persistent decode was removed (DESIGN 4.15)");
-  return TI_OK;
-}
-
-int ti_engine_pds_timestamps(ti_engine* e, unsigned long long* out, size_t) {
-  if (!e || !out) return ti_set_error(TI_ERR_ARG, "ti_engine_pds_timestamps: null");
-  return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_pds_timestamps: persistent decode was removed (DESIGN 4.15)");
-}
-
-int ti_engine_pds_error(ti_engine* e, uint32_t* err) {
-  if (!e || !err) return ti_set_error(TI_ERR_ARG, "ti_engine_pds_error: null");
-  *err = 0;
-  return TI_OK;
-}
-
 int ti_engine_last_tokens(ti_engine* e, int n, int32_t* tokens) {
   if (!e || !tokens || n < 1 || n > e->c.max_batch) return ti_set_error(TI_ERR_ARG, "ti_engine_last_tokens");
   DeviceScope bind_(e);
@@ -1674,3 +1677,149 @@ int ti_engine_time_kernel(ti_engine* e, int which, int n, int kv_len, int reps, 
 }
 
 }  // extern "C"
+
+
+// ------------------------------------------------------------- in-step launch stamps
+unsigned long long* ti_stamp_next(int kind, long grid) {
+  StampCtx& c = g_stamp;
+  if (!c.on) return nullptr;
+  const size_t i = c.info.size() / 3;
+  const bool stamped = grid > 0 && kind != TI_STAMP_KIND_RMSNORM && kind != TI_STAMP_KIND_OTHER;
+  c.info.insert(c.info.end(), {(int32_t)kind, (int32_t)c.tag, stamped ? (int32_t)grid : 0});
+  if (!c.base || i >= c.offs.size() || !stamped) return nullptr;
+  return c.base + c.offs[i];
+}
+
+namespace {
+
+// Capture the replay step graph with the stamp context on (base NULL: record only).
+int capture_stamped(ti_engine* e, unsigned long long* base, const std::vector<size_t>& offs, std::vector<int32_t>& info,
+                    hipGraphExec_t* out) {
+  StampCtx& c = g_stamp;
+  c = StampCtx{};
+  c.on = true;
+  c.base = base;
+  c.offs = offs;
+  TI_TRY(ti_gemm_prepare());
+  hipError_t eb = hipStreamBeginCapture(e->s, hipStreamCaptureModeThreadLocal);
+  if (eb != hipSuccess) {
+    c = StampCtx{};
+    return ti_check_hip(eb, "hipStreamBeginCapture");
+  }
+  const int rc = enqueue_step(e, e->replay_M, 0);
+  hipGraph_t g = nullptr;
+  const hipError_t ec = hipStreamEndCapture(e->s, &g);
+  info = c.info;
+  c = StampCtx{};
+  if (rc != TI_OK) {
+    if (g) hipGraphDestroy(g);
+    return rc;
+  }
+  E_CHECK(ec, "hipStreamEndCapture");
+  if (!out) {
+    hipGraphDestroy(g);
+    return TI_OK;
+  }
+  const hipError_t ei = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  E_CHECK(ei, "hipGraphInstantiate");
+  return TI_OK;
+}
+
+}  // namespace
+
+int ti_engine_stamp_steps(ti_engine* e, int steps, int cap, int32_t* info_out, double* t_out, int* n_launch) {
+  if (!e || e->replay_M < 1 || steps < 1 || cap < 1 || !info_out || !t_out || !n_launch)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_stamp_steps: call ti_engine_replay_prepare first; steps, cap >= 1");
+  DeviceScope bind_(e);
+  TI_TRY(ti_stream_sync(e->s));
+  // pass 1: the launch list and grids; pass 2: the graph with each stamped launch's slot
+  std::vector<int32_t> info, info2;
+  TI_TRY(capture_stamped(e, nullptr, {}, info, nullptr));
+  const size_t n = info.size() / 3;
+  std::vector<size_t> offs(n);
+  size_t words = 0;
+  for (size_t i = 0; i < n; ++i) {
+    offs[i] = words;
+    words += (size_t)info[3 * i + 2] * kStampWords;
+  }
+  if (words == 0) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_stamp_steps: no stamped launch in the step");
+  void* buf = nullptr;
+  TI_TRY(ti_malloc(&buf, words * 8));
+  unsigned long long* st = static_cast<unsigned long long*>(buf);
+  hipGraphExec_t g = nullptr;
+  int rc = capture_stamped(e, st, offs, info2, &g);
+  if (rc == TI_OK && info2 != info) rc = ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_stamp_steps: the two captures differ");
+  std::vector<unsigned long long> h(words);
+  std::vector<double> acc(n * TI_STAMP_FIELDS, 0.0);
+  constexpr double kUs = 0.01;   // s_memrealtime: 100 MHz
+  for (int it = 0; rc == TI_OK && it <= steps; ++it) {   // it 0: untimed
+    hipError_t he = hipMemsetAsync(st, 0, words * 8, e->s);
+    if (he == hipSuccess) he = hipGraphLaunch(g, e->s);
+    if (he == hipSuccess) he = hipMemcpyAsync(h.data(), st, words * 8, hipMemcpyDeviceToHost, e->s);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->s);
+    if (he != hipSuccess) {
+      rc = ti_check_hip(he, "ti_engine_stamp_steps: replay");
+      break;
+    }
+    if (it == 0) continue;
+    // per launch: first / last entry, last end, median workgroup end, mean in-workgroup wave skew
+    std::vector<double> first(n, 0.0), last_end(n, 0.0);
+    for (size_t i = 0; i < n; ++i) {
+      const int wgs = info[3 * i + 2];
+      if (wgs == 0) continue;
+      unsigned long long f = ~0ull, le = 0, lent = 0;
+      double wskew = 0.0;
+      std::vector<unsigned long long> ends, cus;   // cus: (XCC, SE / SH / CU) of each workgroup
+      ends.reserve(wgs);
+      for (int w = 0; w < wgs; ++w) {
+        const unsigned long long* p = h.data() + offs[i] + (size_t)w * kStampWords;
+        if (p[0]) {
+          f = std::min(f, p[0]);
+          lent = std::max(lent, p[0]);
+        }
+        if (p[kStampWords - 1]) cus.push_back((p[kStampWords - 1] & 0x7FFFFFFF00000000ull) | (p[kStampWords - 1] & 0xFF00ull));
+        unsigned long long mn = ~0ull, mx = 0;
+        for (int k = 1; k < kStampWords - 1; ++k)
+          if (p[k]) {
+            mn = std::min(mn, p[k]);
+            mx = std::max(mx, p[k]);
+          }
+        if (mx) {
+          ends.push_back(mx);
+          le = std::max(le, mx);
+          wskew += (double)(mx - mn);
+        }
+      }
+      if (f == ~0ull || ends.empty()) continue;
+      std::nth_element(ends.begin(), ends.begin() + ends.size() / 2, ends.end());
+      const unsigned long long med = ends[ends.size() / 2];
+      first[i] = (double)f;
+      last_end[i] = (double)le;
+      double* a = acc.data() + i * TI_STAMP_FIELDS;
+      a[0] += (double)(le - f) * kUs;
+      a[2] += (double)(lent - f) * kUs;
+      a[3] += wskew / (double)ends.size() * kUs;
+      a[4] += (double)(le - med) * kUs;
+      std::sort(cus.begin(), cus.end());
+      a[6] += (double)(cus.end() - std::unique(cus.begin(), cus.end())) ;   // workgroups on an already-used CU
+    }
+    for (size_t i = 0; i < n; ++i) {
+      if (!first[i]) continue;
+      size_t j = i + 1;
+      while (j < n && !first[j]) ++j;
+      double* a = acc.data() + i * TI_STAMP_FIELDS;
+      a[1] += j < n ? (first[j] - first[i]) * kUs : (last_end[i] - first[i]) * kUs;
+      a[5] += j < n ? (first[j] - last_end[i]) * kUs : 0.0;
+    }
+  }
+  if (g) hipGraphExecDestroy(g);
+  ti_free(buf);
+  TI_TRY(rc);
+  *n_launch = (int)n;
+  for (size_t i = 0; i < n && (int)i < cap; ++i) {
+    for (int k = 0; k < 3; ++k) info_out[3 * i + k] = info[3 * i + k];
+    for (int k = 0; k < TI_STAMP_FIELDS; ++k) t_out[i * TI_STAMP_FIELDS + k] = acc[i * TI_STAMP_FIELDS + k] / steps;
+  }
+  return TI_OK;
+}

@@ -29,6 +29,7 @@ struct AttnArgs {
   // h >> kv_shift.  The G q-heads of a kv-head then stream its K/V from the L2 / MALL in parallel
   // instead of one workgroup serving all of them (one stream, partials mode: DESIGN 4.16).
   int32_t kv_shift;
+  unsigned long long* stamp;   // in-step launch stamps (common.hpp stamp_end), NULL in product launches
 };
 
 #ifndef TI_ATTN_RING

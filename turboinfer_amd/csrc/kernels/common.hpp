@@ -187,7 +187,39 @@ __host__ __device__ __forceinline__ size_t tile_index(int nt, int kt, int KT) {
   return (size_t)nt * KT + kt;
 }
 
+// ---------------------------------------------------------------- in-step launch stamps
+// ti_engine_stamp_steps (ti_engine.h): the step graph captured with every decode kernel writing,
+// per workgroup, wave 0's entry time and each wave's end time (s_memrealtime, 100 MHz) with plain
+// vector stores into a host-owned device buffer.  `st` is NULL in every product launch (one scalar
+// branch at the kernel end).
+// per workgroup: [0] entry of wave 0, [1 + w] end of wave w (w < 14), [15] where wave 0 ran:
+// XCC_ID << 32 | HW_ID (SE / SH / CU fields: which CU; two workgroups of a launch on one CU show here)
+constexpr int kStampWords = 16;
+__device__ __forceinline__ unsigned long long stamp_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void stamp_end(unsigned long long* st, unsigned long long t_entry) {
+  if (st == nullptr) return;
+  if ((threadIdx.x & 63) == 0) {
+    const unsigned wave = threadIdx.x >> 6;
+    const size_t wg = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
+    unsigned long long* p = st + wg * kStampWords;
+    if (wave < kStampWords - 2) p[1 + wave] = stamp_now();
+    if (wave == 0) {
+      p[0] = t_entry;
+      // s_getreg_b32 HW_REG_HW_ID (4) and HW_REG_XCC_ID (20), all 32 bits
+      const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11)), xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+      p[kStampWords - 1] = ((unsigned long long)xcc << 32) | hw | (1ull << 63);
+    }
+  }
+}
+// kinds reported with each stamped launch
+enum { STAMP_OTHER = 0, STAMP_GEMV = 1, STAMP_ATTN = 2, STAMP_BEGIN = 3, STAMP_ROWS = 4, STAMP_TILE = 5,
+       STAMP_RMSNORM = 6, STAMP_MB = 7 };
+
 }  // namespace ti
+
+// The stamp buffer slot of the next launch (host side, engine.cpp): NULL unless this thread is
+// capturing a stamped step graph (ti_engine_stamp_steps) and the grid fits the buffer.
+extern "C++" unsigned long long* ti_stamp_next(int kind, long grid);
 
 // error helper shared by the launchers (defined in host/capi.cpp)
 extern "C++" int ti_set_error(int code, const char* fmt, ...);

@@ -80,6 +80,7 @@ struct GemvArgs {
   float eps;
   int32_t x_kind, ldx, M, N, K;
   ti_epilogue epi;
+  unsigned long long* stamp;   // in-step launch stamps (common.hpp stamp_end), NULL in product launches
 };
 
 __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
@@ -332,6 +333,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
                                                                    const void* p_x, const float* p_aux, int p_mgk,
                                                                    int p_N, int p_kx, int p_ldo, const float* p_pre,
                                                                    GemvArgs a) {
+  const unsigned long long t_entry = stamp_now();
   const unsigned bid = blockIdx.x;
   a.tiles = p_tiles;
   a.scales = p_scales;
@@ -799,6 +801,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
     }
   }
   GEMV_TS(4);
+  stamp_end(a.stamp, t_entry);
 }
 
 // ================================================================= batched rows
@@ -912,7 +915,15 @@ __device__ __forceinline__ void dma_1k(const void* src_lane, void* lds_wave) {  
 }
 
 template <int MB, int NTL>
+__device__ __forceinline__ void gemv_mb_body(const GemvArgs a, int grid);
+template <int MB, int NTL>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemv_mb_kernel(const GemvArgs a, int grid) {
+  const unsigned long long t_entry = stamp_now();
+  gemv_mb_body<MB, NTL>(a, grid);
+  stamp_end(a.stamp, t_entry);
+}
+template <int MB, int NTL>
+__device__ __forceinline__ void gemv_mb_body(const GemvArgs a, int grid) {
   constexpr int XDMA = 2 * 16 * MB / kGemvWaves;   // x-chunk DMA instructions per wave (2 per row)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KT = a.K >> 7, NT = a.N >> 4, NC = (KT + kGemvWaves - 1) / kGemvWaves;
@@ -1058,7 +1069,15 @@ struct MbrChunk {       // one chunk's operands of one wave
 // k-tile straight into registers, one chunk ahead, so no barrier is needed until the end;
 // at <= 16 rows this beats the LDS-staged kernel (bench.py --batch 8/16).
 template <int MB, int NTL>
+__device__ __forceinline__ void gemv_mbr_body(const GemvArgs a, int grid);
+template <int MB, int NTL>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemv_mbr_kernel(const GemvArgs a, int grid) {
+  const unsigned long long t_entry = stamp_now();
+  gemv_mbr_body<MB, NTL>(a, grid);
+  stamp_end(a.stamp, t_entry);
+}
+template <int MB, int NTL>
+__device__ __forceinline__ void gemv_mbr_body(const GemvArgs a, int grid) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KT = a.K >> 7, NT = a.N >> 4, NC = (KT + kGemvWaves - 1) / kGemvWaves;
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, kq = lane >> 4;
@@ -1219,8 +1238,16 @@ __device__ __forceinline__ void fold_rms_finish(const GemvArgs& a, const float* 
 // G32: group-32 int4 tiles (GGUF Q4_0 blocks, TI_BITS_G32; row-major x only): MFMA step s4 of a
 // k-tile reads k-chunk 32 s4 + 8 kq and is scaled by its own block's scale (4 per tile row and
 // k-tile), as in the fused and tile kernels.
+template <int MB, int NTL, int RG, bool XP, bool G32>
+__device__ __forceinline__ void gemm_rows_body(const GemvArgs a, int n_cg, int n_rb);
 template <int MB, int NTL, int RG, bool XP, bool G32 = false>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemm_rows_kernel(const GemvArgs a, int n_cg, int n_rb) {
+  const unsigned long long t_entry = stamp_now();
+  gemm_rows_body<MB, NTL, RG, XP, G32>(a, n_cg, n_rb);
+  stamp_end(a.stamp, t_entry);
+}
+template <int MB, int NTL, int RG, bool XP, bool G32>
+__device__ __forceinline__ void gemm_rows_body(const GemvArgs a, int n_cg, int n_rb) {
   static_assert(!(XP && G32), "group-32 rows take row-major activations");
   constexpr int SG = G32 ? 4 : 1;   // scales per tile row and k-tile
   constexpr int GW = RowsCfg<MB, NTL, RG>::kGroupWaves, WD = RowsCfg<MB, NTL, RG>::kWD;
@@ -1655,8 +1682,16 @@ __device__ __forceinline__ void tile_epilogue_lds(const GemvArgs& a, int tn, int
 #endif
 __device__ __forceinline__ int tile_swz(int row) { return TI_TILE_SWZ4 ? (row + 4) & 15 : row & 15; }
 
+template <int TPW, bool G32, int WMR, int XB, int RB>
+__device__ __forceinline__ void gemm_tile_body(const GemvArgs a, int n_cb, int n_rb, int n_ks);
 template <int TPW, bool G32 = false, int WMR = 2, int XB = 2, int RB = 4>
 __global__ __launch_bounds__(kGemvThreads, 1) void gemm_tile_kernel(const GemvArgs a, int n_cb, int n_rb, int n_ks) {
+  const unsigned long long t_entry = stamp_now();
+  gemm_tile_body<TPW, G32, WMR, XB, RB>(a, n_cb, n_rb, n_ks);
+  stamp_end(a.stamp, t_entry);
+}
+template <int TPW, bool G32, int WMR, int XB, int RB>
+__device__ __forceinline__ void gemm_tile_body(const GemvArgs a, int n_cb, int n_rb, int n_ks) {
   constexpr int WCOL = kGemvWaves / WMR, BM = 16 * RB * WMR;   // column-waves, rows per workgroup
   constexpr int ND = BM / 32;                                  // activation DMA instructions per wave and group
   static_assert(RB == 4 || (RB == 2 && WMR == 1), "32-row waves: one row-wave per workgroup");
@@ -2129,8 +2164,20 @@ __host__ inline int gemv_xmode(int x_kind, int M, int K) {
   return M == 1 && (K >> 3) <= kGemvThreads ? XM_NORM1 : XM_NORM;
 }
 
+// Dynamic LDS floor of the fused kernel's launch (A/B knob TI_GEMV_LDS_FLOOR, bytes): an image
+// above half the CU's 160 KiB admits one workgroup per CU whatever the registers allow.
+__host__ inline int gemv_lds_floor() {
+  static const int v = [] {
+    const char* e = getenv("TI_GEMV_LDS_FLOOR");
+    const int b = e ? atoi(e) : 0;
+    return b < 0 ? 0 : (b > 160 * 1024 ? 160 * 1024 : b);
+  }();
+  return v;
+}
+
 template <int BITS, bool G32 = false, bool AFF = false>
 static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid) {
+  if (lds < gemv_lds_floor()) lds = gemv_lds_floor();
   const float* pre = a.epi.kind == TI_EPI_RESID_F32 ? (const float*)a.epi.out
                      : a.epi.kind == TI_EPI_QKV_ROPE_KV ? (const float*)a.epi.pos : (const float*)a.x;
   const int xm = gemv_xmode(a.x_kind, a.M, a.K);
@@ -2462,6 +2509,7 @@ extern "C" int ti_rmsnorm_f16(const float* x, int ldx, const float* w, float eps
   if (!x || !w || !y) return ti_set_error(TI_ERR_ARG, "ti_rmsnorm_f16: null pointer");
   if (M < 1 || K < 8 || (K & 7) || ldx < K || ldy < K)
     return ti_set_error(TI_ERR_ARG, "ti_rmsnorm_f16: bad shape (M=%d K=%d ldx=%d ldy=%d)", M, K, ldx, ldy);
+  ti_stamp_next(ti::STAMP_RMSNORM, 0);   // (unstamped; keeps the stamped step's launch list whole)
   hipLaunchKernelGGL(ti::rmsnorm_f16_kernel, dim3(M), dim3(ti::kGemvThreads), 0, (hipStream_t)stream, x, ldx, w, eps,
                      y, ldy, K, 0);
   TI_LAUNCH_CHECK("rmsnorm_f16_kernel");
@@ -2473,6 +2521,7 @@ extern "C" int ti_rmsnorm_f16_packed(const float* x, int ldx, const float* w, fl
   if (!x || !w || !y) return ti_set_error(TI_ERR_ARG, "ti_rmsnorm_f16_packed: null pointer");
   if (M < 1 || K < 128 || (K & 127) || ldx < K)
     return ti_set_error(TI_ERR_ARG, "ti_rmsnorm_f16_packed: bad shape (M=%d K=%d ldx=%d)", M, K, ldx);
+  ti_stamp_next(ti::STAMP_RMSNORM, 0);   // (unstamped; keeps the stamped step's launch list whole)
   hipLaunchKernelGGL(ti::rmsnorm_f16_kernel, dim3(M), dim3(ti::kGemvThreads), 0, (hipStream_t)stream, x, ldx, w, eps,
                      y, K, K, K >> 7);
   TI_LAUNCH_CHECK("rmsnorm_f16_kernel");
@@ -2632,6 +2681,10 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   a.N = N;
   a.K = K;
   a.epi = *epi;
+  {   // workgroups of the launch below (stamp buffer sizing)
+    const long wgs = tile ? grid : rows ? (long)((grid + 7) / 8 * 8) * r_rb : grid;
+    a.stamp = ti_stamp_next(tile ? STAMP_TILE : rows ? STAMP_ROWS : batched ? STAMP_MB : STAMP_GEMV, wgs);
+  }
   hipStream_t s = (hipStream_t)stream;
   if (tile) {
     const void* f = tile_fn(tpw, g32, wmr, xbuf, trb);

@@ -10,7 +10,13 @@ namespace ti {
 // One block per stream m.  The decode loop runs entirely on the device: the token of
 // step s is the prompt token while s < n_in[m], else the previous step's greedy argmax
 // (the key packs (value, 0xFFFFFFFF - index), so the max is the lowest-index maximum).
-__global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a) {
+__device__ __forceinline__ void step_begin_body(const ti_step_args a);
+__global__ __launch_bounds__(256) void step_begin_kernel(const ti_step_args a, unsigned long long* stamp) {
+  const unsigned long long t_entry = stamp_now();
+  step_begin_body(a);
+  stamp_end(stamp, t_entry);
+}
+__device__ __forceinline__ void step_begin_body(const ti_step_args a) {
   __shared__ int s_tok;
   const int m = blockIdx.x, tid = threadIdx.x;
   // With hidden % 8 == 0 (<= 8192): the embedding row moves in 16-byte pieces, all
@@ -264,7 +270,8 @@ extern "C" int ti_step_begin(const ti_step_args* a, ti_stream_t stream) {
   if (a->n_in && !a->in_tokens) return ti_set_error(TI_ERR_ARG, "ti_step_begin: in_tokens required");
   if (a->fold_x && (!a->fold_w || !a->fold_ss || a->placeholder_first >= 0))
     return ti_set_error(TI_ERR_ARG, "ti_step_begin: fold_x needs fold_w, fold_ss and the embedding gather");
-  hipLaunchKernelGGL(step_begin_kernel, dim3(a->M), dim3(256), 0, (hipStream_t)stream, *a);
+  hipLaunchKernelGGL(step_begin_kernel, dim3(a->M), dim3(256), 0, (hipStream_t)stream, *a,
+                     ti_stamp_next(STAMP_BEGIN, a->M));
   TI_LAUNCH_CHECK("step_begin_kernel");
   return TI_OK;
 }

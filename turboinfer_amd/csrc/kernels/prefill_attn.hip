@@ -334,8 +334,12 @@ __global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const 
                                                                  float scale, uint16_t* __restrict__ out) {
   constexpr int HD = 128, DV = HD / 16, KW = HD / 32, NB = 2, BI = NB * HALVES;   // BI: blocks per iteration
   static_assert(R % BI == 0 && R >= 2 * BI, "ring: whole iterations, one in flight beside the one computed");
-  __shared__ __attribute__((aligned(16))) uint16_t sk[R][16 * HD];
-  __shared__ __attribute__((aligned(16))) uint16_t sv[R][16 * HD];
+  // K and V rings in ONE array: the halves' merge at the end reuses it as scratch (4 query blocks x
+  // 64 lanes x (4 DV + 2) floats), which is larger than the K ring alone
+  __shared__ __attribute__((aligned(16))) uint16_t skv[2][R][16 * HD];
+  static_assert(HALVES == 1 || 4 * 64 * (4 * DV + 2) * sizeof(float) <= sizeof(skv), "halves' merge scratch");
+  auto& sk = skv[0];
+  auto& sv = skv[1];
   __shared__ int s_kmax[4];
   const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), qw = wave & 3, half = wave >> 2;
@@ -520,7 +524,7 @@ __global__ __launch_bounds__(256 * HALVES, 1) void attn_prefill_wg_kernel(const 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if constexpr (HALVES == 2) {   // half 1 hands (m, l, O) to half 0 through the ring's LDS
-    float* xs = (float*)&sk[0][0] + (size_t)qw * 64 * (4 * DV + 2);
+    float* xs = (float*)&skv[0][0][0] + (size_t)qw * 64 * (4 * DV + 2);   // (within skv: static_assert above)
     if (half == 1) {
 #pragma unroll
       for (int t = 0; t < DV; ++t) *(f32x4*)(xs + (4 * t) * 64 + 4 * lane) = acc[t];

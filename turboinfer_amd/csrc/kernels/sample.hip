@@ -478,6 +478,7 @@ static int sample_launch(ti::SampArgs a, int M, ti_stream_t stream) {
     hipLaunchKernelGGL(ti::sample_kernel<false>, dim3(M), dim3(ti::kSampThreads), 0, (hipStream_t)stream, a);
   }
   TI_LAUNCH_CHECK("sample_kernel");
+  ti_stamp_next(ti::STAMP_OTHER, 0);   // (unstamped; keeps the stamped step's launch list whole)
   return TI_OK;
 }
 
