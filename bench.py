@@ -217,6 +217,7 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0x7157)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--stamp-steps", type=int, default=20, help="stamped step replays for the in-step roofline")
     ap.add_argument("--attn-splits", type=int, default=0, help="0 = the engine's policy")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU-only rehearsal of the replica launch / barrier / max-over-ranks path: no GPU, "
@@ -297,24 +298,56 @@ def main() -> int:
             xk = T.X_F16_PACKED if bits == 4 and lib.ti_gemm_packed_rows(bits, B) else T.X_F16
         return T.gemm_kernel_name(bits, xk, B, N_, K_)
 
+    # In-step timing: the replay step graph captured with per-workgroup
+    # s_memrealtime stamps (ti_engine_stamp_steps).  A launch's duration is its period in the step:
+    # its first workgroup's entry -> the next launch's first entry (its boundary included; the
+    # periods of a step add up to the step), averaged over the class's launches and `stamp_steps`
+    # replays -- what a kernel trace's dispatch-to-completion duration measures.  The in-kernel span
+    # (first entry -> last wave end) and the isolated class timing (ti_engine_time_kernel: graphs of
+    # one class's launches; it also gives each class's algorithmic bytes) are reported beside it.
+    stamps = e.stamp_steps(args.stamp_steps)
+    in_step = {}
+    for d in stamps:
+        if d["workgroups"] == 0:
+            continue
+        c = in_step.setdefault(d["tag"], {"n": 0, "span": 0.0, "period": 0.0, "gap": 0.0, "cu_shared": 0.0})
+        c["n"] += 1
+        c["span"] += d["span_us"]
+        c["period"] += d["period_us"]
+        c["gap"] += d["gap_us"]
+        c["cu_shared"] += d["cu_shared_wgs"]
+    tag_of = {"qkv": "qkv", "o": "o", "gate_up": "gate_up", "down": "down", "lm_head": "lm_head", "attention": "attention"}
     per = {}
-    gemv_bytes = gemv_us = 0.0
+    gemv_bytes = gemv_us = gemv_iso_us = gemv_span_us = 0.0
     n_launch = 0
     kernels_used = {}
-    for w, name in enumerate(names):
-        us, by = e.time_kernel(w, B, L, args.kernel_reps)
-        cnt = 1 if name == "lm_head" else layers
-        kname = class_kernel(name)
-        per[name] = {"avg_us": round(us, 3), "bytes": int(by), "GBps": round(by / us / 1e3, 1), "kernel": kname}
+    for w, name in enumerate(names + ["attention"]):
+        iso_us, by = e.time_kernel(w, B, L, args.kernel_reps)
+        c = in_step[tag_of[name]]
+        us = c["period"] / c["n"]
+        kname = "attn_split_kernel" if name == "attention" else class_kernel(name)
+        per[name] = {"avg_us": round(us, 3), "bytes": int(by), "GBps": round(by / us / 1e3, 1), "kernel": kname,
+                     "in_step_launches": c["n"], "span_us": round(c["span"] / c["n"], 3),
+                     "gap_us": round(c["gap"] / c["n"], 3), "cu_shared_wgs": round(c["cu_shared"] / c["n"], 2),
+                     "isolated_us": round(iso_us, 3)}
+        if name == "attention":
+            break
+        cnt = c["n"]
         kernels_used.setdefault(kname, []).append(name)
         gemv_bytes += by * cnt
         gemv_us += us * cnt
+        gemv_iso_us += iso_us * cnt
+        gemv_span_us += c["span"]
         n_launch += cnt
-    att_us, att_bytes = e.time_kernel(5, B, L, args.kernel_reps)
-    per["attention"] = {"avg_us": round(att_us, 3), "bytes": int(att_bytes), "GBps": round(att_bytes / att_us / 1e3, 1),
-                        "kernel": "attn_split_kernel"}
+    att_us, att_bytes = per["attention"]["avg_us"], per["attention"]["bytes"]
     dom = {"kernel": " + ".join(f"{k} ({', '.join(v)})" for k, v in kernels_used.items()),
-           "bytes_per_launch": int(gemv_bytes / n_launch), "avg_launch_us": round(gemv_us / n_launch, 3)}
+           "bytes_per_launch": int(gemv_bytes / n_launch), "avg_launch_us": round(gemv_us / n_launch, 3),
+           "timing": f"in-step: per-workgroup s_memrealtime stamps of the replay step graph, {args.stamp_steps} "
+                     f"replays; launch duration = first workgroup entry -> next launch's first entry "
+                     f"(ti_engine_stamp_steps)",
+           "span_frac": round(gemv_bytes / gemv_span_us / 1e3 / HBM_PEAK_GBS, 4),
+           "isolated_frac": round(gemv_bytes / gemv_iso_us / 1e3 / HBM_PEAK_GBS, 4),
+           "step_stamped_us": round(sum(d["period_us"] for d in stamps), 1)}
     achieved = gemv_bytes / gemv_us / 1e3   # GB/s
     e.close()
 

@@ -163,18 +163,22 @@ int ti_engine_last_tokens(ti_engine* e, int n_streams, int32_t* tokens);
  * times wall clock only, benchmarks/benchmark_inference.cpp:309-384).  The replay step graph
  * (ti_engine_replay_prepare) is captured again with every decode kernel writing, per workgroup,
  * s_memrealtime stamps (100 MHz) of wave 0's entry and of each wave's end into an engine-owned
- * device buffer; the graph is replayed once untimed, then `steps` times, each replay alone on the
- * stream.  Per launch i < min(*n_launch, cap): info[3 i ..] = {kind, tag, workgroups} (workgroups 0:
+ * device buffer; `steps` (<= 256) steps are captured back to back into one graph, which is launched
+ * once untimed and once read.  Per launch i < min(*n_launch, cap): info[3 i ..] = {kind, tag, workgroups} (workgroups 0:
  * the launch writes no stamps) and t[TI_STAMP_FIELDS i ..] the means over the steps, in us, of
  *   [0] span    first workgroup entry -> last wave end
- *   [1] period  first entry -> the next launch's first entry (the last launch: its span)
+ *   [1] period  first entry -> the next launch's first entry (the next step's first launch after a
+ *               step's last): the launch's share of the step, its boundary included (the very last
+ *               launch: its span + the mean boundary)
  *   [2] entry skew  first -> last workgroup entry
  *   [3] wave skew   per workgroup, first -> last wave end, averaged over the workgroups
  *   [4] tail        median workgroup end -> last wave end
- *   [5] gap         last wave end -> the next launch's first entry (the boundary)
+ *   [5] gap         last wave end -> the next launch's first entry (the boundary; the last launch: the mean)
  *   [6] workgroups that ran on a CU another workgroup of the launch also ran on (a count)
+ *   [7..12] diagnostic builds (TI_STAMP_PHASES): wave 0's phase marks, entry -> mark, workgroup mean
+ *   [13]    diagnostic builds: per workgroup, first -> last wave's end of stream, workgroup mean
  * *n_launch receives the launches per step. */
-#define TI_STAMP_FIELDS 7
+#define TI_STAMP_FIELDS 14
 enum { TI_STAMP_KIND_OTHER = 0, TI_STAMP_KIND_GEMV = 1, TI_STAMP_KIND_ATTN = 2, TI_STAMP_KIND_BEGIN = 3,
        TI_STAMP_KIND_ROWS = 4, TI_STAMP_KIND_TILE = 5, TI_STAMP_KIND_RMSNORM = 6, TI_STAMP_KIND_MB = 7 };
 enum { TI_STAMP_TAG_BEGIN = 0, TI_STAMP_TAG_QKV = 1, TI_STAMP_TAG_ATTN = 2, TI_STAMP_TAG_O = 3,

@@ -192,7 +192,8 @@ def lib() -> C.CDLL:
         L.ti_engine_sync.argtypes = [vp]
         L.ti_engine_last_tokens.argtypes = [vp, i32, vp]
         L.ti_engine_time_kernel.argtypes = [vp, i32, i32, i32, i32, C.POINTER(C.c_double), C.POINTER(C.c_double)]
-        L.ti_engine_stamp_steps.argtypes = [vp, i32, i32, vp, vp, C.POINTER(C.c_int)]
+        if hasattr(L, "ti_engine_stamp_steps"):   # (older TI_LIB builds in A/B runs lack it)
+            L.ti_engine_stamp_steps.argtypes = [vp, i32, i32, vp, vp, C.POINTER(C.c_int)]
         L.ti_hbm_calibrate.argtypes = [sz, i32, C.POINTER(C.c_double), C.POINTER(C.c_double), vp]
         L.ti_gemm_kernel_name.argtypes = [i32, i32, i32, i32, i32, C.c_char_p, i32]
         L.ti_rope_table.argtypes = [vp, i32, i32, f32, vp]
@@ -485,7 +486,8 @@ class Engine:
         check(lib().ti_engine_time_kernel(self.h, which, n_streams, kv_len, reps, C.byref(us), C.byref(by)))
         return us.value, by.value
 
-    STAMP_FIELDS = ("span_us", "period_us", "entry_skew_us", "wave_skew_us", "tail_us", "gap_us", "cu_shared_wgs")
+    STAMP_FIELDS = ("span_us", "period_us", "entry_skew_us", "wave_skew_us", "tail_us", "gap_us", "cu_shared_wgs",
+                    "ph1_us", "ph2_us", "ph3_us", "ph4_us", "ph5_us", "ph6_us", "stream_skew_us")
     STAMP_TAGS = ("begin", "qkv", "attention", "o", "gate_up", "down", "lm_head", "other")
     STAMP_KINDS = ("other", "gemv", "attn", "step_begin", "rows", "tile", "rmsnorm", "mb")
 

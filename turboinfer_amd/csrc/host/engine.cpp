@@ -229,7 +229,7 @@ struct DeviceScope {
 // In-step launch stamps (ti_engine_stamp_steps): while a stamped step graph is being captured on this
 // thread, every decode launcher asks ti_stamp_next for its workgroups' slot (kernels/common.hpp
 // stamp_end: kStampWords = 16 words per workgroup) and the launch's kind / tag / grid are recorded.
-constexpr int kStampWords = 16;
+constexpr int kStampWords = 24;   // = ti::kStampWords (kernels/common.hpp)
 struct StampCtx {
   bool on = false;
   unsigned long long* base = nullptr;   // NULL: the sizing pass (record only)
@@ -1692,9 +1692,10 @@ unsigned long long* ti_stamp_next(int kind, long grid) {
 
 namespace {
 
-// Capture the replay step graph with the stamp context on (base NULL: record only).
-int capture_stamped(ti_engine* e, unsigned long long* base, const std::vector<size_t>& offs, std::vector<int32_t>& info,
-                    hipGraphExec_t* out) {
+// Capture `ksteps` replay steps back to back as one graph with the stamp context on (base NULL:
+// record only).
+int capture_stamped(ti_engine* e, int ksteps, unsigned long long* base, const std::vector<size_t>& offs,
+                    std::vector<int32_t>& info, hipGraphExec_t* out) {
   StampCtx& c = g_stamp;
   c = StampCtx{};
   c.on = true;
@@ -1706,7 +1707,8 @@ int capture_stamped(ti_engine* e, unsigned long long* base, const std::vector<si
     c = StampCtx{};
     return ti_check_hip(eb, "hipStreamBeginCapture");
   }
-  const int rc = enqueue_step(e, e->replay_M, 0);
+  int rc = TI_OK;
+  for (int k = 0; k < ksteps && rc == TI_OK; ++k) rc = enqueue_step(e, e->replay_M, 0);
   hipGraph_t g = nullptr;
   const hipError_t ec = hipStreamEndCapture(e->s, &g);
   info = c.info;
@@ -1729,93 +1731,128 @@ int capture_stamped(ti_engine* e, unsigned long long* base, const std::vector<si
 }  // namespace
 
 int ti_engine_stamp_steps(ti_engine* e, int steps, int cap, int32_t* info_out, double* t_out, int* n_launch) {
-  if (!e || e->replay_M < 1 || steps < 1 || cap < 1 || !info_out || !t_out || !n_launch)
-    return ti_set_error(TI_ERR_ARG, "ti_engine_stamp_steps: call ti_engine_replay_prepare first; steps, cap >= 1");
+  if (!e || e->replay_M < 1 || steps < 1 || steps > 256 || cap < 1 || !info_out || !t_out || !n_launch)
+    return ti_set_error(TI_ERR_ARG, "ti_engine_stamp_steps: call ti_engine_replay_prepare first; 1 <= steps <= 256, "
+                        "cap >= 1");
   DeviceScope bind_(e);
   TI_TRY(ti_stream_sync(e->s));
-  // pass 1: the launch list and grids; pass 2: the graph with each stamped launch's slot
+  // pass 1: one step's launch list and grids; pass 2: `steps` steps back to back in one graph, every
+  // stamped launch with its own slot (so the timed steps run as replays do: no host gap between them)
   std::vector<int32_t> info, info2;
-  TI_TRY(capture_stamped(e, nullptr, {}, info, nullptr));
-  const size_t n = info.size() / 3;
-  std::vector<size_t> offs(n);
+  TI_TRY(capture_stamped(e, 1, nullptr, {}, info, nullptr));
+  const size_t n = info.size() / 3, nt = n * (size_t)steps;
+  std::vector<size_t> offs(nt);
   size_t words = 0;
-  for (size_t i = 0; i < n; ++i) {
+  for (size_t i = 0; i < nt; ++i) {
     offs[i] = words;
-    words += (size_t)info[3 * i + 2] * kStampWords;
+    words += (size_t)info[3 * (i % n) + 2] * kStampWords;
   }
   if (words == 0) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_stamp_steps: no stamped launch in the step");
   void* buf = nullptr;
   TI_TRY(ti_malloc(&buf, words * 8));
   unsigned long long* st = static_cast<unsigned long long*>(buf);
   hipGraphExec_t g = nullptr;
-  int rc = capture_stamped(e, st, offs, info2, &g);
-  if (rc == TI_OK && info2 != info) rc = ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_stamp_steps: the two captures differ");
+  int rc = capture_stamped(e, steps, st, offs, info2, &g);
+  if (rc == TI_OK && (info2.size() != nt * 3 || !std::equal(info.begin(), info.end(), info2.begin())))
+    rc = ti_set_error(TI_ERR_UNSUPPORTED, "ti_engine_stamp_steps: the two captures differ");
   std::vector<unsigned long long> h(words);
-  std::vector<double> acc(n * TI_STAMP_FIELDS, 0.0);
-  constexpr double kUs = 0.01;   // s_memrealtime: 100 MHz
-  for (int it = 0; rc == TI_OK && it <= steps; ++it) {   // it 0: untimed
+  for (int it = 0; rc == TI_OK && it < 2; ++it) {   // it 0: untimed (caches, clocks); it 1: the one read
     hipError_t he = hipMemsetAsync(st, 0, words * 8, e->s);
     if (he == hipSuccess) he = hipGraphLaunch(g, e->s);
-    if (he == hipSuccess) he = hipMemcpyAsync(h.data(), st, words * 8, hipMemcpyDeviceToHost, e->s);
+    if (he == hipSuccess && it == 1) he = hipMemcpyAsync(h.data(), st, words * 8, hipMemcpyDeviceToHost, e->s);
     if (he == hipSuccess) he = hipStreamSynchronize(e->s);
-    if (he != hipSuccess) {
-      rc = ti_check_hip(he, "ti_engine_stamp_steps: replay");
-      break;
-    }
-    if (it == 0) continue;
-    // per launch: first / last entry, last end, median workgroup end, mean in-workgroup wave skew
-    std::vector<double> first(n, 0.0), last_end(n, 0.0);
-    for (size_t i = 0; i < n; ++i) {
-      const int wgs = info[3 * i + 2];
-      if (wgs == 0) continue;
-      unsigned long long f = ~0ull, le = 0, lent = 0;
-      double wskew = 0.0;
-      std::vector<unsigned long long> ends, cus;   // cus: (XCC, SE / SH / CU) of each workgroup
-      ends.reserve(wgs);
-      for (int w = 0; w < wgs; ++w) {
-        const unsigned long long* p = h.data() + offs[i] + (size_t)w * kStampWords;
-        if (p[0]) {
-          f = std::min(f, p[0]);
-          lent = std::max(lent, p[0]);
-        }
-        if (p[kStampWords - 1]) cus.push_back((p[kStampWords - 1] & 0x7FFFFFFF00000000ull) | (p[kStampWords - 1] & 0xFF00ull));
-        unsigned long long mn = ~0ull, mx = 0;
-        for (int k = 1; k < kStampWords - 1; ++k)
-          if (p[k]) {
-            mn = std::min(mn, p[k]);
-            mx = std::max(mx, p[k]);
-          }
-        if (mx) {
-          ends.push_back(mx);
-          le = std::max(le, mx);
-          wskew += (double)(mx - mn);
-        }
-      }
-      if (f == ~0ull || ends.empty()) continue;
-      std::nth_element(ends.begin(), ends.begin() + ends.size() / 2, ends.end());
-      const unsigned long long med = ends[ends.size() / 2];
-      first[i] = (double)f;
-      last_end[i] = (double)le;
-      double* a = acc.data() + i * TI_STAMP_FIELDS;
-      a[0] += (double)(le - f) * kUs;
-      a[2] += (double)(lent - f) * kUs;
-      a[3] += wskew / (double)ends.size() * kUs;
-      a[4] += (double)(le - med) * kUs;
-      std::sort(cus.begin(), cus.end());
-      a[6] += (double)(cus.end() - std::unique(cus.begin(), cus.end())) ;   // workgroups on an already-used CU
-    }
-    for (size_t i = 0; i < n; ++i) {
-      if (!first[i]) continue;
-      size_t j = i + 1;
-      while (j < n && !first[j]) ++j;
-      double* a = acc.data() + i * TI_STAMP_FIELDS;
-      a[1] += j < n ? (first[j] - first[i]) * kUs : (last_end[i] - first[i]) * kUs;
-      a[5] += j < n ? (first[j] - last_end[i]) * kUs : 0.0;
-    }
+    if (he != hipSuccess) rc = ti_check_hip(he, "ti_engine_stamp_steps: replay");
   }
   if (g) hipGraphExecDestroy(g);
   ti_free(buf);
   TI_TRY(rc);
+  // per launch (all steps): first / last entry, last end, median workgroup end, mean wave-end skew,
+  // workgroups sharing a CU, phase marks
+  constexpr double kUs = 0.01;   // s_memrealtime: 100 MHz
+  std::vector<double> acc(n * TI_STAMP_FIELDS, 0.0), first(nt, 0.0), last_end(nt, 0.0);
+  for (size_t i = 0; i < nt; ++i) {
+    const int wgs = info[3 * (i % n) + 2];
+    if (wgs == 0) continue;
+    unsigned long long f = ~0ull, le = 0, lent = 0;
+    double wskew = 0.0;
+    std::vector<unsigned long long> ends, cus;   // cus: (XCC, SE / SH / CU) of each workgroup
+    ends.reserve(wgs);
+    double ph[6] = {0, 0, 0, 0, 0, 0}, sskew = 0.0;
+    int sskew_n = 0;
+    int phn[6] = {0, 0, 0, 0, 0, 0};
+    for (int w = 0; w < wgs; ++w) {
+      const unsigned long long* p = h.data() + offs[i] + (size_t)w * kStampWords;
+      if (p[0]) {
+        f = std::min(f, p[0]);
+        lent = std::max(lent, p[0]);
+      }
+      if (p[15]) cus.push_back((p[15] & 0x7FFFFFFF00000000ull) | (p[15] & 0xFF00ull));
+      unsigned long long smn = ~0ull, smx = 0;   // diagnostic builds: the waves' ends of stream
+      for (int k = 16; k < 24; ++k)
+        if (p[k]) {
+          smn = std::min(smn, p[k]);
+          smx = std::max(smx, p[k]);
+        }
+      if (smx) {
+        sskew += (double)(smx - smn);
+        ++sskew_n;
+      }
+      unsigned long long mn = ~0ull, mx = 0;
+      for (int k = 1; k <= 8; ++k)   // wave ends (words 1..8)
+        if (p[k]) {
+          mn = std::min(mn, p[k]);
+          mx = std::max(mx, p[k]);
+        }
+      if (mx) {
+        ends.push_back(mx);
+        le = std::max(le, mx);
+        wskew += (double)(mx - mn);
+      }
+      for (int k = 0; k < 6; ++k)   // phase marks of diagnostic builds (words 9..14), relative to entry
+        if (p[0] && p[9 + k] >= p[0]) {
+          ph[k] += (double)(p[9 + k] - p[0]);
+          ++phn[k];
+        }
+    }
+    if (f == ~0ull || ends.empty()) continue;
+    std::nth_element(ends.begin(), ends.begin() + ends.size() / 2, ends.end());
+    const unsigned long long med = ends[ends.size() / 2];
+    first[i] = (double)f;
+    last_end[i] = (double)le;
+    double* a = acc.data() + (i % n) * TI_STAMP_FIELDS;
+    a[0] += (double)(le - f) * kUs;
+    a[2] += (double)(lent - f) * kUs;
+    a[3] += wskew / (double)ends.size() * kUs;
+    a[4] += (double)(le - med) * kUs;
+    std::sort(cus.begin(), cus.end());
+    a[6] += (double)(cus.end() - std::unique(cus.begin(), cus.end()));   // workgroups on an already-used CU
+    for (int k = 0; k < 6; ++k) a[7 + k] += phn[k] ? ph[k] / phn[k] * kUs : 0.0;
+    a[13] += sskew_n ? sskew / sskew_n * kUs : 0.0;
+  }
+  // periods: first entry -> the next stamped launch's first entry (across step boundaries: the steps
+  // ran back to back); the very last launch: its span + the mean boundary
+  double gap_sum = 0.0;
+  int gap_n = 0;
+  size_t last = nt;
+  for (size_t i = 0; i < nt; ++i) {
+    if (!first[i]) continue;
+    size_t j = i + 1;
+    while (j < nt && !first[j]) ++j;
+    double* a = acc.data() + (i % n) * TI_STAMP_FIELDS;
+    if (j < nt) {
+      a[1] += (first[j] - first[i]) * kUs;
+      a[5] += (first[j] - last_end[i]) * kUs;
+      gap_sum += (first[j] - last_end[i]) * kUs;
+      ++gap_n;
+    } else {
+      last = i;
+    }
+  }
+  if (last < nt) {
+    const double gap = gap_n ? gap_sum / gap_n : 0.0;
+    acc[(last % n) * TI_STAMP_FIELDS + 1] += (last_end[last] - first[last]) * kUs + gap;
+    acc[(last % n) * TI_STAMP_FIELDS + 5] += gap;
+  }
   *n_launch = (int)n;
   for (size_t i = 0; i < n && (int)i < cap; ++i) {
     for (int k = 0; k < 3; ++k) info_out[3 * i + k] = info[3 * i + k];

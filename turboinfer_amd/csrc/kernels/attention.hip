@@ -35,30 +35,9 @@ __global__ __launch_bounds__(NW * kWave, 1) void attn_split_kernel(const AttnArg
   stamp_end(a.stamp, t_entry);
 }
 
-// Dynamic LDS added to every decode-attention launch (A/B knob TI_ATTN_LDS_PAD, bytes): a
-// workgroup image above half the CU's 160 KiB admits one workgroup per CU.
-static size_t attn_lds_pad() {
-  static const size_t v = [] {
-    const char* e = getenv("TI_ATTN_LDS_PAD");
-    const long b = e ? atol(e) : 0;
-    return (size_t)(b < 0 ? 0 : (b > 96 * 1024 ? 96 * 1024 : b));
-  }();
-  return v;
-}
-
 template <int HD, int G, int R, bool HP, int NW = kAttnWaves, bool ROT = false>
 static int launch_one(const AttnArgs& a, hipStream_t s, size_t lds_pad = 0) {
   const dim3 grid(a.splits, a.kv_heads, a.M);
-  if (attn_lds_pad() > lds_pad) {
-    lds_pad = attn_lds_pad();
-    static bool attr_set = false;   // per instantiation; the attribute is per function, idempotent
-    if (!attr_set) {
-      TI_HIP_CHECK(hipFuncSetAttribute((const void*)attn_split_kernel<HD, G, R, HP, NW, ROT>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
-                   "hipFuncSetAttribute(attn_split_kernel)");
-      attr_set = true;
-    }
-  }
   hipLaunchKernelGGL((attn_split_kernel<HD, G, R, HP, NW, ROT>), grid, dim3(NW * kWave), lds_pad, s, a);
   TI_LAUNCH_CHECK("attn_split_kernel");
   return TI_OK;

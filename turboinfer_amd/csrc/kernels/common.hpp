@@ -192,22 +192,41 @@ __host__ __device__ __forceinline__ size_t tile_index(int nt, int kt, int KT) {
 // per workgroup, wave 0's entry time and each wave's end time (s_memrealtime, 100 MHz) with plain
 // vector stores into a host-owned device buffer.  `st` is NULL in every product launch (one scalar
 // branch at the kernel end).
-// per workgroup: [0] entry of wave 0, [1 + w] end of wave w (w < 14), [15] where wave 0 ran:
-// XCC_ID << 32 | HW_ID (SE / SH / CU fields: which CU; two workgroups of a launch on one CU show here)
-constexpr int kStampWords = 16;
+// per workgroup: [0] entry of wave 0, [1 + w] end of wave w (w < 8), [9..14] phase marks of
+// diagnostic builds, [15] where wave 0 ran: XCC_ID << 32 | HW_ID (SE / SH / CU fields: which CU; two
+// workgroups of a launch on one CU show here), [16 + w] diagnostic builds: wave w's end of stream
+constexpr int kStampWords = 24;
 __device__ __forceinline__ unsigned long long stamp_now() { return __builtin_amdgcn_s_memrealtime(); }
-__device__ __forceinline__ void stamp_end(unsigned long long* st, unsigned long long t_entry) {
+// Diagnostic builds (TI_STAMP_PHASES=1, never the product) also keep up to 6 phase marks of wave 0 in
+// words 9..14 (kernel-specific; gemv_wq_kernel: DESIGN 4.18).
+#ifndef TI_STAMP_PHASES
+#define TI_STAMP_PHASES 0
+#endif
+#if TI_STAMP_PHASES
+#define STAMP_MARK(var) const unsigned long long var = stamp_now()
+#else
+#define STAMP_MARK(var) const unsigned long long var = 0
+#endif
+__device__ __forceinline__ void stamp_end(unsigned long long* st, unsigned long long t_entry,
+                                          unsigned long long ph0 = 0, unsigned long long ph1 = 0,
+                                          unsigned long long ph2 = 0, unsigned long long ph3 = 0,
+                                          unsigned long long ph4 = 0, unsigned long long ph5 = 0,
+                                          unsigned long long wave_mark = 0) {
   if (st == nullptr) return;
   if ((threadIdx.x & 63) == 0) {
     const unsigned wave = threadIdx.x >> 6;
     const size_t wg = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
     unsigned long long* p = st + wg * kStampWords;
-    if (wave < kStampWords - 2) p[1 + wave] = stamp_now();
+    if (wave < 8) p[1 + wave] = stamp_now();
+    if (TI_STAMP_PHASES && wave < 8) p[16 + wave] = wave_mark;
     if (wave == 0) {
       p[0] = t_entry;
       // s_getreg_b32 HW_REG_HW_ID (4) and HW_REG_XCC_ID (20), all 32 bits
       const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11)), xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
-      p[kStampWords - 1] = ((unsigned long long)xcc << 32) | hw | (1ull << 63);
+      p[15] = ((unsigned long long)xcc << 32) | hw | (1ull << 63);
+      if (TI_STAMP_PHASES) {
+        p[9] = ph0; p[10] = ph1; p[11] = ph2; p[12] = ph3; p[13] = ph4; p[14] = ph5;
+      }
     }
   }
 }

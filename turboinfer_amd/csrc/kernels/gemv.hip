@@ -305,6 +305,16 @@ __device__ __forceinline__ u32x4 ld_w(const u32x4* p) {
 #endif
 }
 
+// Offset-folded int4 input prep of one staged x piece (deq_int4_raw): the high-nibble slots scaled
+// by 1/16 (exact in fp16) and the piece's share of corr[g][m] = 1032 * sum_lo x + 1152 * sum_hi x.
+__device__ __forceinline__ float int4_x_prep(f16x8& h) {
+  const f16 s16 = (f16)0.0625f;
+  h[2] *= s16; h[3] *= s16; h[6] *= s16; h[7] *= s16;
+  const float lo = ((float)h[0] + (float)h[1]) + ((float)h[4] + (float)h[5]);
+  const float hi = ((float)h[2] + (float)h[3]) + ((float)h[6] + (float)h[7]);
+  return 1032.0f * lo + 1152.0f * hi;
+}
+
 // --------------------------------------------------------------------- kernel
 // LDS barrier that leaves the wave's outstanding global loads in flight (a plain
 // __syncthreads() may drain vmcnt): LDS writes retired, then s_barrier.
@@ -340,10 +350,13 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   a.x = p_x;
   a.norm_w = p_aux;
   a.M = p_mgk & 63;
-  a.N = p_N;
+  // p_N = q | r << 8: NT = q * grid + r 16-row tiles, workgroup b takes q (+1 for b < r) of them from
+  // t0 = b q + min(b, r) (scalar arithmetic only; launch_gemv packs it)
+  const int nt_q = p_N & 0xff, nt_r = (int)((unsigned)p_N >> 8);
   a.K = p_kx & 0xffff;
   a.ldx = XM == XM_F16F || XM == XM_ATTN ? a.K : (int)((unsigned)p_kx >> 16);
   const int p_grid = (p_mgk >> 6) & 0xfff;
+  a.N = 16 * (nt_q * p_grid + nt_r);
   constexpr int C = TileFmt<BITS>::kChunks;
   constexpr int R = TI_GEMV_RING_VGPRS / (4 * C) > 2 ? TI_GEMV_RING_VGPRS / (4 * C) : 2;   // ring depth (items)
   constexpr int XPF = 3;                           // fp16 x: 16-byte pieces prefetched per thread
@@ -352,8 +365,9 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   const int KT = a.K >> 7, xs = a.K + 8, NT = a.N >> 4, K8 = a.K >> 3;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: counters live in SGPRs
-  const int t0 = (int)(bid * (unsigned)NT / (unsigned)p_grid);   // NT * grid < 2^32
-  const int ntl = (int)((bid + 1) * (unsigned)NT / (unsigned)p_grid) - t0;
+  const int t0 = (int)bid * nt_q + ((int)bid < nt_r ? (int)bid : nt_r);
+  const int ntl = nt_q + ((int)bid < nt_r ? 1 : 0);
+  constexpr bool kOneRow = XM == XM_F16F || XM == XM_ATTN || XM == XM_NORM1;   // (M == 1 by construction)
   const int KW = wave < KT ? (KT - wave + kGemvWaves - 1) / kGemvWaves : 0;   // k-tiles per tile, this wave
   const int total = ntl * KW;
   static_assert(!G32 || BITS != 16, "group-32 weights: int4 / int8");
@@ -411,7 +425,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
 #pragma unroll
       for (int q = 0; q < XPF; ++q) {
         const int i = tid + q * kGemvThreads < nx16 ? tid + q * kGemvThreads : nx16 - 1;
-        const int m = i / K8, k8 = i - m * K8;
+        const int m = kOneRow ? 0 : i / K8, k8 = i - m * K8;
         xr16[q] = *(const u32x4*)((const f16*)a.x + (size_t)m * a.ldx + 8 * k8);
       }
     }
@@ -432,7 +446,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   const float* pre_p;
   {
     const int idx = tid < n_res ? tid : 0;
-    const int tl = idx / (a.M * 16), rem = idx - tl * a.M * 16, m = rem >> 4, n = rem & 15;
+    const int tl = kOneRow ? idx >> 4 : idx / (a.M * 16), rem = idx - tl * a.M * 16, m = rem >> 4, n = rem & 15;
     pre_p = kind == TI_EPI_RESID_F32 ? p_pre + (size_t)m * ldo + (t0 + tl) * 16 + n
             : kind == TI_EPI_QKV_ROPE_KV ? p_pre + (tid < a.M ? tid : 0) : p_pre;
   }
@@ -483,10 +497,16 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   }
 
   GEMV_TS(1);
+  STAMP_MARK(ph_issued);
   // ---- 3. stage scales and x in LDS (waits only for the loads of step 1)
   if constexpr (BITS != 16) {
     if (tid < n_sc) ((u32x4*)sl)[tid] = sc_reg;
   }
+  // int4 (group 128): the x pieces staged from registers get their 1/16 scaling and offset correction
+  // here, before the staging barrier (no second LDS pass and barrier in front of the stream); every
+  // piece of x must come from registers for that (rare long shapes take the pass below)
+  constexpr bool kRegPrep = BITS == 4 && !G32 && (XM == XM_NORM1 || XM == XM_ATTN || XM == XM_F16 || XM == XM_F16F);
+  const bool reg_prep = kRegPrep && (XM == XM_NORM1 || XM == XM_ATTN || nx16 <= XPF * kGemvThreads);
   if constexpr (XM == XM_NORM1) {
     // rms_norm (tensor_engine.cpp:1488-1505) of the single row, x and w held in registers.
     float ss = 0.0f;
@@ -501,13 +521,19 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
 #pragma unroll
     for (int w = 0; w < kGemvWaves; ++w) tot += red[w];
     const float rms = sqrtf(tot / (float)a.K + a.eps);
+    float part = 0.0f;
     if (tid < K8) {
       f16x8 h;
       h[0] = (f16)((v0.x / rms) * w0.x); h[1] = (f16)((v0.y / rms) * w0.y);
       h[2] = (f16)((v0.z / rms) * w0.z); h[3] = (f16)((v0.w / rms) * w0.w);
       h[4] = (f16)((v1.x / rms) * w1.x); h[5] = (f16)((v1.y / rms) * w1.y);
       h[6] = (f16)((v1.z / rms) * w1.z); h[7] = (f16)((v1.w / rms) * w1.w);
+      if constexpr (kRegPrep) part = int4_x_prep(h);
       *(f16x8*)(xl + 8 * tid) = h;
+    }
+    if constexpr (kRegPrep) {
+      part = group_sum<16>(part);
+      if (tid < K8 && (lane & 15) == 0) corr[(tid >> 4) * 16] = part;
     }
   } else if constexpr (XM == XM_ATTN) {
     // the attention's split merge (attention.hip last-arriver merge): weights
@@ -525,19 +551,36 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
 #pragma unroll
       for (int e = 0; e < 8; ++e) num[e] = fmaf(f, (float)o[e], num[e]);
     }
+    float part = 0.0f;
     if (tid < K8) {
       f16x8 hx;
 #pragma unroll
       for (int e = 0; e < 8; ++e) hx[e] = (f16)(den > 0.0f ? num[e] / den : 0.0f);
+      if constexpr (kRegPrep) part = int4_x_prep(hx);
       *(f16x8*)(xl + 8 * tid) = hx;
+    }
+    if constexpr (kRegPrep) {
+      part = group_sum<16>(part);
+      if (tid < K8 && (lane & 15) == 0) corr[(tid >> 4) * 16] = part;
     }
   } else if constexpr (XM == XM_F16 || XM == XM_F16F) {
 #pragma unroll
     for (int q = 0; q < XPF; ++q) {
       const int i = tid + q * kGemvThreads;
+      const int m = kOneRow || i >= nx16 ? 0 : i / K8, k8 = i - m * K8;
+      float part = 0.0f;
       if (i < nx16) {
-        const int m = i / K8, k8 = i - m * K8;
-        *(u32x4*)(xl + m * xs + 8 * k8) = xr16[q];
+        if (kRegPrep && reg_prep) {
+          f16x8 h = __builtin_bit_cast(f16x8, xr16[q]);
+          part = int4_x_prep(h);
+          *(f16x8*)(xl + m * xs + 8 * k8) = h;
+        } else {
+          *(u32x4*)(xl + m * xs + 8 * k8) = xr16[q];
+        }
+      }
+      if (kRegPrep && reg_prep) {   // (uniform: every lane of a 16-lane group has the same q)
+        part = group_sum<16>(part);
+        if (i < nx16 && (lane & 15) == 0) corr[(k8 >> 4) * 16 + m] = part;
       }
     }
   }
@@ -557,13 +600,14 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   if (a.epi.kind == TI_EPI_QKV_ROPE_KV && tid < a.M) ((int*)(es + a.M * a.epi.head_dim))[tid] = __builtin_bit_cast(int, pre);
   if (tid < 16) best_l[tid] = 0ull;
   lds_barrier();
+  STAMP_MARK(ph_staged);
 #pragma unroll
   for (int s = R0; s < R; ++s) {
     const size_t o = refill_off();
 #pragma unroll
     for (int c = 0; c < C; ++c) ring[s][c] = ld_w(tb + o + c * kWave);
   }
-  if constexpr (BITS == 4) {
+  if constexpr (BITS == 4) if (!reg_prep) {
     // Offset-folded int4 (deq_int4_raw): scale the high-nibble slots of x by 1/16 (exact in
     // fp16) and build corr[g][m] = 1032 * sum_lo a + 1152 * sum_hi a per 128-k group.  A
     // group is 16 consecutive k8 pieces, i.e. 16 consecutive lanes (K8 % 16 == 0).
@@ -607,6 +651,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   }
 
   GEMV_TS(2);
+  STAMP_MARK(ph_stream);
   // ---- 4. the stream: branch-free, R items per block
   const int r = lane & 15, kq = lane >> 4;
   const f16* xrow = xl + (r < a.M ? r : a.M - 1) * xs + kq * 32;
@@ -713,6 +758,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
 
   GEMV_TS(3);
   GEMV_WTS();
+  STAMP_MARK(ph_streamed);
   // ---- 5. epilogue inputs into LDS, reduce the 8 partials per tile, epilogue
   if (tid < n_res) es[tid] = pre;
   if (fold && tid < n_res) es[n_res + tid] = fw_pre;
@@ -741,6 +787,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   }
   lds_barrier();
   GEMV_TS(5);
+  STAMP_MARK(ph_reduce);
   unsigned long long best[4] = {0ull, 0ull, 0ull, 0ull};
   if (a.M <= 4) {
     // rows m < 4 live in lanes 0-15 of each partial (C layout m = 4*(l>>4) + i): one thread per
@@ -765,6 +812,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       epilogue(a, t0 + tl, tl, lane, i4, v, es, best[0], true, fw_l, ssacc);
     }
   }
+  STAMP_MARK(ph_epi);
   if (a.epi.kind == TI_EPI_LOGITS_ARGMAX) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -788,7 +836,14 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       atomicMax(a.epi.argmax + (size_t)tid * TI_ARGMAX_SLOTS + (bid & (TI_ARGMAX_SLOTS - 1)), best_l[tid]);
     if (a.epi.step_ctr && bid == 0 && tid == 0) *a.epi.step_ctr += a.epi.advance;
   }
-  if (fold) {   // this workgroup's sum of h^2, waves in a fixed order (best_l: unused by RESID)
+  if (fold && a.M <= 4 && ntl * 16 <= kWave) {
+    // every output of the workgroup was wave 0's (the M <= 4 epilogue above): its sum alone, no
+    // barrier -- the same value as the general form below, whose other terms are exact zeros
+    if (wave == 0) {
+      const float sw = group_sum<kWave>(ssacc);
+      if (lane == 0) a.epi.fold_ss[bid] = sw;
+    }
+  } else if (fold) {   // this workgroup's sum of h^2, waves in a fixed order (best_l: unused by RESID)
     float* red2 = (float*)best_l;
     const float sw = group_sum<kWave>(ssacc);
     if (lane == 0) red2[wave] = sw;
@@ -801,7 +856,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
     }
   }
   GEMV_TS(4);
-  stamp_end(a.stamp, t_entry);
+  stamp_end(a.stamp, t_entry, ph_issued, ph_staged, ph_stream, ph_streamed, ph_reduce, ph_epi, ph_streamed);
 }
 
 // ================================================================= batched rows
@@ -2164,20 +2219,8 @@ __host__ inline int gemv_xmode(int x_kind, int M, int K) {
   return M == 1 && (K >> 3) <= kGemvThreads ? XM_NORM1 : XM_NORM;
 }
 
-// Dynamic LDS floor of the fused kernel's launch (A/B knob TI_GEMV_LDS_FLOOR, bytes): an image
-// above half the CU's 160 KiB admits one workgroup per CU whatever the registers allow.
-__host__ inline int gemv_lds_floor() {
-  static const int v = [] {
-    const char* e = getenv("TI_GEMV_LDS_FLOOR");
-    const int b = e ? atoi(e) : 0;
-    return b < 0 ? 0 : (b > 160 * 1024 ? 160 * 1024 : b);
-  }();
-  return v;
-}
-
 template <int BITS, bool G32 = false, bool AFF = false>
 static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid) {
-  if (lds < gemv_lds_floor()) lds = gemv_lds_floor();
   const float* pre = a.epi.kind == TI_EPI_RESID_F32 ? (const float*)a.epi.out
                      : a.epi.kind == TI_EPI_QKV_ROPE_KV ? (const float*)a.epi.pos : (const float*)a.x;
   const int xm = gemv_xmode(a.x_kind, a.M, a.K);
@@ -2186,13 +2229,17 @@ static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid) {
   const int mgk = a.M | (grid << 6) | (a.epi.kind << 18) | (xm == XM_ATTN ? (a.epi.head_dim / 64) << 21 : 0);
   const int kx = a.K | ((xm == XM_F16F || xm == XM_ATTN ? a.epi.n_ss : a.ldx) << 16);
   const int ldo = a.epi.ldo;
+  const int NT = a.N >> 4, nt_q = NT / grid, nt_r = NT % grid;   // the kernel's tile split (gemv_wq_kernel)
+  if (nt_q > 255 || nt_r >= (1 << 23))
+    return ti_set_error(TI_ERR_UNSUPPORTED, "gemv_wq_kernel: %d tiles over %d workgroups", NT, grid);
+  const int pn = nt_q | (nt_r << 8);
   switch (xm) {
-    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_ATTN: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_ATTN, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_F16F: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16F, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
-    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, a.N, kx, ldo, pre, a); break;
+    case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
+    case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
+    case XM_ATTN: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_ATTN, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
+    case XM_F16F: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16F, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
+    case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
+    default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
   }
   TI_LAUNCH_CHECK("gemv_wq_kernel");
   return TI_OK;
