@@ -453,7 +453,6 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   const float pre = *pre_p;
   // RESID with fold_x: the fold weight of the same output (one row), consumed by the epilogue
   // (its pointer comes from the kernarg struct: loaded after the ring is issued, below)
-  const bool fold = (XM == XM_F16 || XM == XM_ATTN) && kind == TI_EPI_RESID_F32 && a.epi.fold_x != nullptr;
   float fw_pre = 0.0f;
   // XM_F16F: this lane's share of the producer's partial sums of squares (up to 256 of them),
   // clamped loads; masked and summed after the stream
@@ -491,6 +490,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
 #pragma unroll
     for (int c = 0; c < C; ++c) ring[s][c] = ld_w(tb + o + c * kWave);
   }
+  const bool fold = (XM == XM_F16 || XM == XM_ATTN) && kind == TI_EPI_RESID_F32 && a.epi.fold_x != nullptr;
   if constexpr (XM == XM_F16 || XM == XM_ATTN) {   // fold weight (consumed by the epilogue)
     const float* fw_p = fold ? a.epi.fold_w + (size_t)t0 * 16 + (tid < n_res ? tid : 0) : pre_p;
     fw_pre = *fw_p;
