@@ -31,12 +31,16 @@ $(BUILD)/k_ops_exact.o: turboinfer_amd/csrc/kernels/ops_exact.hip $(HDRS)
 	$(HIPCC) $(DEVFLAGS) -ffp-contract=off -c $< -o $@
 
 # gemv: preload its leading kernel arguments into SGPRs (gfx950 kernarg preload).
-# gemv and attention compile without fp contraction (the rounding sequence the parity tests pin).
+# gemv, attention and qkv_attn compile without fp contraction (the rounding sequence the parity tests pin).
 $(BUILD)/k_gemv.o: turboinfer_amd/csrc/kernels/gemv.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(DEVFLAGS) -ffp-contract=off -mllvm -amdgpu-kernarg-preload-count=16 -c $< -o $@
 
 $(BUILD)/k_attention.o: turboinfer_amd/csrc/kernels/attention.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(DEVFLAGS) -ffp-contract=off -c $< -o $@
+
+$(BUILD)/k_qkv_attn.o: turboinfer_amd/csrc/kernels/qkv_attn.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(DEVFLAGS) -ffp-contract=off -c $< -o $@
 

@@ -279,6 +279,9 @@ def main() -> int:
     shapes = {"qkv": (nh * hd + 2 * nkv * hd, H), "o": (H, nh * hd), "gate_up": (2 * I, H), "down": (H, I),
               "lm_head": (V, H)}
     fold_on = B == 1 and e.set_fold(None)
+    # one stream of a GQA head_dim-64 model: QKV and the attention run as ONE launch (ti_qkv_attn_partials,
+    # DESIGN 4.19); its class "qkv" then carries the attention's bytes too and there is no attention class
+    qa_on = B == 1 and hasattr(e, "set_qkv_attn") and e.set_qkv_attn(None)
     lib = T.lib()
 
     def class_kernel(name):
@@ -321,11 +324,18 @@ def main() -> int:
     gemv_bytes = gemv_us = gemv_iso_us = gemv_span_us = 0.0
     n_launch = 0
     kernels_used = {}
+    att_iso = e.time_kernel(5, B, L, args.kernel_reps) if qa_on else None
     for w, name in enumerate(names + ["attention"]):
+        if name == "attention" and qa_on:
+            break
         iso_us, by = e.time_kernel(w, B, L, args.kernel_reps)
         c = in_step[tag_of[name]]
         us = c["period"] / c["n"]
         kname = "attn_split_kernel" if name == "attention" else class_kernel(name)
+        if name == "qkv" and qa_on:   # the fused launch: the q / k / v weights and the K / V it attends over
+            by += att_iso[1]
+            iso_us += att_iso[0]      # (isolated: the two unfused launches, for comparison)
+            kname = f"qkv_attn_kernel<{bits},64> (QKV + attention, one launch)"
         per[name] = {"avg_us": round(us, 3), "bytes": int(by), "GBps": round(by / us / 1e3, 1), "kernel": kname,
                      "in_step_launches": c["n"], "span_us": round(c["span"] / c["n"], 3),
                      "gap_us": round(c["gap"] / c["n"], 3), "cu_shared_wgs": round(c["cu_shared"] / c["n"], 2),
@@ -339,7 +349,7 @@ def main() -> int:
         gemv_iso_us += iso_us * cnt
         gemv_span_us += c["span"]
         n_launch += cnt
-    att_us, att_bytes = per["attention"]["avg_us"], per["attention"]["bytes"]
+    att_bytes = att_iso[1] if qa_on else per["attention"]["bytes"]
     dom = {"kernel": " + ".join(f"{k} ({', '.join(v)})" for k, v in kernels_used.items()),
            "bytes_per_launch": int(gemv_bytes / n_launch), "avg_launch_us": round(gemv_us / n_launch, 3),
            "timing": f"in-step: per-workgroup s_memrealtime stamps of the replay step graph, {args.stamp_steps} "
@@ -375,10 +385,11 @@ def main() -> int:
             "roofline": dict({"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                               "traffic_source": traffic_src}, **dom),
-            "attention_roofline": {"bound": "hbm", "kernel": "attn_split_kernel", "achieved": per["attention"]["GBps"],
-                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": round(per["attention"]["GBps"] / HBM_PEAK_GBS, 4), "traffic": att_traffic,
-                                   "share_of_step_bytes": round(layers * att_bytes / sb, 4)},
+            "attention_roofline": ({"bound": "hbm", "kernel": "attn_split_kernel", "achieved": per["attention"]["GBps"],
+                                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": round(per["attention"]["GBps"] / HBM_PEAK_GBS, 4), "traffic": att_traffic,
+                                    "share_of_step_bytes": round(layers * att_bytes / sb, 4)} if not qa_on else
+                                   {"fused_into": "qkv", "share_of_step_bytes": round(layers * att_bytes / sb, 4)}),
             "calibration": {"hbm_read_GBps": round(hbm_read, 1), "hbm_copy_GBps": round(hbm_copy, 1),
                             "note": "same run, this GPU: 1 GiB streamed once by 2 workgroups per CU (read) and "
                                     "hipMemcpyAsync device-to-device (read + write bytes); best of 5"},

@@ -23,7 +23,7 @@ ROOT = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("TI_LIB") or os.path.join(HERE, "lib", "libturboinfer_amd.so")
 
 TI_OK = 0
-X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED, X_ATTN_SPLITS, X_F16_PACKED = 0, 1, 2, 3, 4, 5
+X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED, X_ATTN_SPLITS, X_F16_PACKED, X_ATTN_SPLITS_NEW = 0, 1, 2, 3, 4, 5, 6
 ATTN_MAX_PART_SPLITS = 8           # TI_ATTN_MAX_PART_SPLITS (include/ti_hip.h)
 EPI_STORE_F32, EPI_STORE_F16, EPI_RESID_F32, EPI_SILU_MUL_F16, EPI_QKV_ROPE_KV, EPI_LOGITS_ARGMAX = range(6)
 ARGMAX_SLOTS = 32
@@ -87,6 +87,7 @@ EXPORTED = [
     "ti_wpack_q1_host", "ti_engine_set_tensor_q1", "ti_epilogue_bytes",
     "ti_sample_step_ws", "ti_hbm_calibrate", "ti_gemm_kernel_name",
     "ti_gemm_fold_partials", "ti_engine_set_stop", "ti_engine_counters",
+    "ti_qkv_attn_partials", "ti_qkv_attn_part_o_elems", "ti_qkv_attn_part_ml_elems", "ti_engine_set_qkv_attn",
 ]
 
 _lib = None
@@ -186,6 +187,14 @@ def lib() -> C.CDLL:
         if hasattr(L, "ti_engine_set_fold"):   # (older TI_LIB builds in A/B runs lack it)
             L.ti_gemm_grid.argtypes = [i32, i32, i32]
             L.ti_engine_set_fold.argtypes = [vp, i32, C.POINTER(C.c_int)]
+        if hasattr(L, "ti_qkv_attn_partials"):   # (older TI_LIB builds in A/B runs lack it)
+            L.ti_engine_set_qkv_attn.argtypes = [vp, i32, C.POINTER(C.c_int)]
+            L.ti_qkv_attn_partials.argtypes = [vp, vp, i32, vp, vp, i32, f32, vp, vp, vp, vp, i32, i32, i32, i32,
+                                               i32, i32, vp, vp, vp]
+            L.ti_qkv_attn_part_o_elems.argtypes = [i32, i32, i32]
+            L.ti_qkv_attn_part_o_elems.restype = sz
+            L.ti_qkv_attn_part_ml_elems.argtypes = [i32, i32, i32]
+            L.ti_qkv_attn_part_ml_elems.restype = sz
         L.ti_engine_compat_step.argtypes = [vp, i32, vp]
         L.ti_engine_replay_prepare.argtypes = [vp, i32, i32, i32]
         L.ti_engine_replay_run.argtypes = [vp, i32]
@@ -453,6 +462,12 @@ class Engine:
         """Folded rms_norm hand-off on/off (None: query); returns whether 1-stream steps use it."""
         act = C.c_int(0)
         check(lib().ti_engine_set_fold(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
+        return bool(act.value)
+
+    def set_qkv_attn(self, on=None) -> bool:
+        """QKV + attention in one launch on/off (None: query); returns whether 1-stream steps use it."""
+        act = C.c_int(0)
+        check(lib().ti_engine_set_qkv_attn(self.h, -1 if on is None else int(bool(on)), C.byref(act)))
         return bool(act.value)
 
     def step(self, tokens, pos):

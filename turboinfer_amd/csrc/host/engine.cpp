@@ -103,8 +103,11 @@ struct ti_engine {
   // single-stream attention leaves its split merge to the O projection (ti_attn_decode_partials
   // + TI_X_ATTN_SPLITS): no arrival-ticket hand-off at the end of the attention launch
   bool part_on = true;         // TI_ATTN_PART=0 turns it off
-  uint16_t* part_o = nullptr;  // [heads][TI_ATTN_MAX_PART_SPLITS][head_dim]
-  float* part_ml = nullptr;    // [heads][TI_ATTN_MAX_PART_SPLITS][2]
+  uint16_t* part_o = nullptr;  // [heads][TI_ATTN_MAX_PART_SPLITS][head_dim] (+ k_p, v_p: ti_qkv_attn_partials)
+  float* part_ml = nullptr;    // [heads][TI_ATTN_MAX_PART_SPLITS][2] (+ q)
+  // one stream of a GQA head_dim-64 model: QKV and the attention in one launch (ti_qkv_attn_partials,
+  // DESIGN 4.19), the new key merged by the O projection (TI_X_ATTN_SPLITS_NEW); TI_QKV_ATTN=0 turns it off
+  bool qa_on = false;
   // on-device sampling (ti_engine_generate_sampled): the step graph ends with ti_sample_step
   bool samp_on = false;
   float samp_t = 1.0f, samp_p = 1.0f;
@@ -348,6 +351,17 @@ bool part_usable(ti_engine* e, int M) {
 }
 
 
+// QKV + attention in one launch (ti_qkv_attn_partials): one stream with the fold and split partials,
+// a GQA model with head_dim 64 (TinyLlama-1.1B), int8 / int4 group-128 weights.
+bool qa_usable(ti_engine* e, int M) {
+  const ti_engine_config& c = e->c;
+  if (!e->qa_on || M != 1 || !fold_usable(e, M) || !part_usable(e, M)) return false;
+  const int sp = e->splits_for(M), kv_tiles = 2 * e->kvd() / 16;
+  return c.head_dim == 64 && (c.bits == 4 || c.bits == 8) && c.heads > c.kv_heads && c.heads % 8 == 0 &&
+         (c.heads & (c.heads - 1)) == 0 && (c.kv_heads & (c.kv_heads - 1)) == 0 && c.hidden >= 1024 &&
+         c.hidden <= 4096 && kv_tiles <= c.heads * sp && ti_gemm_grid(1, c.hidden, c.inter) <= 256;
+}
+
 // One decode step for streams [0, M) on e->s.  Graph-capturable (no host sync / alloc).
 int enqueue_step(ti_engine* e, int M, int advance) {
   const ti_engine_config& c = e->c;
@@ -369,7 +383,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
   sa.step_ctr = e->step_ctr;
   const int H = c.hidden, qd = e->qd(), kvd = e->kvd(), I = c.inter, V = c.vocab;
   // fold (M == 1): every rms_norm input is handed over as fx + ss partials by its producer
-  const bool fold = fold_usable(e, M), part = part_usable(e, M), pk = packed_rows(e, M);
+  const bool fold = fold_usable(e, M), part = part_usable(e, M), pk = packed_rows(e, M), qa = qa_usable(e, M);
   // batched fold (17..64 rows): O / down write xn = fp16(h * next norm weight) and per-row sums of
   // h^2; QKV (after layer 0), gate/up and the lm_head normalise behind their GEMM (ti_hip.h)
   const bool bfold = !fold && bfold_usable(e, M);
@@ -444,7 +458,18 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     eo.ldo = H;
     eo.out = e->h;
     fold_into(eo, L.ffn_norm, L.gu.N);
-    if (part) {   // the O projection merges the attention's splits while staging its input
+    if (qa) {   // QKV + attention in one launch; O merges the splits and the step's own key
+      stamp_tag(TI_STAMP_TAG_QKV);
+      const int S = e->splits_for(M);
+      TI_TRY(ti_qkv_attn_partials(L.qkv.tiles, L.qkv.scales, c.bits, e->fx, e->ss, n_ss, c.eps, e->rope_cs, e->pos,
+                                  L.kc, L.vc, c.max_seq, H, c.heads, c.kv_heads, c.head_dim, S, e->part_o, e->part_ml,
+                                  e->s));
+      eo.ss_in = e->part_ml;
+      eo.n_ss = S;
+      eo.head_dim = c.head_dim;
+      stamp_tag(TI_STAMP_TAG_O);
+      TI_TRY(gemm(L.o, e->part_o, TI_X_ATTN_SPLITS_NEW, qd, 2, nullptr, eo, 4, false));
+    } else if (part) {   // the O projection merges the attention's splits while staging its input
       stamp_tag(TI_STAMP_TAG_QKV);
       TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));
       stamp_tag(TI_STAMP_TAG_ATTN);
@@ -720,10 +745,11 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
         (rc = e->alloc_t(&e->pf_ones, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->pf_zero, (size_t)1)) ||
         (rc = e->alloc_t(&e->pf_base, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->fx, (size_t)H)) ||
         (rc = e->alloc_t(&e->ss, (size_t)256)) || (rc = e->alloc_t(&e->ss_rows, (size_t)4096 * TI_FOLD_SS_ROWS)) ||
-        (rc = e->alloc_t(&e->part_o, (size_t)c.heads * TI_ATTN_MAX_PART_SPLITS * hd)) ||
-        (rc = e->alloc_t(&e->part_ml, (size_t)c.heads * TI_ATTN_MAX_PART_SPLITS * 2)))
+        (rc = e->alloc_t(&e->part_o, ti_qkv_attn_part_o_elems(c.heads, hd, TI_ATTN_MAX_PART_SPLITS))) ||
+        (rc = e->alloc_t(&e->part_ml, ti_qkv_attn_part_ml_elems(c.heads, hd, TI_ATTN_MAX_PART_SPLITS))))
       return fail(rc);
     if (const char* env = getenv("TI_FOLD")) e->fold_on = atoi(env) != 0;
+    if (const char* env = getenv("TI_QKV_ATTN")) e->qa_on = atoi(env) != 0;
     if ((c.bits & ~TI_BITS_G32) == 4) {   // batched rows and prompt chunks: split-K tile GEMM (TI_SPLITK_MB, 0 = off)
       const char* env = getenv("TI_SPLITK_MB");
       const size_t mb = env ? (size_t)std::max(0, atoi(env)) : 64;
@@ -1518,6 +1544,19 @@ int ti_engine_set_fold(ti_engine* e, int on, int* active) {
     e->fold_on = e->part_on = on != 0;
   }
   if (active) *active = fold_usable(e, 1) ? 1 : 0;
+  return TI_OK;
+}
+
+int ti_engine_set_qkv_attn(ti_engine* e, int on, int* active) {
+  if (!e) return ti_set_error(TI_ERR_ARG, "ti_engine_set_qkv_attn: null");
+  DeviceScope bind_(e);
+  if (on >= 0 && (on != 0) != e->qa_on) {
+    TI_TRY(ti_stream_sync(e->s));   // captured step graphs bake the setting in
+    for (auto& g : e->graphs) hipGraphExecDestroy(g.second);
+    e->graphs.clear();
+    e->qa_on = on != 0;
+  }
+  if (active) *active = qa_usable(e, 1) ? 1 : 0;
   return TI_OK;
 }
 
