@@ -144,8 +144,8 @@ int ti_engine_set_prefill(ti_engine* e, int rows);
 int ti_engine_set_fold(ti_engine* e, int on, int* active);
 
 /* QKV and attention of single-stream steps in one launch (ti_hip.h ti_qkv_attn_partials; GQA models
- * with head_dim 64 and int4 / int8 weights, with the fold and split partials on): default on (env
- * TI_QKV_ATTN=0 turns it off).  on = 0/1 sets it, -1 leaves it; *active (nullable) receives whether
+ * with head_dim 64, hidden 1024..2048 and int4 / int8 weights, with the fold and split partials on,
+ * e.g. TinyLlama-1.1B): default on (env TI_QKV_ATTN=0 turns it off).  on = 0/1 sets it, -1 leaves it; *active (nullable) receives whether
  * 1-stream steps of this engine use it. */
 int ti_engine_set_qkv_attn(ti_engine* e, int on, int* active);
 

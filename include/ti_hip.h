@@ -320,20 +320,25 @@ int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, const uint1
                             int kv_heads, int head_dim, int splits, uint16_t* part_o, float* part_ml,
                             ti_stream_t s);
 /* One decode stream of a GQA model with head_dim 64 (bits 4 or 8, heads a multiple of 8, 1024 <= K <=
- * 4096): the QKV projection of the folded input (TI_X_F16_FOLDED: fx, ss_in[0 .. n_ss)) with the
+ * 2048): the QKV projection of the folded input (TI_X_F16_FOLDED: fx, ss_in[0 .. n_ss)) with the
  * TI_EPI_QKV_ROPE_KV epilogue's arithmetic -- the new K / V row into k_cache / v_cache
  * ([kv_heads][max_seq][head_dim], slot pos[0]) -- and ti_attn_decode_partials over the keys BEFORE
  * pos[0], in one launch of heads x splits workgroups (inference_engine.cpp:203-279 and 291-368 ->
  * tensor_engine.cpp:490-640, 1510-1624, 1254-1388).  The step's own key is left to the O projection
  * (TI_X_ATTN_SPLITS_NEW with x = part_o, ss_in = part_ml, n_ss = splits): part_o holds
  * ti_qkv_attn_part_o_elems and part_ml ti_qkv_attn_part_ml_elems elements.  tiles / scales: the fused
- * q | k | v weight as ti_gemm_wq_a16 takes it (N = (heads + 2 kv_heads) * head_dim). */
+ * q | k | v weight as ti_gemm_wq_a16 takes it (N = (heads + 2 kv_heads) * head_dim).  The S workgroups
+ * of a head split its q rows (tile s % (head_dim / 16), k-part s / (head_dim / 16)) and exchange them
+ * through xchg (ti_qkv_attn_xchg_bytes, zeroed once by the owner, then kept: it holds a generation per
+ * workgroup; one launch at a time per buffer).  splits: a multiple of head_dim / 16 whose k-parts are
+ * whole multiples of 8 k-tiles. */
 int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, int bits, const uint16_t* fx,
                          const float* ss_in, int n_ss, float eps, const float* rope_cs, const int32_t* pos,
                          uint16_t* k_cache, uint16_t* v_cache, int max_seq, int K, int heads, int kv_heads,
-                         int head_dim, int splits, uint16_t* part_o, float* part_ml, ti_stream_t s);
+                         int head_dim, int splits, uint16_t* part_o, float* part_ml, void* xchg, ti_stream_t s);
 size_t ti_qkv_attn_part_o_elems(int heads, int head_dim, int splits);
 size_t ti_qkv_attn_part_ml_elems(int heads, int head_dim, int splits);
+size_t ti_qkv_attn_xchg_bytes(int heads, int splits);
 /* Prefill attention (forward_pass over a prompt chunk, inference_engine.cpp:1429-1491 ->
  * multi_head_attention, tensor_engine.cpp:1149-1252): the M rows are tokens of ONE stream whose
  * cache k_cache / v_cache [kv_heads][max_seq][head_dim] fp16 already holds their K / V; row m

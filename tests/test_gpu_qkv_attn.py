@@ -4,7 +4,8 @@ One stream of a GQA head_dim-64 model (TinyLlama-1.1B, configs[1]): the launch c
 with the fused GEMV's arithmetic (TI_X_F16_FOLDED input, TI_EPI_QKV_ROPE_KV epilogue), writes the
 new K / V row, and attends q to the keys BEFORE the step's own; the O projection merges that key as
 one more split (TI_X_ATTN_SPLITS_NEW).  Checked against the unfused launches on the same inputs:
-  * q, k_p, v_p bit-identical (same items, same order, same reduction and epilogue arithmetic);
+  * k_p, v_p bit-identical (same items, same order, same reduction and epilogue arithmetic); q to fp32
+    summation order (the head's S workgroups each sum one k-part of one q tile, exchanged in the launch);
   * the O output within the split-merge bound of test_gpu_fold.py (the staged activation differs by
     the fp16 rounding of each split's normalised row);
   * an engine with it on vs off, step by step, within the decode tolerance (TOL, test_gpu_engine.py).
@@ -78,15 +79,17 @@ def test_fused_matches_unfused_launches(ti, oracle, bits, K, heads, kv_heads, p,
     kfu, vfu = dev(ti, kc), dev(ti, vc)
     po2 = ti.DeviceBuffer(L_.ti_qkv_attn_part_o_elems(heads, hd, splits) * 2)
     pml2 = ti.DeviceBuffer(L_.ti_qkv_attn_part_ml_elems(heads, hd, splits) * 4)
+    xg = ti.DeviceBuffer(L_.ti_qkv_attn_xchg_bytes(heads, splits))
+    xg.zero()
     ti.check(L_.ti_qkv_attn_partials(td.ptr, sd.ptr, bits, fxd.ptr, ssd.ptr, ss.size, eps, csd.ptr, pd.ptr, kfu.ptr,
-                                     vfu.ptr, max_seq, K, heads, kv_heads, hd, splits, po2.ptr, pml2.ptr, None))
+                                     vfu.ptr, max_seq, K, heads, kv_heads, hd, splits, po2.ptr, pml2.ptr, xg.ptr, None))
     ti.sync()
 
-    # q, k_p, v_p bit-identical; the rest of the caches untouched
-    q_u = qb.download(f32, qd)
+    # q to fp32 summation order, k_p / v_p bit-identical, the rest of the caches untouched
+    q_u = qb.download(f32, qd).astype(np.float64)
     tail = pml2.download(f32, L_.ti_qkv_attn_part_ml_elems(heads, hd, splits))
-    q_f = tail[heads * splits * 2:]
-    assert np.array_equal(q_u.view(np.uint32), q_f.view(np.uint32))
+    q_f = tail[heads * splits * 2:].astype(np.float64)
+    assert np.max(np.abs(q_f - q_u)) <= 1e-5 * np.max(np.abs(q_u)), np.max(np.abs(q_f - q_u))
     for a, b in ((kua, kfu), (vua, vfu)):
         assert np.array_equal(a.download(np.uint16, kc.shape), b.download(np.uint16, kc.shape))
     # the per-q-head copies of k_p / v_p behind the partials

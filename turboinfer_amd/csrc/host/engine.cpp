@@ -107,7 +107,8 @@ struct ti_engine {
   float* part_ml = nullptr;    // [heads][TI_ATTN_MAX_PART_SPLITS][2] (+ q)
   // one stream of a GQA head_dim-64 model: QKV and the attention in one launch (ti_qkv_attn_partials,
   // DESIGN 4.19), the new key merged by the O projection (TI_X_ATTN_SPLITS_NEW); TI_QKV_ATTN=0 turns it off
-  bool qa_on = false;
+  bool qa_on = true;
+  void* qa_xchg = nullptr;     // the q exchange of ti_qkv_attn_partials (zeroed once, generations kept)
   // on-device sampling (ti_engine_generate_sampled): the step graph ends with ti_sample_step
   bool samp_on = false;
   float samp_t = 1.0f, samp_p = 1.0f;
@@ -356,10 +357,16 @@ bool part_usable(ti_engine* e, int M) {
 bool qa_usable(ti_engine* e, int M) {
   const ti_engine_config& c = e->c;
   if (!e->qa_on || M != 1 || !fold_usable(e, M) || !part_usable(e, M)) return false;
-  const int sp = e->splits_for(M), kv_tiles = 2 * e->kvd() / 16;
+  const int sp = e->splits_for(M), kv_tiles = 2 * e->kvd() / 16, KT = c.hidden / 128;
+  // (the kernel's split shape: a multiple of the 4 q tiles of a head, k-parts of whole 8-k-tile waves;
+  // all heads x splits workgroups resident at once for the q exchange)
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  if (sp % 4 || KT % (sp / 4) || (KT / (sp / 4)) % 8 || c.heads * sp > cus) return false;
   return c.head_dim == 64 && (c.bits == 4 || c.bits == 8) && c.heads > c.kv_heads && c.heads % 8 == 0 &&
          (c.heads & (c.heads - 1)) == 0 && (c.kv_heads & (c.kv_heads - 1)) == 0 && c.hidden >= 1024 &&
-         c.hidden <= 4096 && kv_tiles <= c.heads * sp && ti_gemm_grid(1, c.hidden, c.inter) <= 256;
+         c.hidden <= 2048 && kv_tiles <= c.heads * sp && ti_gemm_grid(1, c.hidden, c.inter) <= 256;
 }
 
 // One decode step for streams [0, M) on e->s.  Graph-capturable (no host sync / alloc).
@@ -463,7 +470,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
       const int S = e->splits_for(M);
       TI_TRY(ti_qkv_attn_partials(L.qkv.tiles, L.qkv.scales, c.bits, e->fx, e->ss, n_ss, c.eps, e->rope_cs, e->pos,
                                   L.kc, L.vc, c.max_seq, H, c.heads, c.kv_heads, c.head_dim, S, e->part_o, e->part_ml,
-                                  e->s));
+                                  e->qa_xchg, e->s));
       eo.ss_in = e->part_ml;
       eo.n_ss = S;
       eo.head_dim = c.head_dim;
@@ -746,7 +753,8 @@ int ti_engine_create(const ti_engine_config* cfg, ti_engine** out) {
         (rc = e->alloc_t(&e->pf_base, (size_t)e->pf_rows)) || (rc = e->alloc_t(&e->fx, (size_t)H)) ||
         (rc = e->alloc_t(&e->ss, (size_t)256)) || (rc = e->alloc_t(&e->ss_rows, (size_t)4096 * TI_FOLD_SS_ROWS)) ||
         (rc = e->alloc_t(&e->part_o, ti_qkv_attn_part_o_elems(c.heads, hd, TI_ATTN_MAX_PART_SPLITS))) ||
-        (rc = e->alloc_t(&e->part_ml, ti_qkv_attn_part_ml_elems(c.heads, hd, TI_ATTN_MAX_PART_SPLITS))))
+        (rc = e->alloc_t(&e->part_ml, ti_qkv_attn_part_ml_elems(c.heads, hd, TI_ATTN_MAX_PART_SPLITS))) ||
+        (rc = e->alloc(&e->qa_xchg, ti_qkv_attn_xchg_bytes(c.heads, TI_ATTN_MAX_PART_SPLITS))))
       return fail(rc);
     if (const char* env = getenv("TI_FOLD")) e->fold_on = atoi(env) != 0;
     if (const char* env = getenv("TI_QKV_ATTN")) e->qa_on = atoi(env) != 0;

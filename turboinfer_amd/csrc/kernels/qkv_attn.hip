@@ -3,21 +3,26 @@
 // i.e. TransformerLayer::forward_incremental's q / k / v projections, RoPE, KV append and
 // compute_attention (inference_engine.cpp:203-279, 291-368; tensor_engine.cpp:1254-1388).
 //
-// Workgroup (head h, split s) = blockIdx (h + heads * s): the S workgroups of a head sit on one XCD
-// (blockIdx % 8 = h % 8 when heads % 8 == 0), whose L2 serves them the head's q weights after the first.
+// Workgroup (head h, split s) = blockIdx (s + S h); S = splits workgroups per head.
 //   1. x = fp16(h * nw) of the rms_norm fold (TI_X_F16_FOLDED) staged in LDS, the rms from the
 //      producer's partial sums of squares;
-//   2. the GEMV of the head's q rows (head_dim / 16 tiles) -- every split computes them -- and, on
-//      kv_tiles of the workgroups, one k or v tile besides: gemv_wq_kernel's items, in its order, with
-//      its reduction and QKV epilogue arithmetic (q / k / v bit-identical to the unfused step's), the
-//      new K / V row written into the cache at p = pos[0];
-//   3. the split's share of the OLD keys [0, p) against q_h (attn_split_body's one-query lane layout,
-//      online softmax, wave merge), its normalised row and (max, sum) written as
-//      ti_attn_decode_partials writes them.
+//   2. its share of the head's q rows: tile s % QT of the head (QT = head_dim / 16 tiles), k-part
+//      s / QT of S / QT -- one k-tile per wave at TinyLlama's shape -- with the fused GEMV's item
+//      arithmetic; the 8 waves' partials summed in a fixed order and published as 16 data-tagged
+//      8-byte granules {value, generation} (agent-scope stores);
+//      and on kv_tiles of the workgroups (split S - 1 first), one whole k or v tile: the QKV
+//      epilogue's arithmetic (RoPE of k), the new K / V row into the cache at p = pos[0];
+//   3. the head's 64 q values gathered from its S workgroups' granules (each workgroup keeps a
+//      generation count in its own slot: every launch advances every slot by one, so the siblings'
+//      expected tag is its own), summed over the k-parts in order, / rms, RoPE;
+//   4. the split's share of the OLD keys [0, p) against q_h (attn_split_body's one-query lane
+//      layout, online softmax, wave merge), its normalised row and (max, sum) written as
+//      ti_attn_decode_partials writes them; split S - 1 is shorter by the k / v tile's bytes.
 // The new key is not attended here (another workgroup of this launch is writing it): split 0 of each
 // head leaves q_h, and the k / v workgroups leave k_p, v_p per q-head, behind the partials, and the
 // O projection merges the new key as one more split while it stages its input
-// (TI_X_ATTN_SPLITS_NEW, gemv.hip XM_ATTN).  No hand-off inside the launch.
+// (TI_X_ATTN_SPLITS_NEW, gemv.hip XM_ATTN_NT).  The one hand-off inside the launch is the q exchange
+// among a head's S workgroups; every wait in it is bounded (a lost sibling costs a wrong q, not a hang).
 #include <math.h>
 #include <stdlib.h>
 
@@ -44,10 +49,20 @@ struct QkvAttnArgs {
   float scale;
   uint16_t* part_o;            // [heads][S][HD], then k_p [heads][HD] and v_p [heads][HD]
   float* part_ml;              // [heads][S][2], then q [heads][HD]
+  unsigned long long* xchg;    // [heads * S][16] granules {float value, uint32 generation}
   unsigned long long* stamp;
 };
 
 constexpr int kQaWaves = 8, kQaThreads = kQaWaves * kWave;
+#ifndef TI_QA_KV_RING
+#define TI_QA_KV_RING 3   // K / V slots of 8 keys in flight per wave (5: 1704 vs 1722 tok/s, profiles/r6_qa_ab.txt)
+#endif
+#ifndef TI_QA_KV_LATE
+#define TI_QA_KV_LATE 0   // 1: the K/V ring issued after the q part instead of before the GEMV (A/B)
+#endif
+constexpr int kQaMaxK = 2048;
+constexpr int kQaMaxItems = 2;   // weight items per wave and tile: K <= 2048 (KT <= 16)
+constexpr unsigned kQaSpin = 1u << 20;   // bounded wait per granule (~0.1 s)
 
 // gemv.hip int4_x_prep: the high-nibble slots of an x piece scaled by 1/16 (exact in fp16) and the
 // piece's share of the offset correction 1032 * sum_lo x + 1152 * sum_hi x (deq_int4_raw)
@@ -58,7 +73,6 @@ __device__ __forceinline__ float int4_x_prep_qa(f16x8& h) {
   const float hi = ((float)h[2] + (float)h[3]) + ((float)h[6] + (float)h[7]);
   return 1032.0f * lo + 1152.0f * hi;
 }
-constexpr int kQaMaxK = 4096;
 
 // workgroup (h, s) -> its k / v tile (index into the kv_tiles tiles after the q rows), or -1
 __host__ __device__ inline int qa_kv_tile(int h, int s, int heads, int splits, int kv_tiles) {
@@ -71,60 +85,66 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
   const unsigned long long t_entry = stamp_now();
   constexpr int C = TileFmt<BITS>::kChunks;
   constexpr int QT = HD / 16;                 // q tiles of a head
-  constexpr int kMaxT = QT + 1;
-  constexpr int R = 2;                        // ring items per wave (gemv_wq_kernel's depth at int8)
-  __shared__ __attribute__((aligned(16))) f16 xl[kQaMaxK + 8];
-  __shared__ __attribute__((aligned(16))) uint16_t sl[kMaxT][kQaMaxK / 128][16];
+  __shared__ __attribute__((aligned(16))) f16 xl[kQaMaxK + 8 * kQaThreads];
+  __shared__ __attribute__((aligned(16))) uint16_t sl[2][kQaMaxK / 128][16];   // scales: the q tile, the k / v tile
   __shared__ __attribute__((aligned(16))) float corr[kQaMaxK / 128][16];
   __shared__ u32x4 sl_dummy;
-  __shared__ float slab[kMaxT][kQaWaves][16];
+  __shared__ float slab[2][kQaWaves][16];
   __shared__ float q_s[HD];
   __shared__ float s_m[kQaWaves], s_l[kQaWaves];
   __shared__ __attribute__((aligned(16))) float s_acc[kQaWaves][HD];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = (int)blockIdx.x % a.heads, s = (int)blockIdx.x / a.heads;
+  // blockIdx = s + S h: split s of every head on XCD s % 8 (blockIdx % 8), so the G q-heads of a kv-head
+  // that read the same key range share that XCD's L2 (heads on the same XCD would read every kv-head's
+  // keys from each of the 8 L2s)
+  const int S = a.splits, h = (int)blockIdx.x / S, s = (int)blockIdx.x % S;
   const int K = a.K, KT = K >> 7, K8 = K >> 3;
   const int qd = a.heads * HD, kvd = a.kv_heads * HD;
-  const int jkv = qa_kv_tile(h, s, a.heads, a.splits, a.kv_tiles);
-  const int ntl = QT + (jkv >= 0 ? 1 : 0);
-  auto gtile = [&](int tl) { return tl < QT ? h * QT + tl : qd / 16 + jkv; };
+  const int kparts = S / QT, tq = s % QT, kp = s / QT;   // this workgroup's q tile and k-part
+  const int KTP = KT / kparts;                           // k-tiles of a part (a multiple of 8)
+  const int jkv = qa_kv_tile(h, s, a.heads, S, a.kv_tiles);
+  const int gq = h * QT + tq, gk = qd / 16 + (jkv >= 0 ? jkv : 0);   // global tiles
+  unsigned long long* my_slot = a.xchg + ((size_t)h * S + s) * 16;
 
-  // ---- 1. small inputs first: position, scales, x piece, the rms partials; then the weight ring.
-  // The position goes through a VGPR the compiler cannot prove uniform (a uniform load would be
-  // waited for at once, in front of every other load), and is made scalar after the staging barrier.
+  // ---- 1. small inputs first: position, own generation, scales, x piece, the rms partials, then the
+  // whole weight stream.  The position goes through a VGPR the compiler cannot prove uniform (a
+  // uniform load would be waited for at once, in front of every other load).
   int zero;
   asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
   const int p_v = a.pos[zero];
-  // scales: ntl * KT rows of 16 fp16 = ntl * KT * 2 <= 320 pieces of 16 bytes, one per thread
-  const int n_sc = ntl * KT * 2;
+  const unsigned long long gen_prev = ld_sc1_u64(my_slot + (zero & 15));
+  // scales: the q tile's k-part and the k / v tile, 16-byte pieces (KT * 2 per whole tile)
+  const int n_scq = KTP * 2, n_sc = n_scq + (jkv >= 0 ? KT * 2 : 0);
   u32x4 sc_reg;
   {
-    const int ic = tid < n_sc ? tid : 0, tl = ic / (KT * 2), rem = ic - tl * KT * 2;
-    sc_reg = *((const u32x4*)(a.scales + (size_t)gtile(tl) * KT * 16) + rem);
+    const int ic = tid < n_sc ? tid : 0;
+    const u32x4* src = ic < n_scq ? (const u32x4*)(a.scales + ((size_t)gq * KT + kp * KTP) * 16) + ic
+                                  : (const u32x4*)(a.scales + (size_t)gk * KT * 16) + (ic - n_scq);
+    sc_reg = *src;
   }
   const u32x4 xr = *(const u32x4*)(a.fx + 8 * (tid < K8 ? tid : K8 - 1));
   float ss4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) ss4[j] = a.ss[lane + 64 * j < a.n_ss ? lane + 64 * j : 0];
-
-  const int KW = wave < KT ? (KT - wave + kQaWaves - 1) / kQaWaves : 0;   // k-tiles per tile, this wave
-  const int total = ntl * KW;
-  int rt = 0, rk = 0, rj = 0;
-  auto refill_ptr = [&]() -> const u32x4* {
-    const int t = rj < total ? rt : ntl - 1, k = rj < total ? rk : KW - 1;   // past the end: the last item again
-    ++rj;
-    if (++rk == KW) { rk = 0; ++rt; }
-    return a.tiles + ((size_t)gtile(t) * KT + wave + kQaWaves * k) * (kWave * C) + lane;
-  };
-  u32x4 ring[R][C];   // (total >= 1: K >= 1024; no branch around loads, so no wait at a join)
+  // weights: q items kt = kp * KTP + wave + 8 i (i < KTP / 8), k / v items kt = wave + 8 i (i < KT / 8)
+  const int nq = KTP / kQaWaves, nk = jkv >= 0 ? KT / kQaWaves : 0;
+  u32x4 wq[kQaMaxItems][C], wk[kQaMaxItems][C];
 #pragma unroll
-  for (int q = 0; q < R; ++q) {
-    const u32x4* src = refill_ptr();
+  for (int i = 0; i < kQaMaxItems; ++i)
+    if (i < nq) {   // (wave-uniform)
+      const u32x4* src = a.tiles + ((size_t)gq * KT + kp * KTP + wave + kQaWaves * i) * (kWave * C) + lane;
 #pragma unroll
-    for (int c = 0; c < C; ++c) ring[q][c] = __builtin_nontemporal_load(src + c * kWave);
-  }
+      for (int c = 0; c < C; ++c) wq[i][c] = *(src + c * kWave);
+    }
+#pragma unroll
+  for (int i = 0; i < kQaMaxItems; ++i)
+    if (i < nk) {
+      const u32x4* src = a.tiles + ((size_t)gk * KT + wave + kQaWaves * i) * (kWave * C) + lane;
+#pragma unroll
+      for (int c = 0; c < C; ++c) wk[i][c] = __builtin_nontemporal_load(src + c * kWave);
+    }
 
   // ---- 2. stage x (int4: the high-nibble slots scaled by 1/16 and the offset correction, as
   // gemv_wq_kernel's register prep), the scales; rms of the row
@@ -133,15 +153,16 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     float part = 0.0f;
     if constexpr (BITS == 4) part = int4_x_prep_qa(hx);
     *(f16x8*)(xl + 8 * tid) = hx;   // (every thread: no branch for the compiler to sink the x load into;
-                                    // pieces past K land in unused LDS, 8 * 512 <= kQaMaxK + 8)
+                                    // pieces past K land in LDS no one reads)
     if constexpr (BITS == 4) {
       part = group_sum<16>(part);
       if (tid < K8 && (lane & 15) == 0) corr[tid >> 4][0] = part;
     }
   }
   // (every thread stores, the surplus into a dummy slot: a conditional store lets the compiler sink the
-  // load into the branch, behind the weight ring, and wait for the whole ring there)
-  *(tid < n_sc ? (u32x4*)&sl[0][0][0] + (tid / (KT * 2)) * (kQaMaxK / 128) * 2 + tid % (KT * 2) : &sl_dummy) = sc_reg;
+  // load into the branch, behind the weight stream, and wait for all of it there)
+  *(tid < n_scq ? (u32x4*)&sl[0][0][0] + (kp * KTP * 2 + tid)
+                : tid < n_sc ? (u32x4*)&sl[1][0][0] + (tid - n_scq) : &sl_dummy) = sc_reg;
   float rms;
   {
     float t = 0.0f;
@@ -153,21 +174,22 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  STAMP_MARK(ph_staged);
   const int p = __builtin_amdgcn_readfirstlane(p_v);
+  const unsigned gen = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(gen_prev >> 32)) + 1u;
 
-  // RoPE (cos, sin) of the epilogue thread's output pair (threads < ntl * 16: tile tid >> 4, row tid & 15)
+  // RoPE (cos, sin) of the thread's q dim (threads < HD) or k row (threads 64 + n of the k / v tile)
   // (loaded by every thread, clamped: no branch around the load)
   float2 cs;
   {
-    const int tl = tid < ntl * 16 ? tid >> 4 : 0, ng = gtile(tl) * 16 + (tid & 15);
-    const int d = (ng < qd ? ng : ng - qd) % HD;   // (v rows: an unused pair)
+    const int d = tid < HD ? tid : ((jkv >= 0 ? jkv : 0) * 16 + (tid & 15)) % HD;
     cs = *(const float2*)(a.rope_cs + (size_t)p * HD + (d & ~1));
   }
 
-  // ---- 3. the K/V ring of the attention goes out now (its addresses need only p), ahead of the stream
-  constexpr int LPK = HD / 8, KPW = 64 / LPK, RA = 3;
+  // ---- 3. the K/V ring of the attention goes out now (its addresses need only p)
+  constexpr int LPK = HD / 8, KPW = 64 / LPK, RA = TI_QA_KV_RING;   // (5: a whole 2048-key split in flight)
   const int dl = lane % LPK, kg = lane / LPK;
-  const int S = a.splits, L = p;   // the old keys [0, p); split S - 1 is last_extra keys short
+  const int L = p;   // the old keys [0, p); split S - 1 is last_extra keys short
   const int chunk = (L + a.last_extra + S - 1) / S;
   const int s0 = min(L, s * chunk), s1 = s == S - 1 ? L : min(L, s0 + chunk);
   const int nslot = s1 > s0 ? (s1 - s0 + KPW - 1) / KPW : 0;
@@ -182,19 +204,18 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     kr[q] = ld_kv((const u32x4*)(a.kc + kv_off + (size_t)key * HD + dl * 8));
     vr[q] = ld_kv((const u32x4*)(a.vc + kv_off + (size_t)key * HD + dl * 8));
   };
+#if !TI_QA_KV_LATE
 #pragma unroll
   for (int q = 0; q < RA; ++q) arefill(q);
+#endif
 
-  // ---- 4. the stream (gemv_wq_kernel's item: 4 MFMA steps, the int4 correction, one fp32 FMA by
-  // the group scale; a tile's last item lands in the slab)
+  // ---- 4. the GEMV items (gemv_wq_kernel's: 4 MFMA steps, the int4 correction, one fp32 FMA by the
+  // group scale), the q part and the k / v tile each into its slab row
   const int r = lane & 15, kq = lane >> 4;
   const f16* xrow = xl + kq * 32;
-  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
   uint32_t magic;
   asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(magic));
-  int ct = 0, ck = 0;
-  auto item = [&](const u32x4 (&w)[C]) {
-    const int kt = wave + kQaWaves * ck;
+  auto item = [&](const u32x4 (&w)[C], int kt, const uint16_t* scl, f32x4& acc) {
     f32x4 t = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
@@ -203,77 +224,95 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
       t = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, t, 0, 0, 0);
     }
     if constexpr (BITS == 4) t -= *(const f32x4*)(&corr[kt][4 * kq]);
-    const float sc = h2f(sl[ct][kt][r]);
+    const float sc = h2f(scl[kt * 16 + r]);
     acc[0] = fmaf(sc, t[0], acc[0]);
     acc[1] = fmaf(sc, t[1], acc[1]);
     acc[2] = fmaf(sc, t[2], acc[2]);
     acc[3] = fmaf(sc, t[3], acc[3]);
-    const bool last = ++ck == KW;
-    if (last) {
-      if (lane < 16) slab[ct][wave][lane] = acc[0];   // row 0 of the C layout: lanes 0-15, component 0
-      acc = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-      ck = 0;
-      ++ct;
-    }
   };
-  int j0 = 0;
-  for (; j0 + R <= total; j0 += R) {
+  {   // the q part first: the head's siblings wait for it
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int q = 0; q < R; ++q) {
-      item(ring[q]);
-      const u32x4* src = refill_ptr();
-#pragma unroll
-      for (int c = 0; c < C; ++c) ring[q][c] = __builtin_nontemporal_load(src + c * kWave);
-    }
+    for (int i = 0; i < kQaMaxItems; ++i)
+      if (i < nq) item(wq[i], kp * KTP + wave + kQaWaves * i, &sl[0][0][0], acc);
+    if (lane < 16) slab[0][wave][lane] = acc[0];   // row 0 of the C layout: lanes 0-15, component 0
   }
-#pragma unroll
-  for (int q = 0; q < R; ++q)
-    if (j0 + q < total) item(ring[q]);
-  if (KW == 0)
-    for (int tl = 0; tl < ntl; ++tl)
-      if (lane < 16) slab[tl][wave][lane] = 0.0f;
-
-  // ---- 5. reduce the 8 waves' partials per output (fixed order), / rms, the QKV epilogue
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  if (tid < 2 * kWave) {   // waves 0, 1 (ntl * 16 <= 80 outputs)
-    const int t = tid, ok = t < ntl * 16, tl = ok ? t >> 4 : 0, n = lane & 15;
-    float v = slab[tl][0][n];
+  STAMP_MARK(ph_qpart);
+#if TI_QA_KV_LATE   // the K/V ring after the q part: the keys then do not compete with the q stream
 #pragma unroll
-    for (int w = 1; w < kQaWaves; ++w) v += slab[tl][w][n];
+  for (int q = 0; q < RA; ++q) arefill(q);
+#endif
+  // ---- 5. wave 0: publish the q part (16 sums over the 8 waves, fixed order); then the k / v tile
+  if (wave == 0 && lane < 16) {
+    float v = slab[0][0][lane];
+#pragma unroll
+    for (int w = 1; w < kQaWaves; ++w) v += slab[0][w][lane];
+    st_sc1_u64(my_slot + lane, ((unsigned long long)gen << 32) | __builtin_bit_cast(uint32_t, v));
+  }
+  if (jkv >= 0) {
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < kQaMaxItems; ++i)
+      if (i < nk) item(wk[i], wave + kQaWaves * i, &sl[1][0][0], acc);
+    if (lane < 16) slab[1][wave][lane] = acc[0];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // (uniform: jkv is the workgroup's)
+    asm volatile("" ::: "memory");
+  }
+  // wave 1: the k / v tile's epilogue (/ rms, RoPE of k, the cache row and the per-q-head copies)
+  if (wave == 1 && jkv >= 0) {
+    const int n = lane & 15;
+    float v = slab[1][0][n];
+#pragma unroll
+    for (int w = 1; w < kQaWaves; ++w) v += slab[1][w][n];
     v = v / rms;
     const float partner = lane_xor<1>(v);
-    const int ng = gtile(tl) * 16 + n;
-    if (ok) {
-      const bool qk = ng < qd + kvd;
+    if (lane < 16) {
+      const int ng = gk * 16 + n;
+      const bool is_k = ng < qd + kvd;
       float rr = v;
-      int d = 0;
-      if (qk) {
-        const int base = ng < qd ? 0 : qd;
-        d = (ng - base) % HD;
-        // apply_rope (tensor_engine.cpp:1602-1612), the unfused epilogue's contraction pattern
+      if (is_k) {
+        const int d = (ng - qd) % HD;
         rr = (d & 1) == 0 ? fmaf(-partner, cs.y, v * cs.x) : fmaf(v, cs.x, partner * cs.y);
       }
-      if (ng < qd) {
-        q_s[d] = rr;
-        if (s == 0) a.part_ml[(size_t)a.heads * S * 2 + (size_t)h * HD + d] = rr;
-      } else {
-        const bool is_k = qk;
-        const int c = ng - qd - (is_k ? 0 : kvd), kvh = c / HD, dd = c - kvh * HD;
-        const uint16_t hv = f2h(rr);
-        (is_k ? a.kc : a.vc)[((size_t)kvh * a.max_seq + p) * HD + dd] = hv;
-        // the new key / value for the O projection's merge, once per q-head of the kv-head
-        uint16_t* nt = a.part_o + (size_t)a.heads * S * HD + (is_k ? 0 : (size_t)a.heads * HD);
-        for (int g = 0; g < (1 << a.kv_shift); ++g) nt[(size_t)((kvh << a.kv_shift) + g) * HD + dd] = hv;
-      }
+      const int c = ng - qd - (is_k ? 0 : kvd), kvh = c / HD, dd = c - kvh * HD;
+      const uint16_t hv = f2h(rr);
+      (is_k ? a.kc : a.vc)[((size_t)kvh * a.max_seq + p) * HD + dd] = hv;
+      uint16_t* nt = a.part_o + (size_t)a.heads * S * HD + (is_k ? 0 : (size_t)a.heads * HD);
+      for (int g = 0; g < (1 << a.kv_shift); ++g) nt[(size_t)((kvh << a.kv_shift) + g) * HD + dd] = hv;
     }
+  }
+
+  // ---- 6. wave 0: gather the head's q from its S workgroups (tile d / 16 from workgroups tile + QT
+  // part, parts in order), / rms, RoPE (tensor_engine.cpp:1602-1612, the fused epilogue's pattern)
+  if (wave == 0) {
+    const int d = lane, t = d >> 4, n = d & 15;
+    float v = 0.0f;
+    for (int part = 0; part < kparts; ++part) {
+      const unsigned long long* g = a.xchg + ((size_t)h * S + t + QT * part) * 16 + n;
+      unsigned long long x = ld_sc1_u64(g);
+      unsigned spin = 0;
+      while ((unsigned)(x >> 32) != gen && ++spin < kQaSpin) {
+        __builtin_amdgcn_s_sleep(1);
+        x = ld_sc1_u64(g);
+      }
+      v += __builtin_bit_cast(float, (uint32_t)x);
+    }
+    v = v / rms;
+    const float partner = lane_xor<1>(v);
+    const float rr = (d & 1) == 0 ? fmaf(-partner, cs.y, v * cs.x) : fmaf(v, cs.x, partner * cs.y);
+    q_s[d] = rr;
+    if (s == 0) a.part_ml[(size_t)a.heads * S * 2 + (size_t)h * HD + d] = rr;
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  STAMP_MARK(ph_gathered);
 
-  // ---- 6. attention of q_h over the split's old keys (attn_split_body, one q-head, LPK lanes a key)
+  // ---- 7. attention of q_h over the split's old keys (attn_split_body, one q-head, LPK lanes a key)
   float qf[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) qf[e] = q_s[dl * 8 + e] * a.scale;
@@ -287,11 +326,11 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     float kf[8], vf[8];
     unpack8(kv, kf);
     unpack8(vv, vf);
-    float d = 0.0f;
+    float dq = 0.0f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) d = fmaf(qf[e], kf[e], d);
-    d = group_sum<LPK>(d);
-    const float sc = valid ? d : -INFINITY;
+    for (int e = 0; e < 8; ++e) dq = fmaf(qf[e], kf[e], dq);
+    dq = group_sum<LPK>(dq);
+    const float sc = valid ? dq : -INFINITY;
     const float mn = fmaxf(mrun, sc);
     const float alpha = mrun == mn ? 1.0f : __expf(mrun - mn);
     const float pr = valid ? __expf(sc - mn) : 0.0f;
@@ -321,6 +360,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     mrun = mx;
     lrun = l;
   }
+  STAMP_MARK(ph_attn);
   if (lane < LPK)
 #pragma unroll
     for (int e = 0; e < 8; ++e) s_acc[wave][dl * 8 + e] = oacc[e];
@@ -347,7 +387,8 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     a.part_o[rrow * HD + d] = f2h(l > 0.0f ? o / l : 0.0f);
     if (d == 0) *(float2*)(a.part_ml + 2 * rrow) = make_float2(mx, l);
   }
-  stamp_end(a.stamp, t_entry);
+  STAMP_MARK(ph_end);
+  stamp_end(a.stamp, t_entry, ph_staged, ph_qpart, ph_gathered, ph_attn, ph_end, ph_end, ph_attn);
 }
 
 }  // namespace ti
@@ -360,26 +401,32 @@ extern "C" size_t ti_qkv_attn_part_o_elems(int heads, int head_dim, int splits) 
 extern "C" size_t ti_qkv_attn_part_ml_elems(int heads, int head_dim, int splits) {
   return (size_t)heads * 2 * (size_t)splits + (size_t)heads * head_dim;
 }
+extern "C" size_t ti_qkv_attn_xchg_bytes(int heads, int splits) { return (size_t)heads * splits * 16 * 8; }
 
 extern "C" int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, int bits, const uint16_t* fx,
                                     const float* ss_in, int n_ss, float eps, const float* rope_cs, const int32_t* pos,
                                     uint16_t* k_cache, uint16_t* v_cache, int max_seq, int K, int heads, int kv_heads,
-                                    int head_dim, int splits, uint16_t* part_o, float* part_ml, ti_stream_t stream) {
-  if (!tiles || !scales || !fx || !ss_in || !rope_cs || !pos || !k_cache || !v_cache || !part_o || !part_ml)
+                                    int head_dim, int splits, uint16_t* part_o, float* part_ml, void* xchg,
+                                    ti_stream_t stream) {
+  if (!tiles || !scales || !fx || !ss_in || !rope_cs || !pos || !k_cache || !v_cache || !part_o || !part_ml || !xchg)
     return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_partials: null pointer");
   if (bits != 4 && bits != 8)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_partials: bits %d (4 or 8)", bits);
   if (head_dim != 64) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_partials: head_dim %d (64)", head_dim);
+  const int QT = head_dim / 16, KT = K / 128;
   if (K < 1024 || K > kQaMaxK || K % 128 || n_ss < 1 || n_ss > 256 || max_seq < 1)
-    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_partials: K %d (1024..%d, % 128), n_ss %d (1..256)", K, kQaMaxK, n_ss);
+    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_partials: K %d (1024..%d, %% 128), n_ss %d (1..256)", K, kQaMaxK, n_ss);
   int kv_shift = 0;
   while (kv_heads > 0 && (kv_heads << kv_shift) < heads) ++kv_shift;
   if (kv_heads < 1 || heads <= kv_heads || (kv_heads << kv_shift) != heads || heads % 8)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_partials: heads %d / kv_heads %d (GQA, power of two, heads %% 8)",
                         heads, kv_heads);
   const int kv_tiles = 2 * kv_heads * head_dim / 16;
-  if (splits < 2 || splits > TI_ATTN_MAX_PART_SPLITS || kv_tiles > heads * splits)
-    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_partials: splits %d not in [2, %d]", splits, TI_ATTN_MAX_PART_SPLITS);
+  // splits: a multiple of the q tiles of a head, each k-part a multiple of 8 k-tiles (whole waves)
+  if (splits < QT || splits > TI_ATTN_MAX_PART_SPLITS || splits % QT || KT % (splits / QT) ||
+      (KT / (splits / QT)) % 8 || kv_tiles > heads * splits)
+    return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_partials: splits %d (a multiple of %d up to %d that splits %d k-tiles "
+                        "into multiples of 8)", splits, QT, TI_ATTN_MAX_PART_SPLITS, KT);
   QkvAttnArgs a;
   a.tiles = (const u32x4*)tiles;
   a.scales = scales;
@@ -398,19 +445,22 @@ extern "C" int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, i
   a.kv_shift = kv_shift;
   a.splits = splits;
   a.kv_tiles = kv_tiles;
-  // the last split's workgroups also stream a k / v tile (when every head's has one): give that split
-  // as many fewer keys as the tile has bytes (TI_QA_EXTRA overrides, 0 = equal splits)
+  // the last split's workgroups also compute a k / v tile (when every head's has one): give that split
+  // twice as many fewer keys as the tile has bytes (its epilogue and cache writes besides; 0 / 1x / 2x:
+  // 1684 / 1704 / 1710 tok/s with the 5-slot ring, 1x / 2x 1716 / 1730 with 3 slots, profiles/r6_qa_ab.txt;
+  // TI_QA_EXTRA overrides, 0 = equal splits)
   {
-    const int tile_bytes = (K / 128) * 1024 * (bits / 4), key_bytes = 2 * head_dim * 2;
+    const int tile_bytes = KT * 1024 * (bits / 4), key_bytes = 2 * head_dim * 2;
     static const int env = [] {
       const char* v = getenv("TI_QA_EXTRA");
       return v ? atoi(v) : -1;
     }();
-    a.last_extra = env >= 0 ? env : kv_tiles >= heads ? tile_bytes / key_bytes : 0;
+    a.last_extra = env >= 0 ? env : kv_tiles >= heads ? 2 * tile_bytes / key_bytes : 0;
   }
   a.scale = 1.0f / sqrtf((float)head_dim);   // tensor_engine.cpp:1288, as ti_attn_decode
   a.part_o = part_o;
   a.part_ml = part_ml;
+  a.xchg = (unsigned long long*)xchg;
   const int grid = heads * splits;
   a.stamp = ti_stamp_next(STAMP_ATTN, grid);
   hipStream_t s = (hipStream_t)stream;
