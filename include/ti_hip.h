@@ -339,6 +339,8 @@ int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, int bits, co
 size_t ti_qkv_attn_part_o_elems(int heads, int head_dim, int splits);
 size_t ti_qkv_attn_part_ml_elems(int heads, int head_dim, int splits);
 size_t ti_qkv_attn_xchg_bytes(int heads, int splits);
+/* 1 when ti_qkv_attn_partials has a kernel for this shape (0: it would return TI_ERR_UNSUPPORTED / ARG). */
+int ti_qkv_attn_supported(int bits, int K, int heads, int kv_heads, int head_dim, int splits);
 /* Prefill attention (forward_pass over a prompt chunk, inference_engine.cpp:1429-1491 ->
  * multi_head_attention, tensor_engine.cpp:1149-1252): the M rows are tokens of ONE stream whose
  * cache k_cache / v_cache [kv_heads][max_seq][head_dim] fp16 already holds their K / V; row m

@@ -35,16 +35,20 @@ def gemm(ti, td, sd, bits, x_ptr, x_kind, ldx, M, N, K, ep, eps=1e-5):
     ti.sync()
 
 
-@pytest.mark.parametrize("bits,K,heads,kv_heads,p,splits", [
-    (8, 2048, 32, 4, 2047, 8),    # TinyLlama-1.1B at the bench position
-    (8, 2048, 32, 4, 300, 8),
-    (4, 2048, 32, 4, 777, 8),
-    (8, 1024, 16, 4, 5, 4),       # short: most splits empty
-    (8, 2048, 32, 4, 0, 8),       # first token: every split empty, O merges the new key alone
+@pytest.mark.parametrize("bits,K,heads,kv_heads,p,splits,hd", [
+    (8, 2048, 32, 4, 2047, 8, 64),    # TinyLlama-1.1B at the bench position
+    (8, 2048, 32, 4, 300, 8, 64),
+    (4, 2048, 32, 4, 777, 8, 64),
+    (8, 1024, 16, 4, 5, 4, 64),       # short: most splits empty
+    (8, 2048, 32, 4, 0, 8, 64),       # first token: every split empty, O merges the new key alone
+    (4, 4096, 32, 32, 2047, 8, 128),  # Llama-2-7B (MHA: every workgroup a k and a v tile)
+    (4, 4096, 32, 32, 3, 8, 128),
+    (8, 4096, 32, 32, 1000, 8, 128),
 ])
-def test_fused_matches_unfused_launches(ti, oracle, bits, K, heads, kv_heads, p, splits):
-    rng = np.random.RandomState(bits * 1000 + p + heads)
-    hd, max_seq, H, eps = 64, 2048, 1024, 1e-5
+def test_fused_matches_unfused_launches(ti, oracle, bits, K, heads, kv_heads, p, splits, hd):
+    rng = np.random.RandomState(bits * 1000 + p + heads + hd)
+    max_seq, H, eps = 2048, 1024, 1e-5
+    assert ti.lib().ti_qkv_attn_supported(bits, K, heads, kv_heads, hd, splits) == 1
     qd, kvd = heads * hd, kv_heads * hd
     N = qd + 2 * kvd
     w = (rng.standard_normal((K, N)) * 0.03).astype(f32)
@@ -127,10 +131,11 @@ def test_fused_matches_unfused_launches(ti, oracle, bits, K, heads, kv_heads, p,
     assert np.all(err <= bound), f"max err {err.max()} (bound {bound.min()})"
 
 
-CFGS = {   # vocab, hidden, layers, heads, kv_heads, head_dim, inter, bits
-    "tl_shape_w8": (32000, 2048, 3, 32, 4, 64, 5632, 8),
-    "tl_shape_w4": (32000, 2048, 2, 32, 4, 64, 5632, 4),
-    "gqa16_w8": (4096, 1024, 2, 16, 4, 64, 2816, 8),
+CFGS = {   # vocab, hidden, layers, heads, kv_heads, head_dim, inter, bits, max_seq
+    "tl_shape_w8": (32000, 2048, 3, 32, 4, 64, 5632, 8, 256),
+    "tl_shape_w4": (32000, 2048, 2, 32, 4, 64, 5632, 4, 256),
+    "gqa16_w8": (4096, 1024, 2, 16, 4, 64, 2816, 8, 256),
+    "l2_shape_w4": (32000, 4096, 2, 32, 32, 128, 11008, 4, 512),   # 8 splits from 512 positions
 }
 
 
@@ -139,10 +144,10 @@ def test_engine_qkv_attn_matches_unfused_steps(ti, name):
     """Twin engines (fused QKV + attention on / off) fed the same tokens: logits within the decode
     tolerance every step from position 0 (all old-key splits empty) on, greedy argmax equal wherever
     the top-2 margin exceeds twice it."""
-    v, h, l, nh, nkv, hd, inter, bits = CFGS[name]
+    v, h, l, nh, nkv, hd, inter, bits, ms = CFGS[name]
     eng = {}
     for on in (True, False):
-        e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=bits, max_seq=256, max_batch=1)
+        e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=bits, max_seq=ms, max_batch=1)
         e.synth(0x9a11, 0.1)
         e.set_prefill(0)
         assert e.set_qkv_attn(on) is on
@@ -163,8 +168,12 @@ def test_engine_qkv_attn_matches_unfused_steps(ti, name):
 
 
 def test_qkv_attn_off_paths(ti):
-    """Not taken where it does not apply: MHA (7B shape), head_dim 128, fold off."""
+    """Not taken where it does not apply: splits that do not divide into the q tiles (head_dim 128 at
+    4 splits), int16 weights, fold off."""
     e = ti.Engine(4096, 1024, 1, 8, 8, 128, 2816, bits=4, max_seq=256, max_batch=1)
+    assert e.set_qkv_attn(True) is False
+    e.close()
+    e = ti.Engine(4096, 1024, 1, 16, 4, 64, 2816, bits=16, max_seq=256, max_batch=1)
     assert e.set_qkv_attn(True) is False
     e.close()
     e = ti.Engine(4096, 1024, 1, 16, 4, 64, 2816, bits=8, max_seq=256, max_batch=1)

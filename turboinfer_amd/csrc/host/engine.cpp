@@ -357,16 +357,13 @@ bool part_usable(ti_engine* e, int M) {
 bool qa_usable(ti_engine* e, int M) {
   const ti_engine_config& c = e->c;
   if (!e->qa_on || M != 1 || !fold_usable(e, M) || !part_usable(e, M)) return false;
-  const int sp = e->splits_for(M), kv_tiles = 2 * e->kvd() / 16, KT = c.hidden / 128;
-  // (the kernel's split shape: a multiple of the 4 q tiles of a head, k-parts of whole 8-k-tile waves;
-  // all heads x splits workgroups resident at once for the q exchange)
+  // all heads x splits workgroups resident at once for the in-launch q exchange
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return false;
-  if (sp % 4 || KT % (sp / 4) || (KT / (sp / 4)) % 8 || c.heads * sp > cus) return false;
-  return c.head_dim == 64 && (c.bits == 4 || c.bits == 8) && c.heads > c.kv_heads && c.heads % 8 == 0 &&
-         (c.heads & (c.heads - 1)) == 0 && (c.kv_heads & (c.kv_heads - 1)) == 0 && c.hidden >= 1024 &&
-         c.hidden <= 2048 && kv_tiles <= c.heads * sp && ti_gemm_grid(1, c.hidden, c.inter) <= 256;
+  const int sp = e->splits_for(M);
+  return c.heads * sp <= cus && ti_gemm_grid(1, c.hidden, c.inter) <= 256 &&
+         ti_qkv_attn_supported(c.bits, c.hidden, c.heads, c.kv_heads, c.head_dim, sp);
 }
 
 // One decode step for streams [0, M) on e->s.  Graph-capturable (no host sync / alloc).

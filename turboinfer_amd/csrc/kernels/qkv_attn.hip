@@ -57,11 +57,17 @@ constexpr int kQaWaves = 8, kQaThreads = kQaWaves * kWave;
 #ifndef TI_QA_KV_RING
 #define TI_QA_KV_RING 3   // K / V slots of 8 keys in flight per wave (5: 1704 vs 1722 tok/s, profiles/r6_qa_ab.txt)
 #endif
-#ifndef TI_QA_KV_LATE
-#define TI_QA_KV_LATE 0   // 1: the K/V ring issued after the q part instead of before the GEMV (A/B)
+#ifndef TI_QA_KVW_LATE
+#define TI_QA_KVW_LATE 0   // 1: the k / v tiles' weights issued after the q part instead of after staging (A/B)
 #endif
-constexpr int kQaMaxK = 2048;
-constexpr int kQaMaxItems = 2;   // weight items per wave and tile: K <= 2048 (KT <= 16)
+#ifndef TI_QA_KV_LATE
+// the K/V ring issued after the q part (1) or before the GEMV (0); -1: after at head_dim 128, where a
+// workgroup's keys are 4x a q part's bytes (7B 790.6 vs 776.5 tok/s), before at 64 (TinyLlama 1733 vs
+// 1712; profiles/r6_qa_ab.txt)
+#define TI_QA_KV_LATE -1
+#endif
+constexpr int kQaMaxK = 4096;
+constexpr int kQaMaxKv = 2;      // k / v tiles per workgroup (MHA at 8 splits: a k and a v tile each)
 constexpr unsigned kQaSpin = 1u << 20;   // bounded wait per granule (~0.1 s)
 
 // gemv.hip int4_x_prep: the high-nibble slots of an x piece scaled by 1/16 (exact in fp16) and the
@@ -74,22 +80,27 @@ __device__ __forceinline__ float int4_x_prep_qa(f16x8& h) {
   return 1032.0f * lo + 1152.0f * hi;
 }
 
-// workgroup (h, s) -> its k / v tile (index into the kv_tiles tiles after the q rows), or -1
-__host__ __device__ inline int qa_kv_tile(int h, int s, int heads, int splits, int kv_tiles) {
-  const int j = h + heads * (splits - 1 - s);
+// workgroup (h, s) -> its i-th k / v tile (index into the kv_tiles tiles after the q rows), or -1: tiles
+// j = h + heads (S - 1 - s) + heads S i, so split S - 1 takes them first when there are fewer than
+// workgroups (GQA), and every workgroup two when there are twice as many (MHA)
+__host__ __device__ inline int qa_kv_tile(int h, int s, int i, int heads, int splits, int kv_tiles) {
+  const int j = h + heads * (splits - 1 - s) + heads * splits * i;
   return j < kv_tiles ? j : -1;
 }
 
-template <int BITS, int HD>
+// NQ: q items per wave (k-tiles of the part / 8), NK: items per wave of a k / v tile (k-tiles / 8): compile-time,
+// so the weight loads need no branch (a branch around a load whose value feeds a phi makes the compiler
+// wait for it at once)
+template <int BITS, int HD, int NQ, int NK>
 __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnArgs a) {
   const unsigned long long t_entry = stamp_now();
   constexpr int C = TileFmt<BITS>::kChunks;
   constexpr int QT = HD / 16;                 // q tiles of a head
-  __shared__ __attribute__((aligned(16))) f16 xl[kQaMaxK + 8 * kQaThreads];
-  __shared__ __attribute__((aligned(16))) uint16_t sl[2][kQaMaxK / 128][16];   // scales: the q tile, the k / v tile
+  __shared__ __attribute__((aligned(16))) f16 xl[kQaMaxK + 8];   // (8 * 512 threads = kQaMaxK)
+  __shared__ __attribute__((aligned(16))) uint16_t sl[1 + kQaMaxKv][kQaMaxK / 128][16];   // scales: q tile, k / v tiles
   __shared__ __attribute__((aligned(16))) float corr[kQaMaxK / 128][16];
   __shared__ u32x4 sl_dummy;
-  __shared__ float slab[2][kQaWaves][16];
+  __shared__ float slab[1 + kQaMaxKv][kQaWaves][16];
   __shared__ float q_s[HD];
   __shared__ float s_m[kQaWaves], s_l[kQaWaves];
   __shared__ __attribute__((aligned(16))) float s_acc[kQaWaves][HD];
@@ -104,8 +115,14 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
   const int qd = a.heads * HD, kvd = a.kv_heads * HD;
   const int kparts = S / QT, tq = s % QT, kp = s / QT;   // this workgroup's q tile and k-part
   const int KTP = KT / kparts;                           // k-tiles of a part (a multiple of 8)
-  const int jkv = qa_kv_tile(h, s, a.heads, S, a.kv_tiles);
-  const int gq = h * QT + tq, gk = qd / 16 + (jkv >= 0 ? jkv : 0);   // global tiles
+  int gk[kQaMaxKv], nkv = 0;   // global tiles of the workgroup's k / v tiles (the first nkv)
+#pragma unroll
+  for (int i = 0; i < kQaMaxKv; ++i) {
+    const int j = qa_kv_tile(h, s, i, a.heads, S, a.kv_tiles);
+    gk[i] = qd / 16 + (j >= 0 ? j : 0);
+    nkv += j >= 0 ? 1 : 0;
+  }
+  const int gq = h * QT + tq;   // global tile of the q part
   unsigned long long* my_slot = a.xchg + ((size_t)h * S + s) * 16;
 
   // ---- 1. small inputs first: position, own generation, scales, x piece, the rms partials, then the
@@ -114,38 +131,31 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
   int zero;
   asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
   const int p_v = a.pos[zero];
-  const unsigned long long gen_prev = ld_sc1_u64(my_slot + (zero & 15));
-  // scales: the q tile's k-part and the k / v tile, 16-byte pieces (KT * 2 per whole tile)
-  const int n_scq = KTP * 2, n_sc = n_scq + (jkv >= 0 ? KT * 2 : 0);
+  // (only the tag word: a 64-bit load whose unused half the allocator hands out again waits at once)
+  const uint32_t gen_prev = ld_sc1_u32((const uint32_t*)(my_slot + (zero & 15)) + 1);
+  // scales: the q tile's k-part and the k / v tiles, 16-byte pieces (KT * 2 per whole tile)
+  const int n_scq = KTP * 2, n_sc = n_scq + nkv * KT * 2;
   u32x4 sc_reg;
   {
-    const int ic = tid < n_sc ? tid : 0;
-    const u32x4* src = ic < n_scq ? (const u32x4*)(a.scales + ((size_t)gq * KT + kp * KTP) * 16) + ic
-                                  : (const u32x4*)(a.scales + (size_t)gk * KT * 16) + (ic - n_scq);
-    sc_reg = *src;
+    // (selects, no branch and no dynamic index into gk[]: either would put a wait in front of the loads)
+    const int ic = tid < n_sc ? tid : 0, r2 = ic - n_scq, ik = r2 >= KT * 2 ? 1 : 0;
+    const int g = ic < n_scq ? gq : ik ? gk[1] : gk[0];
+    const int piece = ic < n_scq ? kp * KTP * 2 + ic : r2 - ik * KT * 2;
+    sc_reg = *((const u32x4*)(a.scales + (size_t)g * KT * 16) + piece);
   }
   const u32x4 xr = *(const u32x4*)(a.fx + 8 * (tid < K8 ? tid : K8 - 1));
   float ss4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) ss4[j] = a.ss[lane + 64 * j < a.n_ss ? lane + 64 * j : 0];
+  asm volatile("" ::: "memory");   // (the small loads stay ahead of the weights: staging waits for them only)
   // weights: q items kt = kp * KTP + wave + 8 i (i < KTP / 8), k / v items kt = wave + 8 i (i < KT / 8)
-  const int nq = KTP / kQaWaves, nk = jkv >= 0 ? KT / kQaWaves : 0;
-  u32x4 wq[kQaMaxItems][C], wk[kQaMaxItems][C];
+  u32x4 wq[NQ][C];
 #pragma unroll
-  for (int i = 0; i < kQaMaxItems; ++i)
-    if (i < nq) {   // (wave-uniform)
-      const u32x4* src = a.tiles + ((size_t)gq * KT + kp * KTP + wave + kQaWaves * i) * (kWave * C) + lane;
+  for (int i = 0; i < NQ; ++i) {
+    const u32x4* src = a.tiles + ((size_t)gq * KT + kp * KTP + wave + kQaWaves * i) * (kWave * C) + lane;
 #pragma unroll
-      for (int c = 0; c < C; ++c) wq[i][c] = *(src + c * kWave);
-    }
-#pragma unroll
-  for (int i = 0; i < kQaMaxItems; ++i)
-    if (i < nk) {
-      const u32x4* src = a.tiles + ((size_t)gk * KT + wave + kQaWaves * i) * (kWave * C) + lane;
-#pragma unroll
-      for (int c = 0; c < C; ++c) wk[i][c] = __builtin_nontemporal_load(src + c * kWave);
-    }
-
+    for (int c = 0; c < C; ++c) wq[i][c] = *(src + c * kWave);
+  }
   // ---- 2. stage x (int4: the high-nibble slots scaled by 1/16 and the offset correction, as
   // gemv_wq_kernel's register prep), the scales; rms of the row
   {
@@ -153,7 +163,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     float part = 0.0f;
     if constexpr (BITS == 4) part = int4_x_prep_qa(hx);
     *(f16x8*)(xl + 8 * tid) = hx;   // (every thread: no branch for the compiler to sink the x load into;
-                                    // pieces past K land in LDS no one reads)
+                                    // pieces past K land in LDS no one reads, 8 * 512 = kQaMaxK)
     if constexpr (BITS == 4) {
       part = group_sum<16>(part);
       if (tid < K8 && (lane & 15) == 0) corr[tid >> 4][0] = part;
@@ -161,8 +171,11 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
   }
   // (every thread stores, the surplus into a dummy slot: a conditional store lets the compiler sink the
   // load into the branch, behind the weight stream, and wait for all of it there)
-  *(tid < n_scq ? (u32x4*)&sl[0][0][0] + (kp * KTP * 2 + tid)
-                : tid < n_sc ? (u32x4*)&sl[1][0][0] + (tid - n_scq) : &sl_dummy) = sc_reg;
+  {
+    const int r2 = tid - n_scq, ik = r2 >= KT * 2 ? 1 : 0;
+    *(tid < n_scq ? (u32x4*)&sl[0][0][0] + (kp * KTP * 2 + tid)
+                  : tid < n_sc ? (u32x4*)&sl[1 + ik][0][0] + (r2 - ik * KT * 2) : &sl_dummy) = sc_reg;
+  }
   float rms;
   {
     float t = 0.0f;
@@ -176,15 +189,35 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
   asm volatile("" ::: "memory");
   STAMP_MARK(ph_staged);
   const int p = __builtin_amdgcn_readfirstlane(p_v);
-  const unsigned gen = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(gen_prev >> 32)) + 1u;
+  const unsigned gen = (unsigned)__builtin_amdgcn_readfirstlane((int)gen_prev) + 1u;
 
-  // RoPE (cos, sin) of the thread's q dim (threads < HD) or k row (threads 64 + n of the k / v tile)
-  // (loaded by every thread, clamped: no branch around the load)
+  // RoPE (cos, sin) of the thread's q dim (threads < HD) or k row (wave 2 + i, lanes < 16: the i-th
+  // k / v tile's row) (loaded by every thread, clamped: no branch around the load)
   float2 cs;
   {
-    const int d = tid < HD ? tid : ((jkv >= 0 ? jkv : 0) * 16 + (tid & 15)) % HD;
+    const int gkw = wave == 3 ? gk[1] : gk[0];
+    const int d = tid < HD ? tid : ((gkw - qd / 16) * 16 + (tid & 15)) % HD;
     cs = *(const float2*)(a.rope_cs + (size_t)p * HD + (d & ~1));
   }
+
+  // the k / v tiles' weights after the staging barrier (a branch around loads issued before it would make
+  // the staging wait count them: they are needed only after the q part)
+  u32x4 wk[kQaMaxKv][NK][C];
+  auto load_kv_weights = [&]() {
+#pragma unroll
+    for (int t = 0; t < kQaMaxKv; ++t)
+#pragma unroll
+      for (int i = 0; i < NK; ++i)
+        if (t < nkv) {   // (wave-uniform)
+          const u32x4* src = a.tiles + ((size_t)gk[t] * KT + wave + kQaWaves * i) * (kWave * C) + lane;
+#pragma unroll
+          for (int c = 0; c < C; ++c) wk[t][i][c] = __builtin_nontemporal_load(src + c * kWave);
+        }
+  };
+#if !TI_QA_KVW_LATE
+  load_kv_weights();
+#endif
+
 
   // ---- 3. the K/V ring of the attention goes out now (its addresses need only p)
   constexpr int LPK = HD / 8, KPW = 64 / LPK, RA = TI_QA_KV_RING;   // (5: a whole 2048-key split in flight)
@@ -204,10 +237,11 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     kr[q] = ld_kv((const u32x4*)(a.kc + kv_off + (size_t)key * HD + dl * 8));
     vr[q] = ld_kv((const u32x4*)(a.vc + kv_off + (size_t)key * HD + dl * 8));
   };
-#if !TI_QA_KV_LATE
+  constexpr bool kKvLate = TI_QA_KV_LATE < 0 ? HD == 128 : TI_QA_KV_LATE != 0;
+  if constexpr (!kKvLate) {
 #pragma unroll
-  for (int q = 0; q < RA; ++q) arefill(q);
-#endif
+    for (int q = 0; q < RA; ++q) arefill(q);
+  }
 
   // ---- 4. the GEMV items (gemv_wq_kernel's: 4 MFMA steps, the int4 correction, one fp32 FMA by the
   // group scale), the q part and the k / v tile each into its slab row
@@ -233,18 +267,20 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
   {   // the q part first: the head's siblings wait for it
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int i = 0; i < kQaMaxItems; ++i)
-      if (i < nq) item(wq[i], kp * KTP + wave + kQaWaves * i, &sl[0][0][0], acc);
+    for (int i = 0; i < NQ; ++i) item(wq[i], kp * KTP + wave + kQaWaves * i, &sl[0][0][0], acc);
     if (lane < 16) slab[0][wave][lane] = acc[0];   // row 0 of the C layout: lanes 0-15, component 0
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   STAMP_MARK(ph_qpart);
-#if TI_QA_KV_LATE   // the K/V ring after the q part: the keys then do not compete with the q stream
-#pragma unroll
-  for (int q = 0; q < RA; ++q) arefill(q);
+#if TI_QA_KVW_LATE   // the k / v tiles' weights only now: nothing competes with the q part's bytes
+  load_kv_weights();
 #endif
+  if constexpr (kKvLate) {   // the K/V ring after the q part: the keys then do not compete with the q stream
+#pragma unroll
+    for (int q = 0; q < RA; ++q) arefill(q);
+  }
   // ---- 5. wave 0: publish the q part (16 sums over the 8 waves, fixed order); then the k / v tile
   if (wave == 0 && lane < 16) {
     float v = slab[0][0][lane];
@@ -252,26 +288,29 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     for (int w = 1; w < kQaWaves; ++w) v += slab[0][w][lane];
     st_sc1_u64(my_slot + lane, ((unsigned long long)gen << 32) | __builtin_bit_cast(uint32_t, v));
   }
-  if (jkv >= 0) {
-    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (nkv > 0) {
 #pragma unroll
-    for (int i = 0; i < kQaMaxItems; ++i)
-      if (i < nk) item(wk[i], wave + kQaWaves * i, &sl[1][0][0], acc);
-    if (lane < 16) slab[1][wave][lane] = acc[0];
+    for (int t = 0; t < kQaMaxKv; ++t)
+      if (t < nkv) {
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < NK; ++i) item(wk[t][i], wave + kQaWaves * i, &sl[1 + t][0][0], acc);
+        if (lane < 16) slab[1 + t][wave][lane] = acc[0];
+      }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // (uniform: jkv is the workgroup's)
+    __builtin_amdgcn_s_barrier();   // (uniform: nkv is the workgroup's)
     asm volatile("" ::: "memory");
   }
-  // wave 1: the k / v tile's epilogue (/ rms, RoPE of k, the cache row and the per-q-head copies)
-  if (wave == 1 && jkv >= 0) {
-    const int n = lane & 15;
-    float v = slab[1][0][n];
+  // waves 2, 3: the k / v tiles' epilogues (/ rms, RoPE of k, the cache row and the per-q-head copies)
+  if (wave >= 2 && wave - 2 < nkv) {
+    const int ik = wave - 2, n = lane & 15;
+    float v = slab[1 + ik][0][n];
 #pragma unroll
-    for (int w = 1; w < kQaWaves; ++w) v += slab[1][w][n];
+    for (int w = 1; w < kQaWaves; ++w) v += slab[1 + ik][w][n];
     v = v / rms;
     const float partner = lane_xor<1>(v);
     if (lane < 16) {
-      const int ng = gk * 16 + n;
+      const int ng = (ik ? gk[1] : gk[0]) * 16 + n;
       const bool is_k = ng < qd + kvd;
       float rr = v;
       if (is_k) {
@@ -286,10 +325,10 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     }
   }
 
-  // ---- 6. wave 0: gather the head's q from its S workgroups (tile d / 16 from workgroups tile + QT
-  // part, parts in order), / rms, RoPE (tensor_engine.cpp:1602-1612, the fused epilogue's pattern)
-  if (wave == 0) {
-    const int d = lane, t = d >> 4, n = d & 15;
+  // ---- 6. threads < head_dim: gather the head's q from its S workgroups (tile d / 16 from workgroups
+  // tile + QT part, parts in order), / rms, RoPE (tensor_engine.cpp:1602-1612, the fused epilogue's pattern)
+  if (tid < HD) {
+    const int d = tid, t = d >> 4, n = d & 15;
     float v = 0.0f;
     for (int part = 0; part < kparts; ++part) {
       const unsigned long long* g = a.xchg + ((size_t)h * S + t + QT * part) * 16 + n;
@@ -403,6 +442,23 @@ extern "C" size_t ti_qkv_attn_part_ml_elems(int heads, int head_dim, int splits)
 }
 extern "C" size_t ti_qkv_attn_xchg_bytes(int heads, int splits) { return (size_t)heads * splits * 16 * 8; }
 
+// the (q items, k / v items) per wave a kernel is instantiated for, by bits and head_dim (see the dispatch)
+static bool qa_has_kernel(int bits, int head_dim, int nq, int nk) {
+  if (head_dim == 64) return (bits == 4 || bits == 8) && ((nq == 1 && (nk == 1 || nk == 2)) || (nq == 2 && nk == 2));
+  return head_dim == 128 && (bits == 4 || bits == 8) && nq == 4 && nk == 4;
+}
+
+extern "C" int ti_qkv_attn_supported(int bits, int K, int heads, int kv_heads, int head_dim, int splits) {
+  if ((bits != 4 && bits != 8) || (head_dim != 64 && head_dim != 128) || K < 1024 || K > kQaMaxK || K % 128 ||
+      heads * head_dim > 4096 || kv_heads < 1 || heads < kv_heads || heads % kv_heads || (heads / kv_heads) & (heads / kv_heads - 1))
+    return 0;
+  const int QT = head_dim / 16, KT = K / 128, kv_tiles = 2 * kv_heads * head_dim / 16;
+  if (splits < QT || splits > TI_ATTN_MAX_PART_SPLITS || splits % QT || KT % (splits / QT) || (KT / (splits / QT)) % 8 ||
+      kv_tiles > heads * splits * kQaMaxKv)
+    return 0;
+  return qa_has_kernel(bits, head_dim, KT / (splits / QT) / kQaWaves, KT / kQaWaves) ? 1 : 0;
+}
+
 extern "C" int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, int bits, const uint16_t* fx,
                                     const float* ss_in, int n_ss, float eps, const float* rope_cs, const int32_t* pos,
                                     uint16_t* k_cache, uint16_t* v_cache, int max_seq, int K, int heads, int kv_heads,
@@ -412,19 +468,20 @@ extern "C" int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, i
     return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_partials: null pointer");
   if (bits != 4 && bits != 8)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_partials: bits %d (4 or 8)", bits);
-  if (head_dim != 64) return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_partials: head_dim %d (64)", head_dim);
+  if (head_dim != 64 && head_dim != 128)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_partials: head_dim %d (64 or 128)", head_dim);
   const int QT = head_dim / 16, KT = K / 128;
-  if (K < 1024 || K > kQaMaxK || K % 128 || n_ss < 1 || n_ss > 256 || max_seq < 1)
+  if (K < 1024 || K > kQaMaxK || K % 128 || n_ss < 1 || n_ss > 256 || max_seq < 1 || heads * head_dim > 4096)
     return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_partials: K %d (1024..%d, %% 128), n_ss %d (1..256)", K, kQaMaxK, n_ss);
   int kv_shift = 0;
   while (kv_heads > 0 && (kv_heads << kv_shift) < heads) ++kv_shift;
-  if (kv_heads < 1 || heads <= kv_heads || (kv_heads << kv_shift) != heads || heads % 8)
-    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_partials: heads %d / kv_heads %d (GQA, power of two, heads %% 8)",
-                        heads, kv_heads);
+  if (kv_heads < 1 || heads < kv_heads || (kv_heads << kv_shift) != heads)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_partials: heads %d / kv_heads %d (a power of two)", heads,
+                        kv_heads);
   const int kv_tiles = 2 * kv_heads * head_dim / 16;
   // splits: a multiple of the q tiles of a head, each k-part a multiple of 8 k-tiles (whole waves)
   if (splits < QT || splits > TI_ATTN_MAX_PART_SPLITS || splits % QT || KT % (splits / QT) ||
-      (KT / (splits / QT)) % 8 || kv_tiles > heads * splits)
+      (KT / (splits / QT)) % 8 || kv_tiles > heads * splits * kQaMaxKv)
     return ti_set_error(TI_ERR_ARG, "ti_qkv_attn_partials: splits %d (a multiple of %d up to %d that splits %d k-tiles "
                         "into multiples of 8)", splits, QT, TI_ATTN_MAX_PART_SPLITS, KT);
   QkvAttnArgs a;
@@ -455,7 +512,7 @@ extern "C" int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, i
       const char* v = getenv("TI_QA_EXTRA");
       return v ? atoi(v) : -1;
     }();
-    a.last_extra = env >= 0 ? env : kv_tiles >= heads ? 2 * tile_bytes / key_bytes : 0;
+    a.last_extra = env >= 0 ? env : kv_tiles >= heads && kv_tiles < heads * splits ? 2 * tile_bytes / key_bytes : 0;
   }
   a.scale = 1.0f / sqrtf((float)head_dim);   // tensor_engine.cpp:1288, as ti_attn_decode
   a.part_o = part_o;
@@ -464,8 +521,23 @@ extern "C" int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, i
   const int grid = heads * splits;
   a.stamp = ti_stamp_next(STAMP_ATTN, grid);
   hipStream_t s = (hipStream_t)stream;
-  if (bits == 8) hipLaunchKernelGGL((qkv_attn_kernel<8, 64>), dim3(grid), dim3(kQaThreads), 0, s, a);
-  else hipLaunchKernelGGL((qkv_attn_kernel<4, 64>), dim3(grid), dim3(kQaThreads), 0, s, a);
-  TI_LAUNCH_CHECK("qkv_attn_kernel");
-  return TI_OK;
+  const int nq = KT / (splits / QT) / kQaWaves, nk = KT / kQaWaves, key = nq * 10 + nk;
+  const dim3 g(grid), blk(kQaThreads);
+#define TI_QA_CASE(B, H, Q, KK)                                                          \
+  if (bits == B && head_dim == H && key == Q * 10 + KK) {                                \
+    hipLaunchKernelGGL((qkv_attn_kernel<B, H, Q, KK>), g, blk, 0, s, a);               \
+    TI_LAUNCH_CHECK("qkv_attn_kernel");                                                  \
+    return TI_OK;                                                                        \
+  }
+  TI_QA_CASE(8, 64, 1, 2)   // TinyLlama-1.1B (K 2048, 8 splits: two k-parts of 8 k-tiles)
+  TI_QA_CASE(4, 64, 1, 2)
+  TI_QA_CASE(8, 64, 1, 1)   // K 1024, 4 splits
+  TI_QA_CASE(4, 64, 1, 1)
+  TI_QA_CASE(8, 64, 2, 2)   // K 2048, 4 splits
+  TI_QA_CASE(4, 64, 2, 2)
+  TI_QA_CASE(4, 128, 4, 4)  // Llama-2-7B (K 4096, 8 splits: one q tile each)
+  TI_QA_CASE(8, 128, 4, 4)
+#undef TI_QA_CASE
+  return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_partials: no kernel for bits %d, head_dim %d, %d q / %d k-v items per wave",
+                      bits, head_dim, nq, nk);
 }
