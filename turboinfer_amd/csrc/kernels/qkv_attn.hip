@@ -57,6 +57,9 @@ constexpr int kQaWaves = 8, kQaThreads = kQaWaves * kWave;
 #ifndef TI_QA_KV_RING
 #define TI_QA_KV_RING 3   // K / V slots of 8 keys in flight per wave (5: 1704 vs 1722 tok/s, profiles/r6_qa_ab.txt)
 #endif
+#ifndef TI_QA_ISSUE_BARRIER
+#define TI_QA_ISSUE_BARRIER 0   // head_dim 128: a barrier between the small loads and the weights (802 vs 806 tok/s: off)
+#endif
 #ifndef TI_QA_KVW_LATE
 #define TI_QA_KVW_LATE 0   // 1: the k / v tiles' weights issued after the q part instead of after staging (A/B)
 #endif
@@ -143,11 +146,14 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     const int piece = ic < n_scq ? kp * KTP * 2 + ic : r2 - ik * KT * 2;
     sc_reg = *((const u32x4*)(a.scales + (size_t)g * KT * 16) + piece);
   }
-  const u32x4 xr = *(const u32x4*)(a.fx + 8 * (tid < K8 ? tid : K8 - 1));
+  const u32x4 xr0 = *(const u32x4*)(a.fx + 8 * (tid < K8 ? tid : K8 - 1));
   float ss4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) ss4[j] = a.ss[lane + 64 * j < a.n_ss ? lane + 64 * j : 0];
   asm volatile("" ::: "memory");   // (the small loads stay ahead of the weights: staging waits for them only)
+  // head_dim 128: every wave's small loads enter the CU's queue before any wave's 12 KiB of weights (a
+  // barrier orders the issue only; it waits for no load), so no wave's x waits behind the others' weights
+  if constexpr (HD == 128 && TI_QA_ISSUE_BARRIER) __builtin_amdgcn_s_barrier();
   // weights: q items kt = kp * KTP + wave + 8 i (i < KTP / 8), k / v items kt = wave + 8 i (i < KT / 8)
   u32x4 wq[NQ][C];
 #pragma unroll
@@ -156,6 +162,30 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
 #pragma unroll
     for (int c = 0; c < C; ++c) wq[i][c] = *(src + c * kWave);
   }
+  // The k / v tiles' weights: at head_dim 128 (MHA: every workgroup exactly kQaMaxKv tiles, checked on the
+  // host) right behind the q part's, with no branch, so the CU's queue stays full from the start; with a
+  // runtime count (GQA) after the staging barrier (a branch around loads issued before it would make the
+  // staging wait count them: they are needed only after the q part)
+  constexpr bool kKvwUniform = HD == 128;
+  u32x4 wk[kQaMaxKv][NK][C];
+  auto load_kv_weights = [&]() {
+#pragma unroll
+    for (int t = 0; t < kQaMaxKv; ++t)
+#pragma unroll
+      for (int i = 0; i < NK; ++i)
+        if (kKvwUniform || t < nkv) {   // (wave-uniform)
+          const u32x4* src = a.tiles + ((size_t)gk[t] * KT + wave + kQaWaves * i) * (kWave * C) + lane;
+#pragma unroll
+          for (int c = 0; c < C; ++c) wk[t][i][c] = __builtin_nontemporal_load(src + c * kWave);
+        }
+  };
+  if constexpr (kKvwUniform && !TI_QA_KVW_LATE) load_kv_weights();
+  // every weight load issued before the staging's first wait: memory ops cannot cross the first asm, and
+  // the small loads' values pass through the second, so no use of them is scheduled above the loads
+  asm volatile("" ::: "memory");
+  u32x4 xr = xr0;
+  if constexpr (kKvwUniform)
+    asm volatile("" : "+v"(xr), "+v"(sc_reg), "+v"(ss4[0]), "+v"(ss4[1]), "+v"(ss4[2]), "+v"(ss4[3]));
   // ---- 2. stage x (int4: the high-nibble slots scaled by 1/16 and the offset correction, as
   // gemv_wq_kernel's register prep), the scales; rms of the row
   {
@@ -200,23 +230,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     cs = *(const float2*)(a.rope_cs + (size_t)p * HD + (d & ~1));
   }
 
-  // the k / v tiles' weights after the staging barrier (a branch around loads issued before it would make
-  // the staging wait count them: they are needed only after the q part)
-  u32x4 wk[kQaMaxKv][NK][C];
-  auto load_kv_weights = [&]() {
-#pragma unroll
-    for (int t = 0; t < kQaMaxKv; ++t)
-#pragma unroll
-      for (int i = 0; i < NK; ++i)
-        if (t < nkv) {   // (wave-uniform)
-          const u32x4* src = a.tiles + ((size_t)gk[t] * KT + wave + kQaWaves * i) * (kWave * C) + lane;
-#pragma unroll
-          for (int c = 0; c < C; ++c) wk[t][i][c] = __builtin_nontemporal_load(src + c * kWave);
-        }
-  };
-#if !TI_QA_KVW_LATE
-  load_kv_weights();
-#endif
+  if constexpr (!kKvwUniform && !TI_QA_KVW_LATE) load_kv_weights();
 
 
   // ---- 3. the K/V ring of the attention goes out now (its addresses need only p)
@@ -270,6 +284,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     for (int i = 0; i < NQ; ++i) item(wq[i], kp * KTP + wave + kQaWaves * i, &sl[0][0][0], acc);
     if (lane < 16) slab[0][wave][lane] = acc[0];   // row 0 of the C layout: lanes 0-15, component 0
   }
+  STAMP_MARK(ph_qdata);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -301,6 +316,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     __builtin_amdgcn_s_barrier();   // (uniform: nkv is the workgroup's)
     asm volatile("" ::: "memory");
   }
+  STAMP_MARK(ph_kv);
   // waves 2, 3: the k / v tiles' epilogues (/ rms, RoPE of k, the cache row and the per-q-head copies)
   if (wave >= 2 && wave - 2 < nkv) {
     const int ik = wave - 2, n = lane & 15;
@@ -427,7 +443,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     if (d == 0) *(float2*)(a.part_ml + 2 * rrow) = make_float2(mx, l);
   }
   STAMP_MARK(ph_end);
-  stamp_end(a.stamp, t_entry, ph_staged, ph_qpart, ph_gathered, ph_attn, ph_end, ph_end, ph_attn);
+  stamp_end(a.stamp, t_entry, ph_staged, ph_qdata, ph_qpart, ph_kv, ph_gathered, ph_attn, ph_end);
 }
 
 }  // namespace ti
@@ -443,9 +459,10 @@ extern "C" size_t ti_qkv_attn_part_ml_elems(int heads, int head_dim, int splits)
 extern "C" size_t ti_qkv_attn_xchg_bytes(int heads, int splits) { return (size_t)heads * splits * 16 * 8; }
 
 // the (q items, k / v items) per wave a kernel is instantiated for, by bits and head_dim (see the dispatch)
-static bool qa_has_kernel(int bits, int head_dim, int nq, int nk) {
+// (head_dim 128 kernels assume every workgroup has exactly kQaMaxKv k / v tiles: kv_tiles = 2 heads splits)
+static bool qa_has_kernel(int bits, int head_dim, int nq, int nk, bool kv_uniform) {
   if (head_dim == 64) return (bits == 4 || bits == 8) && ((nq == 1 && (nk == 1 || nk == 2)) || (nq == 2 && nk == 2));
-  return head_dim == 128 && (bits == 4 || bits == 8) && nq == 4 && nk == 4;
+  return head_dim == 128 && (bits == 4 || bits == 8) && nq == 4 && nk == 4 && kv_uniform;
 }
 
 extern "C" int ti_qkv_attn_supported(int bits, int K, int heads, int kv_heads, int head_dim, int splits) {
@@ -456,7 +473,8 @@ extern "C" int ti_qkv_attn_supported(int bits, int K, int heads, int kv_heads, i
   if (splits < QT || splits > TI_ATTN_MAX_PART_SPLITS || splits % QT || KT % (splits / QT) || (KT / (splits / QT)) % 8 ||
       kv_tiles > heads * splits * kQaMaxKv)
     return 0;
-  return qa_has_kernel(bits, head_dim, KT / (splits / QT) / kQaWaves, KT / kQaWaves) ? 1 : 0;
+  return qa_has_kernel(bits, head_dim, KT / (splits / QT) / kQaWaves, KT / kQaWaves, kv_tiles == kQaMaxKv * heads * splits)
+             ? 1 : 0;
 }
 
 extern "C" int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, int bits, const uint16_t* fx,
@@ -521,6 +539,9 @@ extern "C" int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, i
   const int grid = heads * splits;
   a.stamp = ti_stamp_next(STAMP_ATTN, grid);
   hipStream_t s = (hipStream_t)stream;
+  if (head_dim == 128 && kv_tiles != kQaMaxKv * heads * splits)
+    return ti_set_error(TI_ERR_UNSUPPORTED, "ti_qkv_attn_partials: head_dim 128 needs %d k / v tiles per workgroup",
+                        kQaMaxKv);
   const int nq = KT / (splits / QT) / kQaWaves, nk = KT / kQaWaves, key = nq * 10 + nk;
   const dim3 g(grid), blk(kQaThreads);
 #define TI_QA_CASE(B, H, Q, KK)                                                          \
