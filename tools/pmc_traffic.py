@@ -25,7 +25,8 @@ MODELS = {   # bench.py MODELS: vocab, hidden, layers, heads, kv_heads, head_dim
     "tinyllama-1.1b": (32000, 2048, 22, 32, 4, 64, 5632, 8),
     "llama3-8b": (128256, 4096, 32, 32, 8, 128, 14336, 4),
 }
-GEMM = ("gemv_wq_kernel", "gemm_rows_kernel", "gemm_tile_kernel", "gemv_mb_kernel", "gemv_mbr_kernel")
+GEMM = ("gemv_wq_kernel", "gemm_rows_kernel", "gemm_tile_kernel", "gemv_mb_kernel", "gemv_mbr_kernel",
+        "qkv_attn_kernel")   # (the fused QKV + attention of one stream, DESIGN 4.19: its step position is QKV's)
 
 
 def lin_bytes(bits, K, N):
@@ -55,6 +56,9 @@ def main():
     algo, n, bits = class_bytes(a.model, a.batch)
     gemm_key = f"gemv_wq_kernel<{bits}>" if a.batch == 1 else "gemm_family"
     rows = [r for r in csv.DictReader(open(a.src)) if r["Counter_Name"] == "FETCH_SIZE"]
+    if any("qkv_attn_kernel" in r["Kernel_Name"] for r in rows):   # the qkv class also streams the K/V (bench.py)
+        V, H, layers_, nh, nkv, hd, I, _ = MODELS[a.model]
+        algo["qkv"] += 2 * nkv * hd * a.kv * 2 + nh * hd * (4 + 2)
     fam = defaultdict(list)
     names = defaultdict(set)
     for r in rows:
