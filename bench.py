@@ -335,7 +335,7 @@ def main() -> int:
         if name == "qkv" and qa_on:   # the fused launch: the q / k / v weights and the K / V it attends over
             by += att_iso[1]
             iso_us += att_iso[0]      # (isolated: the two unfused launches, for comparison)
-            kname = f"qkv_attn_kernel<{bits},64> (QKV + attention, one launch)"
+            kname = f"qkv_attn_kernel<{bits},{hd}> (QKV + attention, one launch)"
         per[name] = {"avg_us": round(us, 3), "bytes": int(by), "GBps": round(by / us / 1e3, 1), "kernel": kname,
                      "in_step_launches": c["n"], "span_us": round(c["span"] / c["n"], 3),
                      "gap_us": round(c["gap"] / c["n"], 3), "cu_shared_wgs": round(c["cu_shared"] / c["n"], 2),
