@@ -143,10 +143,12 @@ int ti_engine_set_prefill(ti_engine* e, int rows);
  * on = 0/1 sets both, -1 leaves them; *active (nullable) receives whether 1-stream steps fold. */
 int ti_engine_set_fold(ti_engine* e, int on, int* active);
 
-/* QKV and attention of single-stream steps in one launch (ti_hip.h ti_qkv_attn_partials; GQA models
- * with head_dim 64, hidden 1024..2048 and int4 / int8 weights, with the fold and split partials on,
- * e.g. TinyLlama-1.1B): default on (env TI_QKV_ATTN=0 turns it off).  on = 0/1 sets it, -1 leaves it; *active (nullable) receives whether
- * 1-stream steps of this engine use it. */
+/* QKV and attention of single-stream steps in one launch (ti_hip.h ti_qkv_attn_partials; int4 / int8
+ * weights, hidden <= 4096, with the fold and split partials on, at head_dim 64 GQA (TinyLlama-1.1B)
+ * and head_dim 128 MHA (Llama-2-7B); ti_qkv_attn_supported decides).  Default on (env TI_QKV_ATTN=0
+ * turns it off).  Replaces round 4's function of the same name (removed then), with new semantics.
+ * on = 0/1 sets it, -1 leaves it; *active (nullable) receives whether 1-stream steps of this engine
+ * use it.  Changing it drops the engine's captured step graphs. */
 int ti_engine_set_qkv_attn(ti_engine* e, int on, int* active);
 
 /* One decode step: token[s] at position pos[s] for each stream; logits [n][vocab] to host

@@ -105,7 +105,7 @@ struct ti_engine {
   bool part_on = true;         // TI_ATTN_PART=0 turns it off
   uint16_t* part_o = nullptr;  // [heads][TI_ATTN_MAX_PART_SPLITS][head_dim] (+ k_p, v_p: ti_qkv_attn_partials)
   float* part_ml = nullptr;    // [heads][TI_ATTN_MAX_PART_SPLITS][2] (+ q)
-  // one stream of a GQA head_dim-64 model: QKV and the attention in one launch (ti_qkv_attn_partials,
+  // one stream (head_dim 64 GQA or head_dim 128 MHA): QKV and the attention in one launch (ti_qkv_attn_partials,
   // DESIGN 4.19), the new key merged by the O projection (TI_X_ATTN_SPLITS_NEW); TI_QKV_ATTN=0 turns it off
   bool qa_on = true;
   void* qa_xchg = nullptr;     // the q exchange of ti_qkv_attn_partials (zeroed once, generations kept)
@@ -353,7 +353,7 @@ bool part_usable(ti_engine* e, int M) {
 
 
 // QKV + attention in one launch (ti_qkv_attn_partials): one stream with the fold and split partials,
-// a GQA model with head_dim 64 (TinyLlama-1.1B), int8 / int4 group-128 weights.
+// int8 / int4 group-128 weights, head_dim 64 GQA (TinyLlama-1.1B) or head_dim 128 MHA (Llama-2-7B).
 bool qa_usable(ti_engine* e, int M) {
   const ti_engine_config& c = e->c;
   if (!e->qa_on || M != 1 || !fold_usable(e, M) || !part_usable(e, M)) return false;
