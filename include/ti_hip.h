@@ -154,15 +154,11 @@ int ti_fill_kv_uniform(uint64_t seed, uint32_t tensor_id, int n, int kv_heads, i
  * TI_X_ATTN_SPLITS (M == 1, K = heads * head_dim <= 4096, norm_w NULL): x is the attention
  * output still split, x = part_o of ti_attn_decode_partials with epi->ss_in = part_ml,
  * epi->n_ss = splits (<= TI_ATTN_MAX_PART_SPLITS) and epi->head_dim; the launch merges the
- * splits (max-rescaled, sum-weighted, as the attention's own merge) while staging x.
- * TI_X_ATTN_SPLITS_NEW (bits 4 / 8, otherwise as TI_X_ATTN_SPLITS): the splits of
- * ti_qkv_attn_partials, which cover the keys before the step's own; that key is merged as one more
- * split of (max, sum) = (q . k_p / sqrt(head_dim), 1) and row v_p, read from behind the partials:
- * k_p at x + (heads * n_ss + h) * head_dim, v_p at x + (heads * (n_ss + 1) + h) * head_dim (fp16, one
- * row per q-head), q at ss_in + heads * n_ss * 2 + h * head_dim (fp32).
+ * splits (max-rescaled, sum-weighted, as the attention's own merge) while staging x (also the
+ * output of ti_qkv_attn_partials).
  * Epilogue (all outputs of one call): */
 enum ti_x_kind { TI_X_F16 = 0, TI_X_F32 = 1, TI_X_F32_RMSNORM = 2, TI_X_F16_FOLDED = 3, TI_X_ATTN_SPLITS = 4,
-                 TI_X_F16_PACKED = 5, TI_X_ATTN_SPLITS_NEW = 6 };
+                 TI_X_F16_PACKED = 5 };
 /* TI_X_F16_PACKED: fp16 rows in the batched-rows kernel's fragment order, so every load of its
  * MFMA operands is one contiguous KiB per wave (bits 4).  Element (m, k) of an M x K operand
  * (K % 128 == 0) sits at TI_PACKED_INDEX(m, k, K / 128); the buffer holds ceil(M / 16) * 16
@@ -319,13 +315,14 @@ int ti_attn_decode_partials(const float* q, const uint16_t* k_cache, const uint1
                             int64_t kv_stream_stride, int max_seq, const int32_t* pos, int M, int heads,
                             int kv_heads, int head_dim, int splits, uint16_t* part_o, float* part_ml,
                             ti_stream_t s);
-/* One decode stream of a GQA model with head_dim 64 (bits 4 or 8, heads a multiple of 8, 1024 <= K <=
- * 2048): the QKV projection of the folded input (TI_X_F16_FOLDED: fx, ss_in[0 .. n_ss)) with the
- * TI_EPI_QKV_ROPE_KV epilogue's arithmetic -- the new K / V row into k_cache / v_cache
- * ([kv_heads][max_seq][head_dim], slot pos[0]) -- and ti_attn_decode_partials over the keys BEFORE
- * pos[0], in one launch of heads x splits workgroups (inference_engine.cpp:203-279 and 291-368 ->
- * tensor_engine.cpp:490-640, 1510-1624, 1254-1388).  The step's own key is left to the O projection
- * (TI_X_ATTN_SPLITS_NEW with x = part_o, ss_in = part_ml, n_ss = splits): part_o holds
+/* One decode stream (bits 4 or 8; head_dim 64 GQA, or head_dim 128 with heads == kv_heads; 1024 <= K <=
+ * 4096; ti_qkv_attn_supported): the QKV projection of the folded input (TI_X_F16_FOLDED: fx,
+ * ss_in[0 .. n_ss)) with the TI_EPI_QKV_ROPE_KV epilogue's arithmetic -- the new K / V row into
+ * k_cache / v_cache ([kv_heads][max_seq][head_dim], slot pos[0]) -- and ti_attn_decode_partials over
+ * the keys up to pos[0], in one launch of heads x splits workgroups (inference_engine.cpp:203-279 and
+ * 291-368 -> tensor_engine.cpp:490-640, 1510-1624, 1254-1388); the last split also attends the step's own
+ * key (from the k / v rows the launch computes).  The O projection merges the splits with x kind
+ * TI_X_ATTN_SPLITS (x = part_o, ss_in = part_ml, n_ss = splits): part_o holds
  * ti_qkv_attn_part_o_elems and part_ml ti_qkv_attn_part_ml_elems elements.  tiles / scales: the fused
  * q | k | v weight as ti_gemm_wq_a16 takes it (N = (heads + 2 kv_heads) * head_dim).  The S workgroups
  * of a head split its q rows (tile s % (head_dim / 16), k-part s / (head_dim / 16)) and exchange them

@@ -23,7 +23,7 @@ ROOT = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("TI_LIB") or os.path.join(HERE, "lib", "libturboinfer_amd.so")
 
 TI_OK = 0
-X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED, X_ATTN_SPLITS, X_F16_PACKED, X_ATTN_SPLITS_NEW = 0, 1, 2, 3, 4, 5, 6
+X_F16, X_F32, X_F32_RMSNORM, X_F16_FOLDED, X_ATTN_SPLITS, X_F16_PACKED = 0, 1, 2, 3, 4, 5
 ATTN_MAX_PART_SPLITS = 8           # TI_ATTN_MAX_PART_SPLITS (include/ti_hip.h)
 EPI_STORE_F32, EPI_STORE_F16, EPI_RESID_F32, EPI_SILU_MUL_F16, EPI_QKV_ROPE_KV, EPI_LOGITS_ARGMAX = range(6)
 ARGMAX_SLOTS = 32

@@ -103,10 +103,10 @@ struct ti_engine {
   // single-stream attention leaves its split merge to the O projection (ti_attn_decode_partials
   // + TI_X_ATTN_SPLITS): no arrival-ticket hand-off at the end of the attention launch
   bool part_on = true;         // TI_ATTN_PART=0 turns it off
-  uint16_t* part_o = nullptr;  // [heads][TI_ATTN_MAX_PART_SPLITS][head_dim] (+ k_p, v_p: ti_qkv_attn_partials)
-  float* part_ml = nullptr;    // [heads][TI_ATTN_MAX_PART_SPLITS][2] (+ q)
+  uint16_t* part_o = nullptr;  // [heads][TI_ATTN_MAX_PART_SPLITS][head_dim]
+  float* part_ml = nullptr;    // [heads][TI_ATTN_MAX_PART_SPLITS][2]
   // one stream (head_dim 64 GQA or head_dim 128 MHA): QKV and the attention in one launch (ti_qkv_attn_partials,
-  // DESIGN 4.19), the new key merged by the O projection (TI_X_ATTN_SPLITS_NEW); TI_QKV_ATTN=0 turns it off
+  // DESIGN 4.19), O merging its splits (TI_X_ATTN_SPLITS); TI_QKV_ATTN=0 turns it off
   bool qa_on = true;
   void* qa_xchg = nullptr;     // the q exchange of ti_qkv_attn_partials (zeroed once, generations kept)
   // on-device sampling (ti_engine_generate_sampled): the step graph ends with ti_sample_step
@@ -462,7 +462,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
     eo.ldo = H;
     eo.out = e->h;
     fold_into(eo, L.ffn_norm, L.gu.N);
-    if (qa) {   // QKV + attention in one launch; O merges the splits and the step's own key
+    if (qa) {   // QKV + attention in one launch; O merges the splits
       stamp_tag(TI_STAMP_TAG_QKV);
       const int S = e->splits_for(M);
       TI_TRY(ti_qkv_attn_partials(L.qkv.tiles, L.qkv.scales, c.bits, e->fx, e->ss, n_ss, c.eps, e->rope_cs, e->pos,
@@ -472,7 +472,7 @@ int enqueue_step(ti_engine* e, int M, int advance) {
       eo.n_ss = S;
       eo.head_dim = c.head_dim;
       stamp_tag(TI_STAMP_TAG_O);
-      TI_TRY(gemm(L.o, e->part_o, TI_X_ATTN_SPLITS_NEW, qd, 2, nullptr, eo, 4, false));
+      TI_TRY(gemm(L.o, e->part_o, TI_X_ATTN_SPLITS, qd, 2, nullptr, eo, 4, false));
     } else if (part) {   // the O projection merges the attention's splits while staging its input
       stamp_tag(TI_STAMP_TAG_QKV);
       TI_TRY(gemm(L.qkv, e->h, TI_X_F32_RMSNORM, H, 4, L.attn_norm, ep, 4, false));

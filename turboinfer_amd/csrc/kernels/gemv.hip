@@ -155,9 +155,7 @@ __host__ __device__ inline int gemv_lds_bytes_tiles(int M, int K, int tiles_per_
 // XM_F16F: fp16 rows of h * nw (TI_X_F16_FOLDED, one row) staged like XM_F16; the rms comes
 // from the producer's partial sums of squares and divides the outputs before the epilogue.
 // XM_ATTN: the attention's split partials (TI_X_ATTN_SPLITS, one row), merged while staging.
-// XM_ATTN_NT: the same plus the step's own key, which the attention did not see (TI_X_ATTN_SPLITS_NEW,
-// ti_qkv_attn_partials): q, k_p and v_p behind the partials, merged as one more split.
-enum { XM_F16 = 0, XM_F32 = 1, XM_NORM1 = 2, XM_NORM = 3, XM_F16F = 4, XM_ATTN = 5, XM_ATTN_NT = 6 };
+enum { XM_F16 = 0, XM_F32 = 1, XM_NORM1 = 2, XM_NORM = 3, XM_F16F = 4, XM_ATTN = 5 };
 
 // Generic staging (M > 1 with rms_norm, f32 rows, or rows longer than the register
 // prefetch covers).  Runs after the ring is issued, so its loads wait behind the ring.
@@ -346,7 +344,6 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
                                                                    int p_N, int p_kx, int p_ldo, const float* p_pre,
                                                                    GemvArgs a) {
   const unsigned long long t_entry = stamp_now();
-  constexpr bool kAttnX = XM == XM_ATTN || XM == XM_ATTN_NT;   // the attention's split partials as x
   const unsigned bid = blockIdx.x;
   a.tiles = p_tiles;
   a.scales = p_scales;
@@ -357,7 +354,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   // t0 = b q + min(b, r) (scalar arithmetic only; launch_gemv packs it)
   const int nt_q = p_N & 0xff, nt_r = (int)((unsigned)p_N >> 8);
   a.K = p_kx & 0xffff;
-  a.ldx = XM == XM_F16F || kAttnX ? a.K : (int)((unsigned)p_kx >> 16);
+  a.ldx = XM == XM_F16F || XM == XM_ATTN ? a.K : (int)((unsigned)p_kx >> 16);
   const int p_grid = (p_mgk >> 6) & 0xfff;
   a.N = 16 * (nt_q * p_grid + nt_r);
   constexpr int C = TileFmt<BITS>::kChunks;
@@ -370,7 +367,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: counters live in SGPRs
   const int t0 = (int)bid * nt_q + ((int)bid < nt_r ? (int)bid : nt_r);
   const int ntl = nt_q + ((int)bid < nt_r ? 1 : 0);
-  constexpr bool kOneRow = XM == XM_F16F || kAttnX || XM == XM_NORM1;   // (M == 1 by construction)
+  constexpr bool kOneRow = XM == XM_F16F || XM == XM_ATTN || XM == XM_NORM1;   // (M == 1 by construction)
   const int KW = wave < KT ? (KT - wave + kGemvWaves - 1) / kGemvWaves : 0;   // k-tiles per tile, this wave
   const int total = ntl * KW;
   static_assert(!G32 || BITS != 16, "group-32 weights: int4 / int8");
@@ -407,12 +404,10 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   // x rows and the epilogue input depend on the previous launch
   // XM_ATTN: this thread's 8 dims (one head) of every split, and the splits' (max, sum)
   constexpr int kPS = TI_ATTN_MAX_PART_SPLITS;
-  u32x4 po[kAttnX ? kPS : 1];
-  float2 pml[kAttnX ? kPS : 1];
-  u32x4 nt_k = {0u, 0u, 0u, 0u}, nt_v = nt_k;   // XM_ATTN_NT: the new key's row pieces and q
-  float4 nt_q0 = {0.0f, 0.0f, 0.0f, 0.0f}, nt_q1 = nt_q0;
+  u32x4 po[XM == XM_ATTN ? kPS : 1];
+  float2 pml[XM == XM_ATTN ? kPS : 1];
   auto load_x = [&]() {
-    if constexpr (kAttnX) {
+    if constexpr (XM == XM_ATTN) {
       const int S = (int)((unsigned)p_kx >> 16), hsh = ((p_mgk >> 21) & 3) == 2 ? 7 : 6;
       const int i = tid < K8 ? tid : K8 - 1, h = (8 * i) >> hsh, d = (8 * i) & ((1 << hsh) - 1);
 #pragma unroll
@@ -420,15 +415,6 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
         const int r = h * S + (sp < S ? sp : S - 1);
         po[sp] = *(const u32x4*)((const f16*)a.x + ((size_t)r << hsh) + d);
         pml[sp] = *(const float2*)(p_aux + 2 * r);
-      }
-      if constexpr (XM == XM_ATTN_NT) {   // behind the partials: k_p, v_p per q-head (fp16), q (fp32)
-        const int heads = a.K >> hsh;
-        const f16* kn = (const f16*)a.x + (((size_t)heads * S + h) << hsh) + d;
-        nt_k = *(const u32x4*)kn;
-        nt_v = *(const u32x4*)(kn + ((size_t)heads << hsh));
-        const float* qn = p_aux + (size_t)heads * S * 2 + ((size_t)h << hsh) + d;
-        nt_q0 = *(const float4*)qn;
-        nt_q1 = *(const float4*)(qn + 4);
       }
     } else if constexpr (XM == XM_NORM1) {
       const int k8 = tid < K8 ? tid : K8 - 1;
@@ -504,8 +490,8 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
 #pragma unroll
     for (int c = 0; c < C; ++c) ring[s][c] = ld_w(tb + o + c * kWave);
   }
-  const bool fold = (XM == XM_F16 || kAttnX) && kind == TI_EPI_RESID_F32 && a.epi.fold_x != nullptr;
-  if constexpr (XM == XM_F16 || kAttnX) {   // fold weight (consumed by the epilogue)
+  const bool fold = (XM == XM_F16 || XM == XM_ATTN) && kind == TI_EPI_RESID_F32 && a.epi.fold_x != nullptr;
+  if constexpr (XM == XM_F16 || XM == XM_ATTN) {   // fold weight (consumed by the epilogue)
     const float* fw_p = fold ? a.epi.fold_w + (size_t)t0 * 16 + (tid < n_res ? tid : 0) : pre_p;
     fw_pre = *fw_p;
   }
@@ -519,8 +505,8 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   // int4 (group 128): the x pieces staged from registers get their 1/16 scaling and offset correction
   // here, before the staging barrier (no second LDS pass and barrier in front of the stream); every
   // piece of x must come from registers for that (rare long shapes take the pass below)
-  constexpr bool kRegPrep = BITS == 4 && !G32 && (XM == XM_NORM1 || kAttnX || XM == XM_F16 || XM == XM_F16F);
-  const bool reg_prep = kRegPrep && (XM == XM_NORM1 || kAttnX || nx16 <= XPF * kGemvThreads);
+  constexpr bool kRegPrep = BITS == 4 && !G32 && (XM == XM_NORM1 || XM == XM_ATTN || XM == XM_F16 || XM == XM_F16F);
+  const bool reg_prep = kRegPrep && (XM == XM_NORM1 || XM == XM_ATTN || nx16 <= XPF * kGemvThreads);
   if constexpr (XM == XM_NORM1) {
     // rms_norm (tensor_engine.cpp:1488-1505) of the single row, x and w held in registers.
     float ss = 0.0f;
@@ -549,28 +535,13 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       part = group_sum<16>(part);
       if (tid < K8 && (lane & 15) == 0) corr[(tid >> 4) * 16] = part;
     }
-  } else if constexpr (kAttnX) {
+  } else if constexpr (XM == XM_ATTN) {
     // the attention's split merge (attention.hip last-arriver merge): weights
     // l_s * exp(m_s - max), normalised rows o_s, empty splits (m = -inf) weigh 0
     const int S = (int)((unsigned)p_kx >> 16);
     float mx = -INFINITY;
 #pragma unroll
     for (int sp = 0; sp < kPS; ++sp) mx = sp < S ? fmaxf(mx, pml[sp].x) : mx;
-    float snew = -INFINITY;
-    if constexpr (XM == XM_ATTN_NT) {
-      const int hsh = ((p_mgk >> 21) & 3) == 2 ? 7 : 6;
-      // the new key's score, as attn_split_body forms it: q * scale, fmaf over the thread's 8 dims,
-      // summed over the head's hd / 8 lanes (8 consecutive threads at hd 64, 16 at hd 128)
-      const float scale = hsh == 6 ? 0.125f : 1.0f / __fsqrt_rn(128.0f);   // 1 / sqrt(head_dim)
-      const float qv[8] = {nt_q0.x * scale, nt_q0.y * scale, nt_q0.z * scale, nt_q0.w * scale,
-                           nt_q1.x * scale, nt_q1.y * scale, nt_q1.z * scale, nt_q1.w * scale};
-      const f16x8 kf = __builtin_bit_cast(f16x8, nt_k);
-      float dq = 0.0f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dq = fmaf(qv[e], (float)kf[e], dq);
-      snew = hsh == 6 ? group_sum<8>(dq) : group_sum<16>(dq);
-      mx = fmaxf(mx, snew);
-    }
     float num[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, den = 0.0f;
 #pragma unroll
     for (int sp = 0; sp < kPS; ++sp) {
@@ -579,13 +550,6 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
       const f16x8 o = __builtin_bit_cast(f16x8, po[sp]);
 #pragma unroll
       for (int e = 0; e < 8; ++e) num[e] = fmaf(f, (float)o[e], num[e]);
-    }
-    if constexpr (XM == XM_ATTN_NT) {   // the new key: one more split of (max, sum) = (score, 1), row v_p
-      const float f = __expf(snew - mx);
-      den += f;
-      const f16x8 vf = __builtin_bit_cast(f16x8, nt_v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) num[e] = fmaf(f, (float)vf[e], num[e]);
     }
     float part = 0.0f;
     if (tid < K8) {
@@ -630,7 +594,7 @@ __global__ __launch_bounds__(kGemvThreads, 1) void gemv_wq_kernel(const u32x4* p
   }
   if constexpr (XM == XM_F16 || XM == XM_F16F) {
     if (nx16 > XPF * kGemvThreads) stage_x_generic<XM>(a, xl, red, XPF * kGemvThreads);
-  } else if constexpr (XM != XM_NORM1 && !kAttnX) {
+  } else if constexpr (XM != XM_NORM1 && XM != XM_ATTN) {
     stage_x_generic<XM>(a, xl, red, 0);
   }
   if (a.epi.kind == TI_EPI_QKV_ROPE_KV && tid < a.M) ((int*)(es + a.M * a.epi.head_dim))[tid] = __builtin_bit_cast(int, pre);
@@ -2251,7 +2215,6 @@ __host__ inline int gemv_xmode(int x_kind, int M, int K) {
   if (x_kind == TI_X_F16) return XM_F16;
   if (x_kind == TI_X_F16_FOLDED) return XM_F16F;
   if (x_kind == TI_X_ATTN_SPLITS) return XM_ATTN;
-  if (x_kind == TI_X_ATTN_SPLITS_NEW) return XM_ATTN_NT;
   if (x_kind == TI_X_F32) return XM_F32;
   return M == 1 && (K >> 3) <= kGemvThreads ? XM_NORM1 : XM_NORM;
 }
@@ -2262,10 +2225,9 @@ static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid) {
                      : a.epi.kind == TI_EPI_QKV_ROPE_KV ? (const float*)a.epi.pos : (const float*)a.x;
   const int xm = gemv_xmode(a.x_kind, a.M, a.K);
   // packed preloaded arguments (see gemv_wq_kernel)
-  const bool attn_x = xm == XM_ATTN || xm == XM_ATTN_NT;
-  const float* aux = xm == XM_F16F || attn_x ? a.epi.ss_in : xm == XM_F16 ? nullptr : a.norm_w;
-  const int mgk = a.M | (grid << 6) | (a.epi.kind << 18) | (attn_x ? (a.epi.head_dim / 64) << 21 : 0);
-  const int kx = a.K | ((xm == XM_F16F || attn_x ? a.epi.n_ss : a.ldx) << 16);
+  const float* aux = xm == XM_F16F || xm == XM_ATTN ? a.epi.ss_in : xm == XM_F16 ? nullptr : a.norm_w;
+  const int mgk = a.M | (grid << 6) | (a.epi.kind << 18) | (xm == XM_ATTN ? (a.epi.head_dim / 64) << 21 : 0);
+  const int kx = a.K | ((xm == XM_F16F || xm == XM_ATTN ? a.epi.n_ss : a.ldx) << 16);
   const int ldo = a.epi.ldo;
   const int NT = a.N >> 4, nt_q = NT / grid, nt_r = NT % grid;   // the kernel's tile split (gemv_wq_kernel)
   if (nt_q > 255 || nt_r >= (1 << 23))
@@ -2275,13 +2237,6 @@ static int launch_gemv(const GemvArgs& a, int lds, hipStream_t s, int grid) {
     case XM_F16: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
     case XM_F32: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F32, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
     case XM_ATTN: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_ATTN, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
-    case XM_ATTN_NT:
-      if constexpr (!G32 && !AFF && BITS != 16) {
-        hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_ATTN_NT, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a);
-        break;
-      } else {
-        return ti_set_error(TI_ERR_UNSUPPORTED, "gemv_wq_kernel: TI_X_ATTN_SPLITS_NEW with bits %d", BITS);
-      }
     case XM_F16F: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_F16F, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
     case XM_NORM1: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM1, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
     default: hipLaunchKernelGGL((gemv_wq_kernel<BITS, XM_NORM, G32, AFF>), dim3(grid), dim3(kGemvThreads), lds, s, a.tiles, a.scales, a.x, aux, mgk, pn, kx, ldo, pre, a); break;
@@ -2509,8 +2464,7 @@ extern "C" int ti_gemm_prepare(void) {
       (const void*)gemv_wq_kernel<16, XM_NORM1>, (const void*)gemv_wq_kernel<16, XM_NORM>,
       (const void*)gemv_wq_kernel<4, XM_F16F>, (const void*)gemv_wq_kernel<8, XM_F16F>,
       (const void*)gemv_wq_kernel<16, XM_F16F>, (const void*)gemv_wq_kernel<4, XM_ATTN>,
-      (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>,
-      (const void*)gemv_wq_kernel<4, XM_ATTN_NT>, (const void*)gemv_wq_kernel<8, XM_ATTN_NT>, TI_MB_FNS, TI_ROWS_FNS,
+      (const void*)gemv_wq_kernel<8, XM_ATTN>, (const void*)gemv_wq_kernel<16, XM_ATTN>, TI_MB_FNS, TI_ROWS_FNS,
       TI_TILE_FNS};
   for (const void* f : fns)
     TI_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024),
@@ -2648,11 +2602,11 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: M must be in [1,%d] (got %d)", TI_GEMM_MAX_ROWS, M);
   if (K <= 0 || (K & 127) || N <= 0 || (N & 15))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: K %% 128 and N %% 16 must be 0 (K=%d N=%d)", K, N);
-  if (x_kind < TI_X_F16 || x_kind > TI_X_ATTN_SPLITS_NEW)
+  if (x_kind < TI_X_F16 || x_kind > TI_X_F16_PACKED)
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: bad x_kind %d", x_kind);
   if (x_kind == TI_X_F16_PACKED && bits != 4)
     return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: TI_X_F16_PACKED needs bits 4 (batched-rows kernel)");
-  if ((x_kind == TI_X_ATTN_SPLITS || x_kind == TI_X_ATTN_SPLITS_NEW) &&
+  if (x_kind == TI_X_ATTN_SPLITS &&
       (M != 1 || !epi->ss_in || epi->n_ss < 1 || epi->n_ss > TI_ATTN_MAX_PART_SPLITS ||
        (epi->head_dim != 64 && epi->head_dim != 128) || K % epi->head_dim || K > 4096))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: TI_X_ATTN_SPLITS needs M == 1, ss_in, 1 <= n_ss <= %d, head_dim "
@@ -2660,8 +2614,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
   if (x_kind == TI_X_F16_FOLDED && (M != 1 || !epi->ss_in || epi->n_ss < 1 || epi->n_ss > 256))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: TI_X_F16_FOLDED needs M == 1, ss_in and 1 <= n_ss <= 256");
   const bool fold_out = epi->kind == TI_EPI_RESID_F32 && epi->fold_x;
-  if (fold_out && M == 1 && (!epi->fold_w || !epi->fold_ss || (x_kind != TI_X_F16 && x_kind != TI_X_ATTN_SPLITS &&
-                                                          x_kind != TI_X_ATTN_SPLITS_NEW)))
+  if (fold_out && M == 1 && (!epi->fold_w || !epi->fold_ss || (x_kind != TI_X_F16 && x_kind != TI_X_ATTN_SPLITS)))
     return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: fold_x needs M == 1, fp16 x, fold_w and fold_ss");
   if (fold_out && M > 1 && (!epi->fold_w || !epi->fold_ss || x_kind != TI_X_F16_PACKED || M > TI_FOLD_SS_ROWS ||
                             (N & 127)))
@@ -2696,7 +2649,7 @@ static int gemm_impl(const void* tiles, const uint16_t* scales, int bits, const 
       return ti_set_error(TI_ERR_ARG, "ti_gemm_wq_a16: unknown epilogue %d", epi->kind);
   }
   if (g32 && !g32_tile && !g32_rowsk && M > g32_rows) {   // pieces of g32_rows rows through the fused kernel
-    if (x_kind == TI_X_ATTN_SPLITS || x_kind == TI_X_ATTN_SPLITS_NEW || x_kind == TI_X_F16_FOLDED || epi->out_packed)
+    if (x_kind == TI_X_ATTN_SPLITS || x_kind == TI_X_F16_FOLDED || epi->out_packed)
       return ti_set_error(TI_ERR_UNSUPPORTED, "ti_gemm_wq_a16: group-32 rows > 16 need plain x rows");
     const size_t x_elem = x_kind == TI_X_F16 ? 2 : 4;
     const size_t out_elem = epi->kind == TI_EPI_STORE_F16 || epi->kind == TI_EPI_SILU_MUL_F16 ? 2 : 4;

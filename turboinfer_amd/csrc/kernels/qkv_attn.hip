@@ -1,28 +1,26 @@
-// qkv_attn.hip -- one decode stream of a GQA model with head_dim 64 (TinyLlama-1.1B, configs[1]): the
-// QKV projection and the attention over the cache in ONE launch (ti_qkv_attn_partials),
-// i.e. TransformerLayer::forward_incremental's q / k / v projections, RoPE, KV append and
+// qkv_attn.hip -- one decode stream (TinyLlama-1.1B GQA head_dim 64, configs[1]; Llama-2-7B MHA head_dim 128,
+// configs[2]): the QKV projection and the attention over the cache in ONE launch (ti_qkv_attn_partials,
+// DESIGN 4.19), i.e. TransformerLayer::forward_incremental's q / k / v projections, RoPE, KV append and
 // compute_attention (inference_engine.cpp:203-279, 291-368; tensor_engine.cpp:1254-1388).
 //
 // Workgroup (head h, split s) = blockIdx (s + S h); S = splits workgroups per head.
 //   1. x = fp16(h * nw) of the rms_norm fold (TI_X_F16_FOLDED) staged in LDS, the rms from the
 //      producer's partial sums of squares;
 //   2. its share of the head's q rows: tile s % QT of the head (QT = head_dim / 16 tiles), k-part
-//      s / QT of S / QT -- one k-tile per wave at TinyLlama's shape -- with the fused GEMV's item
-//      arithmetic; the 8 waves' partials summed in a fixed order and published as 16 data-tagged
-//      8-byte granules {value, generation} (agent-scope stores);
-//      and on kv_tiles of the workgroups (split S - 1 first), one whole k or v tile: the QKV
-//      epilogue's arithmetic (RoPE of k), the new K / V row into the cache at p = pos[0];
-//   3. the head's 64 q values gathered from its S workgroups' granules (each workgroup keeps a
-//      generation count in its own slot: every launch advances every slot by one, so the siblings'
-//      expected tag is its own), summed over the k-parts in order, / rms, RoPE;
+//      s / QT of S / QT, with the fused GEMV's item arithmetic; the 8 waves' partials summed in a
+//      fixed order and published as 16 data-tagged 8-byte granules {value, generation} (agent-scope
+//      stores); then its k / v tiles (qa_kv_tile: GQA, split S - 1 first; MHA, a k and a v tile each):
+//      the QKV epilogue's arithmetic (RoPE of k), the new K / V row into the cache at p = pos[0], and
+//      the row's fp16 values published in pairs as 8 more granules per tile;
+//   3. the head's q gathered from its S workgroups' granules (each workgroup keeps a generation count
+//      in its own slot: every launch advances every slot by one, so the siblings' expected tag is its
+//      own), summed over the k-parts in order, / rms, RoPE;
 //   4. the split's share of the OLD keys [0, p) against q_h (attn_split_body's one-query lane
-//      layout, online softmax, wave merge), its normalised row and (max, sum) written as
-//      ti_attn_decode_partials writes them; split S - 1 is shorter by the k / v tile's bytes.
-// The new key is not attended here (another workgroup of this launch is writing it): split 0 of each
-// head leaves q_h, and the k / v workgroups leave k_p, v_p per q-head, behind the partials, and the
-// O projection merges the new key as one more split while it stages its input
-// (TI_X_ATTN_SPLITS_NEW, gemv.hip XM_ATTN_NT).  The one hand-off inside the launch is the q exchange
-// among a head's S workgroups; every wait in it is bounded (a lost sibling costs a wrong q, not a hang).
+//      layout, online softmax); the last wave of split S - 1 then attends the new key p itself, its
+//      k_p / v_p taken from the k / v tiles' granules; wave merge; the split's normalised row and
+//      (max, sum) written as ti_attn_decode_partials writes them, for the O projection to merge
+//      (TI_X_ATTN_SPLITS).  Split S - 1 is shorter (last_extra keys) for its tiles / the new key.
+// Every wait on a granule is bounded (a lost sibling costs a wrong result, not a hang).
 #include <math.h>
 #include <stdlib.h>
 
@@ -69,6 +67,7 @@ constexpr int kQaWaves = 8, kQaThreads = kQaWaves * kWave;
 // 1712; profiles/r6_qa_ab.txt)
 #define TI_QA_KV_LATE -1
 #endif
+constexpr int kQaSlot = 32;   // granules per workgroup: the q part's 16, then 8 per k / v tile (k_p / v_p pairs)
 constexpr int kQaMaxK = 4096;
 constexpr int kQaMaxKv = 2;      // k / v tiles per workgroup (MHA at 8 splits: a k and a v tile each)
 constexpr unsigned kQaSpin = 1u << 20;   // bounded wait per granule (~0.1 s)
@@ -126,7 +125,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     nkv += j >= 0 ? 1 : 0;
   }
   const int gq = h * QT + tq;   // global tile of the q part
-  unsigned long long* my_slot = a.xchg + ((size_t)h * S + s) * 16;
+  unsigned long long* my_slot = a.xchg + ((size_t)h * S + s) * kQaSlot;
 
   // ---- 1. small inputs first: position, own generation, scales, x piece, the rms partials, then the
   // whole weight stream.  The position goes through a VGPR the compiler cannot prove uniform (a
@@ -336,8 +335,9 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
       const int c = ng - qd - (is_k ? 0 : kvd), kvh = c / HD, dd = c - kvh * HD;
       const uint16_t hv = f2h(rr);
       (is_k ? a.kc : a.vc)[((size_t)kvh * a.max_seq + p) * HD + dd] = hv;
-      uint16_t* nt = a.part_o + (size_t)a.heads * S * HD + (is_k ? 0 : (size_t)a.heads * HD);
-      for (int g = 0; g < (1 << a.kv_shift); ++g) nt[(size_t)((kvh << a.kv_shift) + g) * HD + dd] = hv;
+      // the row's fp16 values in pairs {lo | hi << 16, generation} for the split that attends the new key
+      const uint32_t pair = (uint32_t)hv | (lane_xor_u32<1>((uint32_t)hv) << 16);
+      if ((n & 1) == 0) st_sc1_u64(my_slot + 16 + ik * 8 + (n >> 1), ((unsigned long long)gen << 32) | pair);
     }
   }
 
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     const int d = tid, t = d >> 4, n = d & 15;
     float v = 0.0f;
     for (int part = 0; part < kparts; ++part) {
-      const unsigned long long* g = a.xchg + ((size_t)h * S + t + QT * part) * 16 + n;
+      const unsigned long long* g = a.xchg + ((size_t)h * S + t + QT * part) * kQaSlot + n;
       unsigned long long x = ld_sc1_u64(g);
       unsigned spin = 0;
       while ((unsigned)(x >> 32) != gen && ++spin < kQaSpin) {
@@ -360,12 +360,29 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     const float partner = lane_xor<1>(v);
     const float rr = (d & 1) == 0 ? fmaf(-partner, cs.y, v * cs.x) : fmaf(v, cs.x, partner * cs.y);
     q_s[d] = rr;
-    if (s == 0) a.part_ml[(size_t)a.heads * S * 2 + (size_t)h * HD + d] = rr;
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   STAMP_MARK(ph_gathered);
+
+  // the new key (position p) of the head's kv-head: attended by the last wave of split S - 1 after its old keys
+  constexpr int kNewWave = kQaWaves - 1;
+  const bool new_key = s == S - 1 && wave == kNewWave;   // (wave-uniform)
+  // lane dl: dims 8 dl .. 8 dl + 7 of k_p and v_p, in the granules 16 + 8 i + (dl & 1) * 4 + 0..3 of the owners of
+  // k / v tile j = kv-head * (HD / 16) + dl / 2 (the inverse of qa_kv_tile; j < 2 heads S, and r / heads with r < 512
+  // exact in fp32 from the +0.5 offset)
+  const unsigned long long* nk_base[2];
+  {
+    const int dl0 = lane % (HD / 8), jk = (h >> a.kv_shift) * (HD / 16) + (dl0 >> 1), hs = a.heads * S;
+    const float inv_heads = __builtin_amdgcn_rcpf((float)a.heads);
+#pragma unroll
+    for (int kv = 0; kv < 2; ++kv) {
+      const int j = jk + kv * (a.kv_tiles >> 1), i = j >= hs ? 1 : 0, r2 = j - i * hs;
+      const int q2 = (int)(((float)r2 + 0.5f) * inv_heads);
+      nk_base[kv] = a.xchg + (size_t)((r2 - q2 * a.heads) * S + (S - 1 - q2)) * kQaSlot + 16 + i * 8 + (dl0 & 1) * 4;
+    }
+  }
 
   // ---- 7. attention of q_h over the split's old keys (attn_split_body, one q-head, LPK lanes a key)
   float qf[8];
@@ -375,9 +392,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
 #pragma unroll
   for (int e = 0; e < 8; ++e) oacc[e] = 0.0f;
   int ci = 0;
-  auto consume = [&](const u32x4& kv, const u32x4& vv) {
-    const bool valid = slot_key(ci) < s1;
-    ++ci;
+  auto consume_key = [&](const u32x4& kv, const u32x4& vv, bool valid) {
     float kf[8], vf[8];
     unpack8(kv, kf);
     unpack8(vv, vf);
@@ -394,6 +409,11 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
 #pragma unroll
     for (int e = 0; e < 8; ++e) oacc[e] = fmaf(pr, vf[e], oacc[e] * alpha);
   };
+  auto consume = [&](const u32x4& kv, const u32x4& vv) {
+    const bool valid = slot_key(ci) < s1;
+    ++ci;
+    consume_key(kv, vv, valid);
+  };
   int a0 = 0;
   for (; a0 + RA <= atot; a0 += RA) {
 #pragma unroll
@@ -403,9 +423,38 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
       arefill(q);
     }
   }
+  auto ring_tail = [&]() {
 #pragma unroll
-  for (int q = 0; q < RA; ++q)
-    if (a0 + q < atot) consume(kr[q], vr[q]);
+    for (int q = 0; q < RA; ++q)
+      if (a0 + q < atot) consume(kr[q], vr[q]);
+  };
+  if (new_key) {
+    // k_p / v_p's granules (nk_base), loaded once every refill is out (a younger load would hold up the ring's
+    // waits), checked after the ring's last slots -- the owners' epilogues published them long before (a bounded wait)
+    const unsigned long long* gp[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gp[e] = nk_base[e >> 2] + (e & 3);
+    unsigned long long nkg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) nkg[e] = ld_sc1_u64(gp[e]);
+    // (the last slots' values pass through here: the tail's math stays below the granule loads)
+#pragma unroll
+    for (int q = 0; q < RA; ++q) asm volatile("" : "+v"(kr[q]), "+v"(vr[q])::"memory");
+    ring_tail();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      unsigned spin = 0;
+      while ((unsigned)(nkg[e] >> 32) != gen && ++spin < kQaSpin) {
+        __builtin_amdgcn_s_sleep(1);
+        nkg[e] = ld_sc1_u64(gp[e]);
+      }
+    }
+    const u32x4 kk = {(uint32_t)nkg[0], (uint32_t)nkg[1], (uint32_t)nkg[2], (uint32_t)nkg[3]};
+    const u32x4 vv = {(uint32_t)nkg[4], (uint32_t)nkg[5], (uint32_t)nkg[6], (uint32_t)nkg[7]};
+    consume_key(kk, vv, kg == 0);
+  } else {
+    ring_tail();
+  }
   {   // merge the lane groups of the wave
     const float mx = groups_max<LPK>(mrun);
     const float f = mrun == -INFINITY ? 0.0f : __expf(mrun - mx);
@@ -456,7 +505,7 @@ extern "C" size_t ti_qkv_attn_part_o_elems(int heads, int head_dim, int splits) 
 extern "C" size_t ti_qkv_attn_part_ml_elems(int heads, int head_dim, int splits) {
   return (size_t)heads * 2 * (size_t)splits + (size_t)heads * head_dim;
 }
-extern "C" size_t ti_qkv_attn_xchg_bytes(int heads, int splits) { return (size_t)heads * splits * 16 * 8; }
+extern "C" size_t ti_qkv_attn_xchg_bytes(int heads, int splits) { return (size_t)heads * splits * kQaSlot * 8; }
 
 // the (q items, k / v items) per wave a kernel is instantiated for, by bits and head_dim (see the dispatch)
 // (head_dim 128 kernels assume every workgroup has exactly kQaMaxKv k / v tiles: kv_tiles = 2 heads splits)
@@ -530,7 +579,11 @@ extern "C" int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, i
       const char* v = getenv("TI_QA_EXTRA");
       return v ? atoi(v) : -1;
     }();
-    a.last_extra = env >= 0 ? env : kv_tiles >= heads && kv_tiles < heads * splits ? 2 * tile_bytes / key_bytes : 0;
+    // (MHA, every split with its tiles: with the new key attended in the launch, split S - 1's last wave reads 8
+    // granules before it -- one ring slot of keys per wave less there covers their latency)
+    a.last_extra = env >= 0 ? env
+                   : kv_tiles >= heads && kv_tiles < heads * splits ? 2 * tile_bytes / key_bytes
+                   : kQaWaves * (64 / (head_dim / 8));
   }
   a.scale = 1.0f / sqrtf((float)head_dim);   // tensor_engine.cpp:1288, as ti_attn_decode
   a.part_o = part_o;
