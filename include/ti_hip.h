@@ -336,6 +336,11 @@ int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, int bits, co
 size_t ti_qkv_attn_part_o_elems(int heads, int head_dim, int splits);
 size_t ti_qkv_attn_part_ml_elems(int heads, int head_dim, int splits);
 size_t ti_qkv_attn_xchg_bytes(int heads, int splits);
+/* Byte offset in xchg of the launch's error word (uint32): nonzero once a wait on a sibling's granule
+ * expired (bounded waits: the launch always completes, that head's q or new key is then wrong).  The
+ * owner reads it after the stream's work and, when set, zeroes the whole buffer to resynchronise the
+ * workgroups' generations (the engine does: ti_engine_generate / ti_engine_step return TI_ERR_HIP). */
+size_t ti_qkv_attn_error_offset(int heads, int splits);
 /* 1 when ti_qkv_attn_partials has a kernel for this shape (0: it would return TI_ERR_UNSUPPORTED / ARG). */
 int ti_qkv_attn_supported(int bits, int K, int heads, int kv_heads, int head_dim, int splits);
 /* Prefill attention (forward_pass over a prompt chunk, inference_engine.cpp:1429-1491 ->

@@ -170,3 +170,33 @@ def test_qkv_attn_off_paths(ti):
     e.set_fold(False)
     assert e.set_qkv_attn(None) is False
     e.close()
+
+
+def test_qkv_attn_lost_sibling_is_reported_and_recovered(ti, monkeypatch):
+    """Every wait in the launch is bounded: a workgroup that withholds its q part (TI_QA_DROP, test
+    hook) leaves its siblings to time out -- the launch completes, the engine reports the step as failed
+    (TI_ERR_HIP, the exchange's error word) and zeroes the exchange, and the step re-run and the next
+    ones match a fresh engine's bit for bit."""
+    v, h, l, nh, nkv, hd, inter, bits, ms = CFGS["gqa16_w8"]
+
+    def make():
+        e = ti.Engine(v, h, l, nh, nkv, hd, inter, bits=bits, max_seq=ms, max_batch=1)
+        e.synth(0x1057, 0.1)
+        e.set_prefill(0)
+        assert e.set_qkv_attn(True) is True
+        return e
+
+    bad, ref = make(), make()
+    monkeypatch.setenv("TI_QA_DROP", "3")
+    with pytest.raises(Exception, match="exchange timed out"):
+        bad.step([7], [0])
+    monkeypatch.delenv("TI_QA_DROP")
+    bad.set_qkv_attn(False)   # (drops the step graph captured with the hook)
+    assert bad.set_qkv_attn(True) is True
+    # (the failed step wrote layers 1.. of position 0's K / V from a wrong head 0: the step is re-run)
+    for pos, tok in ((0, 7), (1, 11), (2, 5)):
+        a = bad.step([tok], [pos])[0]
+        b = ref.step([tok], [pos])[0]
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), pos
+    bad.close()
+    ref.close()

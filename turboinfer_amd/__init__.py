@@ -88,7 +88,7 @@ EXPORTED = [
     "ti_sample_step_ws", "ti_hbm_calibrate", "ti_gemm_kernel_name",
     "ti_gemm_fold_partials", "ti_engine_set_stop", "ti_engine_counters",
     "ti_qkv_attn_partials", "ti_qkv_attn_part_o_elems", "ti_qkv_attn_part_ml_elems", "ti_engine_set_qkv_attn",
-    "ti_qkv_attn_xchg_bytes", "ti_qkv_attn_supported",
+    "ti_qkv_attn_xchg_bytes", "ti_qkv_attn_supported", "ti_qkv_attn_error_offset",
 ]
 
 _lib = None
@@ -195,6 +195,8 @@ def lib() -> C.CDLL:
             L.ti_qkv_attn_xchg_bytes.argtypes = [i32, i32]
             L.ti_qkv_attn_supported.argtypes = [i32, i32, i32, i32, i32, i32]
             L.ti_qkv_attn_xchg_bytes.restype = sz
+            L.ti_qkv_attn_error_offset.argtypes = [i32, i32]
+            L.ti_qkv_attn_error_offset.restype = sz
             L.ti_qkv_attn_part_o_elems.argtypes = [i32, i32, i32]
             L.ti_qkv_attn_part_o_elems.restype = sz
             L.ti_qkv_attn_part_ml_elems.argtypes = [i32, i32, i32]

@@ -352,6 +352,22 @@ bool part_usable(ti_engine* e, int M) {
 }
 
 
+// The fused launch's bounded waits: after the stream's work, a set error word means a workgroup's q part or
+// new key never came (wrong results for that step) -- reported, and the exchange zeroed so the generations
+// agree again.  One 4-byte read on the engine's stream (synchronous).
+int qa_fault_check(ti_engine* e) {
+  if (!e->qa_xchg || !e->qa_on) return TI_OK;
+  const ti_engine_config& c = e->c;
+  const size_t off = ti_qkv_attn_error_offset(c.heads, e->splits_for(1));
+  uint32_t err[2] = {0u, 0u};
+  TI_TRY(ti_memcpy_d2h(err, static_cast<char*>(e->qa_xchg) + off, sizeof(err), e->s));
+  if (!err[0] && !err[1]) return TI_OK;
+  TI_TRY(ti_memset(e->qa_xchg, 0, ti_qkv_attn_xchg_bytes(c.heads, TI_ATTN_MAX_PART_SPLITS), e->s));
+  TI_TRY(ti_stream_sync(e->s));
+  return ti_set_error(TI_ERR_HIP, "engine: the fused QKV + attention launch's exchange timed out (a workgroup's q "
+                      "part or the new key never arrived); results of the last call are wrong, exchange reset");
+}
+
 // QKV + attention in one launch (ti_qkv_attn_partials): one stream with the fold and split partials,
 // int8 / int4 group-128 weights, head_dim 64 GQA (TinyLlama-1.1B) or head_dim 128 MHA (Llama-2-7B).
 bool qa_usable(ti_engine* e, int M) {
@@ -1068,6 +1084,7 @@ int ti_engine_generate(ti_engine* e, int n, const int32_t* prompts, const int32_
     }
   }
   if (last_logits) TI_TRY(ti_memcpy_d2h(last_logits, e->logits, (size_t)n * c.vocab * 4, e->s));
+  if (n == 1) TI_TRY(qa_fault_check(e));
   return TI_OK;
 }
 
@@ -1470,6 +1487,7 @@ int ti_engine_step(ti_engine* e, int n, const int32_t* tokens, const int32_t* po
   TI_TRY(run_steps(e, n, 1, 1));
   TI_TRY(ti_stream_sync(e->s));
   if (logits) TI_TRY(ti_memcpy_d2h(logits, e->logits, (size_t)n * c.vocab * 4, e->s));
+  if (n == 1) TI_TRY(qa_fault_check(e));
   return TI_OK;
 }
 

@@ -49,6 +49,8 @@ struct QkvAttnArgs {
   float* part_ml;              // [heads][S][2], then q [heads][HD]
   unsigned long long* xchg;    // [heads * S][16] granules {float value, uint32 generation}
   unsigned long long* stamp;
+  uint32_t* err;               // set to 1 when a wait on a granule expired (behind the granules of xchg)
+  int drop;                    // test hook (TI_QA_DROP): this workgroup withholds its q part; -1 = none
 };
 
 constexpr int kQaWaves = 8, kQaThreads = kQaWaves * kWave;
@@ -70,7 +72,7 @@ constexpr int kQaWaves = 8, kQaThreads = kQaWaves * kWave;
 constexpr int kQaSlot = 32;   // granules per workgroup: the q part's 16, then 8 per k / v tile (k_p / v_p pairs)
 constexpr int kQaMaxK = 4096;
 constexpr int kQaMaxKv = 2;      // k / v tiles per workgroup (MHA at 8 splits: a k and a v tile each)
-constexpr unsigned kQaSpin = 1u << 20;   // bounded wait per granule (~0.1 s)
+constexpr unsigned kQaSpin = 1u << 16;   // bounded wait per granule (a poll is a ~1 us round trip: ~0.1 s)
 
 // gemv.hip int4_x_prep: the high-nibble slots of an x piece scaled by 1/16 (exact in fp16) and the
 // piece's share of the offset correction 1032 * sum_lo x + 1152 * sum_hi x (deq_int4_raw)
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
     for (int q = 0; q < RA; ++q) arefill(q);
   }
   // ---- 5. wave 0: publish the q part (16 sums over the 8 waves, fixed order); then the k / v tile
-  if (wave == 0 && lane < 16) {
+  if (wave == 0 && lane < 16 && (int)blockIdx.x != a.drop) {
     float v = slab[0][0][lane];
 #pragma unroll
     for (int w = 1; w < kQaWaves; ++w) v += slab[0][w][lane];
@@ -346,6 +348,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
   if (tid < HD) {
     const int d = tid, t = d >> 4, n = d & 15;
     float v = 0.0f;
+    bool lost = false;
     for (int part = 0; part < kparts; ++part) {
       const unsigned long long* g = a.xchg + ((size_t)h * S + t + QT * part) * kQaSlot + n;
       unsigned long long x = ld_sc1_u64(g);
@@ -354,8 +357,10 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
         __builtin_amdgcn_s_sleep(1);
         x = ld_sc1_u64(g);
       }
+      lost |= spin >= kQaSpin;
       v += __builtin_bit_cast(float, (uint32_t)x);
     }
+    if (lost) st_sc1_u32(a.err + (tid & 1), 1u);   // (a per-lane address: one vector store)
     v = v / rms;
     const float partner = lane_xor<1>(v);
     const float rr = (d & 1) == 0 ? fmaf(-partner, cs.y, v * cs.x) : fmaf(v, cs.x, partner * cs.y);
@@ -441,6 +446,7 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
 #pragma unroll
     for (int q = 0; q < RA; ++q) asm volatile("" : "+v"(kr[q]), "+v"(vr[q])::"memory");
     ring_tail();
+    bool lost = false;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       unsigned spin = 0;
@@ -448,7 +454,9 @@ __global__ __launch_bounds__(kQaThreads, 1) void qkv_attn_kernel(const QkvAttnAr
         __builtin_amdgcn_s_sleep(1);
         nkg[e] = ld_sc1_u64(gp[e]);
       }
+      lost |= spin >= kQaSpin;
     }
+    if (lost) st_sc1_u32(a.err + (lane & 1), 1u);
     const u32x4 kk = {(uint32_t)nkg[0], (uint32_t)nkg[1], (uint32_t)nkg[2], (uint32_t)nkg[3]};
     const u32x4 vv = {(uint32_t)nkg[4], (uint32_t)nkg[5], (uint32_t)nkg[6], (uint32_t)nkg[7]};
     consume_key(kk, vv, kg == 0);
@@ -505,7 +513,10 @@ extern "C" size_t ti_qkv_attn_part_o_elems(int heads, int head_dim, int splits) 
 extern "C" size_t ti_qkv_attn_part_ml_elems(int heads, int head_dim, int splits) {
   return (size_t)heads * 2 * (size_t)splits + (size_t)heads * head_dim;
 }
-extern "C" size_t ti_qkv_attn_xchg_bytes(int heads, int splits) { return (size_t)heads * splits * kQaSlot * 8; }
+// the granules, then the error words (a wait expired: a sibling's part never came)
+static size_t qa_granule_bytes(int heads, int splits) { return (size_t)heads * splits * kQaSlot * 8; }
+extern "C" size_t ti_qkv_attn_xchg_bytes(int heads, int splits) { return qa_granule_bytes(heads, splits) + 64; }
+extern "C" size_t ti_qkv_attn_error_offset(int heads, int splits) { return qa_granule_bytes(heads, splits); }
 
 // the (q items, k / v items) per wave a kernel is instantiated for, by bits and head_dim (see the dispatch)
 // (head_dim 128 kernels assume every workgroup has exactly kQaMaxKv k / v tiles: kv_tiles = 2 heads splits)
@@ -589,6 +600,11 @@ extern "C" int ti_qkv_attn_partials(const void* tiles, const uint16_t* scales, i
   a.part_o = part_o;
   a.part_ml = part_ml;
   a.xchg = (unsigned long long*)xchg;
+  a.err = (uint32_t*)((char*)xchg + qa_granule_bytes(heads, splits));
+  {   // (read per call: a test sets and clears it; captured graphs keep the value they were captured with)
+    const char* v = getenv("TI_QA_DROP");
+    a.drop = v ? atoi(v) : -1;
+  }
   const int grid = heads * splits;
   a.stamp = ti_stamp_next(STAMP_ATTN, grid);
   hipStream_t s = (hipStream_t)stream;
