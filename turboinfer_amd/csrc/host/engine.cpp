@@ -355,10 +355,13 @@ bool part_usable(ti_engine* e, int M) {
 // The fused launch's bounded waits: after the stream's work, a set error word means a workgroup's q part or
 // new key never came (wrong results for that step) -- reported, and the exchange zeroed so the generations
 // agree again.  One 4-byte read on the engine's stream (synchronous).
+bool qa_usable(ti_engine* e, int M);
 int qa_fault_check(ti_engine* e) {
-  if (!e->qa_xchg || !e->qa_on) return TI_OK;
+  if (!e->qa_xchg || !qa_usable(e, 1)) return TI_OK;   // (only engines whose 1-stream steps take the launch)
   const ti_engine_config& c = e->c;
   const size_t off = ti_qkv_attn_error_offset(c.heads, e->splits_for(1));
+  if (off + 8 > ti_qkv_attn_xchg_bytes(c.heads, TI_ATTN_MAX_PART_SPLITS))
+    return ti_set_error(TI_ERR_ARG, "engine: exchange error word outside the buffer");
   uint32_t err[2] = {0u, 0u};
   TI_TRY(ti_memcpy_d2h(err, static_cast<char*>(e->qa_xchg) + off, sizeof(err), e->s));
   if (!err[0] && !err[1]) return TI_OK;
